@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Bench: BaggingRegressor(DecisionTreeRegressor).fit on the synthetic C3 workload
+(BASELINE.json configs[2]: 10M rows x 100 features, 128 bootstrap depth-8 trees,
+one MI355X).  One step = one full fit (Poisson bag -> split finding -> binning ->
+8 tree levels for all 128 learners -> forest on the host), inputs resident in HBM.
+
+With --gpus N (launched by torch.distributed.run) every rank trains its own
+128 learners [rank*128, (rank+1)*128) of the same ensemble on its own GPU: weak
+scaling, no collective on the data path (learners are independent).
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import sbag_loader  # noqa: E402
+
+SEED_REG = -1395689524  # default seed of BaggingRegressor (class-name hashCode)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--features", type=int, default=100)
+    ap.add_argument("--learners", type=int, default=128, help="learners per GPU")
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--bins", type=int, default=32)
+    ap.add_argument("--partitions", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--cpu-rows", type=int, default=200_000)
+    ap.add_argument("--cpu-learners", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle (CPU restatement, OpenMP over learners) on a bounded sample of the
+    same workload: cpu_rows rows x F features, cpu_learners learners, same depth/bins."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from spark_bagging_amd import synthetic
+
+    n, L = args.cpu_rows, args.cpu_learners
+    cores = min(L, os.cpu_count() or 1, 16)
+    X, y = synthetic.generate(n, args.features, args.seed, 0)
+    part = [int(round(i * n / args.partitions)) for i in range(args.partitions + 1)]
+    counts = oracle.bag(True, 1.0, 0, L, SEED_REG, part, n)
+    subs = [oracle.subspace(1.0, args.features, SEED_REG + i) for i in range(L)]
+    t0 = time.perf_counter()
+    oracle.fit(X, y, counts, subs, max_depth=args.depth, max_bins=args.bins, nthreads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": L * n / dt, "unit": "estimator*rows/s", "cores": cores, "kind": "port",
+            "sample": f"{n} rows x {args.features} features, {L} learners, depth {args.depth}, "
+                      f"{args.partitions} partitions; oracle/sbag_oracle.c fit only "
+                      f"({dt:.1f} s, restatement, not Spark)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    sb = sbag_loader.load()
+    nat = sb._native
+    ctx = nat.Context(local)
+    N, F, L = args.rows, args.features, args.learners
+    ds = nat.DeviceDataset.synthetic(N, F, seed=args.seed, num_classes=0, ctx=ctx)
+    part = [int(round(i * N / args.partitions)) for i in range(args.partitions + 1)]
+    lb = rank * L
+
+    def step():
+        return nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG,
+                       learner_begin=lb, learner_end=lb + L, partition_offsets=part,
+                       max_depth=args.depth, max_bins=args.bins)
+
+    for _ in range(args.warmup):
+        step().free()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    timings = []
+    for _ in range(args.steps):
+        f = step()
+        timings.append(f.timing())
+        f.free()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * L * N * args.steps / elapsed
+
+    hist_ms = sum(t["hist_ms"] for t in timings)
+    hist_launches = sum(t["hist_launches"] for t in timings)
+    alg_bytes = sum(t["hist_alg_bytes"] for t in timings)
+    achieved = alg_bytes / (hist_ms / 1000.0) / 1e9 if hist_ms > 0 else 0.0
+    last = timings[-1]
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "sbag::k_hist<false>",
+                "avg_launch_ms": round(hist_ms / max(hist_launches, 1), 4),
+                "alg_bytes_per_launch": round(alg_bytes / max(hist_launches, 1)),
+                "upper_bound_GBs_survey": round(last["hist_upper_bytes"] / (last["hist_ms"] / 1e3) / 1e9, 1)
+                if last["hist_ms"] > 0 else None}
+    breakdown = {k: round(v, 3) for k, v in last.items() if k.endswith("_ms")}
+    out = {
+        "metric": "estimator×rows trained/sec", "value": round(value, 1),
+        "unit": "estimator*rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (device generator k_synth: splitmix64 codes mod 32, dyadic labels)",
+        "config": {"workload": "C3: BaggingRegressor(DecisionTreeRegressor) fit, synthetic "
+                               f"{N} rows x {F} features, {L} bootstrap depth-{args.depth} trees per GPU",
+                   "rows": N, "features": F, "learners_per_gpu": L, "learners_total": L * world,
+                   "max_depth": args.depth, "max_bins": args.bins, "partitions": args.partitions,
+                   "replacement": True, "sample_ratio": 1.0, "parallelism": f"learner-shard x{world}"},
+        "roofline": roofline, "breakdown_ms": breakdown,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

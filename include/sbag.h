@@ -1,0 +1,167 @@
+/*
+ * sbag.h — C ABI of the MI355X bagging engine (libsbag.so).
+ *
+ * Drop-in boundary for spark-ensemble's bagging hot path: BaggingRegressor /
+ * BaggingClassifier `.fit` (train) and `.transform` (predict) with a
+ * DecisionTree{Regressor,Classifier} base learner.  Every entry point cites the
+ * reference interface it replaces (paths relative to
+ * /root/reference/core/src/main/scala/org/apache/spark/).  The JNI binding a
+ * maintainer adds on the Scala side is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every call returns an int status: SBAG_OK or one of the SBAG_E* codes below.
+ *    The JNI shim maps SBAG_EINVAL to IllegalArgumentException (the reference's
+ *    `require` / ParamValidators), SBAG_EEMPTY to SparkException ("ML algorithm
+ *    was given empty dataset."), everything else to SparkException.
+ *  - sbag_last_error() returns the message of the calling thread's last failure.
+ *  - Host buffers passed in are read during the call only; the library owns
+ *    device memory and the objects it returns until the matching *_free/_destroy.
+ *  - A context is bound to one device; calls on one context must be serialized
+ *    by the caller (the reference runs learner Futures on a pool,
+ *    ml/regression/BaggingRegressor.scala:169-191; the shim serializes per context).
+ */
+#ifndef SBAG_H
+#define SBAG_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBAG_OK 0
+#define SBAG_EINVAL 1       /* IllegalArgumentException (require, ParamValidators)      */
+#define SBAG_EEMPTY 2       /* SparkException: empty dataset / empty subbag             */
+#define SBAG_EDEVICE 3      /* HIP runtime failure                                      */
+#define SBAG_ENOMEM 4       /* device allocation failure                                */
+#define SBAG_EUNSUPPORTED 5 /* input outside what the engine reproduces bit-exactly     */
+
+#define SBAG_IMPURITY_VARIANCE 0 /* DecisionTreeRegressor (impurity "variance")  */
+#define SBAG_IMPURITY_GINI 1     /* DecisionTreeClassifier (impurity "gini")     */
+
+#define SBAG_AGG_MEAN 0 /* BaggingRegressionModel.predict (BaggingRegressor.scala:248-256)      */
+#define SBAG_AGG_MODE 1 /* BaggingClassificationModel.predict (BaggingClassifier.scala:248-257) */
+
+typedef struct sbag_ctx sbag_ctx;
+typedef struct sbag_dataset sbag_dataset;
+typedef struct sbag_forest sbag_forest;
+
+/* ---- contexts ---------------------------------------------------------- */
+int sbag_device_count(int32_t* n);
+int sbag_ctx_create(int32_t device_ordinal, sbag_ctx** out);
+int sbag_ctx_destroy(sbag_ctx* ctx);
+const char* sbag_last_error(void);
+const char* sbag_version(void);
+
+/* ---- sampler: bfunctions.bag (sql/bfunctions.scala:46-68) --------------
+ * Multiplicities of every row for learners [learner_begin, learner_end):
+ *   replacement      -> Poisson(sample_ratio) reseeded seed+i+partitionIndex
+ *                       (sql/catalyst/expressions/Poisson.scala:53-56,73)
+ *   !replacement, 1  -> all ones (bfunctions.scala:56-57)
+ *   !replacement     -> rand(seed+i) < sample_ratio (bfunctions.scala:62-64,
+ *                       Spark Rand = XORShiftRandom(seed+i+partitionIndex))
+ * partition_offsets[P+1] are the Spark partition boundaries of the DataFrame
+ * rows (row j of partition p gets the j-th draw of stream (i, p)).           */
+typedef struct {
+  int32_t replacement;  /* HasSubBag.replacement (HasSubBag.scala:39-45)            */
+  int32_t pad_;
+  double sample_ratio;  /* HasSubBag.sampleRatio (HasSubBag.scala:52-62)            */
+  int64_t seed;         /* HasSeed.seed (default: class-name hashCode)   */
+  int32_t learner_begin, learner_end; /* global learner indices                    */
+} sbag_sampler_params;
+
+int sbag_sample(sbag_ctx* ctx, const sbag_sampler_params* p, const int64_t* partition_offsets,
+                int32_t num_partitions, int64_t num_rows,
+                uint8_t* counts_out /* host [(end-begin) x num_rows] */);
+
+/* ---- subspace: HasSubBag.mkSubspace (ml/ensemble/HasSubBag.scala:90-106) */
+int sbag_subspace(double ratio, int32_t num_features, int64_t seed, int32_t* idx_out,
+                  int32_t* n_out);
+
+/* ---- datasets (the DataFrame's label + features columns) ---------------- */
+/* X row-major [num_rows x num_features] fp64, y [num_rows]; copied to HBM as
+   per-feature value codes (exact distinct-value dictionaries) + labels.       */
+int sbag_dataset_create(sbag_ctx* ctx, int64_t num_rows, int32_t num_features, const double* X,
+                        const double* y, sbag_dataset** out);
+/* Deterministic synthetic data generated directly in HBM (bench workload):
+   x[r,f] = splitmix64(seed ^ (r*F+f)) mod 32; num_classes == 0 -> dyadic
+   regression label, else a class label in [0, num_classes). */
+int sbag_dataset_synthetic(sbag_ctx* ctx, int64_t num_rows, int32_t num_features, uint64_t seed,
+                           int32_t num_classes, sbag_dataset** out);
+int sbag_dataset_info(const sbag_dataset* ds, int64_t* num_rows, int32_t* num_features);
+int sbag_dataset_labels(const sbag_dataset* ds, double* y_out);
+int sbag_dataset_features(const sbag_dataset* ds, int64_t row_begin, int64_t row_end,
+                          double* X_out /* [(row_end-row_begin) x F] */);
+int sbag_dataset_free(sbag_dataset* ds);
+
+/* ---- fit: BaggingRegressor.train / BaggingClassifier.train --------------
+ * (ml/regression/BaggingRegressor.scala:121-199,
+ *  ml/classification/BaggingClassifier.scala:121-199) with the base learner
+ * DecisionTree{Regressor,Classifier}.fit reached through
+ * HasBaseLearner.fitBaseLearner (ml/ensemble/ensembleParams.scala:99-117).     */
+typedef struct {
+  int32_t max_depth;              /* DecisionTree maxDepth (default 5)            */
+  int32_t max_bins;               /* maxBins (default 32), 2..256                 */
+  int32_t min_instances_per_node; /* default 1                                    */
+  int32_t impurity;               /* SBAG_IMPURITY_*                              */
+  double min_info_gain;           /* default 0.0                                  */
+} sbag_tree_params;
+
+typedef struct {
+  sbag_sampler_params sampler;
+  double subspace_ratio;       /* HasSubBag.subspaceRatio                          */
+  int32_t subspace_bug_compat; /* 1: mkSubspace(getSampleRatio, ...) exactly as the
+                                  reference does (BaggingRegressor.scala:174, H1)  */
+  int32_t num_partitions;      /* 0 or 1 -> a single partition                    */
+  const int64_t* partition_offsets; /* [num_partitions+1] or NULL                 */
+  sbag_tree_params tree;
+} sbag_fit_params;
+
+int sbag_fit(sbag_ctx* ctx, sbag_dataset* ds, const sbag_fit_params* p, sbag_forest** out);
+
+/* ---- forest (BaggingRegressionModel / BaggingClassificationModel fields
+ *      `subspaces`, `models`, `numBaseModels`, BaggingRegressor.scala:235-246) */
+typedef struct { /* DecisionTreeModelReadWrite.NodeData, pre-order ids */
+  int32_t id, left, right, feature; /* feature: subspace-local index, -1 for a leaf */
+  int32_t split_bin, pad_;
+  double threshold, prediction, impurity, gain;
+} sbag_node;
+
+int sbag_forest_num_trees(const sbag_forest* f, int32_t* n);
+int sbag_forest_tree_info(const sbag_forest* f, int32_t t, int32_t* num_nodes, int32_t* num_stats,
+                          int32_t* subspace_len, int32_t* exact_splits);
+int sbag_forest_subspace(const sbag_forest* f, int32_t t, int32_t* idx_out);
+int sbag_forest_nodes(const sbag_forest* f, int32_t t, sbag_node* nodes_out,
+                      double* stats_out /* [num_nodes x num_stats] or NULL */);
+/* rebuild a forest from node arrays (model load / JNI round trip) */
+int sbag_forest_create(int32_t num_trees, const int32_t* num_nodes, const sbag_node* nodes,
+                       const int32_t* subspace_len, const int32_t* subspaces, int32_t impurity,
+                       sbag_forest** out);
+int sbag_forest_free(sbag_forest* f);
+
+/* device-side timing of the last fit (HIP events on the context stream) */
+typedef struct {
+  double total_ms, sample_ms, valuecount_ms, bin_ms, compact_ms, hist_ms, split_ms, subtract_ms;
+  int64_t hist_launches;
+  double hist_alg_bytes;   /* Σ over hist launches: entries x (F_r + 4)   */
+  double hist_entries;     /* Σ entries processed by hist launches                    */
+  double hist_upper_bytes; /* SURVEY §8d upper bound: Σ_r Σ_d inbag_r x (F_r + 4) + 3N */
+  int64_t levels;
+} sbag_timing;
+int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
+
+/* ---- transform: PredictionModel.transform -> Bagging*Model.predict ------
+ * slicer(subspace) (HasSubBag.scala:128-131) + tree walk + mean / breeze mode. */
+int sbag_predict(sbag_ctx* ctx, const sbag_forest* f, const double* X, int64_t num_rows,
+                 int32_t num_features, int32_t agg, double* out /* [num_rows] */,
+                 double* per_tree_out /* [trees x num_rows] or NULL */);
+int sbag_predict_dataset(sbag_ctx* ctx, const sbag_forest* f, const sbag_dataset* ds, int32_t agg,
+                         double* out /* [num_rows] */);
+/* ordered aggregation of per-learner predictions gathered from several
+   devices (RCCL all-gather in learner order): votes [num_learners x num_rows] */
+int sbag_aggregate(sbag_ctx* ctx, const double* votes, int32_t num_learners, int64_t num_rows,
+                   int32_t agg, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

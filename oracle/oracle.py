@@ -1,0 +1,184 @@
+"""ctypes front-end to the C oracle (oracle/lib/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product (spark-bagging_amd/).
+PARITY UNPINNED (see oracle/sbag_oracle.h).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "liboracle.so")
+
+DEFAULT_SEED_REGRESSOR = -1395689524   # "org.apache.spark.ml.regression.BaggingRegressor".hashCode
+DEFAULT_SEED_CLASSIFIER = 42087812     # "org.apache.spark.ml.classification.BaggingClassifier".hashCode
+
+
+class TreeParams(ctypes.Structure):
+    _fields_ = [("max_depth", ctypes.c_int32), ("max_bins", ctypes.c_int32),
+                ("min_instances_per_node", ctypes.c_int32), ("impurity", ctypes.c_int32),
+                ("min_info_gain", ctypes.c_double)]
+
+
+NODE_DTYPE = np.dtype([("id", "<i4"), ("left", "<i4"), ("right", "<i4"), ("feature", "<i4"),
+                       ("split_bin", "<i4"), ("pad", "<i4"), ("threshold", "<f8"),
+                       ("prediction", "<f8"), ("impurity", "<f8"), ("gain", "<f8")])
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        i32, i64, dbl = ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        L.or_hash_seed.restype = ctypes.c_uint64
+        L.or_hash_seed.argtypes = [i64]
+        L.or_xorshift_next.argtypes = [i64, i32, i32, P]
+        L.or_xorshift_doubles.argtypes = [i64, i32, P]
+        L.or_well_next.argtypes = [i64, i32, i32, P]
+        L.or_well_doubles.argtypes = [i64, i32, P]
+        L.or_poisson.argtypes = [dbl, i64, i32, P]
+        L.or_bag.argtypes = [i32, dbl, i32, i32, i64, P, i32, i64, P]
+        L.or_subspace.argtypes = [dbl, i32, i64, P, P]
+        L.or_find_splits.argtypes = [P, i64, i32, i32, P, i32, P, P]
+        L.or_fit.argtypes = [P, P, i64, i32, P, i32, P, P, ctypes.POINTER(TreeParams), i32,
+                             P, i32, P, i32, P, P, P]
+        L.or_predict.argtypes = [P, i64, i32, i32, P, P, P, i32, i32, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def hash_seed(seed):
+    return int(lib().or_hash_seed(seed))
+
+
+def xorshift_next(seed, bits, n):
+    out = np.zeros(n, np.int32)
+    lib().or_xorshift_next(seed, bits, n, _p(out))
+    return out
+
+
+def xorshift_doubles(seed, n):
+    out = np.zeros(n, np.float64)
+    lib().or_xorshift_doubles(seed, n, _p(out))
+    return out
+
+
+def well_next(seed, bits, n):
+    out = np.zeros(n, np.int32)
+    lib().or_well_next(seed, bits, n, _p(out))
+    return out
+
+
+def well_doubles(seed, n):
+    out = np.zeros(n, np.float64)
+    lib().or_well_doubles(seed, n, _p(out))
+    return out
+
+
+def poisson(lam, seed, n):
+    out = np.zeros(n, np.int32)
+    lib().or_poisson(lam, seed, n, _p(out))
+    return out
+
+
+def bag(replacement, ratio, learner_begin, learner_end, seed, part_off, n):
+    part_off = np.ascontiguousarray(part_off, dtype=np.int64)
+    out = np.zeros((learner_end - learner_begin, n), np.uint8)
+    rc = lib().or_bag(int(replacement), float(ratio), learner_begin, learner_end, seed,
+                      _p(part_off), len(part_off) - 1, n, _p(out))
+    if rc:
+        raise ValueError(f"or_bag failed rc={rc}")
+    return out
+
+
+def subspace(ratio, nfeat, seed):
+    idx = np.zeros(max(nfeat, 1), np.int32)
+    n = np.zeros(1, np.int32)
+    lib().or_subspace(float(ratio), nfeat, seed, _p(idx), _p(n))
+    return idx[: n[0]].copy()
+
+
+def find_splits(X, counts, feature, max_bins):
+    X = np.ascontiguousarray(X, np.float64)
+    counts = np.ascontiguousarray(counts, np.uint8)
+    thr = np.zeros(max_bins, np.float64)
+    ex = np.zeros(1, np.int32)
+    nt = lib().or_find_splits(_p(X), X.shape[0], X.shape[1], feature, _p(counts), max_bins,
+                              _p(thr), _p(ex))
+    return thr[:nt].copy(), bool(ex[0])
+
+
+class Forest:
+    """Oracle forest: per-learner pre-order node arrays (NodeData layout)."""
+
+    def __init__(self, nodes, stats, num_nodes, num_stats, subspaces, exact):
+        self.nodes, self.stats = nodes, stats
+        self.num_nodes, self.num_stats = num_nodes, num_stats
+        self.subspaces, self.exact = subspaces, exact
+
+    def tree(self, l):
+        n = int(self.num_nodes[l])
+        return self.nodes[l, :n], self.stats[l, :n, : int(self.num_stats[l])]
+
+
+def fit(X, y, counts, subspaces, max_depth=5, max_bins=32, min_instances_per_node=1,
+        min_info_gain=0.0, classification=False, nthreads=None, max_stats=None):
+    X = np.ascontiguousarray(X, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    counts = np.ascontiguousarray(counts, np.uint8)
+    L, N = counts.shape
+    F = X.shape[1]
+    sub = np.zeros((L, F), np.int32)
+    nsub = np.zeros(L, np.int32)
+    for l, s in enumerate(subspaces):
+        sub[l, : len(s)] = s
+        nsub[l] = len(s)
+    max_nodes = (1 << (max_depth + 1)) - 1
+    if max_stats is None:
+        max_stats = 3 if not classification else int(y.max()) + 1
+    nodes = np.zeros((L, max_nodes), NODE_DTYPE)
+    stats = np.zeros((L, max_nodes, max_stats), np.float64)
+    num_nodes = np.zeros(L, np.int32)
+    num_stats = np.zeros(L, np.int32)
+    exact = np.zeros(L, np.int32)
+    p = TreeParams(max_depth, max_bins, min_instances_per_node, 1 if classification else 0,
+                   min_info_gain)
+    rc = lib().or_fit(_p(X), _p(y), N, F, _p(counts), L, _p(sub), _p(nsub), ctypes.byref(p),
+                      nthreads or os.cpu_count() or 1, _p(nodes), max_nodes, _p(stats), max_stats,
+                      _p(num_nodes), _p(num_stats), _p(exact))
+    if rc:
+        raise ValueError(f"or_fit failed rc={rc}")
+    return Forest(nodes, stats, num_nodes, num_stats, [np.asarray(s, np.int32) for s in subspaces],
+                  exact.astype(bool))
+
+
+def predict(forest, X, classification=False, per_tree=False):
+    X = np.ascontiguousarray(X, np.float64)
+    N, F = X.shape
+    L = forest.nodes.shape[0]
+    sub = np.zeros((L, F), np.int32)
+    nsub = np.zeros(L, np.int32)
+    for l, s in enumerate(forest.subspaces):
+        sub[l, : len(s)] = s
+        nsub[l] = len(s)
+    out = np.zeros(N, np.float64)
+    pt = np.zeros((L, N), np.float64) if per_tree else None
+    lib().or_predict(_p(X), N, F, L, _p(sub), _p(nsub), _p(forest.nodes), forest.nodes.shape[1],
+                     1 if classification else 0, _p(out), _p(pt) if per_tree else None)
+    return (out, pt) if per_tree else out

@@ -1,0 +1,1611 @@
+// sbag_host.cpp — C ABI (include/sbag.h) and host orchestration of the bagging
+// engine.  The host mirrors the control flow of the reference's
+// BaggingRegressor.train (ml/regression/BaggingRegressor.scala:121-199): bag ->
+// per-learner subspace -> base-learner fit -> model of (subspaces, models), but
+// all learners of a context are trained together, level by level, by the HIP
+// kernels of sbag_kernels.hip.  The per-node bookkeeping of Spark 2.4.3's
+// RandomForest (LearningNode, binsToBestSplit's ImpurityStats chain,
+// toNode(prune = true)) lives here; every histogram and split search runs on
+// the device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "sbag.h"
+#include "sbag_internal.h"
+
+using namespace sbag;
+
+// ---------------------------------------------------------------- errors
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIP_TRY(x)                                                                   \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess)                                                            \
+      return fail(e_ == hipErrorOutOfMemory ? SBAG_ENOMEM : SBAG_EDEVICE,            \
+                  std::string(#x) + " failed: " + hipGetErrorString(e_));            \
+  } while (0)
+#define TRY(x)                   \
+  do {                           \
+    int rc_ = (x);               \
+    if (rc_ != SBAG_OK) return rc_; \
+  } while (0)
+
+static const double kDoubleMinValue = -std::numeric_limits<double>::max();  // Scala Double.MinValue
+
+// ---------------------------------------------------------------- context
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+struct sbag_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::unordered_map<std::string, DevBuf> ws;
+  uint64_t* d_jump = nullptr;
+};
+
+static int ws_get(sbag_ctx* c, const std::string& name, size_t bytes, void** out) {
+  DevBuf& b = c->ws[name];
+  if (bytes == 0) bytes = 16;
+  if (b.cap < bytes) {
+    if (b.p) HIP_TRY(hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = bytes + bytes / 8;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      e = hipMalloc(&b.p, bytes);
+      want = bytes;
+    }
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      b.p = nullptr;
+      return fail(SBAG_ENOMEM, "device allocation of " + std::to_string(bytes) + " bytes (" +
+                                   name + ") failed: " + hipGetErrorString(e));
+    }
+    b.cap = want;
+  }
+  *out = b.p;
+  return SBAG_OK;
+}
+
+template <typename T>
+static int ws_typed(sbag_ctx* c, const std::string& name, size_t count, T** out) {
+  void* p;
+  TRY(ws_get(c, name, count * sizeof(T), &p));
+  *out = (T*)p;
+  return SBAG_OK;
+}
+
+template <typename T>
+static int h2d(sbag_ctx* c, T* dst, const T* src, size_t count) {
+  if (count == 0) return SBAG_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return SBAG_OK;
+}
+template <typename T>
+static int d2h(sbag_ctx* c, T* dst, const T* src, size_t count) {
+  if (count == 0) return SBAG_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SBAG_OK;
+}
+
+// ---------------------------------------------------------------- host RNG (subspace, seeds)
+// XORShiftRandom.hashSeed + nextDouble (Spark 2.4.3), used by mkSubspace
+// (ml/ensemble/HasSubBag.scala:97-103) and to build the GF(2) jump tables.
+static uint32_t h_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static uint32_t h_mix_last(uint32_t h, uint32_t k) {
+  k *= 0xcc9e2d51u;
+  k = h_rotl(k, 15);
+  k *= 0x1b873593u;
+  return h ^ k;
+}
+static uint32_t h_mix(uint32_t h, uint32_t k) {
+  h = h_mix_last(h, k);
+  h = h_rotl(h, 13);
+  return h * 5u + 0xe6546b64u;
+}
+static uint32_t h_hash8(const uint8_t* d, uint32_t seed) {
+  uint32_t h = seed;
+  for (int i = 0; i < 8; i += 4) {
+    const uint32_t k = (uint32_t)d[i] | ((uint32_t)d[i + 1] << 8) | ((uint32_t)d[i + 2] << 16) |
+                       ((uint32_t)d[i + 3] << 24);
+    h = h_mix(h, k);
+  }
+  h ^= 8u;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+static uint64_t h_hash_seed(int64_t seed) {
+  uint8_t b[8];
+  const uint64_t u = (uint64_t)seed;
+  for (int i = 0; i < 8; i++) b[i] = (uint8_t)(u >> (56 - 8 * i));
+  const uint32_t lo = h_hash8(b, 0x3c074a61u);
+  const uint32_t hi = h_hash8(b, lo);
+  return ((uint64_t)hi << 32) | lo;
+}
+static uint64_t h_xs_step(uint64_t s) {
+  s ^= s << 21;
+  s ^= s >> 35;
+  s ^= s << 4;
+  return s;
+}
+struct HostXS {
+  uint64_t s;
+  explicit HostXS(int64_t seed) : s(h_hash_seed(seed)) {}
+  int32_t next(int bits) {
+    s = h_xs_step(s);
+    return (int32_t)(uint32_t)(s & ((1ull << bits) - 1));
+  }
+  double next_double() {
+    const int64_t a = next(26);
+    const int64_t b = next(27);
+    return (double)((a << 27) + b) * 0x1.0p-53;
+  }
+};
+
+static int ensure_jump(sbag_ctx* c) {
+  if (c->d_jump) return SBAG_OK;
+  // jump[k][b] = M^(2^k) e_b, M = one XORShift step (linear over GF(2))
+  std::vector<uint64_t> J(63 * 64);
+  for (int b = 0; b < 64; b++) J[b] = h_xs_step(1ull << b);
+  for (int k = 1; k < 63; k++) {
+    for (int b = 0; b < 64; b++) {
+      uint64_t x = J[(k - 1) * 64 + b], acc = 0;
+      for (int q = 0; q < 64; q++)
+        if ((x >> q) & 1) acc ^= J[(k - 1) * 64 + q];
+      J[k * 64 + b] = acc;
+    }
+  }
+  HIP_TRY(hipMalloc(&c->d_jump, J.size() * 8));
+  HIP_TRY(hipMemcpy(c->d_jump, J.data(), J.size() * 8, hipMemcpyHostToDevice));
+  return SBAG_OK;
+}
+
+// ---------------------------------------------------------------- dataset
+struct sbag_dataset {
+  sbag_ctx* ctx = nullptr;
+  int64_t N = 0;
+  int32_t F = 0, S = 0;     // S: row stride in code elements
+  int code_bytes = 1;
+  void* d_codes = nullptr;
+  std::vector<std::vector<double>> dict;  // sorted distinct values per feature (-0.0 == 0.0)
+  std::vector<int32_t> zero_code;         // code of 0.0, -1 when absent
+  std::vector<double> y;
+  int32_t* d_labk = nullptr;              // labels as fixed point k = y * 2^shift
+  int shift = 0;
+  bool label_ok = false;                  // representable as |k| < 2^23
+  int64_t kmin = 0, kmax = 0;
+  bool integral = false;                  // all labels integers >= 0 (classifiable)
+  double* d_dict = nullptr;
+  int64_t* d_dict_off = nullptr;
+};
+
+static int32_t row_stride(int32_t F) {
+  if (F <= 64) return (F + 15) / 16 * 16;
+  return (F + 127) / 128 * 128;
+}
+
+static void analyze_labels(sbag_dataset* ds) {
+  ds->label_ok = false;
+  ds->integral = true;
+  for (double v : ds->y)
+    if (!(v >= 0 && v == std::floor(v) && v < 8388608.0)) {
+      ds->integral = false;
+      break;
+    }
+  for (int s = 0; s <= 40 && !ds->label_ok; s++) {
+    bool ok = true;
+    int64_t mn = 0, mx = 0;
+    bool first = true;
+    for (double v : ds->y) {
+      if (!std::isfinite(v)) {
+        ok = false;
+        break;
+      }
+      const double k = std::ldexp(v, s);
+      if (k != std::floor(k) || std::fabs(k) >= 8388608.0) {
+        ok = false;
+        break;
+      }
+      const int64_t ki = (int64_t)k;
+      if (first) {
+        mn = mx = ki;
+        first = false;
+      }
+      mn = std::min(mn, ki);
+      mx = std::max(mx, ki);
+    }
+    if (ok) {
+      ds->label_ok = true;
+      ds->shift = s;
+      ds->kmin = mn;
+      ds->kmax = mx;
+    }
+  }
+}
+
+static int upload_labels(sbag_dataset* ds) {
+  sbag_ctx* c = ds->ctx;
+  HIP_TRY(hipMalloc(&ds->d_labk, std::max<int64_t>(ds->N, 1) * 4));
+  if (!ds->label_ok) return SBAG_OK;
+  std::vector<int32_t> k(ds->N);
+  for (int64_t i = 0; i < ds->N; i++) k[i] = (int32_t)std::ldexp(ds->y[i], ds->shift);
+  HIP_TRY(hipMemcpy(ds->d_labk, k.data(), ds->N * 4, hipMemcpyHostToDevice));
+  (void)c;
+  return SBAG_OK;
+}
+
+static int upload_dict(sbag_dataset* ds) {
+  std::vector<int64_t> off(ds->F + 1, 0);
+  for (int f = 0; f < ds->F; f++) off[f + 1] = off[f] + (int64_t)ds->dict[f].size();
+  std::vector<double> flat(std::max<int64_t>(off[ds->F], 1));
+  for (int f = 0; f < ds->F; f++)
+    std::copy(ds->dict[f].begin(), ds->dict[f].end(), flat.begin() + off[f]);
+  HIP_TRY(hipMalloc(&ds->d_dict, flat.size() * 8));
+  HIP_TRY(hipMalloc(&ds->d_dict_off, off.size() * 8));
+  HIP_TRY(hipMemcpy(ds->d_dict, flat.data(), flat.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ds->d_dict_off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+  return SBAG_OK;
+}
+
+// ---------------------------------------------------------------- forest
+struct HTree {
+  std::vector<int32_t> sub;
+  std::vector<sbag_node> nodes;
+  std::vector<double> stats;
+  int32_t ns = 0;
+  int32_t exact = 1;
+};
+
+struct sbag_forest {
+  std::vector<HTree> trees;
+  int32_t impurity = 0;
+  sbag_timing timing{};
+  int dev_id = -1;
+  DevNode* d_nodes = nullptr;
+  int64_t* d_off = nullptr;
+  int32_t nclasses = 0;
+  ~sbag_forest() {
+    if (d_nodes) (void)hipFree(d_nodes);
+    if (d_off) (void)hipFree(d_off);
+  }
+};
+
+// ---------------------------------------------------------------- impurity (host, fp64, Spark order)
+struct Calc {  // ImpurityCalculator over exact integer stats
+  const int64_t* st;
+  int ns;
+  bool gini;
+  int shift;
+  double count_d() const {
+    if (!gini) return (double)st[0];
+    double t = 0.0;
+    for (int i = 0; i < ns; i++) t += (double)st[i];
+    return t;
+  }
+  int64_t count() const { return (int64_t)count_d(); }
+  double stat(int i) const {  // the fp64 stats the reference accumulates
+    if (gini) return (double)st[i];
+    if (i == 0) return (double)st[0];
+    if (i == 1) return std::ldexp((double)st[1], -shift);
+    return std::ldexp((double)(uint64_t)st[2], -2 * shift);
+  }
+  double impurity() const {
+    if (!gini) {  // Variance.calculate
+      const double count = stat(0), sum = stat(1), sumsq = stat(2);
+      if (count == 0) return 0.0;
+      const double squared_loss = sumsq - (sum * sum) / count;
+      return squared_loss / count;
+    }
+    const double total = count_d();  // Gini.calculate
+    if (total == 0) return 0.0;
+    double imp = 1.0;
+    for (int i = 0; i < ns; i++) {
+      const double f = (double)st[i] / total;
+      imp -= f * f;
+    }
+    return imp;
+  }
+  double predict() const {
+    const int64_t cnt = count();
+    if (cnt == 0) return 0.0;
+    if (!gini) return stat(1) / (double)cnt;
+    int best = -1;
+    double bv = kDoubleMinValue;
+    for (int i = 0; i < ns; i++)
+      if ((double)st[i] > bv) {
+        bv = (double)st[i];
+        best = i;
+      }
+    return (double)best;
+  }
+};
+
+struct HNode {  // LearningNode
+  int left = -1, right = -1;
+  bool is_leaf = false, has_split = false;
+  int fl = -1, s = -1;
+  double thr = 0.0;
+  std::vector<int64_t> stats;
+  double impurity = 0.0, gain = NAN;
+  bool valid = true;
+};
+
+struct ToNodeRet {
+  bool leaf;
+  double pred;
+};
+
+// LearningNode.toNode(prune = true), emitted as NodeData pre-order
+static ToNodeRet emit(const std::vector<HNode>& nodes, int idx, HTree& t, int ns, bool gini,
+                      int shift, int stats_out) {
+  const HNode& n = nodes[idx];
+  const int my = (int)t.nodes.size();
+  t.nodes.push_back(sbag_node{});
+  t.stats.resize((size_t)(my + 1) * stats_out);
+  Calc c{n.stats.data(), ns, gini, shift};
+  auto fill_stats = [&](int at) {
+    for (int i = 0; i < stats_out; i++) t.stats[(size_t)at * stats_out + i] = c.stat(i);
+  };
+  if (n.has_split) {
+    const size_t mark = t.nodes.size();
+    const int lid = (int)t.nodes.size();
+    ToNodeRet l = emit(nodes, n.left, t, ns, gini, shift, stats_out);
+    const int rid = (int)t.nodes.size();
+    ToNodeRet r = emit(nodes, n.right, t, ns, gini, shift, stats_out);
+    sbag_node& o = t.nodes[my];
+    if (l.leaf && r.leaf && l.pred == r.pred) {
+      t.nodes.resize(mark);
+      t.stats.resize(mark * stats_out);
+      sbag_node& p = t.nodes[my];
+      p = sbag_node{};
+      p.id = my;
+      p.left = p.right = -1;
+      p.feature = -1;
+      p.split_bin = -1;
+      p.prediction = l.pred;
+      p.impurity = n.impurity;
+      p.gain = -1.0;
+      fill_stats(my);
+      return {true, l.pred};
+    }
+    o.id = my;
+    o.left = lid;
+    o.right = rid;
+    o.feature = n.fl;
+    o.split_bin = n.s;
+    o.threshold = n.thr;
+    o.prediction = c.predict();
+    o.impurity = n.impurity;
+    o.gain = n.gain;
+    fill_stats(my);
+    return {false, o.prediction};
+  }
+  sbag_node& o = t.nodes[my];
+  o.id = my;
+  o.left = o.right = -1;
+  o.feature = -1;
+  o.split_bin = -1;
+  o.prediction = c.predict();
+  o.impurity = n.valid ? n.impurity : -1.0;
+  o.gain = -1.0;
+  fill_stats(my);
+  return {true, o.prediction};
+}
+
+// ---------------------------------------------------------------- split finding (host)
+// RandomForest.findSplitsForContinuousFeature over a replica's weighted value
+// counts (the subbag replicates each row `count` times).  `cnt[c]` is the
+// weighted count of dictionary value `vals[c]` among in-bag rows.
+static int find_splits(const std::vector<double>& vals, const uint32_t* cnt, int zero_code, int64_t n,
+                       int max_bins, std::vector<double>& thr) {
+  thr.clear();
+  int64_t nnz = 0;
+  for (size_t c = 0; c < vals.size(); c++)
+    if ((int)c != zero_code) nnz += cnt[c];
+  if (nnz == 0) return 0;  // featureSamples.isEmpty
+  const int64_t max_possible_bins = std::min<int64_t>(max_bins, n);
+  const int64_t num_splits = max_possible_bins - 1;
+  const int64_t num_samples = n;
+  std::vector<std::pair<double, int64_t>> vc;
+  vc.reserve(vals.size());
+  const int64_t zeros = num_samples - nnz;
+  for (size_t c = 0; c < vals.size(); c++) {
+    if ((int)c == zero_code) {
+      if (zeros > 0) vc.emplace_back(0.0, zeros);
+      continue;
+    }
+    if (cnt[c] == 0) continue;
+    vc.emplace_back(vals[c], (int64_t)cnt[c]);
+  }
+  if (zero_code < 0 && zeros > 0) {  // zeros implied although no 0.0 code (cannot happen here)
+    vc.emplace_back(0.0, zeros);
+    std::sort(vc.begin(), vc.end());
+  }
+  const int64_t possible = (int64_t)vc.size() - 1;
+  if (possible == 0) return 0;
+  if (possible <= num_splits) {
+    for (int64_t i = 1; i <= possible; i++) thr.push_back((vc[i - 1].first + vc[i].first) / 2.0);
+  } else {
+    const double stride = (double)num_samples / (double)(num_splits + 1);
+    int32_t current = (int32_t)vc[0].second;
+    double target = stride;
+    for (size_t i = 1; i < vc.size(); i++) {
+      const int32_t prev = current;
+      current += (int32_t)vc[i].second;
+      if (std::fabs((double)prev - target) < std::fabs((double)current - target)) {
+        thr.push_back((vc[i - 1].first + vc[i].first) / 2.0);
+        target += stride;
+      }
+    }
+  }
+  return (int)thr.size();
+}
+
+// ---------------------------------------------------------------- timing
+struct EventTimer {
+  hipStream_t st;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;  // category
+  int begin(int cat) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
+    (void)hipEventRecord(a, st);
+    ev.push_back({cat, {a, b}});
+    return (int)ev.size() - 1;
+  }
+  void end(int h) {
+    if (h >= 0) (void)hipEventRecord(ev[h].second.second, st);
+  }
+  void collect(double* cats, std::vector<double>* hist_each, int hist_cat) {
+    for (auto& e : ev) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e.second.first, e.second.second);
+      cats[e.first] += ms;
+      if (e.first == hist_cat && hist_each) hist_each->push_back(ms);
+    }
+  }
+  ~EventTimer() {
+    for (auto& e : ev) {
+      (void)hipEventDestroy(e.second.first);
+      (void)hipEventDestroy(e.second.second);
+    }
+  }
+};
+enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_NCAT };
+
+// ---------------------------------------------------------------- C ABI
+extern "C" {
+
+const char* sbag_last_error(void) { return g_err.c_str(); }
+const char* sbag_version(void) { return "sbag 0.1 (gfx950)"; }
+
+int sbag_device_count(int32_t* n) {
+  int c = 0;
+  HIP_TRY(hipGetDeviceCount(&c));
+  *n = c;
+  return SBAG_OK;
+}
+
+int sbag_ctx_create(int32_t device_ordinal, sbag_ctx** out) {
+  if (!out) return fail(SBAG_EINVAL, "out is NULL");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device_ordinal < 0 || device_ordinal >= n)
+    return fail(SBAG_EINVAL, "device ordinal " + std::to_string(device_ordinal) + " out of range");
+  HIP_TRY(hipSetDevice(device_ordinal));
+  auto* c = new sbag_ctx();
+  c->device = device_ordinal;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(SBAG_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return SBAG_OK;
+}
+
+int sbag_ctx_destroy(sbag_ctx* c) {
+  if (!c) return SBAG_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->ws)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  if (c->d_jump) (void)hipFree(c->d_jump);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return SBAG_OK;
+}
+
+int sbag_subspace(double ratio, int32_t F, int64_t seed, int32_t* idx, int32_t* n_out) {
+  if (F < 0 || !idx || !n_out) return fail(SBAG_EINVAL, "bad arguments");
+  int n = 0;
+  if (ratio == 1.0) {
+    for (int f = 0; f < F; f++) idx[n++] = f;
+  } else {
+    HostXS r(seed);
+    for (int f = 0; f < F; f++)
+      if (r.next_double() < ratio) idx[n++] = f;
+  }
+  *n_out = n;
+  return SBAG_OK;
+}
+
+static int check_sampler(const sbag_sampler_params* p) {
+  if (!(p->sample_ratio >= 0.0 && p->sample_ratio <= 1.0))
+    return fail(SBAG_EINVAL, "sampleRatio given invalid value " + std::to_string(p->sample_ratio) +
+                                 " (ParamValidators.inRange(0, 1))");
+  if (!(p->sample_ratio > 0)) return fail(SBAG_EINVAL, "requirement failed: sampleRatio must be strictly positive");
+  if (p->learner_end <= p->learner_begin || p->learner_begin < 0)
+    return fail(SBAG_EINVAL, "numBaseLearners given invalid value (learner range empty)");
+  return SBAG_OK;
+}
+
+// counts [R][N] on the device (bfunctions.bag)
+static int run_sampler(sbag_ctx* c, const sbag_sampler_params* p, const std::vector<int64_t>& poff,
+                       int64_t N, uint8_t* d_counts) {
+  const int R = p->learner_end - p->learner_begin;
+  const int P = (int)poff.size() - 1;
+  int64_t* d_poff;
+  TRY(ws_typed(c, "poff", poff.size(), &d_poff));
+  TRY(h2d(c, d_poff, poff.data(), poff.size()));
+  if (p->replacement) {
+    int* d_err;
+    TRY(ws_typed(c, "err", 1, &d_err));
+    HIP_TRY(hipMemsetAsync(d_err, 0, 4, c->stream));
+    const double p_exp = std::exp(-p->sample_ratio);  // PoissonDistribution: FastMath.exp(-mean)
+    launch_poisson(c->stream, d_counts, N, d_poff, P, R, p->learner_begin, p->seed, p->sample_ratio,
+                   p_exp, d_err);
+    HIP_TRY(hipGetLastError());
+    int err = 0;
+    TRY(d2h(c, &err, d_err, 1));
+    if (err) return fail(SBAG_EUNSUPPORTED, "a Poisson draw exceeded 255");
+  } else if (p->sample_ratio == 1.0) {
+    launch_fill(c->stream, d_counts, 1, (int64_t)R * N);
+    HIP_TRY(hipGetLastError());
+  } else {
+    TRY(ensure_jump(c));
+    std::vector<int64_t> cpre(P + 1, 0);
+    for (int q = 0; q < P; q++) cpre[q + 1] = cpre[q] + (poff[q + 1] - poff[q] + 255) / 256;
+    int64_t* d_cpre;
+    TRY(ws_typed(c, "cpre", cpre.size(), &d_cpre));
+    TRY(h2d(c, d_cpre, cpre.data(), cpre.size()));
+    launch_bernoulli(c->stream, d_counts, N, d_poff, d_cpre, P, cpre[P], R, p->learner_begin,
+                     p->seed, p->sample_ratio, c->d_jump);
+    HIP_TRY(hipGetLastError());
+  }
+  return SBAG_OK;
+}
+
+static int check_partitions(int32_t P, const int64_t* off, int64_t N, std::vector<int64_t>& poff) {
+  if (P <= 1 || !off) {
+    poff = {0, N};
+    return SBAG_OK;
+  }
+  poff.assign(off, off + P + 1);
+  if (poff[0] != 0 || poff[P] != N)
+    return fail(SBAG_EINVAL, "partition_offsets must start at 0 and end at num_rows");
+  for (int i = 0; i < P; i++)
+    if (poff[i + 1] < poff[i]) return fail(SBAG_EINVAL, "partition_offsets must be non-decreasing");
+  return SBAG_OK;
+}
+
+int sbag_sample(sbag_ctx* c, const sbag_sampler_params* p, const int64_t* partition_offsets,
+                int32_t P, int64_t N, uint8_t* counts_out) {
+  if (!c || !p || !counts_out || N < 0) return fail(SBAG_EINVAL, "bad arguments");
+  TRY(check_sampler(p));
+  std::vector<int64_t> poff;
+  TRY(check_partitions(P, partition_offsets, N, poff));
+  HIP_TRY(hipSetDevice(c->device));
+  const int R = p->learner_end - p->learner_begin;
+  uint8_t* d_counts;
+  TRY(ws_typed(c, "counts", (size_t)R * std::max<int64_t>(N, 1), &d_counts));
+  TRY(run_sampler(c, p, poff, N, d_counts));
+  TRY(d2h(c, counts_out, d_counts, (size_t)R * N));
+  return SBAG_OK;
+}
+
+int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, const double* y,
+                        sbag_dataset** out) {
+  if (!c || !out || N < 0 || F <= 0 || (N > 0 && (!X || !y))) return fail(SBAG_EINVAL, "bad arguments");
+  if (N == 0) return fail(SBAG_EEMPTY, "ML algorithm was given empty dataset.");
+  if (N >= (int64_t)1 << 32) return fail(SBAG_EUNSUPPORTED, "more than 2^32 rows");
+  HIP_TRY(hipSetDevice(c->device));
+  auto ds = std::make_unique<sbag_dataset>();
+  ds->ctx = c;
+  ds->N = N;
+  ds->F = F;
+  ds->S = row_stride(F);
+  ds->dict.resize(F);
+  ds->zero_code.assign(F, -1);
+  size_t maxd = 0;
+  std::vector<double> col(N);
+  for (int f = 0; f < F; f++) {
+    for (int64_t i = 0; i < N; i++) {
+      double v = X[i * F + f];
+      if (std::isnan(v)) return fail(SBAG_EINVAL, "NaN feature value");
+      if (v == 0.0) v = 0.0;  // -0.0 and 0.0 are one value for split finding
+      col[i] = v;
+    }
+    std::vector<double> d(col);
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    maxd = std::max(maxd, d.size());
+    for (size_t k = 0; k < d.size(); k++)
+      if (d[k] == 0.0) ds->zero_code[f] = (int)k;
+    ds->dict[f] = std::move(d);
+  }
+  if (maxd > 65536)
+    return fail(SBAG_EUNSUPPORTED, "a feature has more than 65536 distinct values");
+  ds->code_bytes = maxd <= 256 ? 1 : 2;
+  const size_t bytes = (size_t)N * ds->S * ds->code_bytes;
+  HIP_TRY(hipMalloc(&ds->d_codes, bytes));
+  {
+    std::vector<uint8_t> buf(bytes, 0);
+    for (int f = 0; f < F; f++) {
+      const auto& d = ds->dict[f];
+      for (int64_t i = 0; i < N; i++) {
+        double v = X[i * F + f];
+        if (v == 0.0) v = 0.0;
+        const size_t k = (size_t)(std::lower_bound(d.begin(), d.end(), v) - d.begin());
+        if (ds->code_bytes == 1)
+          buf[(size_t)i * ds->S + f] = (uint8_t)k;
+        else
+          ((uint16_t*)buf.data())[(size_t)i * ds->S + f] = (uint16_t)k;
+      }
+    }
+    HIP_TRY(hipMemcpy(ds->d_codes, buf.data(), bytes, hipMemcpyHostToDevice));
+  }
+  ds->y.assign(y, y + N);
+  analyze_labels(ds.get());
+  TRY(upload_labels(ds.get()));
+  TRY(upload_dict(ds.get()));
+  *out = ds.release();
+  return SBAG_OK;
+}
+
+int sbag_dataset_synthetic(sbag_ctx* c, int64_t N, int32_t F, uint64_t seed, int32_t num_classes,
+                           sbag_dataset** out) {
+  if (!c || !out || N <= 0 || F <= 0 || num_classes < 0 || num_classes > 256)
+    return fail(SBAG_EINVAL, "bad arguments");
+  if (N >= (int64_t)1 << 32) return fail(SBAG_EUNSUPPORTED, "more than 2^32 rows");
+  HIP_TRY(hipSetDevice(c->device));
+  auto ds = std::make_unique<sbag_dataset>();
+  ds->ctx = c;
+  ds->N = N;
+  ds->F = F;
+  ds->S = row_stride(F);
+  ds->code_bytes = 1;
+  ds->dict.assign(F, std::vector<double>(32));
+  for (int f = 0; f < F; f++)
+    for (int v = 0; v < 32; v++) ds->dict[f][v] = (double)v;
+  ds->zero_code.assign(F, 0);
+  HIP_TRY(hipMalloc(&ds->d_codes, (size_t)N * ds->S));
+  HIP_TRY(hipMalloc(&ds->d_labk, (size_t)N * 4));
+  launch_synth(c->stream, (uint8_t*)ds->d_codes, ds->S, N, F, seed, num_classes, ds->d_labk);
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> k(N);
+  TRY(d2h(c, k.data(), ds->d_labk, (size_t)N));
+  ds->shift = num_classes ? 0 : 6;
+  ds->y.resize(N);
+  ds->kmin = ds->kmax = k[0];
+  for (int64_t i = 0; i < N; i++) {
+    ds->y[i] = std::ldexp((double)k[i], -ds->shift);
+    ds->kmin = std::min<int64_t>(ds->kmin, k[i]);
+    ds->kmax = std::max<int64_t>(ds->kmax, k[i]);
+  }
+  ds->label_ok = true;
+  ds->integral = ds->kmin >= 0 && num_classes > 0;
+  if (num_classes == 0) {
+    ds->integral = true;
+    for (int64_t i = 0; i < N && ds->integral; i++)
+      if (ds->y[i] < 0 || ds->y[i] != std::floor(ds->y[i])) ds->integral = false;
+  }
+  TRY(upload_dict(ds.get()));
+  *out = ds.release();
+  return SBAG_OK;
+}
+
+int sbag_dataset_info(const sbag_dataset* ds, int64_t* N, int32_t* F) {
+  if (!ds) return fail(SBAG_EINVAL, "dataset is NULL");
+  if (N) *N = ds->N;
+  if (F) *F = ds->F;
+  return SBAG_OK;
+}
+
+int sbag_dataset_labels(const sbag_dataset* ds, double* y) {
+  if (!ds || !y) return fail(SBAG_EINVAL, "bad arguments");
+  std::copy(ds->y.begin(), ds->y.end(), y);
+  return SBAG_OK;
+}
+
+int sbag_dataset_features(const sbag_dataset* ds, int64_t r0, int64_t r1, double* X) {
+  if (!ds || !X || r0 < 0 || r1 > ds->N || r1 < r0) return fail(SBAG_EINVAL, "bad arguments");
+  sbag_ctx* c = ds->ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t n = r1 - r0;
+  std::vector<uint8_t> buf((size_t)n * ds->S * ds->code_bytes);
+  HIP_TRY(hipMemcpy(buf.data(), (const uint8_t*)ds->d_codes + (size_t)r0 * ds->S * ds->code_bytes,
+                    buf.size(), hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < n; i++)
+    for (int f = 0; f < ds->F; f++) {
+      const size_t k = ds->code_bytes == 1 ? buf[(size_t)i * ds->S + f]
+                                           : ((uint16_t*)buf.data())[(size_t)i * ds->S + f];
+      X[i * ds->F + f] = ds->dict[f][k];
+    }
+  return SBAG_OK;
+}
+
+int sbag_dataset_free(sbag_dataset* ds) {
+  if (!ds) return SBAG_OK;
+  (void)hipSetDevice(ds->ctx->device);
+  (void)hipStreamSynchronize(ds->ctx->stream);
+  if (ds->d_codes) (void)hipFree(ds->d_codes);
+  if (ds->d_labk) (void)hipFree(ds->d_labk);
+  if (ds->d_dict) (void)hipFree(ds->d_dict);
+  if (ds->d_dict_off) (void)hipFree(ds->d_dict_off);
+  delete ds;
+  return SBAG_OK;
+}
+
+// ---------------------------------------------------------------- fit
+struct HistGeom {
+  int T, FT, FPH, FPW, ntiles;
+  size_t lds;
+};
+
+static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g) {
+  g.T = std::max(16, std::min(128, 16384 / S));
+  const int align = gini_layout ? 32 : 16;
+  const size_t per_feat = gini_layout ? (size_t)NS * NB * 4 : (size_t)2 * NB * 8;
+  const size_t fixed = (size_t)g.T * S + (size_t)g.T * 25 + 1024;
+  auto lds_for = [&](int ft) {
+    const int fph = (ft + align - 1) / align * align;
+    return ((per_feat * fph + 15) & ~(size_t)15) + fixed + (size_t)ft * 2;
+  };
+  int cap_ft = std::min(256, (Fmax + align - 1) / align * align);
+  int ft = cap_ft;
+  const size_t soft = 80 * 1024, hard = 160 * 1024 - 256;
+  while (ft > align && lds_for(ft) > soft) ft -= align;
+  if (lds_for(ft) > soft) {  // even one aligned tile over budget: allow up to the whole LDS
+    if (lds_for(ft) > hard) return false;
+  }
+  g.FT = std::min(ft, Fmax);
+  ft = g.FT;
+  g.FPH = (g.FT + align - 1) / align * align;
+  g.FPW = 1;
+  while (g.FPW < g.FT) g.FPW <<= 1;
+  g.ntiles = (Fmax + g.FT - 1) / g.FT;
+  g.lds = lds_for(g.FT);
+  return true;
+}
+
+int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
+  if (!c || !ds || !fp || !out) return fail(SBAG_EINVAL, "bad arguments");
+  const sbag_tree_params& tp = fp->tree;
+  TRY(check_sampler(&fp->sampler));
+  if (tp.max_depth < 0 || tp.max_depth > 30)
+    return fail(SBAG_EINVAL, "maxDepth given invalid value (must be in [0, 30])");
+  if (tp.max_depth > 24) return fail(SBAG_EUNSUPPORTED, "maxDepth > 24");
+  if (tp.max_bins < 2 || tp.max_bins > 256)
+    return fail(SBAG_EINVAL, "maxBins given invalid value (must be in [2, 256])");
+  if (tp.min_instances_per_node < 1)
+    return fail(SBAG_EINVAL, "minInstancesPerNode given invalid value (must be >= 1)");
+  if (!(tp.min_info_gain >= 0.0)) return fail(SBAG_EINVAL, "minInfoGain given invalid value");
+  if (!fp->subspace_bug_compat && !(fp->subspace_ratio >= 0 && fp->subspace_ratio <= 1))
+    return fail(SBAG_EINVAL, "subspaceRatio given invalid value");
+  const bool gini = tp.impurity == SBAG_IMPURITY_GINI;
+  if (tp.impurity != SBAG_IMPURITY_GINI && tp.impurity != SBAG_IMPURITY_VARIANCE)
+    return fail(SBAG_EINVAL, "unknown impurity");
+  if (!ds->label_ok)
+    return fail(SBAG_EUNSUPPORTED,
+                "labels are not dyadic fixed-point values (|y * 2^s| < 2^23 for some s <= 40)");
+  if (gini && !ds->integral)
+    return fail(SBAG_EINVAL, "Classifier was given dataset with invalid label: labels must be "
+                             "integers in [0, 2^23)");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t N = ds->N;
+  const int F = ds->F;
+  const int lb = fp->sampler.learner_begin;
+  const int R = fp->sampler.learner_end - lb;
+  const int D = tp.max_depth;
+  std::vector<int64_t> poff;
+  TRY(check_partitions(fp->num_partitions, fp->partition_offsets, N, poff));
+
+  // ---- subspaces: mkSubspace(getSampleRatio, numFeatures, getSeed + iter) (H1)
+  const double sratio = fp->subspace_bug_compat ? fp->sampler.sample_ratio : fp->subspace_ratio;
+  std::vector<std::vector<int32_t>> sub(R);
+  int Fmax = 0;
+  for (int r = 0; r < R; r++) {
+    std::vector<int32_t> idx(F);
+    int n = 0;
+    TRY(sbag_subspace(sratio, F, (int64_t)((uint64_t)fp->sampler.seed + (uint64_t)(int64_t)(lb + r)),
+                      idx.data(), &n));
+    if (n == 0)
+      return fail(SBAG_EINVAL, "requirement failed: VectorSlicer requires that at least one "
+                               "feature be selected.");
+    idx.resize(n);
+    sub[r] = idx;
+    Fmax = std::max(Fmax, n);
+  }
+  // ---- fixed-point label packing limits
+  const int64_t K0 = -ds->kmin;
+  const int64_t kspan = ds->kmax - ds->kmin + 1;
+  const int64_t kabs = std::max(std::llabs(ds->kmin), std::llabs(ds->kmax));
+  int64_t ch_cap = 16384;
+  if (!gini) {
+    while (ch_cap > 16 && (double)ch_cap * 255.0 * (double)kspan >= std::ldexp(1.0, 40)) ch_cap /= 2;
+    if ((double)ch_cap * 255.0 * (double)kspan >= std::ldexp(1.0, 40))
+      return fail(SBAG_EUNSUPPORTED, "label range too wide for the packed LDS histogram");
+    if ((double)N * 255.0 * (double)kabs * (double)kabs >= std::ldexp(1.0, 53))
+      return fail(SBAG_EUNSUPPORTED, "sum of squared labels would exceed 2^53 (not exact in fp64)");
+  }
+  auto forest = std::make_unique<sbag_forest>();
+  forest->impurity = tp.impurity;
+  EventTimer tm{c->stream, {}};
+  hipEvent_t ev_start, ev_stop;
+  HIP_TRY(hipEventCreate(&ev_start));
+  HIP_TRY(hipEventCreate(&ev_stop));
+  HIP_TRY(hipEventRecord(ev_start, c->stream));
+
+  // ---- 1. bag: counts [R][N]
+  uint8_t* d_counts;
+  TRY(ws_typed(c, "counts", (size_t)R * N, &d_counts));
+  {
+    int h = tm.begin(T_SAMPLE);
+    TRY(run_sampler(c, &fp->sampler, poff, N, d_counts));
+    tm.end(h);
+  }
+  // ---- 2. in-bag entry lists (two ping-pong buffers, capacity N per replica)
+  const int64_t cap = N;
+  uint64_t *entA, *entB;
+  TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
+  TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
+  unsigned long long *d_inbag, *d_wsum;
+  TRY(ws_typed(c, "inbag", (size_t)R * 2, &d_inbag));
+  d_wsum = d_inbag + R;
+  HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 16, c->stream));
+  {
+    int h = tm.begin(T_COMPACT);
+    launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum);
+    HIP_TRY(hipGetLastError());
+    tm.end(h);
+  }
+  std::vector<unsigned long long> inbag(2 * R);
+  TRY(d2h(c, inbag.data(), d_inbag, (size_t)2 * R));
+  std::vector<int64_t> nw(R);
+  for (int r = 0; r < R; r++) {
+    nw[r] = (int64_t)inbag[R + r];
+    if (nw[r] == 0)
+      return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
+                               "empty one (learner " + std::to_string(lb + r) + ")");
+    if (gini && (double)nw[r] >= 4294967295.0)
+      return fail(SBAG_EUNSUPPORTED, "class counts exceed 32 bits");
+  }
+
+  // ---- per-replica tables
+  std::vector<int32_t> h_sub((size_t)R * Fmax, 0), h_Fr(R);
+  for (int r = 0; r < R; r++) {
+    h_Fr[r] = (int32_t)sub[r].size();
+    for (size_t k = 0; k < sub[r].size(); k++) h_sub[(size_t)r * Fmax + k] = sub[r][k];
+  }
+  int32_t *d_sub, *d_Fr;
+  TRY(ws_typed(c, "sub", h_sub.size(), &d_sub));
+  TRY(ws_typed(c, "Fr", (size_t)R, &d_Fr));
+  TRY(h2d(c, d_sub, h_sub.data(), h_sub.size()));
+  TRY(h2d(c, d_Fr, h_Fr.data(), (size_t)R));
+  std::vector<int64_t> vcoff((size_t)R * Fmax + 1, 0);
+  {
+    int64_t o = 0;
+    for (int r = 0; r < R; r++)
+      for (int fl = 0; fl < Fmax; fl++) {
+        vcoff[(size_t)r * Fmax + fl] = o;
+        if (fl < h_Fr[r]) o += (int64_t)ds->dict[sub[r][fl]].size();
+      }
+    vcoff[(size_t)R * Fmax] = o;
+  }
+  const int64_t vc_total = vcoff[(size_t)R * Fmax];
+
+  // root "parents": one per replica, no routing, histogram slot = replica
+  std::vector<ParentInfo> h_par(R);
+  std::vector<HistChunk> h_chunks;
+  std::vector<std::pair<int64_t, int64_t>> seg(R);  // current-level segments per slot
+  for (int r = 0; r < R; r++) {
+    h_par[r] = ParentInfo{r, -1, 0, 0, 0, r, 0, 0};
+    seg[r] = {(int64_t)r * cap, (int64_t)r * cap + (int64_t)inbag[r]};
+  }
+  auto make_chunks = [&](const std::vector<std::pair<int64_t, int64_t>>& segs,
+                         const std::vector<int>& which, int T, std::vector<HistChunk>& chunks) {
+    int64_t tot = 0;
+    for (int i : which) tot += segs[i].second - segs[i].first;
+    int64_t ch = std::max<int64_t>(T, std::min<int64_t>(ch_cap, (tot / 4096 + T - 1) / T * T));
+    chunks.clear();
+    for (int i : which)
+      for (int64_t a = segs[i].first; a < segs[i].second; a += ch)
+        chunks.push_back(HistChunk{i, 0, a, std::min(a + ch, segs[i].second)});
+  };
+  ParentInfo* d_par;
+  HistChunk* d_chunks;
+
+  // ---- 3. value counts per (replica, local feature, code)
+  std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1), 0);
+  {
+    int h = tm.begin(T_VC);
+    int ncmax = 0;
+    for (int f = 0; f < F; f++) ncmax = std::max(ncmax, (int)ds->dict[f].size());
+    HistGeom g;
+    if (ds->code_bytes == 1 && hist_geometry(ds->S, Fmax, ncmax, 1, true, g)) {
+      // LDS-privatized counting pass (k_hist, count-only layout), codes as bins
+      std::vector<int16_t> h_pos((size_t)R * Fmax, 0);
+      for (int r = 0; r < R; r++)
+        for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)sub[r][fl];
+      int16_t* d_pos;
+      TRY(ws_typed(c, "pos", h_pos.size(), &d_pos));
+      TRY(h2d(c, d_pos, h_pos.data(), h_pos.size()));
+      std::vector<int> all(R);
+      for (int r = 0; r < R; r++) all[r] = r;
+      make_chunks(seg, all, g.T, h_chunks);
+      TRY(ws_typed(c, "par", (size_t)R, &d_par));
+      TRY(h2d(c, d_par, h_par.data(), (size_t)R));
+      TRY(ws_typed(c, "chunks", h_chunks.size(), &d_chunks));
+      TRY(h2d(c, d_chunks, h_chunks.data(), h_chunks.size()));
+      const int64_t slot_words = (int64_t)Fmax * ncmax;
+      uint32_t* d_vch;
+      TRY(ws_typed(c, "vch", (size_t)R * slot_words, &d_vch));
+      HIP_TRY(hipMemsetAsync(d_vch, 0, (size_t)R * slot_words * 4, c->stream));
+      HistArgs a{};
+      a.bins = (const uint8_t*)ds->d_codes;
+      a.bins_rstride = 0;
+      a.S = ds->S;
+      a.Fmax = Fmax;
+      a.pos = d_pos;
+      a.Fr = d_Fr;
+      a.chunks = d_chunks;
+      a.parents = d_par;
+      a.ent_in = entA;
+      a.ent_out = nullptr;
+      a.cursors = nullptr;
+      a.hist = d_vch;
+      a.NB = ncmax;
+      a.NS = 1;
+      a.K0 = 0;
+      a.FT = g.FT;
+      a.FPH = g.FPH;
+      a.FPW = g.FPW;
+      a.T = g.T;
+      a.do_write = 0;
+      a.count_only = 1;
+      launch_hist(c->stream, a, (int)h_chunks.size(), g.ntiles, true, g.lds);
+      HIP_TRY(hipGetLastError());
+      std::vector<uint32_t> tmp((size_t)R * slot_words);
+      TRY(d2h(c, tmp.data(), d_vch, tmp.size()));
+      for (int r = 0; r < R; r++)
+        for (int fl = 0; fl < h_Fr[r]; fl++) {
+          const size_t nc = ds->dict[sub[r][fl]].size();
+          std::copy(tmp.begin() + ((size_t)r * Fmax + fl) * ncmax,
+                    tmp.begin() + ((size_t)r * Fmax + fl) * ncmax + nc,
+                    vc.begin() + vcoff[(size_t)r * Fmax + fl]);
+        }
+    } else {
+      uint32_t* d_vc;
+      int64_t* d_vcoff;
+      TRY(ws_typed(c, "vc", (size_t)std::max<int64_t>(vc_total, 1), &d_vc));
+      TRY(ws_typed(c, "vcoff", vcoff.size(), &d_vcoff));
+      TRY(h2d(c, d_vcoff, vcoff.data(), vcoff.size()));
+      HIP_TRY(hipMemsetAsync(d_vc, 0, (size_t)std::max<int64_t>(vc_total, 1) * 4, c->stream));
+      launch_vc_global(c->stream, ds->d_codes, ds->code_bytes, ds->S, entA, cap, d_inbag, d_sub,
+                       d_Fr, Fmax, R, d_vcoff, d_vc);
+      HIP_TRY(hipGetLastError());
+      TRY(d2h(c, vc.data(), d_vc, (size_t)vc_total));
+    }
+    tm.end(h);
+  }
+
+  // ---- 4. thresholds, LUTs (code -> bin), numSplits per (replica, feature)
+  std::vector<std::vector<double>> thr((size_t)R * Fmax);
+  std::vector<int32_t> h_nbins((size_t)R * Fmax, 1);
+  std::vector<uint8_t> lut((size_t)std::max<int64_t>(vc_total, 1), 0);
+  std::vector<int32_t> exact(R, 1);
+  bool identity = ds->code_bytes == 1;
+  int NB = 1;
+  for (int r = 0; r < R; r++) {
+    const int64_t required = std::max<int64_t>((int64_t)tp.max_bins * tp.max_bins, 10000);
+    if (required < nw[r]) exact[r] = 0;  // reference samples for split finding
+    for (int fl = 0; fl < h_Fr[r]; fl++) {
+      const int g = sub[r][fl];
+      const size_t o = (size_t)vcoff[(size_t)r * Fmax + fl];
+      std::vector<double>& t = thr[(size_t)r * Fmax + fl];
+      const int nt = find_splits(ds->dict[g], vc.data() + o, ds->zero_code[g], nw[r], tp.max_bins, t);
+      h_nbins[(size_t)r * Fmax + fl] = nt + 1;
+      NB = std::max(NB, nt + 1);
+      const auto& d = ds->dict[g];
+      for (size_t k = 0; k < d.size(); k++) {
+        const int b = (int)(std::lower_bound(t.begin(), t.end(), d[k]) - t.begin());  // #{t < v}
+        lut[o + k] = (uint8_t)b;
+        if (b != (int)k) identity = false;
+      }
+      if ((int)d.size() > nt + 1) identity = false;
+    }
+  }
+  // per global feature: is the LUT the same for every replica that uses it?
+  bool shared = true;
+  {
+    std::vector<int64_t> first_off(F, -1);
+    for (int r = 0; r < R && shared; r++)
+      for (int fl = 0; fl < h_Fr[r] && shared; fl++) {
+        const int g = sub[r][fl];
+        const int64_t o = vcoff[(size_t)r * Fmax + fl];
+        if (first_off[g] < 0) {
+          first_off[g] = o;
+        } else if (!std::equal(lut.begin() + o, lut.begin() + o + (int64_t)ds->dict[g].size(),
+                               lut.begin() + first_off[g])) {
+          shared = false;
+        }
+      }
+  }
+  // ---- 5. bins
+  const uint8_t* d_bins;
+  int64_t bins_rstride = 0;
+  int32_t S;
+  std::vector<int16_t> h_pos((size_t)R * Fmax, 0);
+  {
+    int h = tm.begin(T_BIN);
+    uint8_t* d_lut;
+    int64_t* d_lutoff;
+    if (identity) {
+      d_bins = (const uint8_t*)ds->d_codes;
+      S = ds->S;
+      for (int r = 0; r < R; r++)
+        for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)sub[r][fl];
+    } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30)) {
+      // one bins matrix in global feature coordinates
+      S = row_stride(F);
+      std::vector<int64_t> goff(F, 0);
+      std::vector<int32_t> gsub(F), gF(1, F);
+      for (int g = 0; g < F; g++) gsub[g] = g;
+      std::vector<int64_t> gl(F + 1, 0);
+      for (int g = 0; g < F; g++) gl[g + 1] = gl[g] + (int64_t)ds->dict[g].size();
+      std::vector<uint8_t> glut((size_t)std::max<int64_t>(gl[F], 1), 0);
+      for (int r = 0; r < R; r++)
+        for (int fl = 0; fl < h_Fr[r]; fl++) {
+          const int g = sub[r][fl];
+          std::copy(lut.begin() + vcoff[(size_t)r * Fmax + fl],
+                    lut.begin() + vcoff[(size_t)r * Fmax + fl] + (int64_t)ds->dict[g].size(),
+                    glut.begin() + gl[g]);
+        }
+      int32_t *d_gsub, *d_gF;
+      TRY(ws_typed(c, "gsub", (size_t)F, &d_gsub));
+      TRY(ws_typed(c, "gF", 1, &d_gF));
+      TRY(ws_typed(c, "lut", glut.size(), &d_lut));
+      TRY(ws_typed(c, "lutoff", (size_t)F + 1, &d_lutoff));
+      TRY(h2d(c, d_gsub, gsub.data(), (size_t)F));
+      TRY(h2d(c, d_gF, gF.data(), 1));
+      TRY(h2d(c, d_lut, glut.data(), glut.size()));
+      TRY(h2d(c, d_lutoff, gl.data(), (size_t)F + 1));
+      uint8_t* d_b;
+      TRY(ws_typed(c, "bins", (size_t)N * S, &d_b));
+      launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_lut,
+                         d_lutoff, d_b, S);
+      HIP_TRY(hipGetLastError());
+      d_bins = d_b;
+      for (int r = 0; r < R; r++)
+        for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)sub[r][fl];
+    } else {
+      S = row_stride(Fmax);
+      if ((double)R * N * S > 48.0 * (1ull << 30))
+        return fail(SBAG_EUNSUPPORTED, "per-replica binning of this size is not implemented "
+                                       "(thresholds differ across replicas)");
+      TRY(ws_typed(c, "lut", lut.size(), &d_lut));
+      TRY(ws_typed(c, "lutoff", vcoff.size(), &d_lutoff));
+      TRY(h2d(c, d_lut, lut.data(), lut.size()));
+      TRY(h2d(c, d_lutoff, vcoff.data(), vcoff.size()));
+      uint8_t* d_b;
+      TRY(ws_typed(c, "bins", (size_t)R * N * S, &d_b));
+      launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
+                         d_lut, d_lutoff, d_b, S);
+      HIP_TRY(hipGetLastError());
+      d_bins = d_b;
+      bins_rstride = (int64_t)N * S;
+      for (int r = 0; r < R; r++)
+        for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)fl;
+    }
+    tm.end(h);
+  }
+  int16_t* d_pos;
+  int32_t* d_nbins;
+  TRY(ws_typed(c, "pos", h_pos.size(), &d_pos));
+  TRY(ws_typed(c, "nbins", h_nbins.size(), &d_nbins));
+  TRY(h2d(c, d_pos, h_pos.data(), h_pos.size()));
+  TRY(h2d(c, d_nbins, h_nbins.data(), h_nbins.size()));
+
+  // ---- 6. level-wise growth
+  int NS = 3;
+  if (gini) NS = (int)ds->kmax + 1;
+  HistGeom g;
+  if (!hist_geometry(S, Fmax, NB, NS, gini, g))
+    return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
+  const int64_t slot_words = (int64_t)Fmax * NB * NS;
+  const size_t word_bytes = gini ? 4 : 8;
+  std::vector<std::vector<HNode>> trees(R);
+  std::vector<std::pair<int, int>> slots(R);  // (replica, node index)
+  for (int r = 0; r < R; r++) {
+    trees[r].push_back(HNode{});
+    slots[r] = {r, 0};
+  }
+  // level 0 histograms: virtual parents (h_par, seg) already set
+  void* hist_cur;
+  {
+    std::string nm = "histA";
+    TRY(ws_get(c, nm, (size_t)R * slot_words * word_bytes, &hist_cur));
+  }
+  HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * slot_words * word_bytes, c->stream));
+  std::vector<int> all(R);
+  for (int r = 0; r < R; r++) all[r] = r;
+  make_chunks(seg, all, g.T, h_chunks);
+  TRY(ws_typed(c, "par", (size_t)R, &d_par));
+  TRY(h2d(c, d_par, h_par.data(), (size_t)R));
+  TRY(ws_typed(c, "chunks", h_chunks.size(), &d_chunks));
+  TRY(h2d(c, d_chunks, h_chunks.data(), h_chunks.size()));
+  HistArgs ha{};
+  ha.bins = d_bins;
+  ha.bins_rstride = bins_rstride;
+  ha.S = S;
+  ha.Fmax = Fmax;
+  ha.pos = d_pos;
+  ha.Fr = d_Fr;
+  ha.NB = NB;
+  ha.NS = NS;
+  ha.K0 = (int32_t)K0;
+  ha.FT = g.FT;
+  ha.FPH = g.FPH;
+  ha.FPW = g.FPW;
+  ha.T = g.T;
+  ha.count_only = 0;
+  double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0;
+  int64_t hist_launches = 0;
+  {
+    ha.chunks = d_chunks;
+    ha.parents = d_par;
+    ha.ent_in = entA;
+    ha.ent_out = nullptr;
+    ha.cursors = nullptr;
+    ha.hist = hist_cur;
+    ha.do_write = 0;
+    int h = tm.begin(T_HIST);
+    launch_hist(c->stream, ha, (int)h_chunks.size(), g.ntiles, gini, g.lds);
+    HIP_TRY(hipGetLastError());
+    tm.end(h);
+    hist_launches++;
+    for (int r = 0; r < R; r++) {
+      hist_entries += (double)inbag[r];
+      hist_alg_bytes += (double)inbag[r] * (h_Fr[r] + 4);
+    }
+  }
+  for (int r = 0; r < R; r++) hist_upper += (double)inbag[r] * (h_Fr[r] + 4) * D + 3.0 * N * D;
+  const double inv_scale = std::ldexp(1.0, -ds->shift), inv_scale2 = std::ldexp(1.0, -2 * ds->shift);
+  uint64_t* ent_cur = entA;
+  uint64_t* ent_nxt = entB;
+  std::string hist_nxt_name = "histB", hist_cur_name = "histA";
+  int levels = 0;
+  for (int level = 0; level <= D; level++) {
+    const int M = (int)slots.size();
+    if (M == 0) break;
+    levels++;
+    // --- split search on the device
+    std::vector<int32_t> h_slot_r(M);
+    for (int i = 0; i < M; i++) h_slot_r[i] = slots[i].first;
+    int32_t* d_slot_r;
+    SplitOut* d_sout;
+    int64_t* d_sstats;
+    TRY(ws_typed(c, "slot_r", (size_t)M, &d_slot_r));
+    TRY(ws_typed(c, "sout", (size_t)M, &d_sout));
+    TRY(ws_typed(c, "sstats", (size_t)M * 3 * NS, &d_sstats));
+    TRY(h2d(c, d_slot_r, h_slot_r.data(), (size_t)M));
+    SplitArgs sa{};
+    sa.hist = hist_cur;
+    sa.Fmax = Fmax;
+    sa.NB = NB;
+    sa.NS = NS;
+    sa.slot_r = d_slot_r;
+    sa.Fr = d_Fr;
+    sa.nbins = d_nbins;
+    sa.min_inst = tp.min_instances_per_node;
+    sa.min_gain = tp.min_info_gain;
+    sa.inv_scale = inv_scale;
+    sa.inv_scale2 = inv_scale2;
+    sa.out = d_sout;
+    sa.stats = d_sstats;
+    {
+      int h = tm.begin(T_SPLIT);
+      launch_split(c->stream, sa, M, gini);
+      HIP_TRY(hipGetLastError());
+      tm.end(h);
+    }
+    std::vector<SplitOut> sout(M);
+    std::vector<int64_t> sst((size_t)M * 3 * NS);
+    TRY(d2h(c, sout.data(), d_sout, (size_t)M));
+    TRY(d2h(c, sst.data(), d_sstats, sst.size()));
+    // --- node updates (RandomForest.findBestSplits, host part)
+    std::vector<ParentInfo> par;
+    std::vector<std::pair<int64_t, int64_t>> pseg;
+    std::vector<std::pair<int, int>> next_slots;
+    std::vector<int32_t> triples;
+    struct Pending {
+      int r, node, side, parent;
+    };
+    std::vector<Pending> pend;  // next-level slot -> (replica, child node, side, parent index)
+    for (int i = 0; i < M; i++) {
+      const int r = slots[i].first;
+      const int ni = slots[i].second;
+      const int64_t* tot = &sst[(size_t)i * 3 * NS];
+      const int64_t* lef = tot + NS;
+      const int64_t* rig = tot + 2 * NS;
+      {
+        HNode& n = trees[r][ni];
+        if (level == 0) {
+          n.stats.assign(tot, tot + NS);
+          n.impurity = Calc{n.stats.data(), NS, gini, ds->shift}.impurity();
+        }
+        const SplitOut& so = sout[i];
+        if (so.fl < 0) {  // no feature has splits: invalid stats on the parent aggregate
+          n.gain = kDoubleMinValue;
+          n.valid = false;
+        } else {
+          n.gain = so.gain;
+          n.valid = so.valid != 0;
+        }
+        n.is_leaf = (n.gain <= 0) || (level == D);
+        if (n.is_leaf) continue;
+        n.has_split = true;
+        n.fl = so.fl;
+        n.s = so.s;
+        n.thr = thr[(size_t)r * Fmax + so.fl][so.s];
+      }
+      const bool child_leaf = (level + 1) == D;
+      HNode L, Rn;
+      L.stats.assign(lef, lef + NS);
+      Rn.stats.assign(rig, rig + NS);
+      L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
+      Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
+      L.is_leaf = child_leaf || L.impurity == 0.0;
+      Rn.is_leaf = child_leaf || Rn.impurity == 0.0;
+      const int li = (int)trees[r].size();
+      trees[r].push_back(L);
+      trees[r].push_back(Rn);
+      trees[r][ni].left = li;
+      trees[r][ni].right = li + 1;
+      const bool wl = !trees[r][li].is_leaf, wr = !trees[r][li + 1].is_leaf;
+      if (!wl && !wr) continue;
+      ParentInfo p{};
+      p.r = r;
+      p.pos = h_pos[(size_t)r * Fmax + trees[r][ni].fl];
+      p.s = trees[r][ni].s;
+      p.write_l = wl;
+      p.write_r = wr;
+      const int pidx = (int)par.size();
+      int sl = -1, sr = -1;
+      if (wl) {
+        sl = (int)next_slots.size();
+        next_slots.push_back({r, li});
+        pend.push_back({r, li, 0, pidx});
+      }
+      if (wr) {
+        sr = (int)next_slots.size();
+        next_slots.push_back({r, li + 1});
+        pend.push_back({r, li + 1, 1, pidx});
+      }
+      if (wl && wr) {
+        const int64_t lc = Calc{lef, NS, gini, ds->shift}.count();
+        const int64_t rc = Calc{rig, NS, gini, ds->shift}.count();
+        const bool small_left = lc <= rc;
+        p.hist_slot = small_left ? sl : sr;
+        p.hist_side = small_left ? 0 : 1;
+        triples.push_back(small_left ? sr : sl);  // dst (larger child)
+        triples.push_back(i);                     // parent slot (current level)
+        triples.push_back(small_left ? sl : sr);  // small child
+      } else {
+        p.hist_slot = wl ? sl : sr;
+        p.hist_side = wl ? 0 : 1;
+      }
+      par.push_back(p);
+      pseg.push_back(seg[i]);
+    }
+    if (next_slots.empty()) break;
+    // --- route rows + histograms of level+1
+    const int Mn = (int)next_slots.size();
+    void* hist_nxt;
+    TRY(ws_get(c, hist_nxt_name, (size_t)Mn * slot_words * word_bytes, &hist_nxt));
+    HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * slot_words * word_bytes, c->stream));
+    const int NP = (int)par.size();
+    std::vector<unsigned long long> cur((size_t)2 * NP);
+    for (int q = 0; q < NP; q++) {
+      cur[2 * q] = (unsigned long long)pseg[q].first;
+      cur[2 * q + 1] = (unsigned long long)pseg[q].second;
+    }
+    unsigned long long* d_cur;
+    TRY(ws_typed(c, "cursors", cur.size(), &d_cur));
+    TRY(h2d(c, d_cur, cur.data(), cur.size()));
+    std::vector<int> allp(NP);
+    for (int q = 0; q < NP; q++) allp[q] = q;
+    make_chunks(pseg, allp, g.T, h_chunks);
+    TRY(ws_typed(c, "par", (size_t)NP, &d_par));
+    TRY(h2d(c, d_par, par.data(), (size_t)NP));
+    TRY(ws_typed(c, "chunks", h_chunks.size(), &d_chunks));
+    TRY(h2d(c, d_chunks, h_chunks.data(), h_chunks.size()));
+    ha.chunks = d_chunks;
+    ha.parents = d_par;
+    ha.ent_in = ent_cur;
+    ha.ent_out = ent_nxt;
+    ha.cursors = d_cur;
+    ha.hist = hist_nxt;
+    ha.do_write = 1;
+    {
+      int h = tm.begin(T_HIST);
+      launch_hist(c->stream, ha, (int)h_chunks.size(), g.ntiles, gini, g.lds);
+      HIP_TRY(hipGetLastError());
+      tm.end(h);
+      hist_launches++;
+      for (int q = 0; q < NP; q++) {
+        const double ne = (double)(pseg[q].second - pseg[q].first);
+        hist_entries += ne;
+        hist_alg_bytes += ne * (h_Fr[par[q].r] + 4);
+      }
+    }
+    if (!triples.empty()) {
+      int32_t* d_tri;
+      TRY(ws_typed(c, "triples", triples.size(), &d_tri));
+      TRY(h2d(c, d_tri, triples.data(), triples.size()));
+      int h = tm.begin(T_SUB);
+      launch_subtract(c->stream, hist_nxt, hist_cur, d_tri, (int)triples.size() / 3, slot_words, gini);
+      HIP_TRY(hipGetLastError());
+      tm.end(h);
+    }
+    TRY(d2h(c, cur.data(), d_cur, cur.size()));
+    std::vector<std::pair<int64_t, int64_t>> nseg(Mn);
+    for (int k = 0; k < Mn; k++) {
+      const Pending& pd = pend[k];
+      if (pd.side == 0)
+        nseg[k] = {pseg[pd.parent].first, (int64_t)cur[2 * pd.parent]};
+      else
+        nseg[k] = {(int64_t)cur[2 * pd.parent + 1], pseg[pd.parent].second};
+    }
+    seg = nseg;
+    slots = next_slots;
+    std::swap(hist_cur_name, hist_nxt_name);
+    hist_cur = hist_nxt;
+    std::swap(ent_cur, ent_nxt);
+  }
+  HIP_TRY(hipEventRecord(ev_stop, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+
+  // ---- 7. models (toNode(prune = true)) + subspaces
+  forest->trees.resize(R);
+  int nclasses = 0;
+  for (int r = 0; r < R; r++) {
+    HTree& t = forest->trees[r];
+    t.sub = sub[r];
+    t.exact = exact[r];
+    int ns_out = 3;
+    if (gini) {  // Classifier.getNumClasses on the subbag: max label + 1
+      ns_out = 0;
+      for (int k = 0; k < NS; k++)
+        if (trees[r][0].stats[k] > 0) ns_out = k + 1;
+      nclasses = std::max(nclasses, ns_out);
+    }
+    t.ns = ns_out;
+    emit(trees[r], 0, t, NS, gini, ds->shift, ns_out);
+  }
+  forest->nclasses = gini ? std::max(nclasses, (int)ds->kmax + 1) : 0;
+  double cats[T_NCAT] = {0};
+  tm.collect(cats, nullptr, -1);
+  float total_ms = 0;
+  (void)hipEventElapsedTime(&total_ms, ev_start, ev_stop);
+  (void)hipEventDestroy(ev_start);
+  (void)hipEventDestroy(ev_stop);
+  sbag_timing& T = forest->timing;
+  T.total_ms = total_ms;
+  T.sample_ms = cats[T_SAMPLE];
+  T.valuecount_ms = cats[T_VC];
+  T.bin_ms = cats[T_BIN];
+  T.compact_ms = cats[T_COMPACT];
+  T.hist_ms = cats[T_HIST];
+  T.split_ms = cats[T_SPLIT];
+  T.subtract_ms = cats[T_SUB];
+  T.hist_launches = hist_launches;
+  T.hist_alg_bytes = hist_alg_bytes;
+  T.hist_entries = hist_entries;
+  T.hist_upper_bytes = hist_upper;
+  T.levels = levels;
+  *out = forest.release();
+  return SBAG_OK;
+}
+
+// ---------------------------------------------------------------- forest accessors
+int sbag_forest_num_trees(const sbag_forest* f, int32_t* n) {
+  if (!f || !n) return fail(SBAG_EINVAL, "bad arguments");
+  *n = (int32_t)f->trees.size();
+  return SBAG_OK;
+}
+int sbag_forest_tree_info(const sbag_forest* f, int32_t t, int32_t* nn, int32_t* ns, int32_t* sl,
+                          int32_t* ex) {
+  if (!f || t < 0 || t >= (int)f->trees.size()) return fail(SBAG_EINVAL, "tree index out of range");
+  const HTree& h = f->trees[t];
+  if (nn) *nn = (int32_t)h.nodes.size();
+  if (ns) *ns = h.ns;
+  if (sl) *sl = (int32_t)h.sub.size();
+  if (ex) *ex = h.exact;
+  return SBAG_OK;
+}
+int sbag_forest_subspace(const sbag_forest* f, int32_t t, int32_t* idx) {
+  if (!f || !idx || t < 0 || t >= (int)f->trees.size()) return fail(SBAG_EINVAL, "bad arguments");
+  std::copy(f->trees[t].sub.begin(), f->trees[t].sub.end(), idx);
+  return SBAG_OK;
+}
+int sbag_forest_nodes(const sbag_forest* f, int32_t t, sbag_node* nodes, double* stats) {
+  if (!f || !nodes || t < 0 || t >= (int)f->trees.size()) return fail(SBAG_EINVAL, "bad arguments");
+  const HTree& h = f->trees[t];
+  std::copy(h.nodes.begin(), h.nodes.end(), nodes);
+  if (stats) std::copy(h.stats.begin(), h.stats.end(), stats);
+  return SBAG_OK;
+}
+int sbag_forest_timing(const sbag_forest* f, sbag_timing* out) {
+  if (!f || !out) return fail(SBAG_EINVAL, "bad arguments");
+  *out = f->timing;
+  return SBAG_OK;
+}
+int sbag_forest_create(int32_t T, const int32_t* num_nodes, const sbag_node* nodes,
+                       const int32_t* sub_len, const int32_t* subs, int32_t impurity,
+                       sbag_forest** out) {
+  if (T <= 0 || !num_nodes || !nodes || !sub_len || !subs || !out)
+    return fail(SBAG_EINVAL, "bad arguments");
+  auto f = std::make_unique<sbag_forest>();
+  f->impurity = impurity;
+  f->trees.resize(T);
+  int64_t no = 0, so = 0;
+  int nclasses = 0;
+  for (int t = 0; t < T; t++) {
+    HTree& h = f->trees[t];
+    h.nodes.assign(nodes + no, nodes + no + num_nodes[t]);
+    h.sub.assign(subs + so, subs + so + sub_len[t]);
+    for (int i = 0; i < num_nodes[t]; i++) {
+      const sbag_node& n = h.nodes[i];
+      if (n.left >= num_nodes[t] || n.right >= num_nodes[t] || (n.left >= 0 && (n.feature < 0 || n.feature >= sub_len[t])))
+        return fail(SBAG_EINVAL, "malformed tree " + std::to_string(t));
+      if (n.left < 0 && impurity == SBAG_IMPURITY_GINI)
+        nclasses = std::max(nclasses, (int)n.prediction + 1);
+    }
+    no += num_nodes[t];
+    so += sub_len[t];
+  }
+  f->nclasses = nclasses;
+  *out = f.release();
+  return SBAG_OK;
+}
+int sbag_forest_free(sbag_forest* f) {
+  delete f;
+  return SBAG_OK;
+}
+
+// ---------------------------------------------------------------- predict
+static int upload_forest(sbag_ctx* c, const sbag_forest* fc) {
+  sbag_forest* f = const_cast<sbag_forest*>(fc);
+  if (f->d_nodes && f->dev_id == c->device) return SBAG_OK;
+  if (f->d_nodes) (void)hipFree(f->d_nodes);
+  if (f->d_off) (void)hipFree(f->d_off);
+  f->d_nodes = nullptr;
+  f->d_off = nullptr;
+  std::vector<DevNode> dn;
+  std::vector<int64_t> off;
+  for (const HTree& t : f->trees) {
+    off.push_back((int64_t)dn.size());
+    for (const sbag_node& n : t.nodes) {
+      DevNode d{};
+      d.left = n.left;
+      d.right = n.right;
+      d.value = n.left >= 0 ? n.threshold : n.prediction;
+      d.gfeat = n.left >= 0 ? t.sub[n.feature] : 0;
+      dn.push_back(d);
+    }
+  }
+  HIP_TRY(hipMalloc(&f->d_nodes, std::max<size_t>(dn.size(), 1) * sizeof(DevNode)));
+  HIP_TRY(hipMalloc(&f->d_off, std::max<size_t>(off.size(), 1) * 8));
+  HIP_TRY(hipMemcpy(f->d_nodes, dn.data(), dn.size() * sizeof(DevNode), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(f->d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+  f->dev_id = c->device;
+  return SBAG_OK;
+}
+
+static int check_agg(const sbag_forest* f, int agg) {
+  if (agg != SBAG_AGG_MEAN && agg != SBAG_AGG_MODE) return fail(SBAG_EINVAL, "unknown aggregation");
+  if (agg == SBAG_AGG_MODE && (f->nclasses <= 0 || f->nclasses > 4096))
+    return fail(SBAG_EINVAL, "mode aggregation needs class-valued trees");
+  return SBAG_OK;
+}
+
+int sbag_predict(sbag_ctx* c, const sbag_forest* f, const double* X, int64_t N, int32_t F, int32_t agg,
+                 double* out, double* per_tree) {
+  if (!c || !f || !X || !out || N < 0 || F <= 0) return fail(SBAG_EINVAL, "bad arguments");
+  TRY(check_agg(f, agg));
+  for (const HTree& t : f->trees)
+    for (int32_t g : t.sub)
+      if (g >= F) return fail(SBAG_EINVAL, "feature vector shorter than a subspace index");
+  if (N == 0) return SBAG_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  TRY(upload_forest(c, f));
+  const int L = (int)f->trees.size();
+  double *d_X, *d_out, *d_pt = nullptr;
+  TRY(ws_typed(c, "pX", (size_t)N * F, &d_X));
+  TRY(ws_typed(c, "pout", (size_t)N, &d_out));
+  if (per_tree) TRY(ws_typed(c, "ppt", (size_t)N * L, &d_pt));
+  TRY(h2d(c, d_X, X, (size_t)N * F));
+  launch_predict(c->stream, d_X, nullptr, 1, nullptr, nullptr, N, F, F, f->d_nodes, f->d_off, L, agg,
+                 std::max(f->nclasses, 1), d_out, d_pt);
+  HIP_TRY(hipGetLastError());
+  TRY(d2h(c, out, d_out, (size_t)N));
+  if (per_tree) TRY(d2h(c, per_tree, d_pt, (size_t)N * L));
+  return SBAG_OK;
+}
+
+int sbag_predict_dataset(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* ds, int32_t agg,
+                         double* out) {
+  if (!c || !f || !ds || !out) return fail(SBAG_EINVAL, "bad arguments");
+  TRY(check_agg(f, agg));
+  for (const HTree& t : f->trees)
+    for (int32_t g : t.sub)
+      if (g >= ds->F) return fail(SBAG_EINVAL, "dataset has fewer features than the model");
+  HIP_TRY(hipSetDevice(c->device));
+  TRY(upload_forest(c, f));
+  double* d_out;
+  TRY(ws_typed(c, "pout", (size_t)ds->N, &d_out));
+  launch_predict(c->stream, nullptr, ds->d_codes, ds->code_bytes, ds->d_dict, ds->d_dict_off, ds->N,
+                 ds->F, ds->S, f->d_nodes, f->d_off, (int)f->trees.size(), agg,
+                 std::max(f->nclasses, 1), d_out, nullptr);
+  HIP_TRY(hipGetLastError());
+  TRY(d2h(c, out, d_out, (size_t)ds->N));
+  return SBAG_OK;
+}
+
+int sbag_aggregate(sbag_ctx* c, const double* votes, int32_t L, int64_t N, int32_t agg, double* out) {
+  if (!c || !votes || !out || L <= 0 || N < 0) return fail(SBAG_EINVAL, "bad arguments");
+  if (agg != SBAG_AGG_MEAN && agg != SBAG_AGG_MODE) return fail(SBAG_EINVAL, "unknown aggregation");
+  if (N == 0) return SBAG_OK;
+  int ncls = 1;
+  if (agg == SBAG_AGG_MODE) {
+    for (int64_t i = 0; i < (int64_t)L * N; i++) {
+      const double v = votes[i];
+      if (!(v >= 0 && v == std::floor(v) && v < 4096)) return fail(SBAG_EINVAL, "votes must be class ids");
+      ncls = std::max(ncls, (int)v + 1);
+    }
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  double *d_v, *d_out;
+  TRY(ws_typed(c, "agv", (size_t)L * N, &d_v));
+  TRY(ws_typed(c, "agout", (size_t)N, &d_out));
+  TRY(h2d(c, d_v, votes, (size_t)L * N));
+  launch_aggregate(c->stream, d_v, L, N, agg, ncls, d_out);
+  HIP_TRY(hipGetLastError());
+  TRY(d2h(c, out, d_out, (size_t)N));
+  return SBAG_OK;
+}
+
+}  // extern "C"

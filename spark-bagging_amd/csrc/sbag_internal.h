@@ -1,0 +1,115 @@
+// sbag_internal.h — device-side structs and kernel launchers shared by
+// sbag_kernels.hip (gfx950 kernels) and sbag_host.cpp (C-ABI orchestration).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sbag {
+
+// Entry of a replica's row list (one per in-bag row): low 32 bits row index,
+// high 32 bits (label_fixed << 8) | count.  Replaces the reference's
+// explode(array_repeat) replication (sql/bfunctions.scala:42-44) by a weight.
+__host__ __device__ inline uint64_t pack_entry(uint32_t row, int32_t k, uint32_t c) {
+  return (uint64_t)row | ((uint64_t)(uint32_t)(((uint32_t)k << 8) | (c & 0xffu)) << 32);
+}
+
+struct HistChunk {  // one workgroup: entries [a, b) of one parent segment
+  int32_t parent;
+  int32_t pad;
+  int64_t a, b;
+};
+
+struct ParentInfo {  // a node of level d whose rows are routed to level d+1
+  int32_t r;          // replica (local index)
+  int32_t pos;        // byte position of the split feature in a bins row; -1: no routing
+  int32_t s;          // split bin: left iff bin <= s (ContinuousSplit.shouldGoLeft)
+  int32_t write_l;    // left child is not a leaf -> its entries are written
+  int32_t write_r;
+  int32_t hist_slot;  // histogram slot accumulated by this pass, -1 none
+  int32_t hist_side;  // 0 = left child, 1 = right child
+  int32_t pad;
+};
+
+struct HistArgs {
+  const uint8_t* bins;   // [R?][N][S] bins (or value codes in count mode)
+  int64_t bins_rstride;  // bytes between replica matrices (0: shared)
+  int32_t S;             // row stride in bytes (multiple of 16)
+  int32_t Fmax;
+  const int16_t* pos;    // [R][Fmax] byte position of local feature fl in a row
+  const int32_t* Fr;     // [R]
+  const HistChunk* chunks;
+  const ParentInfo* parents;
+  const uint64_t* ent_in;
+  uint64_t* ent_out;
+  unsigned long long* cursors;  // [2 * parents]: left cursor (grows), right cursor (shrinks)
+  void* hist;            // [slot][Fmax][NB][NS] u64 (variance) or u32 (gini / counts)
+  int32_t NB, NS;
+  int32_t K0;            // label offset for the packed LDS word (variance)
+  int32_t FT, FPH, FPW;  // features per tile, LDS pitch, thread-feature width (pow2)
+  int32_t T;             // rows per tile
+  int32_t do_write;      // route + write entries (levels > 0)
+  int32_t count_only;    // gini layout with the label ignored (value counts)
+};
+
+struct SplitOut {
+  double gain;  // Double.MinValue when invalid
+  int32_t fl;   // best local feature, -1 when no feature has splits
+  int32_t s;    // best split bin
+  int32_t valid;
+  int32_t pad;
+};
+
+struct SplitArgs {
+  const void* hist;
+  int32_t Fmax, NB, NS;
+  const int32_t* slot_r;  // [M] replica of each slot
+  const int32_t* Fr;      // [R]
+  const int32_t* nbins;   // [R][Fmax]  numSplits + 1
+  int32_t min_inst;
+  double min_gain;
+  double inv_scale, inv_scale2;  // 2^-s, 2^-2s (fixed-point labels)
+  SplitOut* out;                  // [M]
+  int64_t* stats;                 // [M][3][NS]: total, left, right (integers)
+};
+
+struct DevNode {  // packed tree node for predict
+  double value;   // threshold (internal) or prediction (leaf)
+  int32_t left;   // -1 for a leaf
+  int32_t right;
+  int32_t gfeat;  // global feature index (subspace resolved)
+  int32_t pad;
+};
+
+// ---- launchers (sbag_kernels.hip) ----
+void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
+                    int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err);
+void launch_bernoulli(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off,
+                      const int64_t* d_chunk_pre, int P, int64_t chunks_total, int R,
+                      int learner0, int64_t seed, double ratio, const uint64_t* d_jump);
+void launch_fill(hipStream_t st, uint8_t* p, uint8_t v, int64_t n);
+void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
+                    uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
+                    unsigned long long* d_wsum);
+void launch_hist(hipStream_t st, const HistArgs& a, int nchunks, int ntiles, bool gini,
+                 size_t lds_bytes);
+void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini);
+void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
+                     int ntriples, int64_t words_per_slot, bool u32words);
+void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
+                        const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
+                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out);
+void launch_synth(hipStream_t st, uint8_t* codes, int32_t S, int64_t N, int32_t F, uint64_t seed,
+                  int32_t num_classes, int32_t* labk);
+void launch_predict(hipStream_t st, const double* X, const void* codes, int code_bytes,
+                    const double* dict, const int64_t* dict_off, int64_t N, int32_t F, int32_t S,
+                    const DevNode* nodes, const int64_t* tree_off, int L, int agg, int nclasses,
+                    double* out, double* per_tree);
+void launch_aggregate(hipStream_t st, const double* votes, int L, int64_t N, int agg, int nclasses,
+                      double* out);
+void launch_vc_global(hipStream_t st, const void* codes, int code_bytes, int32_t S, const uint64_t* ent,
+                      int64_t cap, const unsigned long long* d_inbag, const int32_t* d_sub,
+                      const int32_t* d_Fr, int32_t Fmax, int R, const int64_t* d_off, uint32_t* vc);
+size_t hist_lds_limit();
+
+}  // namespace sbag

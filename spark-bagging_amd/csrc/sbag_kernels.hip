@@ -1,0 +1,970 @@
+// sbag_kernels.hip — gfx950 kernels of the bagging engine.
+//
+// Kernels (DESIGN.md §3 gives the roofline and algorithmic bytes of each):
+//   k_poisson     per-(learner, partition) Well19937c + PoissonDistribution streams
+//                 (sql/catalyst/expressions/Poisson.scala:53-56,73)
+//   k_bernoulli   counter-based XORShiftRandom streams via GF(2) jump-ahead
+//                 (Rand at sql/bfunctions.scala:62-64)
+//   k_compact     per-replica in-bag row lists (replaces explode/replicate_row,
+//                 sql/bfunctions.scala:42-44, HasSubBag.scala:112-114)
+//   k_hist        fused route-rows + LDS-privatized histogram (the hot loop of
+//                 Spark's RandomForest.findBestSplits, reached via
+//                 ml/ensemble/ensembleParams.scala:113-115)
+//   k_split       prefix scan over bins + fp64 gain + first-max argmax
+//                 (RandomForest.binsToBestSplit / calculateImpurityStats)
+//   k_subtract    sibling histogram = parent - smaller child
+//   k_materialize per-replica bins from value codes (TreePoint.findBin)
+//   k_predict     slicer + tree walk + in-order mean / breeze mode
+//                 (BaggingRegressor.scala:248-256, BaggingClassifier.scala:248-257)
+//   k_synth       bench data generator
+// Built with -ffp-contract=off: every fp64 op of the gain formula is rounded
+// separately, as the JVM does.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+#include <algorithm>
+#include <cstdint>
+
+#include "sbag_internal.h"
+
+namespace sbag {
+
+#define HIPCHK(x) (void)(x)
+
+// ======================================================================
+// Poisson sampler: Well19937c state in LDS, one lane per stream, all lanes
+// advance their generators in lockstep so the ring index is wave-uniform and
+// every LDS access is conflict-free ([position][lane] layout).
+// ======================================================================
+__device__ __forceinline__ uint32_t well_step(uint32_t* st, int lane, int& index, uint32_t& v0) {
+  const int i = index;
+  const int rm1 = (i == 0) ? 623 : i - 1;
+  const int rm2 = (i <= 1) ? i + 622 : i - 2;
+  const int i1 = (i + 70 >= 624) ? i + 70 - 624 : i + 70;
+  const int i2 = (i + 179 >= 624) ? i + 179 - 624 : i + 179;
+  const int i3 = (i + 449 >= 624) ? i + 449 - 624 : i + 449;
+  const uint32_t vm1 = st[i1 * 64 + lane];
+  const uint32_t vm2 = st[i2 * 64 + lane];
+  const uint32_t vm3 = st[i3 * 64 + lane];
+  const uint32_t vr1 = st[rm1 * 64 + lane];
+  const uint32_t vr2 = st[rm2 * 64 + lane];
+  const uint32_t z0 = (0x80000000u & vr1) ^ (0x7FFFFFFFu & vr2);
+  const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (vm1 ^ (vm1 >> 27));
+  const uint32_t z2 = (vm2 >> 9) ^ (vm3 ^ (vm3 >> 1));
+  const uint32_t z3 = z1 ^ z2;
+  uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
+  st[i * 64 + lane] = z3;
+  st[rm1 * 64 + lane] = z4;
+  st[rm2 * 64 + lane] = vr2 & 0x80000000u;
+  index = rm1;
+  v0 = z4;
+  z4 ^= (z4 << 7) & 0xe46e1700u;
+  z4 ^= (z4 << 15) & 0x9b868000u;
+  return z4;
+}
+
+__global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, int64_t N,
+                                                const int64_t* __restrict__ part_off, int P, int R,
+                                                int learner0, int64_t seed, double mean,
+                                                double p_exp, int* err) {
+  __shared__ uint32_t st[624 * 64];
+  const int lane = threadIdx.x;
+  const int64_t sid = (int64_t)blockIdx.x * 64 + lane;
+  const bool active = sid < (int64_t)R * P;
+  const int r = active ? (int)(sid / P) : 0;
+  const int p = active ? (int)(sid % P) : 0;
+  // PoissonDistribution.reseedRandomGenerator(seed + i + partitionIndex) -> AbstractWell.setSeed
+  const uint64_t s64 = (uint64_t)seed + (uint64_t)(int64_t)(learner0 + r) + (uint64_t)(int64_t)p;
+  uint32_t vm2 = (uint32_t)(s64 >> 32), vm1 = (uint32_t)s64;
+  st[0 * 64 + lane] = vm2;
+  st[1 * 64 + lane] = vm1;
+  for (int i = 2; i < 624; i++) {
+    const int64_t l = (int64_t)(int32_t)vm2;
+    const uint32_t v = (uint32_t)(1812433253ull * (uint64_t)(l ^ (l >> 30)) + (uint64_t)i);
+    st[i * 64 + lane] = v;
+    vm2 = vm1;
+    vm1 = v;
+  }
+  int64_t row = active ? part_off[p] : 0;
+  const int64_t row_end = active ? part_off[p + 1] : 0;
+  uint8_t* out = counts + (int64_t)r * N;
+  int index = 0;
+  uint32_t v0 = st[lane];
+  const double cap = 1000.0 * mean;
+  int n = 0, bad = 0;
+  double racc = 1.0;
+  while (__any(row < row_end)) {
+    const uint32_t a = well_step(st, lane, index, v0) >> 6;  // next(26)
+    const uint32_t b = well_step(st, lane, index, v0) >> 6;
+    const double u = (double)((((uint64_t)a) << 26) | (uint64_t)b) * 0x1.0p-52;
+    if (row < row_end) {
+      racc *= u;
+      bool emit;
+      if (racc >= p_exp) {
+        n++;
+        emit = !((double)n < cap);
+      } else {
+        emit = true;
+      }
+      if (emit) {
+        if (n > 255) bad = 1;
+        out[row] = (uint8_t)(n > 255 ? 255 : n);
+        row++;
+        n = 0;
+        racc = 1.0;
+      }
+    }
+  }
+  if (bad) atomicOr(err, 1);
+}
+
+void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
+                    int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err) {
+  const int64_t streams = (int64_t)R * P;
+  const int blocks = (int)((streams + 63) / 64);
+  hipLaunchKernelGGL(k_poisson, dim3(blocks), dim3(64), 0, st, counts, N, d_part_off, P, R,
+                     learner0, seed, mean, p_exp, d_err);
+}
+
+// ======================================================================
+// Bernoulli sampler: XORShiftRandom is GF(2)-linear; a thread jumps its
+// stream to row j0 with precomputed M^(2^k) matrices and then steps 256 rows.
+// ======================================================================
+__device__ __forceinline__ uint32_t d_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ uint32_t d_mix_last(uint32_t h, uint32_t k) {
+  k *= 0xcc9e2d51u;
+  k = d_rotl(k, 15);
+  k *= 0x1b873593u;
+  return h ^ k;
+}
+__device__ __forceinline__ uint32_t d_mix(uint32_t h, uint32_t k) {
+  h = d_mix_last(h, k);
+  h = d_rotl(h, 13);
+  return h * 5u + 0xe6546b64u;
+}
+__device__ uint32_t d_hash8(uint32_t k0, uint32_t k1, uint32_t seed) {
+  uint32_t h = d_mix(d_mix(seed, k0), k1);
+  h ^= 8u;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ uint64_t d_hash_seed(int64_t seed) {  // XORShiftRandom.hashSeed
+  const uint64_t u = (uint64_t)seed;
+  // big-endian bytes b0..b7; little-endian 4-byte blocks of that array
+  const uint32_t b0 = (uint32_t)(u >> 56) & 0xff, b1 = (uint32_t)(u >> 48) & 0xff;
+  const uint32_t b2 = (uint32_t)(u >> 40) & 0xff, b3 = (uint32_t)(u >> 32) & 0xff;
+  const uint32_t b4 = (uint32_t)(u >> 24) & 0xff, b5 = (uint32_t)(u >> 16) & 0xff;
+  const uint32_t b6 = (uint32_t)(u >> 8) & 0xff, b7 = (uint32_t)u & 0xff;
+  const uint32_t k0 = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  const uint32_t k1 = b4 | (b5 << 8) | (b6 << 16) | (b7 << 24);
+  const uint32_t lo = d_hash8(k0, k1, 0x3c074a61u);
+  const uint32_t hi = d_hash8(k0, k1, lo);
+  return ((uint64_t)hi << 32) | (uint64_t)lo;
+}
+__device__ __forceinline__ uint64_t xs_step(uint64_t s) {
+  s ^= s << 21;
+  s ^= s >> 35;
+  s ^= s << 4;
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_bernoulli(uint8_t* __restrict__ counts, int64_t N,
+                                                   const int64_t* __restrict__ part_off,
+                                                   const int64_t* __restrict__ chunk_pre, int P,
+                                                   int64_t chunks_total, int R, int learner0,
+                                                   int64_t seed, double ratio,
+                                                   const uint64_t* __restrict__ jump) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)R * chunks_total) return;
+  const int r = (int)(t / chunks_total);
+  const int64_t c = t % chunks_total;
+  int lo = 0, hi = P;  // largest p with chunk_pre[p] <= c
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (chunk_pre[mid] <= c)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const int p = lo;
+  const int64_t j0 = (c - chunk_pre[p]) * 256;
+  const int64_t row0 = part_off[p] + j0;
+  const int64_t row1 = min(row0 + 256, part_off[p + 1]);
+  const int i = learner0 + r;
+  int64_t rs;
+  if (seed >= (int64_t)INT_MIN && seed <= (int64_t)INT_MAX) {  // SQL Int addition (H15)
+    const int32_t s32 = (int32_t)((uint32_t)(int32_t)seed + (uint32_t)i);
+    rs = (int64_t)s32 + p;
+  } else {
+    rs = (int64_t)((uint64_t)seed + (uint64_t)(int64_t)i + (uint64_t)(int64_t)p);
+  }
+  uint64_t s = d_hash_seed(rs);
+  const uint64_t steps = 2ull * (uint64_t)j0;
+  for (int k = 0; k < 63; k++) {
+    if ((steps >> k) & 1ull) {
+      const uint64_t* m = jump + k * 64;
+      uint64_t acc = 0, x = s;
+      while (x) {
+        const int b = __ffsll((long long)x) - 1;
+        acc ^= m[b];
+        x &= x - 1;
+      }
+      s = acc;
+    }
+  }
+  uint8_t* out = counts + (int64_t)r * N;
+  for (int64_t row = row0; row < row1; row++) {
+    s = xs_step(s);
+    const int64_t a = (int64_t)(s & ((1ull << 26) - 1));
+    s = xs_step(s);
+    const int64_t b = (int64_t)(s & ((1ull << 27) - 1));
+    const double u = (double)((a << 27) + b) * 0x1.0p-53;
+    out[row] = (u < ratio) ? 1 : 0;
+  }
+}
+
+void launch_bernoulli(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off,
+                      const int64_t* d_chunk_pre, int P, int64_t chunks_total, int R,
+                      int learner0, int64_t seed, double ratio, const uint64_t* d_jump) {
+  const int64_t threads = (int64_t)R * chunks_total;
+  const int blocks = (int)((threads + 255) / 256);
+  hipLaunchKernelGGL(k_bernoulli, dim3(blocks), dim3(256), 0, st, counts, N, d_part_off,
+                     d_chunk_pre, P, chunks_total, R, learner0, seed, ratio, d_jump);
+}
+
+__global__ void k_fill(uint8_t* p, uint8_t v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+void launch_fill(hipStream_t st, uint8_t* p, uint8_t v, int64_t n) {
+  int blocks = (int)std::min<int64_t>((n + 255) / 256, 65536);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, p, v, n);
+}
+
+// ======================================================================
+// In-bag compaction: entries of rows with count > 0, one wave-ballot + one
+// atomic per wave.  Order inside a segment is irrelevant (integer stats).
+// ======================================================================
+__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ counts, int64_t N,
+                                                 const int32_t* __restrict__ labk,
+                                                 uint64_t* __restrict__ ent, int64_t cap,
+                                                 unsigned long long* cursor,
+                                                 unsigned long long* wsum) {
+  const int r = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  unsigned long long mysum = 0;
+  const uint8_t* cr = counts + (int64_t)r * N;
+  uint64_t* er = ent + (int64_t)r * cap;
+  for (int k = 0; k < 4; k++) {
+    const int64_t row = (int64_t)blockIdx.x * 1024 + k * 256 + threadIdx.x;
+    const uint32_t c = (row < N) ? cr[row] : 0;
+    mysum += c;
+    const uint64_t m = __ballot(c > 0);
+    unsigned long long base = 0;
+    if (lane == 0 && m) base = atomicAdd(&cursor[r], (unsigned long long)__popcll(m));
+    base = __shfl(base, 0);
+    if (c) er[base + __popcll(m & lt)] = pack_entry((uint32_t)row, labk[row], c);
+  }
+  __shared__ unsigned long long red[256];
+  red[threadIdx.x] = mysum;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && red[0]) atomicAdd(&wsum[r], red[0]);
+}
+
+void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
+                    uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
+                    unsigned long long* d_wsum) {
+  dim3 grid((unsigned)((N + 1023) / 1024), (unsigned)R);
+  hipLaunchKernelGGL(k_compact, grid, dim3(256), 0, st, counts, N, d_labk, ent, cap, d_cursor,
+                     d_wsum);
+}
+
+// ======================================================================
+// Fused route + histogram.  One workgroup = one chunk of a parent's entry
+// segment x one feature tile.  Per tile of T rows: entries -> LDS, gather the
+// rows' bins (16 B per lane) -> LDS, route each row by the parent's split and
+// append it to its child's segment (wave ballot, one atomic per wave and side),
+// then accumulate the histogram child in LDS with per-thread-fixed feature
+// lanes ([word][bin][feature] layout: lanes of a 16/32-lane group touch
+// distinct banks whatever the bins are).  Variance stats are packed into two
+// u64 LDS words: (count << 40) + count*(k + K0) and count*k^2 (integer, hence
+// order-independent and bit-exact).  Flush: global u64/u32 atomics.
+// ======================================================================
+static __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+template <bool GINI>
+__global__ __launch_bounds__(256) void k_hist(HistArgs A) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const HistChunk ch = A.chunks[blockIdx.x];
+  const ParentInfo pi = A.parents[ch.parent];
+  const int r = pi.r;
+  const int Fr = A.Fr[r];
+  const int ft0 = blockIdx.y * A.FT;
+  const int ftn = min(A.FT, Fr - ft0);
+  if (ftn <= 0) return;
+  const bool tile0 = blockIdx.y == 0;
+  const bool do_hist = pi.hist_slot >= 0;
+  const bool do_write = tile0 && A.do_write;
+  if (!do_hist && !do_write) return;
+  const int NB = A.NB, NS = A.NS, FPH = A.FPH, S = A.S, T = A.T;
+
+  const size_t hist_bytes = GINI ? (size_t)NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
+  size_t off = align16(hist_bytes);
+  uint8_t* tile = smem + off;
+  off += align16((size_t)T * S);
+  uint64_t* s_e = (uint64_t*)(smem + off);
+  off += (size_t)T * 8;
+  uint64_t* s_w0 = (uint64_t*)(smem + off);
+  off += (size_t)T * 8;
+  uint64_t* s_w1 = (uint64_t*)(smem + off);
+  off += (size_t)T * 8;
+  int16_t* s_pos = (int16_t*)(smem + off);
+  off += align16((size_t)A.FT * 2);
+  uint8_t* s_flag = smem + off;
+
+  uint64_t* h64 = (uint64_t*)smem;
+  uint32_t* h32 = (uint32_t*)smem;
+  if (do_hist) {
+    for (size_t i = (size_t)tid * 16; i < hist_bytes; i += 256 * 16)
+      *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+  }
+  for (int i = tid; i < ftn; i += 256) s_pos[i] = A.pos[(int64_t)r * A.Fmax + ft0 + i];
+  __syncthreads();
+
+  const uint8_t* binsr = A.bins + (int64_t)r * A.bins_rstride;
+  const int lpr = S >> 4;
+  const int rpp = 256 / lpr;
+  const int myrow = tid / lpr, mypart = tid - myrow * lpr;
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  const int FPW = A.FPW;
+  const int fl = tid & (FPW - 1), g0 = tid / FPW, G = 256 / FPW;
+  const int K0 = A.K0;
+
+  for (int64_t base = ch.a; base < ch.b; base += T) {
+    const int nt = (int)min((int64_t)T, ch.b - base);
+    for (int i = tid; i < nt; i += 256) {
+      const uint64_t e = A.ent_in[base + i];
+      s_e[i] = e;
+      const int32_t hi = (int32_t)(e >> 32);
+      const uint32_t c = (uint32_t)hi & 0xffu;
+      const int32_t k = hi >> 8;
+      if (GINI) {
+        s_w0[i] = A.count_only ? (uint64_t)c : (((uint64_t)(uint32_t)k << 32) | c);
+      } else {
+        s_w0[i] = ((uint64_t)c << 40) + (uint64_t)c * (uint64_t)(int64_t)(k + K0);
+        s_w1[i] = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);
+      }
+    }
+    __syncthreads();
+    if (myrow < rpp) {
+      for (int i = myrow; i < nt; i += rpp) {
+        const uint32_t row = (uint32_t)s_e[i];
+        const uint4 v = *((const uint4*)(binsr + (int64_t)row * S) + mypart);
+        *((uint4*)(tile + (size_t)i * S) + mypart) = v;
+      }
+    }
+    __syncthreads();
+    const int ntr = (nt + 63) & ~63;
+    for (int i = tid; i < ntr; i += 256) {
+      const bool valid = i < nt;
+      int side = 0;
+      if (valid && pi.pos >= 0) side = (tile[(size_t)i * S + pi.pos] <= pi.s) ? 0 : 1;
+      if (do_write) {
+        const bool wl = valid && side == 0 && pi.write_l;
+        const bool wr = valid && side == 1 && pi.write_r;
+        const uint64_t ml = __ballot(wl), mr = __ballot(wr);
+        unsigned long long bl = 0, br = 0;
+        if (lane == 0) {
+          if (ml) bl = atomicAdd(&A.cursors[2 * ch.parent], (unsigned long long)__popcll(ml));
+          if (mr) {
+            const unsigned long long nr = (unsigned long long)__popcll(mr);
+            br = atomicAdd(&A.cursors[2 * ch.parent + 1], (unsigned long long)(-(long long)nr)) - nr;
+          }
+        }
+        bl = __shfl(bl, 0);
+        br = __shfl(br, 0);
+        if (wl) A.ent_out[bl + __popcll(ml & lt)] = s_e[i];
+        if (wr) A.ent_out[br + __popcll(mr & lt)] = s_e[i];
+      }
+      if (valid) s_flag[i] = (do_hist && side == pi.hist_side) ? 1 : 0;
+    }
+    __syncthreads();
+    if (do_hist && fl < ftn) {
+      const int p = s_pos[fl];
+      for (int i = g0; i < nt; i += G) {
+        if (s_flag[i]) {
+          const int b = tile[(size_t)i * S + p];
+          if (GINI) {
+            const uint64_t w = s_w0[i];
+            const int cls = (int)(w >> 32);
+            atomicAdd(&h32[((size_t)cls * NB + b) * FPH + fl], (uint32_t)(w & 0xffffffffu));
+          } else {
+            atomicAdd((unsigned long long*)&h64[(size_t)b * FPH + fl],
+                      (unsigned long long)s_w0[i]);
+            atomicAdd((unsigned long long*)&h64[((size_t)NB + b) * FPH + fl],
+                      (unsigned long long)s_w1[i]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!do_hist) return;
+  const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
+  if (GINI) {
+    uint32_t* gh = (uint32_t*)A.hist + (int64_t)pi.hist_slot * slot_words;
+    for (int q = tid; q < ftn * NB * NS; q += 256) {
+      const int cls = q % NS, b = (q / NS) % NB, f = q / (NS * NB);
+      const uint32_t v = h32[((size_t)cls * NB + b) * FPH + f];
+      if (v) atomicAdd(&gh[((int64_t)(ft0 + f) * NB + b) * NS + cls], v);
+    }
+  } else {
+    unsigned long long* gh = (unsigned long long*)A.hist + (int64_t)pi.hist_slot * slot_words;
+    const uint64_t M40 = (1ull << 40) - 1;
+    for (int q = tid; q < ftn * NB; q += 256) {
+      const int b = q % NB, f = q / NB;
+      const uint64_t w0 = h64[(size_t)b * FPH + f];
+      if (w0) {
+        const uint64_t cnt = w0 >> 40;
+        const int64_t sk = (int64_t)(w0 & M40) - (int64_t)K0 * (int64_t)cnt;
+        const uint64_t w1 = h64[((size_t)NB + b) * FPH + f];
+        const int64_t gb = ((int64_t)(ft0 + f) * NB + b) * 3;
+        atomicAdd(&gh[gb], (unsigned long long)cnt);
+        atomicAdd(&gh[gb + 1], (unsigned long long)sk);
+        atomicAdd(&gh[gb + 2], (unsigned long long)w1);
+      }
+    }
+  }
+}
+
+size_t hist_lds_limit() { return 160 * 1024; }
+
+void launch_hist(hipStream_t st, const HistArgs& a, int nchunks, int ntiles, bool gini,
+                 size_t lds_bytes) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_hist<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)k_hist<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  dim3 grid((unsigned)nchunks, (unsigned)ntiles);
+  if (gini)
+    hipLaunchKernelGGL(k_hist<true>, grid, dim3(256), lds_bytes, st, a);
+  else
+    hipLaunchKernelGGL(k_hist<false>, grid, dim3(256), lds_bytes, st, a);
+}
+
+// ======================================================================
+// Split search: one workgroup per node slot; thread per local feature does
+// the prefix scan over bins and the fp64 gain of every candidate in Spark's
+// operation order; first max over splits, then first max over features.
+// ======================================================================
+__device__ __forceinline__ double var_impurity(int64_t cnt, int64_t sk, uint64_t sq, double is,
+                                               double is2) {
+  const double count = (double)cnt;
+  if (count == 0) return 0.0;
+  const double sum = (double)sk * is;
+  const double sumsq = (double)sq * is2;
+  const double squared_loss = sumsq - (sum * sum) / count;
+  return squared_loss / count;
+}
+
+template <bool GINI>
+__global__ __launch_bounds__(256) void k_split(SplitArgs A) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int slot = blockIdx.x, tid = threadIdx.x;
+  const int r = A.slot_r[slot];
+  const int Fr = A.Fr[r];
+  const int NB = A.NB, NS = A.NS;
+  const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
+  double* s_gain = (double*)smem;
+  int* s_fl = (int*)(s_gain + 256);
+  int* s_s = s_fl + 256;
+  int* s_valid = s_s + 256;
+  int64_t* s_tot = (int64_t*)(s_valid + 256);  // [NS]
+  uint32_t* s_left = (uint32_t*)(s_tot + NS);  // GINI: [NS][256]
+  const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
+
+  // node total = sum over the bins of local feature 0 (every feature sums to it)
+  if (GINI) {
+    const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
+    for (int c = tid; c < NS; c += 256) {
+      int64_t t = 0;
+      for (int b = 0; b < NB; b++) t += h[(int64_t)b * NS + c];
+      s_tot[c] = t;
+    }
+  } else {
+    const uint64_t* h = (const uint64_t*)A.hist + (int64_t)slot * slot_words;
+    if (tid < 3) {
+      int64_t t = 0;
+      for (int b = 0; b < NB; b++) t += (int64_t)h[(int64_t)b * 3 + tid];
+      s_tot[tid] = t;
+    }
+  }
+  __syncthreads();
+
+  double bgain = -INFINITY;
+  int bfl = INT_MAX, bs = -1, bvalid = 0;
+  const double is = A.inv_scale, is2 = A.inv_scale2;
+  if (GINI) {
+    double ttot = 0.0;
+    for (int c = 0; c < NS; c++) ttot += (double)s_tot[c];
+    double imp = 0.0;
+    if (ttot != 0) {
+      imp = 1.0;
+      for (int c = 0; c < NS; c++) {
+        const double f = (double)s_tot[c] / ttot;
+        imp -= f * f;
+      }
+    }
+    const int64_t tcount = (int64_t)ttot;
+    uint32_t* left = s_left + tid;  // stride 256
+    for (int fl = tid; fl < Fr; fl += 256) {
+      const int nsp = nb_r[fl] - 1;
+      if (nsp <= 0) continue;
+      const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words + (int64_t)fl * NB * NS;
+      for (int c = 0; c < NS; c++) left[c * 256] = 0;
+      double fg = 0.0;
+      int fs = -1, fv = 0;
+      for (int s = 0; s < nsp; s++) {
+        double lt = 0.0;
+        for (int c = 0; c < NS; c++) {
+          const uint32_t v = left[c * 256] + h[(int64_t)s * NS + c];
+          left[c * 256] = v;
+          lt += (double)v;
+        }
+        const int64_t lc = (int64_t)lt;
+        const int64_t rc = tcount - lc;
+        double gain;
+        int valid;
+        if (lc < A.min_inst || rc < A.min_inst) {
+          gain = -DBL_MAX;
+          valid = 0;
+        } else {
+          double li = 0.0, ri = 0.0;
+          if (lt != 0) {
+            li = 1.0;
+            for (int c = 0; c < NS; c++) {
+              const double f = (double)left[c * 256] / lt;
+              li -= f * f;
+            }
+          }
+          double rt = 0.0;
+          for (int c = 0; c < NS; c++) rt += (double)(s_tot[c] - (int64_t)left[c * 256]);
+          if (rt != 0) {
+            ri = 1.0;
+            for (int c = 0; c < NS; c++) {
+              const double f = (double)(s_tot[c] - (int64_t)left[c * 256]) / rt;
+              ri -= f * f;
+            }
+          }
+          const double lw = (double)lc / (double)(lc + rc);
+          const double rw = (double)rc / (double)(lc + rc);
+          gain = imp - lw * li - rw * ri;
+          valid = 1;
+          if (gain < A.min_gain) {
+            gain = -DBL_MAX;
+            valid = 0;
+          }
+        }
+        if (fs < 0 || gain > fg) {
+          fg = gain;
+          fs = s;
+          fv = valid;
+        }
+      }
+      if (fg > bgain || (fg == bgain && fl < bfl)) {
+        bgain = fg;
+        bfl = fl;
+        bs = fs;
+        bvalid = fv;
+      }
+    }
+  } else {
+    const int64_t tc = s_tot[0], tsk = s_tot[1];
+    const uint64_t tsq = (uint64_t)s_tot[2];
+    const double imp = var_impurity(tc, tsk, tsq, is, is2);
+    for (int fl = tid; fl < Fr; fl += 256) {
+      const int nsp = nb_r[fl] - 1;
+      if (nsp <= 0) continue;
+      const uint64_t* h = (const uint64_t*)A.hist + (int64_t)slot * slot_words + (int64_t)fl * NB * 3;
+      int64_t lc = 0, lsk = 0;
+      uint64_t lsq = 0;
+      double fg = 0.0;
+      int fs = -1, fv = 0;
+      for (int s = 0; s < nsp; s++) {
+        lc += (int64_t)h[s * 3];
+        lsk += (int64_t)h[s * 3 + 1];
+        lsq += h[s * 3 + 2];
+        const int64_t rc = tc - lc;
+        double gain;
+        int valid;
+        if (lc < A.min_inst || rc < A.min_inst) {
+          gain = -DBL_MAX;
+          valid = 0;
+        } else {
+          const double li = var_impurity(lc, lsk, lsq, is, is2);
+          const double ri = var_impurity(rc, tsk - lsk, tsq - lsq, is, is2);
+          const double lw = (double)lc / (double)(lc + rc);
+          const double rw = (double)rc / (double)(lc + rc);
+          gain = imp - lw * li - rw * ri;
+          valid = 1;
+          if (gain < A.min_gain) {
+            gain = -DBL_MAX;
+            valid = 0;
+          }
+        }
+        if (fs < 0 || gain > fg) {
+          fg = gain;
+          fs = s;
+          fv = valid;
+        }
+      }
+      if (fg > bgain || (fg == bgain && fl < bfl)) {
+        bgain = fg;
+        bfl = fl;
+        bs = fs;
+        bvalid = fv;
+      }
+    }
+  }
+  s_gain[tid] = bgain;
+  s_fl[tid] = bfl;
+  s_s[tid] = bs;
+  s_valid[tid] = bvalid;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const double g2 = s_gain[tid + o];
+      const int f2 = s_fl[tid + o];
+      if (g2 > s_gain[tid] || (g2 == s_gain[tid] && f2 < s_fl[tid])) {
+        s_gain[tid] = g2;
+        s_fl[tid] = f2;
+        s_s[tid] = s_s[tid + o];
+        s_valid[tid] = s_valid[tid + o];
+      }
+    }
+    __syncthreads();
+  }
+  int64_t* so = A.stats + (int64_t)slot * 3 * NS;
+  if (tid == 0) {
+    SplitOut o;
+    const int fl = s_fl[0];
+    if (fl == INT_MAX) {
+      o.gain = -DBL_MAX;
+      o.fl = -1;
+      o.s = -1;
+      o.valid = 0;
+    } else {
+      o.gain = s_gain[0];
+      o.fl = fl;
+      o.s = s_s[0];
+      o.valid = s_valid[0];
+    }
+    o.pad = 0;
+    A.out[slot] = o;
+  }
+  const int bf = s_fl[0], bsp = s_s[0];
+  for (int c = tid; c < NS; c += 256) {
+    int64_t l = 0;
+    if (bf != INT_MAX) {
+      if (GINI) {
+        const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words + (int64_t)bf * NB * NS;
+        for (int s = 0; s <= bsp; s++) l += h[(int64_t)s * NS + c];
+      } else {
+        const uint64_t* h = (const uint64_t*)A.hist + (int64_t)slot * slot_words + (int64_t)bf * NB * 3;
+        for (int s = 0; s <= bsp; s++) l += (int64_t)h[s * 3 + c];
+      }
+    }
+    so[c] = s_tot[c];
+    so[NS + c] = l;
+    so[2 * NS + c] = s_tot[c] - l;
+  }
+}
+
+void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
+  const size_t lds = 256 * (8 + 4 + 4 + 4) + 8 * (size_t)a.NS + (gini ? (size_t)a.NS * 256 * 4 : 0);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_split<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)k_split<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  if (gini)
+    hipLaunchKernelGGL(k_split<true>, dim3(M), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL(k_split<false>, dim3(M), dim3(256), lds, st, a);
+}
+
+// sibling = parent - smaller child  (triples: dst slot, parent slot, small slot)
+template <typename W>
+__global__ __launch_bounds__(256) void k_subtract(W* __restrict__ dst_hist,
+                                                  const W* __restrict__ par_hist,
+                                                  const int32_t* __restrict__ triples,
+                                                  int64_t words) {
+  const int t = blockIdx.y;
+  const int64_t d = triples[3 * t], p = triples[3 * t + 1], s = triples[3 * t + 2];
+  for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < words;
+       w += (int64_t)gridDim.x * 256)
+    dst_hist[d * words + w] = par_hist[p * words + w] - dst_hist[s * words + w];
+}
+
+void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
+                     int ntriples, int64_t words_per_slot, bool u32words) {
+  if (ntriples <= 0) return;
+  const unsigned gx = (unsigned)std::min<int64_t>((words_per_slot + 255) / 256, 64);
+  dim3 grid(gx, (unsigned)ntriples);
+  if (u32words)
+    hipLaunchKernelGGL(k_subtract<uint32_t>, grid, dim3(256), 0, st, (uint32_t*)dst_hist,
+                       (const uint32_t*)parent_hist, d_triples, words_per_slot);
+  else
+    hipLaunchKernelGGL(k_subtract<uint64_t>, grid, dim3(256), 0, st, (uint64_t*)dst_hist,
+                       (const uint64_t*)parent_hist, d_triples, words_per_slot);
+}
+
+// ======================================================================
+// Per-replica bins from value codes: bin = lut[r][fl][code] (TreePoint.findBin
+// = Arrays.binarySearch over the replica's thresholds, precomputed per code).
+// ======================================================================
+template <typename CT>
+__global__ __launch_bounds__(256) void k_materialize(const CT* __restrict__ codes, int64_t N,
+                                                     int32_t S_codes, const int32_t* __restrict__ sub,
+                                                     const int32_t* __restrict__ Fr, int32_t Fmax,
+                                                     const uint8_t* __restrict__ lut,
+                                                     const int64_t* __restrict__ lutoff,
+                                                     uint8_t* __restrict__ out, int32_t S_out) {
+  const int r = blockIdx.y;
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= N) return;
+  const int fr = Fr[r];
+  uint8_t* o = out + ((int64_t)r * N + row) * S_out;
+  const CT* c = codes + row * S_codes;
+  for (int fl = 0; fl < S_out; fl++) {
+    uint8_t b = 0;
+    if (fl < fr) {
+      const int g = sub[(int64_t)r * Fmax + fl];
+      b = lut[lutoff[(int64_t)r * Fmax + fl] + (int64_t)c[g]];
+    }
+    o[fl] = b;
+  }
+}
+
+void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
+                        const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
+                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out) {
+  dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
+  if (code_bytes == 1)
+    hipLaunchKernelGGL(k_materialize<uint8_t>, grid, dim3(256), 0, st, (const uint8_t*)codes, N,
+                       S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
+  else
+    hipLaunchKernelGGL(k_materialize<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)codes, N,
+                       S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
+}
+
+// Value counts with global atomics (u16 codes / dictionaries too large for LDS)
+template <typename CT>
+__global__ __launch_bounds__(256) void k_vc_global(const CT* __restrict__ codes, int32_t S,
+                                                   const uint64_t* __restrict__ ent, int64_t cap,
+                                                   const unsigned long long* __restrict__ inbag,
+                                                   const int32_t* __restrict__ sub,
+                                                   const int32_t* __restrict__ Fr, int32_t Fmax,
+                                                   const int64_t* __restrict__ off, uint32_t* vc) {
+  const int r = blockIdx.y;
+  const int64_t n = (int64_t)inbag[r];
+  const int fr = Fr[r];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = ent[(int64_t)r * cap + i];
+    const uint32_t row = (uint32_t)e;
+    const uint32_t cnt = (uint32_t)(e >> 32) & 0xffu;
+    for (int fl = 0; fl < fr; fl++) {
+      const int g = sub[(int64_t)r * Fmax + fl];
+      atomicAdd(&vc[off[(int64_t)r * Fmax + fl] + (int64_t)codes[(int64_t)row * S + g]], cnt);
+    }
+  }
+}
+
+void launch_vc_global(hipStream_t st, const void* codes, int code_bytes, int32_t S, const uint64_t* ent,
+                      int64_t cap, const unsigned long long* d_inbag, const int32_t* d_sub,
+                      const int32_t* d_Fr, int32_t Fmax, int R, const int64_t* d_off, uint32_t* vc) {
+  dim3 grid(256, (unsigned)R);
+  if (code_bytes == 1)
+    hipLaunchKernelGGL(k_vc_global<uint8_t>, grid, dim3(256), 0, st, (const uint8_t*)codes, S, ent,
+                       cap, d_inbag, d_sub, d_Fr, Fmax, d_off, vc);
+  else
+    hipLaunchKernelGGL(k_vc_global<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)codes, S,
+                       ent, cap, d_inbag, d_sub, d_Fr, Fmax, d_off, vc);
+}
+
+// ======================================================================
+// Synthetic workload
+// ======================================================================
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ codes, int32_t S, int64_t N,
+                                               int32_t F, uint64_t seed, int32_t C,
+                                               int32_t* __restrict__ labk) {
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= N) return;
+  uint8_t* o = codes + row * S;
+  int x[8];
+  for (int f = 0; f < 8; f++) x[f] = 0;
+  for (int f0 = 0; f0 < S; f0 += 4) {
+    uint32_t w = 0;
+    for (int j = 0; j < 4; j++) {
+      const int f = f0 + j;
+      uint32_t v = 0;
+      if (f < F) v = (uint32_t)(splitmix64(seed ^ (uint64_t)(row * (int64_t)F + f)) & 31u);
+      if (f < 8) x[f] = (int)v;
+      w |= v << (8 * j);
+    }
+    *(uint32_t*)(o + f0) = w;
+  }
+  const uint64_t h2 = splitmix64(~seed ^ (uint64_t)row);
+  if (C == 0) {
+    int k = 0;
+    for (int f = 0; f < 8 && f < F; f++) k += (f + 1) * x[f];
+    labk[row] = k + (int)(h2 & 63u) - 32;
+  } else {
+    labk[row] = (x[0] + 3 * x[1] + 7 * x[2] + (int)(h2 & 7u)) % C;
+  }
+}
+
+void launch_synth(hipStream_t st, uint8_t* codes, int32_t S, int64_t N, int32_t F, uint64_t seed,
+                  int32_t num_classes, int32_t* labk) {
+  hipLaunchKernelGGL(k_synth, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, codes, S, N, F,
+                     seed, num_classes, labk);
+}
+
+// ======================================================================
+// Prediction: thread per row, trees in learner order (breeze sum order /
+// breeze mode "first value to reach the final max count").
+// ======================================================================
+__global__ __launch_bounds__(256) void k_predict(const double* __restrict__ X,
+                                                 const void* __restrict__ codes, int code_bytes,
+                                                 const double* __restrict__ dict,
+                                                 const int64_t* __restrict__ dict_off, int64_t N,
+                                                 int32_t F, int32_t S,
+                                                 const DevNode* __restrict__ nodes,
+                                                 const int64_t* __restrict__ tree_off, int L,
+                                                 int agg, int nclasses, double* __restrict__ out,
+                                                 double* __restrict__ per_tree) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t* cnt = (uint16_t*)smem;  // [nclasses][256]
+  const int tid = threadIdx.x;
+  const int64_t row = (int64_t)blockIdx.x * 256 + tid;
+  if (row >= N) return;
+  if (agg == 1)
+    for (int c = 0; c < nclasses; c++) cnt[c * 256 + tid] = 0;
+  double sum = 0.0, mode = 0.0;
+  int maxc = 0;
+  for (int l = 0; l < L; l++) {
+    const DevNode* t = nodes + tree_off[l];
+    int id = 0;
+    while (t[id].left >= 0) {
+      const int g = t[id].gfeat;
+      double v;
+      if (X) {
+        v = X[row * F + g];
+      } else {
+        const int64_t c = (code_bytes == 1) ? (int64_t)((const uint8_t*)codes)[row * S + g]
+                                            : (int64_t)((const uint16_t*)codes)[row * S + g];
+        v = dict[dict_off[g] + c];
+      }
+      id = (v <= t[id].value) ? t[id].left : t[id].right;
+    }
+    const double pred = t[id].value;
+    if (per_tree) per_tree[(int64_t)l * N + row] = pred;
+    if (agg == 0) {
+      sum += pred;
+    } else {
+      const int c = (int)pred;
+      const int k = ++cnt[c * 256 + tid];
+      if (k > maxc) {
+        maxc = k;
+        mode = pred;
+      }
+    }
+  }
+  out[row] = (agg == 0) ? sum / (double)L : mode;
+}
+
+void launch_predict(hipStream_t st, const double* X, const void* codes, int code_bytes,
+                    const double* dict, const int64_t* dict_off, int64_t N, int32_t F, int32_t S,
+                    const DevNode* nodes, const int64_t* tree_off, int L, int agg, int nclasses,
+                    double* out, double* per_tree) {
+  const size_t lds = (agg == 1) ? (size_t)nclasses * 256 * 2 : 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_predict, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_predict, dim3((unsigned)((N + 255) / 256)), dim3(256), lds, st, X, codes,
+                     code_bytes, dict, dict_off, N, F, S, nodes, tree_off, L, agg, nclasses, out,
+                     per_tree);
+}
+
+__global__ __launch_bounds__(256) void k_aggregate(const double* __restrict__ votes, int L,
+                                                   int64_t N, int agg, int nclasses,
+                                                   double* __restrict__ out) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t* cnt = (uint16_t*)smem;
+  const int tid = threadIdx.x;
+  const int64_t row = (int64_t)blockIdx.x * 256 + tid;
+  if (row >= N) return;
+  if (agg == 1)
+    for (int c = 0; c < nclasses; c++) cnt[c * 256 + tid] = 0;
+  double sum = 0.0, mode = 0.0;
+  int maxc = 0;
+  for (int l = 0; l < L; l++) {
+    const double v = votes[(int64_t)l * N + row];
+    if (agg == 0) {
+      sum += v;
+    } else {
+      const int k = ++cnt[(int)v * 256 + tid];
+      if (k > maxc) {
+        maxc = k;
+        mode = v;
+      }
+    }
+  }
+  out[row] = (agg == 0) ? sum / (double)L : mode;
+}
+
+void launch_aggregate(hipStream_t st, const double* votes, int L, int64_t N, int agg, int nclasses,
+                      double* out) {
+  const size_t lds = (agg == 1) ? (size_t)nclasses * 256 * 2 : 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_aggregate, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_aggregate, dim3((unsigned)((N + 255) / 256)), dim3(256), lds, st, votes, L,
+                     N, agg, nclasses, out);
+}
+
+}  // namespace sbag

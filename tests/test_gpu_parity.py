@@ -1,0 +1,164 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact: bag counts, subspaces, thresholds, tree structure, impurities, gains,
+node stats and classification votes.  Regression predictions: within 1e-5
+relative (north_star tolerance); they come out bit-exact for the dyadic labels used.
+Reference workloads: data/cpusmall (BaggingRegressorSuite.scala:12) and
+data/vehicle (BaggingClassifierSuite.scala:12), copied under tests/golden/data.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import DATA
+from parity_utils import assert_forest_equal, oracle_forest
+
+import spark_bagging_amd as sb
+from spark_bagging_amd import _native as nat
+
+pytestmark = pytest.mark.gpu
+
+SEED_REG = oracle.DEFAULT_SEED_REGRESSOR
+SEED_CLS = oracle.DEFAULT_SEED_CLASSIFIER
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return sb.default_context(0)
+
+
+@pytest.fixture(scope="module")
+def cpusmall():
+    return sb.load_libsvm(os.path.join(DATA, "cpusmall.svm"))
+
+
+@pytest.fixture(scope="module")
+def vehicle():
+    return sb.load_libsvm(os.path.join(DATA, "vehicle.svm"))
+
+
+# ---------------------------------------------------------------- sampler
+@pytest.mark.parametrize("seed", [SEED_REG, SEED_CLS, 0, 7, 2**40 + 3, -5])
+@pytest.mark.parametrize("ratio", [1.0, 0.7, 0.05])
+def test_poisson_bag_bit_exact(ctx, seed, ratio):
+    N = 5000
+    off = [0, 1234, 1234, 4000, 5000]  # includes an empty partition
+    got = nat.sample(ctx, True, ratio, seed, 3, 11, N, off)
+    want = oracle.bag(True, ratio, 3, 11, seed, off, N)
+    assert (got == want).all()
+
+
+@pytest.mark.parametrize("seed", [SEED_REG, SEED_CLS, 2**31 - 3, -2**31 + 1, 2**40 + 3])
+@pytest.mark.parametrize("ratio", [0.5, 0.3, 0.999])
+def test_bernoulli_bag_bit_exact(ctx, seed, ratio):
+    N = 70000
+    off = [0, 300, 30000, 30001, 70000]
+    got = nat.sample(ctx, False, ratio, seed, 0, 6, N, off)
+    want = oracle.bag(False, ratio, 0, 6, seed, off, N)
+    assert (got == want).all()
+
+
+def test_all_ones_bag(ctx):
+    got = nat.sample(ctx, False, 1.0, SEED_REG, 0, 4, 1000)
+    assert (got == 1).all()
+
+
+def test_sampler_rejects_bad_ratio(ctx):
+    with pytest.raises(sb.IllegalArgumentException):
+        nat.sample(ctx, True, 0.0, 1, 0, 2, 10)
+    with pytest.raises(sb.IllegalArgumentException):
+        nat.sample(ctx, False, 1.5, 1, 0, 2, 10)
+
+
+# ---------------------------------------------------------------- fit
+def _fit_both(ctx, X, y, L, *, replacement, ratio, seed, depth, bins, cls, subspace_ratio=1.0,
+              bug_compat=True, part=None, min_inst=1, min_gain=0.0):
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    forest = nat.fit(ctx, ds, replacement=replacement, sample_ratio=ratio, seed=seed,
+                     learner_begin=0, learner_end=L, subspace_ratio=subspace_ratio,
+                     subspace_bug_compat=bug_compat, partition_offsets=part, max_depth=depth,
+                     max_bins=bins, min_instances_per_node=min_inst, min_info_gain=min_gain,
+                     impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    N, F = X.shape
+    off = part if part is not None else [0, N]
+    counts = oracle.bag(replacement, ratio, 0, L, seed, off, N)
+    sratio = ratio if bug_compat else subspace_ratio
+    subs = [oracle.subspace(sratio, F, seed + i) for i in range(L)]
+    orf = oracle_forest(X, y, counts, subs, depth, bins, cls, min_inst, min_gain)
+    return forest, orf, ds
+
+
+def test_cpusmall_c1_parity(ctx, cpusmall):
+    """BASELINE config 1: BaggingRegressor(DecisionTreeRegressor) on cpusmall, 10 learners."""
+    X, y = cpusmall
+    forest, orf, _ = _fit_both(ctx, X, y, 10, replacement=True, ratio=1.0, seed=SEED_REG,
+                               depth=5, bins=32, cls=False)
+    assert_forest_equal(forest, orf)
+    pred = nat.predict(ctx, forest, X, nat.AGG_MEAN)
+    np.testing.assert_allclose(pred, oracle.predict(orf, X), rtol=1e-5, atol=0)
+
+
+def test_cpusmall_reference_grid_point(ctx, cpusmall):
+    """One CV grid point of BaggingRegressorSuite.scala:30-38 (depth 10, bins 30, ratio 0.7)."""
+    X, y = cpusmall
+    forest, orf, _ = _fit_both(ctx, X, y, 10, replacement=True, ratio=0.7, seed=SEED_REG,
+                               depth=10, bins=30, cls=False)
+    assert_forest_equal(forest, orf)
+    np.testing.assert_allclose(nat.predict(ctx, forest, X, nat.AGG_MEAN), oracle.predict(orf, X),
+                               rtol=1e-5, atol=0)
+
+
+def test_vehicle_c2_parity(ctx, vehicle):
+    """BASELINE config 2: BaggingClassifier on vehicle, 32 learners, subspaceRatio 0.7 (H1: no-op)."""
+    X, y = vehicle
+    forest, orf, _ = _fit_both(ctx, X, y, 32, replacement=False, ratio=1.0, seed=SEED_CLS,
+                               depth=5, bins=32, cls=True, subspace_ratio=0.7)
+    assert_forest_equal(forest, orf)
+    got = nat.predict(ctx, forest, X, nat.AGG_MODE)
+    assert (got == oracle.predict(orf, X, classification=True)).all()
+
+
+def test_vehicle_replacement_ratio07(ctx, vehicle):
+    X, y = vehicle
+    forest, orf, _ = _fit_both(ctx, X, y, 32, replacement=True, ratio=0.7, seed=SEED_CLS,
+                               depth=6, bins=32, cls=True)
+    assert_forest_equal(forest, orf)
+    assert (nat.predict(ctx, forest, X, nat.AGG_MODE) ==
+            oracle.predict(orf, X, classification=True)).all()
+
+
+def test_vehicle_bernoulli_min_instances(ctx, vehicle):
+    X, y = vehicle
+    forest, orf, _ = _fit_both(ctx, X, y, 8, replacement=False, ratio=0.6, seed=SEED_CLS,
+                               depth=7, bins=16, cls=True, min_inst=5, min_gain=0.01)
+    assert_forest_equal(forest, orf)
+
+
+def test_synthetic_partitions_regression(ctx):
+    """Device-generated synthetic data, P=3 partitions (pins per-partition seeding, H4)."""
+    ds = nat.DeviceDataset.synthetic(30000, 20, seed=5, num_classes=0, ctx=ctx)
+    X, y = ds.features(), ds.labels()
+    part = [0, 10000, 17000, 30000]
+    forest = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                     learner_end=6, partition_offsets=part, max_depth=6, max_bins=32)
+    counts = oracle.bag(True, 1.0, 0, 6, SEED_REG, part, 30000)
+    subs = [oracle.subspace(1.0, 20, SEED_REG + i) for i in range(6)]
+    orf = oracle_forest(X, y, counts, subs, 6, 32, False)
+    assert_forest_equal(forest, orf)
+    np.testing.assert_allclose(nat.predict_dataset(ctx, forest, ds, nat.AGG_MEAN),
+                               oracle.predict(orf, X), rtol=1e-5, atol=0)
+
+
+def test_synthetic_classification_subspace(ctx):
+    ds = nat.DeviceDataset.synthetic(20000, 24, seed=11, num_classes=7, ctx=ctx)
+    X, y = ds.features(), ds.labels()
+    forest = nat.fit(ctx, ds, replacement=False, sample_ratio=0.5, seed=SEED_CLS, learner_begin=0,
+                     learner_end=5, max_depth=8, max_bins=32, impurity=nat.IMPURITY_GINI)
+    counts = oracle.bag(False, 0.5, 0, 5, SEED_CLS, [0, 20000], 20000)
+    subs = [oracle.subspace(0.5, 24, SEED_CLS + i) for i in range(5)]
+    orf = oracle_forest(X, y, counts, subs, 8, 32, True)
+    assert_forest_equal(forest, orf)
+    assert (nat.predict_dataset(ctx, forest, ds, nat.AGG_MODE) ==
+            oracle.predict(orf, X, classification=True)).all()
