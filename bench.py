@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--learners", type=int, default=128, help="learners per GPU")
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--bins", type=int, default=32)
-    ap.add_argument("--partitions", type=int, default=64)
+    ap.add_argument("--partitions", type=int, default=128)
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--cpu-learners", type=int, default=16)

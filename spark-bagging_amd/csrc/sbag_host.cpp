@@ -770,34 +770,63 @@ int sbag_dataset_free(sbag_dataset* ds) {
 
 // ---------------------------------------------------------------- fit
 struct HistGeom {
-  int T, FT, FPH, FPW, ntiles;
+  int T, FT, FPH, ntiles;
   size_t lds;
 };
+
+static int roundup(int x, int a) { return (x + a - 1) / a * a; }
 
 static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g) {
   g.T = std::max(16, std::min(128, 16384 / S));
   const int align = gini_layout ? 32 : 16;
-  const size_t per_feat = gini_layout ? (size_t)NS * NB * 4 : (size_t)2 * NB * 8;
-  const size_t fixed = (size_t)g.T * S + (size_t)g.T * 25 + 1024;
   auto lds_for = [&](int ft) {
-    const int fph = (ft + align - 1) / align * align;
-    return ((per_feat * fph + 15) & ~(size_t)15) + fixed + (size_t)ft * 2;
+    return hist_lds_bytes(S, g.T, NB, NS, roundup(ft, align), gini_layout);
   };
-  int cap_ft = std::min(256, (Fmax + align - 1) / align * align);
-  int ft = cap_ft;
+  int ft = std::min(256, roundup(Fmax, align));
   const size_t soft = 80 * 1024, hard = 160 * 1024 - 256;
   while (ft > align && lds_for(ft) > soft) ft -= align;
-  if (lds_for(ft) > soft) {  // even one aligned tile over budget: allow up to the whole LDS
-    if (lds_for(ft) > hard) return false;
-  }
+  if (lds_for(ft) > hard) return false;
   g.FT = std::min(ft, Fmax);
-  ft = g.FT;
-  g.FPH = (g.FT + align - 1) / align * align;
-  g.FPW = 1;
-  while (g.FPW < g.FT) g.FPW <<= 1;
+  g.FPH = roundup(g.FT, align);
   g.ntiles = (Fmax + g.FT - 1) / g.FT;
   g.lds = lds_for(g.FT);
   return true;
+}
+
+// Work of one histogram launch: pieces (slices of parent segments, parent order)
+// and a balanced contiguous piece range per workgroup.
+struct HistWork {
+  std::vector<HistChunk> pieces;
+  std::vector<int32_t> wg;
+  int nwg = 0;
+  double entries = 0;
+};
+
+static void build_work(const std::vector<std::pair<int64_t, int64_t>>& segs, int64_t ps_max,
+                       int nwg_max, int T, HistWork& w) {
+  int64_t tot = 0;
+  for (auto& s : segs) tot += s.second - s.first;
+  int64_t ps = tot / std::max<int64_t>(1, 2 * (int64_t)nwg_max);
+  ps = std::max<int64_t>(T, std::min<int64_t>(ps_max, (ps + T - 1) / T * T));
+  w.pieces.clear();
+  for (size_t q = 0; q < segs.size(); q++)
+    for (int64_t a = segs[q].first; a < segs[q].second; a += ps)
+      w.pieces.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + ps, segs[q].second)});
+  const int np = (int)w.pieces.size();
+  w.nwg = std::max(1, std::min(np, nwg_max));
+  w.wg.assign(w.nwg + 1, np);
+  w.wg[0] = 0;
+  int64_t run = 0;
+  int cur = 0;
+  for (int p = 0; p < np; p++) {
+    const int64_t len = w.pieces[p].b - w.pieces[p].a;
+    int target = tot > 0 ? (int)(((double)run + 0.5 * len) * w.nwg / (double)tot) : 0;
+    target = std::min(std::max(target, cur), w.nwg - 1);
+    while (cur < target) w.wg[++cur] = p;
+    run += len;
+  }
+  while (cur < w.nwg) w.wg[++cur] = np;
+  w.entries = (double)tot;
 }
 
 int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
@@ -848,18 +877,6 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     sub[r] = idx;
     Fmax = std::max(Fmax, n);
   }
-  // ---- fixed-point label packing limits
-  const int64_t K0 = -ds->kmin;
-  const int64_t kspan = ds->kmax - ds->kmin + 1;
-  const int64_t kabs = std::max(std::llabs(ds->kmin), std::llabs(ds->kmax));
-  int64_t ch_cap = 16384;
-  if (!gini) {
-    while (ch_cap > 16 && (double)ch_cap * 255.0 * (double)kspan >= std::ldexp(1.0, 40)) ch_cap /= 2;
-    if ((double)ch_cap * 255.0 * (double)kspan >= std::ldexp(1.0, 40))
-      return fail(SBAG_EUNSUPPORTED, "label range too wide for the packed LDS histogram");
-    if ((double)N * 255.0 * (double)kabs * (double)kabs >= std::ldexp(1.0, 53))
-      return fail(SBAG_EUNSUPPORTED, "sum of squared labels would exceed 2^53 (not exact in fp64)");
-  }
   auto forest = std::make_unique<sbag_forest>();
   forest->impurity = tp.impurity;
   EventTimer tm{c->stream, {}};
@@ -881,27 +898,50 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   uint64_t *entA, *entB;
   TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
   TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
-  unsigned long long *d_inbag, *d_wsum;
-  TRY(ws_typed(c, "inbag", (size_t)R * 2, &d_inbag));
-  d_wsum = d_inbag + R;
-  HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 16, c->stream));
+  unsigned long long* d_inbag;
+  TRY(ws_typed(c, "inbag", (size_t)R * 3, &d_inbag));
+  unsigned long long* d_wsum = d_inbag + R;
+  unsigned int* d_cmax = (unsigned int*)(d_inbag + 2 * R);
+  HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 24, c->stream));
   {
     int h = tm.begin(T_COMPACT);
-    launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum);
+    launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax);
     HIP_TRY(hipGetLastError());
     tm.end(h);
   }
-  std::vector<unsigned long long> inbag(2 * R);
-  TRY(d2h(c, inbag.data(), d_inbag, (size_t)2 * R));
+  std::vector<unsigned long long> inbag(3 * R);
+  TRY(d2h(c, inbag.data(), d_inbag, (size_t)3 * R));
   std::vector<int64_t> nw(R);
+  unsigned int cmax = 1;
   for (int r = 0; r < R; r++) {
     nw[r] = (int64_t)inbag[R + r];
+    cmax = std::max(cmax, ((const unsigned int*)(inbag.data() + 2 * R))[r]);
     if (nw[r] == 0)
       return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
                                "empty one (learner " + std::to_string(lb + r) + ")");
     if (gini && (double)nw[r] >= 4294967295.0)
       return fail(SBAG_EUNSUPPORTED, "class counts exceed 32 bits");
   }
+  // ---- LDS packing: count field at bit cshift, flush_limit entries between flushes
+  const int64_t K0 = -ds->kmin;
+  const double kspan = (double)(ds->kmax - ds->kmin + 1);
+  const double kabs = (double)std::max(std::llabs(ds->kmin), std::llabs(ds->kmax));
+  int64_t flush_limit = (int64_t)1 << 22;
+  int cshift = 40;
+  for (;; flush_limit /= 2) {
+    if (flush_limit < 256)
+      return fail(SBAG_EUNSUPPORTED, "label range too wide for the packed LDS histogram");
+    const double wmax = (double)flush_limit * cmax;
+    if (gini) {
+      if (wmax < 4294967295.0) break;
+      continue;
+    }
+    cshift = (int)std::ceil(std::log2(wmax * kspan + 1.0));
+    const int cbits = 64 - cshift;
+    if (cbits >= 1 && std::ldexp(1.0, cbits) > wmax && wmax * kabs * kabs < 1.8e19) break;
+  }
+  if (!gini && (double)N * cmax * kabs * kabs >= std::ldexp(1.0, 53))
+    return fail(SBAG_EUNSUPPORTED, "sum of squared labels would exceed 2^53 (not exact in fp64)");
 
   // ---- per-replica tables
   std::vector<int32_t> h_sub((size_t)R * Fmax, 0), h_Fr(R);
@@ -925,78 +965,140 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     vcoff[(size_t)R * Fmax] = o;
   }
   const int64_t vc_total = vcoff[(size_t)R * Fmax];
+  int ncmax = 0;
+  for (int f = 0; f < F; f++) ncmax = std::max(ncmax, (int)ds->dict[f].size());
 
   // root "parents": one per replica, no routing, histogram slot = replica
   std::vector<ParentInfo> h_par(R);
-  std::vector<HistChunk> h_chunks;
-  std::vector<std::pair<int64_t, int64_t>> seg(R);  // current-level segments per slot
+  std::vector<std::pair<int64_t, int64_t>> seg(R);
   for (int r = 0; r < R; r++) {
     h_par[r] = ParentInfo{r, -1, 0, 0, 0, r, 0, 0};
     seg[r] = {(int64_t)r * cap, (int64_t)r * cap + (int64_t)inbag[r]};
   }
-  auto make_chunks = [&](const std::vector<std::pair<int64_t, int64_t>>& segs,
-                         const std::vector<int>& which, int T, std::vector<HistChunk>& chunks) {
-    int64_t tot = 0;
-    for (int i : which) tot += segs[i].second - segs[i].first;
-    int64_t ch = std::max<int64_t>(T, std::min<int64_t>(ch_cap, (tot / 4096 + T - 1) / T * T));
-    chunks.clear();
-    for (int i : which)
-      for (int64_t a = segs[i].first; a < segs[i].second; a += ch)
-        chunks.push_back(HistChunk{i, 0, a, std::min(a + ch, segs[i].second)});
-  };
+  const int NS = gini ? (int)ds->kmax + 1 : 3;
+  const size_t word_bytes = gini ? 4 : 8;
+  HistWork work;
   ParentInfo* d_par;
-  HistChunk* d_chunks;
+  HistChunk* d_pieces;
+  int32_t* d_wg;
+  auto upload_work = [&](const std::vector<ParentInfo>& par) -> int {
+    TRY(ws_typed(c, "par", std::max<size_t>(par.size(), 1), &d_par));
+    TRY(h2d(c, d_par, par.data(), par.size()));
+    TRY(ws_typed(c, "pieces", std::max<size_t>(work.pieces.size(), 1), &d_pieces));
+    TRY(h2d(c, d_pieces, work.pieces.data(), work.pieces.size()));
+    TRY(ws_typed(c, "wgp", work.wg.size(), &d_wg));
+    TRY(h2d(c, d_wg, work.wg.data(), work.wg.size()));
+    return SBAG_OK;
+  };
+  HistArgs ha{};
+  ha.Fmax = Fmax;
+  ha.Fr = d_Fr;
+  ha.K0 = (int32_t)K0;
+  ha.cshift = cshift;
+  ha.flush_limit = flush_limit;
+  double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0;
+  int64_t hist_launches = 0;
+  auto launch = [&](const HistGeom& g, bool gini_layout, int cat,
+                    const std::vector<std::pair<int64_t, int64_t>>& segs,
+                    const std::vector<ParentInfo>& par) -> int {
+    const int wpc = std::max(1, std::min(8, (int)((160 * 1024) / g.lds)));
+    build_work(segs, flush_limit, 256 * wpc, g.T, work);
+    TRY(upload_work(par));
+    ha.chunks = d_pieces;
+    ha.wg_piece = d_wg;
+    ha.parents = d_par;
+    ha.T = g.T;
+    ha.FT = g.FT;
+    ha.FPH = g.FPH;
+    int h = tm.begin(cat);
+    launch_hist(c->stream, ha, work.nwg, g.ntiles, gini_layout, g.lds);
+    HIP_TRY(hipGetLastError());
+    tm.end(h);
+    if (cat == T_HIST) {
+      hist_launches++;
+      for (size_t q = 0; q < segs.size(); q++) {
+        const double ne = (double)(segs[q].second - segs[q].first);
+        hist_entries += ne;
+        hist_alg_bytes += ne * (h_Fr[par[q].r] + 4);
+      }
+    }
+    return SBAG_OK;
+  };
 
-  // ---- 3. value counts per (replica, local feature, code)
+  // ---- 3. value counts -> thresholds.  Optimistic path: when every feature has
+  // at most maxBins distinct values, histogram the root over the value codes
+  // directly; its count stats ARE the value counts, and if every replica's
+  // thresholds turn out to be all midpoints (code == bin) that root histogram is
+  // already the level-0 histogram.
+  void* hist_cur;
+  TRY(ws_get(c, "histA", (size_t)R * Fmax * std::max(ncmax, tp.max_bins) * NS * word_bytes, &hist_cur));
+  std::vector<int16_t> h_pos_codes((size_t)R * Fmax, 0);
+  for (int r = 0; r < R; r++)
+    for (int fl = 0; fl < h_Fr[r]; fl++) h_pos_codes[(size_t)r * Fmax + fl] = (int16_t)sub[r][fl];
+  int16_t* d_pos;
+  TRY(ws_typed(c, "pos", h_pos_codes.size(), &d_pos));
+  TRY(h2d(c, d_pos, h_pos_codes.data(), h_pos_codes.size()));
   std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1), 0);
-  {
+  const bool optimistic = ds->code_bytes == 1 && ncmax <= tp.max_bins;
+  bool root_done = false;
+  HistGeom g0{};
+  if (optimistic) {
+    if (!hist_geometry(ds->S, Fmax, ncmax, NS, gini, g0))
+      return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
+    HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * Fmax * ncmax * NS * word_bytes, c->stream));
+    ha.bins = (const uint8_t*)ds->d_codes;
+    ha.bins_rstride = 0;
+    ha.S = ds->S;
+    ha.pos = d_pos;
+    ha.ent_in = entA;
+    ha.ent_out = nullptr;
+    ha.cursors = nullptr;
+    ha.hist = hist_cur;
+    ha.NB = ncmax;
+    ha.NS = NS;
+    ha.do_write = 0;
+    ha.count_only = 0;
+    TRY(launch(g0, gini, T_HIST, seg, h_par));
+    const int64_t words = (int64_t)R * Fmax * ncmax * NS;
+    std::vector<uint8_t> tmp((size_t)words * word_bytes);
+    TRY(d2h(c, tmp.data(), (const uint8_t*)hist_cur, tmp.size()));
+    for (int r = 0; r < R; r++)
+      for (int fl = 0; fl < h_Fr[r]; fl++) {
+        const size_t nc = ds->dict[sub[r][fl]].size();
+        for (size_t k = 0; k < nc; k++) {
+          const int64_t wi = (((int64_t)r * Fmax + fl) * ncmax + (int64_t)k) * NS;
+          uint64_t cnt = 0;
+          if (gini) {
+            for (int q = 0; q < NS; q++) cnt += ((const uint32_t*)tmp.data())[wi + q];
+          } else {
+            cnt = ((const uint64_t*)tmp.data())[wi];
+          }
+          vc[vcoff[(size_t)r * Fmax + fl] + k] = (uint32_t)cnt;
+        }
+      }
+  } else {
     int h = tm.begin(T_VC);
-    int ncmax = 0;
-    for (int f = 0; f < F; f++) ncmax = std::max(ncmax, (int)ds->dict[f].size());
     HistGeom g;
     if (ds->code_bytes == 1 && hist_geometry(ds->S, Fmax, ncmax, 1, true, g)) {
-      // LDS-privatized counting pass (k_hist, count-only layout), codes as bins
-      std::vector<int16_t> h_pos((size_t)R * Fmax, 0);
-      for (int r = 0; r < R; r++)
-        for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)sub[r][fl];
-      int16_t* d_pos;
-      TRY(ws_typed(c, "pos", h_pos.size(), &d_pos));
-      TRY(h2d(c, d_pos, h_pos.data(), h_pos.size()));
-      std::vector<int> all(R);
-      for (int r = 0; r < R; r++) all[r] = r;
-      make_chunks(seg, all, g.T, h_chunks);
-      TRY(ws_typed(c, "par", (size_t)R, &d_par));
-      TRY(h2d(c, d_par, h_par.data(), (size_t)R));
-      TRY(ws_typed(c, "chunks", h_chunks.size(), &d_chunks));
-      TRY(h2d(c, d_chunks, h_chunks.data(), h_chunks.size()));
       const int64_t slot_words = (int64_t)Fmax * ncmax;
       uint32_t* d_vch;
       TRY(ws_typed(c, "vch", (size_t)R * slot_words, &d_vch));
       HIP_TRY(hipMemsetAsync(d_vch, 0, (size_t)R * slot_words * 4, c->stream));
-      HistArgs a{};
-      a.bins = (const uint8_t*)ds->d_codes;
-      a.bins_rstride = 0;
-      a.S = ds->S;
-      a.Fmax = Fmax;
-      a.pos = d_pos;
-      a.Fr = d_Fr;
-      a.chunks = d_chunks;
-      a.parents = d_par;
-      a.ent_in = entA;
-      a.ent_out = nullptr;
-      a.cursors = nullptr;
-      a.hist = d_vch;
-      a.NB = ncmax;
-      a.NS = 1;
-      a.K0 = 0;
-      a.FT = g.FT;
-      a.FPH = g.FPH;
-      a.FPW = g.FPW;
-      a.T = g.T;
-      a.do_write = 0;
-      a.count_only = 1;
-      launch_hist(c->stream, a, (int)h_chunks.size(), g.ntiles, true, g.lds);
-      HIP_TRY(hipGetLastError());
+      HistArgs save = ha;
+      ha.bins = (const uint8_t*)ds->d_codes;
+      ha.bins_rstride = 0;
+      ha.S = ds->S;
+      ha.pos = d_pos;
+      ha.ent_in = entA;
+      ha.ent_out = nullptr;
+      ha.cursors = nullptr;
+      ha.hist = d_vch;
+      ha.NB = ncmax;
+      ha.NS = 1;
+      ha.do_write = 0;
+      ha.count_only = 1;
+      TRY(launch(g, true, T_VC, seg, h_par));
+      ha = save;
       std::vector<uint32_t> tmp((size_t)R * slot_words);
       TRY(d2h(c, tmp.data(), d_vch, tmp.size()));
       for (int r = 0; r < R; r++)
@@ -1047,6 +1149,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       if ((int)d.size() > nt + 1) identity = false;
     }
   }
+  if (optimistic && identity) {
+    NB = ncmax;  // the codes-as-bins root histogram already has this layout
+    root_done = true;
+  }
   // per global feature: is the LUT the same for every replica that uses it?
   bool shared = true;
   {
@@ -1075,12 +1181,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     if (identity) {
       d_bins = (const uint8_t*)ds->d_codes;
       S = ds->S;
-      for (int r = 0; r < R; r++)
-        for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)sub[r][fl];
+      h_pos = h_pos_codes;
     } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30)) {
       // one bins matrix in global feature coordinates
       S = row_stride(F);
-      std::vector<int64_t> goff(F, 0);
       std::vector<int32_t> gsub(F), gF(1, F);
       for (int g = 0; g < F; g++) gsub[g] = g;
       std::vector<int64_t> gl(F + 1, 0);
@@ -1108,8 +1212,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
                          d_lutoff, d_b, S);
       HIP_TRY(hipGetLastError());
       d_bins = d_b;
-      for (int r = 0; r < R; r++)
-        for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)sub[r][fl];
+      h_pos = h_pos_codes;
     } else {
       S = row_stride(Fmax);
       if ((double)R * N * S > 48.0 * (1ull << 30))
@@ -1131,7 +1234,6 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     }
     tm.end(h);
   }
-  int16_t* d_pos;
   int32_t* d_nbins;
   TRY(ws_typed(c, "pos", h_pos.size(), &d_pos));
   TRY(ws_typed(c, "nbins", h_nbins.size(), &d_nbins));
@@ -1139,67 +1241,32 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   TRY(h2d(c, d_nbins, h_nbins.data(), h_nbins.size()));
 
   // ---- 6. level-wise growth
-  int NS = 3;
-  if (gini) NS = (int)ds->kmax + 1;
   HistGeom g;
   if (!hist_geometry(S, Fmax, NB, NS, gini, g))
     return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
   const int64_t slot_words = (int64_t)Fmax * NB * NS;
-  const size_t word_bytes = gini ? 4 : 8;
   std::vector<std::vector<HNode>> trees(R);
   std::vector<std::pair<int, int>> slots(R);  // (replica, node index)
   for (int r = 0; r < R; r++) {
     trees[r].push_back(HNode{});
     slots[r] = {r, 0};
   }
-  // level 0 histograms: virtual parents (h_par, seg) already set
-  void* hist_cur;
-  {
-    std::string nm = "histA";
-    TRY(ws_get(c, nm, (size_t)R * slot_words * word_bytes, &hist_cur));
-  }
-  HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * slot_words * word_bytes, c->stream));
-  std::vector<int> all(R);
-  for (int r = 0; r < R; r++) all[r] = r;
-  make_chunks(seg, all, g.T, h_chunks);
-  TRY(ws_typed(c, "par", (size_t)R, &d_par));
-  TRY(h2d(c, d_par, h_par.data(), (size_t)R));
-  TRY(ws_typed(c, "chunks", h_chunks.size(), &d_chunks));
-  TRY(h2d(c, d_chunks, h_chunks.data(), h_chunks.size()));
-  HistArgs ha{};
   ha.bins = d_bins;
   ha.bins_rstride = bins_rstride;
   ha.S = S;
-  ha.Fmax = Fmax;
   ha.pos = d_pos;
-  ha.Fr = d_Fr;
   ha.NB = NB;
   ha.NS = NS;
-  ha.K0 = (int32_t)K0;
-  ha.FT = g.FT;
-  ha.FPH = g.FPH;
-  ha.FPW = g.FPW;
-  ha.T = g.T;
   ha.count_only = 0;
-  double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0;
-  int64_t hist_launches = 0;
-  {
-    ha.chunks = d_chunks;
-    ha.parents = d_par;
+  if (!root_done) {
+    TRY(ws_get(c, "histA", (size_t)R * slot_words * word_bytes, &hist_cur));
+    HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * slot_words * word_bytes, c->stream));
     ha.ent_in = entA;
     ha.ent_out = nullptr;
     ha.cursors = nullptr;
     ha.hist = hist_cur;
     ha.do_write = 0;
-    int h = tm.begin(T_HIST);
-    launch_hist(c->stream, ha, (int)h_chunks.size(), g.ntiles, gini, g.lds);
-    HIP_TRY(hipGetLastError());
-    tm.end(h);
-    hist_launches++;
-    for (int r = 0; r < R; r++) {
-      hist_entries += (double)inbag[r];
-      hist_alg_bytes += (double)inbag[r] * (h_Fr[r] + 4);
-    }
+    TRY(launch(g, gini, T_HIST, seg, h_par));
   }
   for (int r = 0; r < R; r++) hist_upper += (double)inbag[r] * (h_Fr[r] + 4) * D + 3.0 * N * D;
   const double inv_scale = std::ldexp(1.0, -ds->shift), inv_scale2 = std::ldexp(1.0, -2 * ds->shift);
@@ -1251,9 +1318,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     std::vector<std::pair<int, int>> next_slots;
     std::vector<int32_t> triples;
     struct Pending {
-      int r, node, side, parent;
+      int side, parent;
     };
-    std::vector<Pending> pend;  // next-level slot -> (replica, child node, side, parent index)
+    std::vector<Pending> pend;
     for (int i = 0; i < M; i++) {
       const int r = slots[i].first;
       const int ni = slots[i].second;
@@ -1307,12 +1374,12 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       if (wl) {
         sl = (int)next_slots.size();
         next_slots.push_back({r, li});
-        pend.push_back({r, li, 0, pidx});
+        pend.push_back({0, pidx});
       }
       if (wr) {
         sr = (int)next_slots.size();
         next_slots.push_back({r, li + 1});
-        pend.push_back({r, li + 1, 1, pidx});
+        pend.push_back({1, pidx});
       }
       if (wl && wr) {
         const int64_t lc = Calc{lef, NS, gini, ds->shift}.count();
@@ -1345,32 +1412,12 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     unsigned long long* d_cur;
     TRY(ws_typed(c, "cursors", cur.size(), &d_cur));
     TRY(h2d(c, d_cur, cur.data(), cur.size()));
-    std::vector<int> allp(NP);
-    for (int q = 0; q < NP; q++) allp[q] = q;
-    make_chunks(pseg, allp, g.T, h_chunks);
-    TRY(ws_typed(c, "par", (size_t)NP, &d_par));
-    TRY(h2d(c, d_par, par.data(), (size_t)NP));
-    TRY(ws_typed(c, "chunks", h_chunks.size(), &d_chunks));
-    TRY(h2d(c, d_chunks, h_chunks.data(), h_chunks.size()));
-    ha.chunks = d_chunks;
-    ha.parents = d_par;
     ha.ent_in = ent_cur;
     ha.ent_out = ent_nxt;
     ha.cursors = d_cur;
     ha.hist = hist_nxt;
     ha.do_write = 1;
-    {
-      int h = tm.begin(T_HIST);
-      launch_hist(c->stream, ha, (int)h_chunks.size(), g.ntiles, gini, g.lds);
-      HIP_TRY(hipGetLastError());
-      tm.end(h);
-      hist_launches++;
-      for (int q = 0; q < NP; q++) {
-        const double ne = (double)(pseg[q].second - pseg[q].first);
-        hist_entries += ne;
-        hist_alg_bytes += ne * (h_Fr[par[q].r] + 4);
-      }
-    }
+    TRY(launch(g, gini, T_HIST, pseg, par));
     if (!triples.empty()) {
       int32_t* d_tri;
       TRY(ws_typed(c, "triples", triples.size(), &d_tri));

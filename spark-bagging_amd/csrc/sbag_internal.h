@@ -38,7 +38,8 @@ struct HistArgs {
   int32_t Fmax;
   const int16_t* pos;    // [R][Fmax] byte position of local feature fl in a row
   const int32_t* Fr;     // [R]
-  const HistChunk* chunks;
+  const HistChunk* chunks;   // pieces: slices of parent segments, in parent order
+  const int32_t* wg_piece;   // [nwg + 1]: workgroup w walks pieces [wg_piece[w], wg_piece[w+1])
   const ParentInfo* parents;
   const uint64_t* ent_in;
   uint64_t* ent_out;
@@ -46,6 +47,8 @@ struct HistArgs {
   void* hist;            // [slot][Fmax][NB][NS] u64 (variance) or u32 (gini / counts)
   int32_t NB, NS;
   int32_t K0;            // label offset for the packed LDS word (variance)
+  int32_t cshift;        // bit position of the count field in the packed word
+  int64_t flush_limit;   // max entries accumulated in LDS between flushes
   int32_t FT, FPH, FPW;  // features per tile, LDS pitch, thread-feature width (pow2)
   int32_t T;             // rows per tile
   int32_t do_write;      // route + write entries (levels > 0)
@@ -90,9 +93,10 @@ void launch_bernoulli(hipStream_t st, uint8_t* counts, int64_t N, const int64_t*
 void launch_fill(hipStream_t st, uint8_t* p, uint8_t v, int64_t n);
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
-                    unsigned long long* d_wsum);
-void launch_hist(hipStream_t st, const HistArgs& a, int nchunks, int ntiles, bool gini,
+                    unsigned long long* d_wsum, unsigned int* d_cmax);
+void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gini,
                  size_t lds_bytes);
+size_t hist_lds_bytes(int S, int T, int NB, int NS, int FPH, bool gini);
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini);
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words);

@@ -37,32 +37,15 @@ namespace sbag {
 // advance their generators in lockstep so the ring index is wave-uniform and
 // every LDS access is conflict-free ([position][lane] layout).
 // ======================================================================
-__device__ __forceinline__ uint32_t well_step(uint32_t* st, int lane, int& index, uint32_t& v0) {
-  const int i = index;
-  const int rm1 = (i == 0) ? 623 : i - 1;
-  const int rm2 = (i <= 1) ? i + 622 : i - 2;
-  const int i1 = (i + 70 >= 624) ? i + 70 - 624 : i + 70;
-  const int i2 = (i + 179 >= 624) ? i + 179 - 624 : i + 179;
-  const int i3 = (i + 449 >= 624) ? i + 449 - 624 : i + 449;
-  const uint32_t vm1 = st[i1 * 64 + lane];
-  const uint32_t vm2 = st[i2 * 64 + lane];
-  const uint32_t vm3 = st[i3 * 64 + lane];
-  const uint32_t vr1 = st[rm1 * 64 + lane];
-  const uint32_t vr2 = st[rm2 * 64 + lane];
-  const uint32_t z0 = (0x80000000u & vr1) ^ (0x7FFFFFFFu & vr2);
-  const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (vm1 ^ (vm1 >> 27));
-  const uint32_t z2 = (vm2 >> 9) ^ (vm3 ^ (vm3 >> 1));
-  const uint32_t z3 = z1 ^ z2;
-  uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
-  st[i * 64 + lane] = z3;
-  st[rm1 * 64 + lane] = z4;
-  st[rm2 * 64 + lane] = vr2 & 0x80000000u;
-  index = rm1;
-  v0 = z4;
-  z4 ^= (z4 << 7) & 0xe46e1700u;
-  z4 ^= (z4 << 15) & 0x9b868000u;
-  return z4;
-}
+// Well19937c runs its ring index downwards one slot per step.  Within a batch of
+// WB <= 69 consecutive steps starting at index i, every value read (v[i-t+70],
+// v[i-t+179], v[i-t+449], the high bit of v[i-t-1], the low bits of v[i-t-2])
+// was written before the batch, so all 5*WB LDS reads are issued up front; the
+// batch then leaves v[i-t] = z3_t (t < WB), v[i-WB] = z4_{WB-1} and the masked
+// v[i-WB-1] -- the same state the sequential recurrence leaves.
+constexpr int kWB = 16;
+
+__device__ __forceinline__ int wrap624(int x) { return x < 0 ? x + 624 : (x >= 624 ? x - 624 : x); }
 
 __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, int64_t N,
                                                 const int64_t* __restrict__ part_off, int P, int R,
@@ -95,24 +78,53 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
   int n = 0, bad = 0;
   double racc = 1.0;
   while (__any(row < row_end)) {
-    const uint32_t a = well_step(st, lane, index, v0) >> 6;  // next(26)
-    const uint32_t b = well_step(st, lane, index, v0) >> 6;
-    const double u = (double)((((uint64_t)a) << 26) | (uint64_t)b) * 0x1.0p-52;
-    if (row < row_end) {
-      racc *= u;
-      bool emit;
-      if (racc >= p_exp) {
-        n++;
-        emit = !((double)n < cap);
-      } else {
-        emit = true;
-      }
-      if (emit) {
-        if (n > 255) bad = 1;
-        out[row] = (uint8_t)(n > 255 ? 255 : n);
-        row++;
-        n = 0;
-        racc = 1.0;
+    uint32_t m1[kWB], m2[kWB], m3[kWB], hb[kWB], lo[kWB], z3v[kWB], o[kWB];
+#pragma unroll
+    for (int t = 0; t < kWB; t++) {
+      const int i = wrap624(index - t);
+      m1[t] = st[wrap624(i + 70) * 64 + lane];
+      m2[t] = st[wrap624(i + 179) * 64 + lane];
+      m3[t] = st[wrap624(i + 449 - 624) * 64 + lane];
+      hb[t] = st[wrap624(i - 1) * 64 + lane];
+      lo[t] = st[wrap624(i - 2) * 64 + lane];
+    }
+#pragma unroll
+    for (int t = 0; t < kWB; t++) {
+      const uint32_t z0 = (0x80000000u & hb[t]) ^ (0x7FFFFFFFu & lo[t]);
+      const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1[t] ^ (m1[t] >> 27));
+      const uint32_t z2 = (m2[t] >> 9) ^ (m3[t] ^ (m3[t] >> 1));
+      const uint32_t z3 = z1 ^ z2;
+      uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
+      z3v[t] = z3;
+      v0 = z4;
+      z4 ^= (z4 << 7) & 0xe46e1700u;
+      z4 ^= (z4 << 15) & 0x9b868000u;
+      o[t] = z4 >> 6;  // next(26)
+    }
+#pragma unroll
+    for (int t = 0; t < kWB; t++) st[wrap624(index - t) * 64 + lane] = z3v[t];
+    st[wrap624(index - kWB) * 64 + lane] = v0;
+    st[wrap624(index - kWB - 1) * 64 + lane] = lo[kWB - 1] & 0x80000000u;
+    index = wrap624(index - kWB);
+#pragma unroll
+    for (int u = 0; u < kWB / 2; u++) {
+      const double x = (double)((((uint64_t)o[2 * u]) << 26) | (uint64_t)o[2 * u + 1]) * 0x1.0p-52;
+      if (row < row_end) {
+        racc *= x;
+        bool emit;
+        if (racc >= p_exp) {
+          n++;
+          emit = !((double)n < cap);
+        } else {
+          emit = true;
+        }
+        if (emit) {
+          if (n > 255) bad = 1;
+          out[row] = (uint8_t)(n > 255 ? 255 : n);
+          row++;
+          n = 0;
+          racc = 1.0;
+        }
       }
     }
   }
@@ -249,197 +261,141 @@ void launch_fill(hipStream_t st, uint8_t* p, uint8_t v, int64_t n) {
 }
 
 // ======================================================================
-// In-bag compaction: entries of rows with count > 0, one wave-ballot + one
-// atomic per wave.  Order inside a segment is irrelevant (integer stats).
+// In-bag compaction: entries of rows with count > 0.  A block owns 8192 rows of
+// one replica (replicas interleaved over the grid so concurrent blocks hit
+// different cursors); per 1024 rows a block-wide scan and ONE atomic reserve the
+// output slots.  Order inside a segment is irrelevant (integer stats).  Also
+// reports the weighted row count and the largest count per replica.
 // ======================================================================
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ counts, int64_t N,
                                                  const int32_t* __restrict__ labk,
                                                  uint64_t* __restrict__ ent, int64_t cap,
                                                  unsigned long long* cursor,
-                                                 unsigned long long* wsum) {
-  const int r = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  unsigned long long mysum = 0;
+                                                 unsigned long long* wsum, unsigned int* cmax,
+                                                 int R) {
+  const int r = blockIdx.x % R;
+  const int64_t chunk = blockIdx.x / R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ int s_wave[4];
+  __shared__ unsigned long long s_base;
+  __shared__ unsigned long long s_red[4];
+  __shared__ unsigned int s_max[4];
   const uint8_t* cr = counts + (int64_t)r * N;
   uint64_t* er = ent + (int64_t)r * cap;
-  for (int k = 0; k < 4; k++) {
-    const int64_t row = (int64_t)blockIdx.x * 1024 + k * 256 + threadIdx.x;
-    const uint32_t c = (row < N) ? cr[row] : 0;
-    mysum += c;
-    const uint64_t m = __ballot(c > 0);
-    unsigned long long base = 0;
-    if (lane == 0 && m) base = atomicAdd(&cursor[r], (unsigned long long)__popcll(m));
-    base = __shfl(base, 0);
-    if (c) er[base + __popcll(m & lt)] = pack_entry((uint32_t)row, labk[row], c);
-  }
-  __shared__ unsigned long long red[256];
-  red[threadIdx.x] = mysum;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+  unsigned long long mysum = 0;
+  unsigned int mymax = 0;
+  for (int it = 0; it < 8; it++) {
+    const int64_t row0 = chunk * 8192 + (int64_t)it * 1024 + (int64_t)tid * 4;
+    uint32_t c[4];
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      c[j] = (row0 + j < N) ? cr[row0 + j] : 0u;
+      n += c[j] ? 1 : 0;
+      mysum += c[j];
+      mymax = max(mymax, c[j]);
+    }
+    const int incl = wave_incl_scan(n, lane);
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < 4; w++) {
+      if (w < wave) before += s_wave[w];
+      total += s_wave[w];
+    }
+    if (tid == 0) s_base = total ? atomicAdd(&cursor[r], (unsigned long long)total) : 0ull;
+    __syncthreads();
+    unsigned long long pos = s_base + (unsigned long long)(before + incl - n);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (c[j]) er[pos++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
     __syncthreads();
   }
-  if (threadIdx.x == 0 && red[0]) atomicAdd(&wsum[r], red[0]);
+  for (int o = 32; o > 0; o >>= 1) {
+    mysum += __shfl_down(mysum, o);
+    mymax = max(mymax, (unsigned int)__shfl_down((int)mymax, o));
+  }
+  if (lane == 0) {
+    s_red[wave] = mysum;
+    s_max[wave] = mymax;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned long long s = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    const unsigned int m = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+    if (s) atomicAdd(&wsum[r], s);
+    if (m) atomicMax(&cmax[r], m);
+  }
 }
 
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
-                    unsigned long long* d_wsum) {
-  dim3 grid((unsigned)((N + 1023) / 1024), (unsigned)R);
-  hipLaunchKernelGGL(k_compact, grid, dim3(256), 0, st, counts, N, d_labk, ent, cap, d_cursor,
-                     d_wsum);
+                    unsigned long long* d_wsum, unsigned int* d_cmax) {
+  const int64_t chunks = (N + 8191) / 8192;
+  hipLaunchKernelGGL(k_compact, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, d_labk,
+                     ent, cap, d_cursor, d_wsum, d_cmax, R);
 }
 
 // ======================================================================
-// Fused route + histogram.  One workgroup = one chunk of a parent's entry
-// segment x one feature tile.  Per tile of T rows: entries -> LDS, gather the
-// rows' bins (16 B per lane) -> LDS, route each row by the parent's split and
-// append it to its child's segment (wave ballot, one atomic per wave and side),
-// then accumulate the histogram child in LDS with per-thread-fixed feature
-// lanes ([word][bin][feature] layout: lanes of a 16/32-lane group touch
-// distinct banks whatever the bins are).  Variance stats are packed into two
-// u64 LDS words: (count << 40) + count*(k + K0) and count*k^2 (integer, hence
-// order-independent and bit-exact).  Flush: global u64/u32 atomics.
+// Fused route + histogram (the hot kernel).
+//
+// Grid: (workgroups, feature tiles).  Workgroup w walks the pieces
+// [wg_piece[w], wg_piece[w+1]) -- contiguous slices of parent segments, in
+// parent order -- and keeps the histogram of the current parent's child in LDS
+// until the parent changes (or flush_limit entries were added), so a flush of
+// Fr x NB bins happens once per (workgroup, parent run), not per tile.
+// Per tile of T entries the loop is software-pipelined:
+//   top:  staged rows of tile t (registers) -> LDS, split byte captured by the
+//         lane holding it; entries of tile t+1 -> LDS; weights of tile t
+//   B1:   issue the 16-B gathers of tile t+1's rows and the loads of tile t+2's
+//         entries (in flight during the LDS work below)
+//         route tile t: left/right by the parent's split, append to the child
+//         segments (wave ballot, one global atomic per wave and side), compact
+//         the entries of the histogram child into s_list
+//   B2:   wave-per-entry accumulation: lane -> feature, [word][bin][feature]
+//         layout so every lane group hits distinct banks whatever the bins
+//   B3
+// Variance stats are two u64 words per (bin, feature): (count << cshift) +
+// count*(k + K0) and count*k^2 -- integers, so the result is order-independent
+// and bit-exact; the field split `cshift` and flush_limit are chosen on the host
+// from the label range and the largest count.
 // ======================================================================
 static __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 template <bool GINI>
-__global__ __launch_bounds__(256) void k_hist(HistArgs A) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const HistChunk ch = A.chunks[blockIdx.x];
-  const ParentInfo pi = A.parents[ch.parent];
-  const int r = pi.r;
-  const int Fr = A.Fr[r];
-  const int ft0 = blockIdx.y * A.FT;
-  const int ftn = min(A.FT, Fr - ft0);
-  if (ftn <= 0) return;
-  const bool tile0 = blockIdx.y == 0;
-  const bool do_hist = pi.hist_slot >= 0;
-  const bool do_write = tile0 && A.do_write;
-  if (!do_hist && !do_write) return;
-  const int NB = A.NB, NS = A.NS, FPH = A.FPH, S = A.S, T = A.T;
-
-  const size_t hist_bytes = GINI ? (size_t)NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
-  size_t off = align16(hist_bytes);
-  uint8_t* tile = smem + off;
-  off += align16((size_t)T * S);
-  uint64_t* s_e = (uint64_t*)(smem + off);
-  off += (size_t)T * 8;
-  uint64_t* s_w0 = (uint64_t*)(smem + off);
-  off += (size_t)T * 8;
-  uint64_t* s_w1 = (uint64_t*)(smem + off);
-  off += (size_t)T * 8;
-  int16_t* s_pos = (int16_t*)(smem + off);
-  off += align16((size_t)A.FT * 2);
-  uint8_t* s_flag = smem + off;
-
-  uint64_t* h64 = (uint64_t*)smem;
-  uint32_t* h32 = (uint32_t*)smem;
-  if (do_hist) {
-    for (size_t i = (size_t)tid * 16; i < hist_bytes; i += 256 * 16)
-      *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
-  }
-  for (int i = tid; i < ftn; i += 256) s_pos[i] = A.pos[(int64_t)r * A.Fmax + ft0 + i];
-  __syncthreads();
-
-  const uint8_t* binsr = A.bins + (int64_t)r * A.bins_rstride;
-  const int lpr = S >> 4;
-  const int rpp = 256 / lpr;
-  const int myrow = tid / lpr, mypart = tid - myrow * lpr;
-  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  const int FPW = A.FPW;
-  const int fl = tid & (FPW - 1), g0 = tid / FPW, G = 256 / FPW;
-  const int K0 = A.K0;
-
-  for (int64_t base = ch.a; base < ch.b; base += T) {
-    const int nt = (int)min((int64_t)T, ch.b - base);
-    for (int i = tid; i < nt; i += 256) {
-      const uint64_t e = A.ent_in[base + i];
-      s_e[i] = e;
-      const int32_t hi = (int32_t)(e >> 32);
-      const uint32_t c = (uint32_t)hi & 0xffu;
-      const int32_t k = hi >> 8;
-      if (GINI) {
-        s_w0[i] = A.count_only ? (uint64_t)c : (((uint64_t)(uint32_t)k << 32) | c);
-      } else {
-        s_w0[i] = ((uint64_t)c << 40) + (uint64_t)c * (uint64_t)(int64_t)(k + K0);
-        s_w1[i] = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);
-      }
-    }
-    __syncthreads();
-    if (myrow < rpp) {
-      for (int i = myrow; i < nt; i += rpp) {
-        const uint32_t row = (uint32_t)s_e[i];
-        const uint4 v = *((const uint4*)(binsr + (int64_t)row * S) + mypart);
-        *((uint4*)(tile + (size_t)i * S) + mypart) = v;
-      }
-    }
-    __syncthreads();
-    const int ntr = (nt + 63) & ~63;
-    for (int i = tid; i < ntr; i += 256) {
-      const bool valid = i < nt;
-      int side = 0;
-      if (valid && pi.pos >= 0) side = (tile[(size_t)i * S + pi.pos] <= pi.s) ? 0 : 1;
-      if (do_write) {
-        const bool wl = valid && side == 0 && pi.write_l;
-        const bool wr = valid && side == 1 && pi.write_r;
-        const uint64_t ml = __ballot(wl), mr = __ballot(wr);
-        unsigned long long bl = 0, br = 0;
-        if (lane == 0) {
-          if (ml) bl = atomicAdd(&A.cursors[2 * ch.parent], (unsigned long long)__popcll(ml));
-          if (mr) {
-            const unsigned long long nr = (unsigned long long)__popcll(mr);
-            br = atomicAdd(&A.cursors[2 * ch.parent + 1], (unsigned long long)(-(long long)nr)) - nr;
-          }
-        }
-        bl = __shfl(bl, 0);
-        br = __shfl(br, 0);
-        if (wl) A.ent_out[bl + __popcll(ml & lt)] = s_e[i];
-        if (wr) A.ent_out[br + __popcll(mr & lt)] = s_e[i];
-      }
-      if (valid) s_flag[i] = (do_hist && side == pi.hist_side) ? 1 : 0;
-    }
-    __syncthreads();
-    if (do_hist && fl < ftn) {
-      const int p = s_pos[fl];
-      for (int i = g0; i < nt; i += G) {
-        if (s_flag[i]) {
-          const int b = tile[(size_t)i * S + p];
-          if (GINI) {
-            const uint64_t w = s_w0[i];
-            const int cls = (int)(w >> 32);
-            atomicAdd(&h32[((size_t)cls * NB + b) * FPH + fl], (uint32_t)(w & 0xffffffffu));
-          } else {
-            atomicAdd((unsigned long long*)&h64[(size_t)b * FPH + fl],
-                      (unsigned long long)s_w0[i]);
-            atomicAdd((unsigned long long*)&h64[((size_t)NB + b) * FPH + fl],
-                      (unsigned long long)s_w1[i]);
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (!do_hist) return;
+__device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* smem, int slot,
+                                           int ft0, int ftn) {
+  const int tid = threadIdx.x;
+  const int NB = A.NB, NS = A.NS, FPH = A.FPH;
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
   if (GINI) {
-    uint32_t* gh = (uint32_t*)A.hist + (int64_t)pi.hist_slot * slot_words;
+    const uint32_t* h32 = (const uint32_t*)smem;
+    uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
     for (int q = tid; q < ftn * NB * NS; q += 256) {
       const int cls = q % NS, b = (q / NS) % NB, f = q / (NS * NB);
       const uint32_t v = h32[((size_t)cls * NB + b) * FPH + f];
       if (v) atomicAdd(&gh[((int64_t)(ft0 + f) * NB + b) * NS + cls], v);
     }
   } else {
-    unsigned long long* gh = (unsigned long long*)A.hist + (int64_t)pi.hist_slot * slot_words;
-    const uint64_t M40 = (1ull << 40) - 1;
+    const uint64_t* h64 = (const uint64_t*)smem;
+    unsigned long long* gh = (unsigned long long*)A.hist + (int64_t)slot * slot_words;
+    const int cs = A.cshift;
+    const uint64_t MS = (1ull << cs) - 1;
     for (int q = tid; q < ftn * NB; q += 256) {
       const int b = q % NB, f = q / NB;
       const uint64_t w0 = h64[(size_t)b * FPH + f];
       if (w0) {
-        const uint64_t cnt = w0 >> 40;
-        const int64_t sk = (int64_t)(w0 & M40) - (int64_t)K0 * (int64_t)cnt;
+        const uint64_t cnt = w0 >> cs;
+        const int64_t sk = (int64_t)(w0 & MS) - (int64_t)A.K0 * (int64_t)cnt;
         const uint64_t w1 = h64[((size_t)NB + b) * FPH + f];
         const int64_t gb = ((int64_t)(ft0 + f) * NB + b) * 3;
         atomicAdd(&gh[gb], (unsigned long long)cnt);
@@ -450,9 +406,229 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
   }
 }
 
-size_t hist_lds_limit() { return 160 * 1024; }
+template <bool GINI>
+__global__ __launch_bounds__(256) void k_hist(HistArgs A) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NB = A.NB, NS = A.NS, FPH = A.FPH, S = A.S, T = A.T;
+  const int ft0 = blockIdx.y * A.FT;
+  const bool tile0 = blockIdx.y == 0;
 
-void launch_hist(hipStream_t st, const HistArgs& a, int nchunks, int ntiles, bool gini,
+  const size_t hist_bytes = GINI ? (size_t)NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
+  size_t off = align16(hist_bytes);
+  uint8_t* tile = smem + off;
+  off += align16((size_t)T * S);
+  uint64_t* s_e0 = (uint64_t*)(smem + off);
+  off += (size_t)T * 8;
+  uint64_t* s_e1 = (uint64_t*)(smem + off);
+  off += (size_t)T * 8;
+  uint4* s_w = (uint4*)(smem + off);
+  off += (size_t)T * 16;
+  uint16_t* s_list = (uint16_t*)(smem + off);
+  off += align16((size_t)T * 2);
+  uint8_t* s_side = smem + off;
+  off += align16((size_t)T);
+  int* s_cnt = (int*)(smem + off);
+
+  for (size_t i = (size_t)tid * 16; i < hist_bytes; i += 256 * 16)
+    *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+
+  const int lpr = S >> 4;          // 16-B parts per row
+  const int rpp = 256 / lpr;       // rows per gather pass
+  const int npass = (T + rpp - 1) / rpp;
+  const int grow = tid / lpr, gpart = tid - (tid / lpr) * lpr;
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  const int K0 = A.K0, cs = A.cshift;
+
+  const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
+  int cur_slot = -1, cur_ftn = 0, cur_r = -1;
+  int64_t acc = 0;
+  int posr[4] = {0, 0, 0, 0};
+  __syncthreads();
+
+  for (int p = p0; p < p1; p++) {
+    const HistChunk pc = A.chunks[p];
+    const ParentInfo pi = A.parents[pc.parent];
+    const int r = pi.r;
+    const int ftn = min(A.FT, A.Fr[r] - ft0);
+    if (ftn <= 0) continue;
+    const bool do_write = tile0 && A.do_write;
+    const int slot = pi.hist_slot;
+    if (slot < 0 && !do_write) continue;
+    const int64_t a = pc.a, b = pc.b;
+    if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
+      if (cur_slot >= 0) {
+        __syncthreads();
+        hist_flush<GINI>(A, smem, cur_slot, ft0, cur_ftn);
+        __syncthreads();
+        for (size_t i = (size_t)tid * 16; i < hist_bytes; i += 256 * 16)
+          *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+      }
+      cur_slot = slot;
+      cur_ftn = ftn;
+      acc = 0;
+    }
+    acc += b - a;
+    if (r != cur_r) {
+      for (int j = 0; j < 4; j++) {
+        const int fl = lane + 64 * j;
+        posr[j] = (fl < ftn) ? A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0;
+      }
+      cur_r = r;
+    }
+    const uint8_t* binsr = A.bins + (int64_t)r * A.bins_rstride;
+    const int ntile = (int)((b - a + T - 1) / T);
+    const int spos = pi.pos, spart = spos >> 4, sbyte = spos & 15;
+
+    // prologue: entries of tile 0, gathers of tile 0, entries of tile 1
+    if (tid < T) s_e0[tid] = (a + tid < b) ? A.ent_in[a + tid] : 0ull;
+    __syncthreads();
+    uint4 rreg[4];
+    {
+      const int nt0 = (int)min((int64_t)T, b - a);
+      #pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (q >= npass) break;
+        const int i = q * rpp + grow;
+        if (grow < rpp && i < nt0)
+          rreg[q] = *((const uint4*)(binsr + (int64_t)(uint32_t)s_e0[i] * S) + gpart);
+      }
+    }
+    uint64_t enext = 0;
+    if (tid < T && a + T + tid < b) enext = A.ent_in[a + T + tid];
+
+    for (int t = 0; t < ntile; t++) {
+      uint64_t* s_ec = (t & 1) ? s_e1 : s_e0;
+      uint64_t* s_en = (t & 1) ? s_e0 : s_e1;
+      const int64_t base = a + (int64_t)t * T;
+      const int nt = (int)min((int64_t)T, b - base);
+      // ---- top: commit staged rows, next entries, weights
+      #pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (q >= npass) break;
+        const int i = q * rpp + grow;
+        if (grow < rpp && i < nt) {
+          *((uint4*)(tile + (size_t)i * S) + gpart) = rreg[q];
+          if (spos >= 0 && gpart == spart) {
+            const uint32_t wd = (sbyte < 4) ? rreg[q].x : (sbyte < 8) ? rreg[q].y
+                                : (sbyte < 12) ? rreg[q].z : rreg[q].w;
+            s_side[i] = ((wd >> (8 * (sbyte & 3))) & 0xffu) <= (uint32_t)pi.s ? 0 : 1;
+          }
+        }
+      }
+      if (tid < T) s_en[tid] = enext;
+      if (tid < nt) {
+        const uint64_t e = s_ec[tid];
+        const int32_t hi = (int32_t)(e >> 32);
+        const uint32_t c = (uint32_t)hi & 0xffu;
+        const int32_t k = hi >> 8;
+        uint4 w;
+        if (GINI) {
+          w = make_uint4(A.count_only ? 0u : (uint32_t)k, c, 0, 0);
+        } else {
+          const uint64_t w0 = ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)(int64_t)(k + K0);
+          const uint64_t w1 = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);
+          w = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+        }
+        s_w[tid] = w;
+      }
+      if (tid == 0) *s_cnt = 0;
+      __syncthreads();  // B1
+      // ---- prefetch: rows of tile t+1, entries of tile t+2
+      if (t + 1 < ntile) {
+        const int nt1 = (int)min((int64_t)T, b - (base + T));
+        #pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (q >= npass) break;
+          const int i = q * rpp + grow;
+          if (grow < rpp && i < nt1)
+            rreg[q] = *((const uint4*)(binsr + (int64_t)(uint32_t)s_en[i] * S) + gpart);
+        }
+      }
+      enext = 0;
+      if (tid < T && base + 2 * T + tid < b) enext = A.ent_in[base + 2 * T + tid];
+      // ---- route tile t
+      const int ntr = (nt + 63) & ~63;
+      if (tid < ntr) {
+        const bool valid = tid < nt;
+        const int side = (valid && spos >= 0) ? s_side[tid] : 0;
+        if (do_write) {
+          const bool wl = valid && side == 0 && pi.write_l;
+          const bool wr = valid && side == 1 && pi.write_r;
+          const uint64_t ml = __ballot(wl), mr = __ballot(wr);
+          unsigned long long bl = 0, br = 0;
+          if (lane == 0) {
+            if (ml) bl = atomicAdd(&A.cursors[2 * pc.parent], (unsigned long long)__popcll(ml));
+            if (mr) {
+              const unsigned long long nr = (unsigned long long)__popcll(mr);
+              br = atomicAdd(&A.cursors[2 * pc.parent + 1], (unsigned long long)(-(long long)nr)) - nr;
+            }
+          }
+          bl = __shfl(bl, 0);
+          br = __shfl(br, 0);
+          if (wl) A.ent_out[bl + __popcll(ml & lt)] = s_ec[tid];
+          if (wr) A.ent_out[br + __popcll(mr & lt)] = s_ec[tid];
+        }
+        if (slot >= 0) {
+          const bool fl = valid && side == pi.hist_side;
+          const uint64_t mf = __ballot(fl);
+          int lbase = 0;
+          if (lane == 0 && mf) lbase = atomicAdd(s_cnt, (int)__popcll(mf));
+          lbase = __shfl(lbase, 0);
+          if (fl) s_list[lbase + __popcll(mf & lt)] = (uint16_t)tid;
+        }
+      }
+      __syncthreads();  // B2
+      // ---- accumulate the histogram child: one entry per wave, one feature per lane
+      if (slot >= 0) {
+        const int cnt = *s_cnt;
+        for (int j = wave; j < cnt; j += 4) {
+          const int i = s_list[j];
+          const uint4 w = s_w[i];
+          const uint8_t* row = tile + (size_t)i * S;
+          if (GINI) {
+            uint32_t* h32 = (uint32_t*)smem;
+            const size_t cb = (size_t)w.x * NB;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+              const int fl = lane + 64 * jj;
+              if (fl < ftn) {
+                const int bb = row[posr[jj]];
+                atomicAdd(&h32[(cb + bb) * FPH + fl], w.y);
+              }
+            }
+          } else {
+            unsigned long long* h64 = (unsigned long long*)smem;
+            const unsigned long long w0 = ((unsigned long long)w.y << 32) | w.x;
+            const unsigned long long w1 = ((unsigned long long)w.w << 32) | w.z;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+              const int fl = lane + 64 * jj;
+              if (fl < ftn) {
+                const int bb = row[posr[jj]];
+                atomicAdd(&h64[(size_t)bb * FPH + fl], w0);
+                atomicAdd(&h64[((size_t)NB + bb) * FPH + fl], w1);
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();  // B3
+    }
+  }
+  if (cur_slot >= 0) {
+    __syncthreads();
+    hist_flush<GINI>(A, smem, cur_slot, ft0, cur_ftn);
+  }
+}
+
+size_t hist_lds_bytes(int S, int T, int NB, int NS, int FPH, bool gini) {
+  const size_t hist_bytes = gini ? (size_t)NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
+  return align16(hist_bytes) + align16((size_t)T * S) + (size_t)T * 32 + align16((size_t)T * 2) +
+         align16((size_t)T) + 16;
+}
+
+void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gini,
                  size_t lds_bytes) {
   static bool attr_set = false;
   if (!attr_set) {
@@ -462,12 +638,14 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nchunks, int ntiles, boo
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  dim3 grid((unsigned)nchunks, (unsigned)ntiles);
+  dim3 grid((unsigned)nwg, (unsigned)ntiles);
   if (gini)
     hipLaunchKernelGGL(k_hist<true>, grid, dim3(256), lds_bytes, st, a);
   else
     hipLaunchKernelGGL(k_hist<false>, grid, dim3(256), lds_bytes, st, a);
 }
+
+size_t hist_lds_limit() { return 160 * 1024; }
 
 // ======================================================================
 // Split search: one workgroup per node slot; thread per local feature does
