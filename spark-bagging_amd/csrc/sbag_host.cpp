@@ -777,7 +777,7 @@ struct HistGeom {
 static int roundup(int x, int a) { return (x + a - 1) / a * a; }
 
 static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g) {
-  g.T = std::max(16, std::min(128, 16384 / S));
+  g.T = std::max(16, std::min(128, 32768 / S));  // npass <= 2 at 512 threads
   const int align = gini_layout ? 32 : 16;
   auto lds_for = [&](int ft) {
     return hist_lds_bytes(S, g.T, NB, NS, roundup(ft, align), gini_layout);
@@ -1001,7 +1001,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   auto launch = [&](const HistGeom& g, bool gini_layout, int cat,
                     const std::vector<std::pair<int64_t, int64_t>>& segs,
                     const std::vector<ParentInfo>& par) -> int {
-    const int wpc = std::max(1, std::min(8, (int)((160 * 1024) / g.lds)));
+    const int wpc = std::max(1, std::min(2, (int)((160 * 1024) / g.lds)));  // 16 waves/CU
     build_work(segs, flush_limit, 256 * wpc, g.T, work);
     TRY(upload_work(par));
     ha.chunks = d_pieces;

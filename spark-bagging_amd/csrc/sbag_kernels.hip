@@ -380,7 +380,7 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* sme
   if (GINI) {
     const uint32_t* h32 = (const uint32_t*)smem;
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
-    for (int q = tid; q < ftn * NB * NS; q += 256) {
+    for (int q = tid; q < ftn * NB * NS; q += blockDim.x) {
       const int cls = q % NS, b = (q / NS) % NB, f = q / (NS * NB);
       const uint32_t v = h32[((size_t)cls * NB + b) * FPH + f];
       if (v) atomicAdd(&gh[((int64_t)(ft0 + f) * NB + b) * NS + cls], v);
@@ -390,7 +390,7 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* sme
     unsigned long long* gh = (unsigned long long*)A.hist + (int64_t)slot * slot_words;
     const int cs = A.cshift;
     const uint64_t MS = (1ull << cs) - 1;
-    for (int q = tid; q < ftn * NB; q += 256) {
+    for (int q = tid; q < ftn * NB; q += blockDim.x) {
       const int b = q % NB, f = q / NB;
       const uint64_t w0 = h64[(size_t)b * FPH + f];
       if (w0) {
@@ -406,15 +406,18 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* sme
   }
 }
 
+constexpr int kHistThreads = 512;  // 8 waves; two workgroups per CU at <= 80 KB of LDS
+constexpr int kHistWaves = kHistThreads / 64;
+
 template <bool GINI>
-__global__ __launch_bounds__(256) void k_hist(HistArgs A) {
+__global__ __launch_bounds__(kHistThreads) void k_hist(HistArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int NB = A.NB, NS = A.NS, FPH = A.FPH, S = A.S, T = A.T;
+  const int NB = A.NB, FPH = A.FPH, S = A.S, T = A.T;
   const int ft0 = blockIdx.y * A.FT;
   const bool tile0 = blockIdx.y == 0;
 
-  const size_t hist_bytes = GINI ? (size_t)NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
+  const size_t hist_bytes = GINI ? (size_t)A.NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
   size_t off = align16(hist_bytes);
   uint8_t* tile = smem + off;
   off += align16((size_t)T * S);
@@ -422,20 +425,18 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
   off += (size_t)T * 8;
   uint64_t* s_e1 = (uint64_t*)(smem + off);
   off += (size_t)T * 8;
-  uint4* s_w = (uint4*)(smem + off);
+  uint4* s_wl = (uint4*)(smem + off);  // compacted histogram entries: weights + tile row
   off += (size_t)T * 16;
-  uint16_t* s_list = (uint16_t*)(smem + off);
-  off += align16((size_t)T * 2);
   uint8_t* s_side = smem + off;
   off += align16((size_t)T);
   int* s_cnt = (int*)(smem + off);
 
-  for (size_t i = (size_t)tid * 16; i < hist_bytes; i += 256 * 16)
+  for (size_t i = (size_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
     *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 
-  const int lpr = S >> 4;          // 16-B parts per row
-  const int rpp = 256 / lpr;       // rows per gather pass
-  const int npass = (T + rpp - 1) / rpp;
+  const int lpr = S >> 4;                  // 16-B parts per row
+  const int rpp = kHistThreads / lpr;      // rows per gather pass
+  const int npass = (T + rpp - 1) / rpp;   // <= 2 (host: T * S <= 32 KB)
   const int grow = tid / lpr, gpart = tid - (tid / lpr) * lpr;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   const int K0 = A.K0, cs = A.cshift;
@@ -461,7 +462,7 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
         __syncthreads();
         hist_flush<GINI>(A, smem, cur_slot, ft0, cur_ftn);
         __syncthreads();
-        for (size_t i = (size_t)tid * 16; i < hist_bytes; i += 256 * 16)
+        for (size_t i = (size_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
           *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
       }
       cur_slot = slot;
@@ -470,6 +471,7 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
     }
     acc += b - a;
     if (r != cur_r) {
+#pragma unroll
       for (int j = 0; j < 4; j++) {
         const int fl = lane + 64 * j;
         posr[j] = (fl < ftn) ? A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0;
@@ -483,14 +485,13 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
     // prologue: entries of tile 0, gathers of tile 0, entries of tile 1
     if (tid < T) s_e0[tid] = (a + tid < b) ? A.ent_in[a + tid] : 0ull;
     __syncthreads();
-    uint4 rreg[4];
+    uint4 rreg[2];
     {
       const int nt0 = (int)min((int64_t)T, b - a);
-      #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        if (q >= npass) break;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
         const int i = q * rpp + grow;
-        if (grow < rpp && i < nt0)
+        if (q < npass && grow < rpp && i < nt0)
           rreg[q] = *((const uint4*)(binsr + (int64_t)(uint32_t)s_e0[i] * S) + gpart);
       }
     }
@@ -502,12 +503,11 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
       uint64_t* s_en = (t & 1) ? s_e0 : s_e1;
       const int64_t base = a + (int64_t)t * T;
       const int nt = (int)min((int64_t)T, b - base);
-      // ---- top: commit staged rows, next entries, weights
-      #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        if (q >= npass) break;
+      // ---- top: commit staged rows (+ split byte), entries of tile t+1
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
         const int i = q * rpp + grow;
-        if (grow < rpp && i < nt) {
+        if (q < npass && grow < rpp && i < nt) {
           *((uint4*)(tile + (size_t)i * S) + gpart) = rreg[q];
           if (spos >= 0 && gpart == spart) {
             const uint32_t wd = (sbyte < 4) ? rreg[q].x : (sbyte < 8) ? rreg[q].y
@@ -517,41 +517,26 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
         }
       }
       if (tid < T) s_en[tid] = enext;
-      if (tid < nt) {
-        const uint64_t e = s_ec[tid];
-        const int32_t hi = (int32_t)(e >> 32);
-        const uint32_t c = (uint32_t)hi & 0xffu;
-        const int32_t k = hi >> 8;
-        uint4 w;
-        if (GINI) {
-          w = make_uint4(A.count_only ? 0u : (uint32_t)k, c, 0, 0);
-        } else {
-          const uint64_t w0 = ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)(int64_t)(k + K0);
-          const uint64_t w1 = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);
-          w = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-        }
-        s_w[tid] = w;
-      }
       if (tid == 0) *s_cnt = 0;
       __syncthreads();  // B1
       // ---- prefetch: rows of tile t+1, entries of tile t+2
       if (t + 1 < ntile) {
         const int nt1 = (int)min((int64_t)T, b - (base + T));
-        #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        if (q >= npass) break;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
           const int i = q * rpp + grow;
-          if (grow < rpp && i < nt1)
+          if (q < npass && grow < rpp && i < nt1)
             rreg[q] = *((const uint4*)(binsr + (int64_t)(uint32_t)s_en[i] * S) + gpart);
         }
       }
       enext = 0;
       if (tid < T && base + 2 * T + tid < b) enext = A.ent_in[base + 2 * T + tid];
-      // ---- route tile t
+      // ---- route tile t; compact the histogram child's entries with their weights
       const int ntr = (nt + 63) & ~63;
       if (tid < ntr) {
         const bool valid = tid < nt;
         const int side = (valid && spos >= 0) ? s_side[tid] : 0;
+        const uint64_t e = valid ? s_ec[tid] : 0ull;
         if (do_write) {
           const bool wl = valid && side == 0 && pi.write_l;
           const bool wr = valid && side == 1 && pi.write_r;
@@ -566,8 +551,8 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
           }
           bl = __shfl(bl, 0);
           br = __shfl(br, 0);
-          if (wl) A.ent_out[bl + __popcll(ml & lt)] = s_ec[tid];
-          if (wr) A.ent_out[br + __popcll(mr & lt)] = s_ec[tid];
+          if (wl) A.ent_out[bl + __popcll(ml & lt)] = e;
+          if (wr) A.ent_out[br + __popcll(mr & lt)] = e;
         }
         if (slot >= 0) {
           const bool fl = valid && side == pi.hist_side;
@@ -575,39 +560,61 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
           int lbase = 0;
           if (lane == 0 && mf) lbase = atomicAdd(s_cnt, (int)__popcll(mf));
           lbase = __shfl(lbase, 0);
-          if (fl) s_list[lbase + __popcll(mf & lt)] = (uint16_t)tid;
+          if (fl) {
+            const int32_t hi = (int32_t)(e >> 32);
+            const uint32_t c = (uint32_t)hi & 0xffu;
+            const int32_t k = hi >> 8;
+            uint4 w;
+            if (GINI) {
+              w = make_uint4(A.count_only ? 0u : (uint32_t)k, c, (uint32_t)tid, 0);
+            } else {
+              const uint64_t w0 = ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)(int64_t)(k + K0);
+              const uint64_t w1 = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);  // < 2^56
+              w = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1,
+                             (uint32_t)(w1 >> 32) | ((uint32_t)tid << 24));
+            }
+            s_wl[lbase + __popcll(mf & lt)] = w;
+          }
         }
       }
       __syncthreads();  // B2
-      // ---- accumulate the histogram child: one entry per wave, one feature per lane
+      // ---- accumulate: 4 entries per wave per step, all reads before the atomics
       if (slot >= 0) {
         const int cnt = *s_cnt;
-        for (int j = wave; j < cnt; j += 4) {
-          const int i = s_list[j];
-          const uint4 w = s_w[i];
-          const uint8_t* row = tile + (size_t)i * S;
-          if (GINI) {
-            uint32_t* h32 = (uint32_t*)smem;
-            const size_t cb = (size_t)w.x * NB;
+        for (int j0 = wave * 4; j0 < cnt; j0 += kHistWaves * 4) {
+          uint4 w[4];
+          int bb[4][4];
 #pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-              const int fl = lane + 64 * jj;
-              if (fl < ftn) {
-                const int bb = row[posr[jj]];
-                atomicAdd(&h32[(cb + bb) * FPH + fl], w.y);
+          for (int u = 0; u < 4; u++) w[u] = (j0 + u < cnt) ? s_wl[j0 + u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const int i = GINI ? (int)w[u].z : (int)(w[u].w >> 24);
+            const uint8_t* row = tile + (size_t)i * S;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) bb[u][jj] = (lane + 64 * jj < ftn) ? row[posr[jj]] : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            if (j0 + u >= cnt) break;
+            if (GINI) {
+              uint32_t* h32 = (uint32_t*)smem;
+              const size_t cb = (size_t)w[u].x * NB;
+#pragma unroll
+              for (int jj = 0; jj < 4; jj++) {
+                const int fl = lane + 64 * jj;
+                if (fl < ftn) atomicAdd(&h32[(cb + bb[u][jj]) * FPH + fl], w[u].y);
               }
-            }
-          } else {
-            unsigned long long* h64 = (unsigned long long*)smem;
-            const unsigned long long w0 = ((unsigned long long)w.y << 32) | w.x;
-            const unsigned long long w1 = ((unsigned long long)w.w << 32) | w.z;
+            } else {
+              unsigned long long* h64 = (unsigned long long*)smem;
+              const unsigned long long w0 = ((unsigned long long)w[u].y << 32) | w[u].x;
+              const unsigned long long w1 = ((unsigned long long)(w[u].w & 0xffffffu) << 32) | w[u].z;
 #pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-              const int fl = lane + 64 * jj;
-              if (fl < ftn) {
-                const int bb = row[posr[jj]];
-                atomicAdd(&h64[(size_t)bb * FPH + fl], w0);
-                atomicAdd(&h64[((size_t)NB + bb) * FPH + fl], w1);
+              for (int jj = 0; jj < 4; jj++) {
+                const int fl = lane + 64 * jj;
+                if (fl < ftn) {
+                  atomicAdd(&h64[(size_t)bb[u][jj] * FPH + fl], w0);
+                  atomicAdd(&h64[((size_t)NB + bb[u][jj]) * FPH + fl], w1);
+                }
               }
             }
           }
@@ -624,8 +631,7 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs A) {
 
 size_t hist_lds_bytes(int S, int T, int NB, int NS, int FPH, bool gini) {
   const size_t hist_bytes = gini ? (size_t)NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
-  return align16(hist_bytes) + align16((size_t)T * S) + (size_t)T * 32 + align16((size_t)T * 2) +
-         align16((size_t)T) + 16;
+  return align16(hist_bytes) + align16((size_t)T * S) + (size_t)T * 32 + align16((size_t)T) + 16;
 }
 
 void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gini,
@@ -640,9 +646,9 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gi
   }
   dim3 grid((unsigned)nwg, (unsigned)ntiles);
   if (gini)
-    hipLaunchKernelGGL(k_hist<true>, grid, dim3(256), lds_bytes, st, a);
+    hipLaunchKernelGGL(k_hist<true>, grid, dim3(kHistThreads), lds_bytes, st, a);
   else
-    hipLaunchKernelGGL(k_hist<false>, grid, dim3(256), lds_bytes, st, a);
+    hipLaunchKernelGGL(k_hist<false>, grid, dim3(kHistThreads), lds_bytes, st, a);
 }
 
 size_t hist_lds_limit() { return 160 * 1024; }

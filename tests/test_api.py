@@ -1,0 +1,112 @@
+"""CPU: the Spark-API mirror -- names, defaults, validation and error behaviour
+of the reference's BaggingRegressor / BaggingClassifier (no GPU calls)."""
+import warnings
+
+import numpy as np
+import pytest
+
+import spark_bagging_amd as sb
+
+
+def test_defaults_match_reference():
+    br = sb.BaggingRegressor()
+    assert br.getNumBaseLearners() == 10          # BaggingParams.scala:31
+    assert br.getReplacement() is False           # HasSubBag.scala:45
+    assert br.getSampleRatio() == 1.0             # HasSubBag.scala:62
+    assert br.getSubspaceRatio() == 1.0           # HasSubBag.scala:79
+    assert br.getParallelism() == 1
+    assert br.getSeed() == -1395689524            # H3
+    assert sb.BaggingClassifier().getSeed() == 42087812
+    dt = sb.DecisionTreeRegressor()
+    assert (dt.getMaxDepth(), dt.getMaxBins(), dt.getMinInstancesPerNode(), dt.getMinInfoGain(),
+            dt.getImpurity()) == (5, 32, 1, 0.0, "variance")
+    assert sb.DecisionTreeClassifier().getImpurity() == "gini"
+
+
+def test_setters_chain_and_store():
+    br = (sb.BaggingRegressor().setBaseLearner(sb.DecisionTreeRegressor().setMaxDepth(10))
+          .setNumBaseLearners(7).setReplacement(True).setSampleRatio(0.7).setSubspaceRatio(0.5)
+          .setParallelism(4))
+    assert (br.getNumBaseLearners(), br.getReplacement(), br.getSampleRatio(),
+            br.getSubspaceRatio(), br.getParallelism()) == (7, True, 0.7, 0.5, 4)
+    assert br.getBaseLearner().getMaxDepth() == 10
+
+
+@pytest.mark.parametrize("bad", [-0.1, 1.5])
+def test_ratio_validators_raise_illegal_argument(bad):
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.BaggingRegressor().setSampleRatio(bad)
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.BaggingClassifier().setSubspaceRatio(bad)
+
+
+def test_num_base_learners_must_be_positive():
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.BaggingRegressor().setNumBaseLearners(0)
+
+
+def test_tree_param_validators():
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.DecisionTreeRegressor().setMaxDepth(31)
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.DecisionTreeRegressor().setMaxBins(1)
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.DecisionTreeClassifier().setMinInstancesPerNode(0)
+
+
+def test_no_set_seed_on_bagging_but_param_map_works():
+    """The reference exposes no setSeed (H3); the seed is reachable through set/copy."""
+    br = sb.BaggingRegressor()
+    assert not hasattr(br, "setSeed")
+    br2 = br.copy({"seed": 7})
+    assert br2.getSeed() == 7 and br.getSeed() == -1395689524
+
+
+def test_copy_deep_copies_base_learner():
+    bl = sb.DecisionTreeRegressor()
+    br = sb.BaggingRegressor().setBaseLearner(bl)
+    br2 = br.copy({"numBaseLearners": 3})
+    br2.getBaseLearner().setMaxDepth(9)
+    assert bl.getMaxDepth() == 5 and br2.getNumBaseLearners() == 3 and br.getNumBaseLearners() == 10
+
+
+def test_fit_without_base_learner_raises():
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.BaggingRegressor().fit(sb.Frame(np.zeros((4, 2)), np.zeros(4)))
+
+
+def test_unsupported_base_learner_is_rejected():
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.BaggingRegressor().setBaseLearner(object())
+
+
+def test_frame_validates_lengths_and_partitions():
+    with pytest.raises(sb.IllegalArgumentException):
+        sb.Frame(np.zeros((3, 2)), np.zeros(4))
+    assert sb.even_partitions(10, 3) == [0, 3, 7, 10]
+
+
+def test_weight_col_warning_h10(monkeypatch):
+    """weightCol is ignored for DecisionTree (Spark 2.4) with a warning (BaggingRegressor.scala:141)."""
+    br = sb.BaggingRegressor().setBaseLearner(sb.DecisionTreeRegressor()).setWeightCol("w")
+    import spark_bagging_amd.ml as ml
+
+    def boom(*a, **k):
+        raise RuntimeError("stop after validation")
+
+    monkeypatch.setattr(ml.nat, "default_context", boom)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        with pytest.raises(RuntimeError):
+            br.fit(sb.Frame(np.zeros((4, 2)), np.zeros(4)))
+    assert any("weightCol is ignored" in str(x.message) for x in w)
+
+
+def test_learner_shards_cover_in_order():
+    from spark_bagging_amd.ml import _learner_shards
+
+    for L in (1, 7, 10, 128):
+        for k in (1, 2, 3, 8):
+            sh = _learner_shards(L, k)
+            assert sh[0][0] == 0 and sh[-1][1] == L
+            assert all(sh[i][1] == sh[i + 1][0] for i in range(k - 1))
