@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -991,6 +992,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     return SBAG_OK;
   };
   HistArgs ha{};
+  if (const char* ab = std::getenv("SBAG_HIST_ABLATE")) ha.ablate = std::atoi(ab);  // timing only
   ha.Fmax = Fmax;
   ha.Fr = d_Fr;
   ha.K0 = (int32_t)K0;

@@ -53,6 +53,7 @@ struct HistArgs {
   int32_t T;             // rows per tile
   int32_t do_write;      // route + write entries (levels > 0)
   int32_t count_only;    // gini layout with the label ignored (value counts)
+  int32_t ablate;        // timing-only builds: 1 skip atomics, 2 skip accumulate, 4 skip writes
 };
 
 struct SplitOut {

@@ -77,6 +77,8 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
   const double cap = 1000.0 * mean;
   int n = 0, bad = 0;
   double racc = 1.0;
+  uint64_t wbuf = 0;      // counts of rows [wrow0, row), one byte each
+  int64_t wrow0 = row;
   while (__any(row < row_end)) {
     uint32_t m1[kWB], m2[kWB], m3[kWB], hb[kWB], lo[kWB], z3v[kWB], o[kWB];
 #pragma unroll
@@ -120,10 +122,21 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
         }
         if (emit) {
           if (n > 255) bad = 1;
-          out[row] = (uint8_t)(n > 255 ? 255 : n);
+          wbuf |= (uint64_t)(n > 255 ? 255 : n) << (8 * (int)(row - wrow0));
           row++;
           n = 0;
           racc = 1.0;
+          if ((((uintptr_t)(out + row)) & 7) == 0 || row == row_end) {  // flush 8 counts
+            uint8_t* dst = out + wrow0;
+            const int nb = (int)(row - wrow0);
+            if (nb == 8) {
+              *(uint64_t*)dst = wbuf;
+            } else {
+              for (int j = 0; j < nb; j++) dst[j] = (uint8_t)(wbuf >> (8 * j));
+            }
+            wbuf = 0;
+            wrow0 = row;
+          }
         }
       }
     }
@@ -392,11 +405,11 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* sme
     const uint64_t MS = (1ull << cs) - 1;
     for (int q = tid; q < ftn * NB; q += blockDim.x) {
       const int b = q % NB, f = q / NB;
-      const uint64_t w0 = h64[(size_t)b * FPH + f];
+      const uint64_t w0 = h64[((size_t)b * FPH + f) * 2];
       if (w0) {
         const uint64_t cnt = w0 >> cs;
         const int64_t sk = (int64_t)(w0 & MS) - (int64_t)A.K0 * (int64_t)cnt;
-        const uint64_t w1 = h64[((size_t)NB + b) * FPH + f];
+        const uint64_t w1 = h64[((size_t)b * FPH + f) * 2 + 1];
         const int64_t gb = ((int64_t)(ft0 + f) * NB + b) * 3;
         atomicAdd(&gh[gb], (unsigned long long)cnt);
         atomicAdd(&gh[gb + 1], (unsigned long long)sk);
@@ -408,43 +421,216 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* sme
 
 constexpr int kHistThreads = 512;  // 8 waves; two workgroups per CU at <= 80 KB of LDS
 constexpr int kHistWaves = kHistThreads / 64;
+constexpr int kDepth = 3;           // tiles of rows in flight per workgroup (register ring)
 
-template <bool GINI>
-__global__ __launch_bounds__(kHistThreads) void k_hist(HistArgs A) {
-  extern __shared__ __align__(16) unsigned char smem[];
+struct HistState {  // per-thread pipeline registers
+  uint4 rreg[kDepth][2];
+  uint64_t ereg[kDepth];
+};
+
+struct HistCtx {  // per-piece constants + LDS carve
+  const uint8_t* binsr;
+  const uint64_t* ent_in;
+  int64_t a, b;
+  int ntile, T, S, npass, rpp, grow, gpart, spos, spart, sbyte, ssplit;
+  uint8_t* tile;
+  uint64_t* s_e;  // ring of 4 tiles of entries: tile t at s_e + (t & 3) * T
+  uint4* s_wl;
+  uint8_t* s_side;
+  int* s_cnt;
+};
+
+__device__ __forceinline__ void issue_rows(const HistCtx& c, int t, const uint64_t* se, uint4 (&rr)[2]) {
+  if (t >= c.ntile) return;
+  const int nt = (int)min((int64_t)c.T, c.b - (c.a + (int64_t)t * c.T));
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int i = q * c.rpp + c.grow;
+    if (q < c.npass && c.grow < c.rpp && i < nt)
+      rr[q] = *((const uint4*)(c.binsr + (int64_t)(uint32_t)se[i] * c.S) + c.gpart);
+  }
+}
+
+__device__ __forceinline__ uint64_t load_entry(const HistCtx& c, int t, int tid) {
+  const int64_t i = c.a + (int64_t)t * c.T + tid;
+  return (tid < c.T && t < c.ntile && i < c.b) ? c.ent_in[i] : 0ull;
+}
+
+template <bool GINI, int NJ, int SLOT>
+__device__ __forceinline__ void hist_tile(const HistArgs& A, const HistCtx& c, HistState& st,
+                                          const ParentInfo& pi, int parent, int t,
+                                          const int (&posr)[4], const uint32_t (&amul)[4],
+                                          const uint32_t (&abase)[4], const uint32_t (&amask)[4],
+                                          bool do_write, int slot, unsigned char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  const int64_t base = c.a + (int64_t)t * c.T;
+  const int nt = (int)min((int64_t)c.T, c.b - base);
+  uint64_t* s_ec = c.s_e + (size_t)(t & 3) * c.T;
+  uint64_t* s_e3 = c.s_e + (size_t)((t + 3) & 3) * c.T;
+  // ---- top: commit staged rows of tile t (+ split byte); entries of tile t+3 -> LDS
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int i = q * c.rpp + c.grow;
+    if (q < c.npass && c.grow < c.rpp && i < nt) {
+      const uint4 v = st.rreg[SLOT][q];
+      *((uint4*)(c.tile + (size_t)i * c.S) + c.gpart) = v;
+      if (c.spos >= 0 && c.gpart == c.spart) {
+        const uint32_t wd = (c.sbyte < 4) ? v.x : (c.sbyte < 8) ? v.y : (c.sbyte < 12) ? v.z : v.w;
+        c.s_side[i] = ((wd >> (8 * (c.sbyte & 3))) & 0xffu) <= (uint32_t)c.ssplit ? 0 : 1;
+      }
+    }
+  }
+  if (tid < c.T) s_e3[tid] = st.ereg[SLOT];
+  if (tid == 0) *c.s_cnt = 0;
+  __syncthreads();  // B1
+  // ---- prefetch: rows of tile t+3 (entries already in LDS), entries of tile t+6
+  issue_rows(c, t + 3, s_e3, st.rreg[SLOT]);
+  st.ereg[SLOT] = load_entry(c, t + 6, tid);
+  // ---- route tile t; compact the histogram child's entries with their weights
+  const int ntr = (nt + 63) & ~63;
+  if (tid < ntr) {
+    const bool valid = tid < nt;
+    const int side = (valid && c.spos >= 0) ? c.s_side[tid] : 0;
+    const uint64_t e = valid ? s_ec[tid] : 0ull;
+    if (do_write && !(A.ablate & 4)) {
+      const bool wl = valid && side == 0 && pi.write_l;
+      const bool wr = valid && side == 1 && pi.write_r;
+      const uint64_t ml = __ballot(wl), mr = __ballot(wr);
+      unsigned long long bl = 0, br = 0;
+      if (lane == 0) {
+        if (ml) bl = atomicAdd(&A.cursors[2 * parent], (unsigned long long)__popcll(ml));
+        if (mr) {
+          const unsigned long long nr = (unsigned long long)__popcll(mr);
+          br = atomicAdd(&A.cursors[2 * parent + 1], (unsigned long long)(-(long long)nr)) - nr;
+        }
+      }
+      bl = __shfl(bl, 0);
+      br = __shfl(br, 0);
+      if (wl) A.ent_out[bl + __popcll(ml & lt)] = e;
+      if (wr) A.ent_out[br + __popcll(mr & lt)] = e;
+    }
+    if (slot >= 0) {
+      const bool fl = valid && side == pi.hist_side;
+      const uint64_t mf = __ballot(fl);
+      int lbase = 0;
+      if (lane == 0 && mf) lbase = atomicAdd(c.s_cnt, (int)__popcll(mf));
+      lbase = __shfl(lbase, 0);
+      if (fl) {
+        const int32_t hi = (int32_t)(e >> 32);
+        const uint32_t cc = (uint32_t)hi & 0xffu;
+        const int32_t k = hi >> 8;
+        uint4 w;
+        if (GINI) {
+          w = make_uint4(A.count_only ? 0u : (uint32_t)k, cc, (uint32_t)tid, 0);
+        } else {
+          const uint64_t w0 = ((uint64_t)cc << A.cshift) + (uint64_t)cc * (uint64_t)(int64_t)(k + A.K0);
+          const uint64_t w1 = (uint64_t)cc * (uint64_t)((int64_t)k * (int64_t)k);  // < 2^56
+          w = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1,
+                         (uint32_t)(w1 >> 32) | ((uint32_t)tid << 24));
+        }
+        c.s_wl[lbase + __popcll(mf & lt)] = w;
+      }
+    }
+  }
+  __syncthreads();  // B2
+  // ---- accumulate: 4 entries per wave per step, branch-free so every LDS read
+  // of the step is issued before the atomics (counted lgkmcnt).  Each lane owns
+  // one feature column per 64-lane group jj; its histogram byte address for bin b
+  // is b * amul[jj] + abase[jj] (one 24-bit mad): variance words (w0, w1) are
+  // interleaved per (bin, feature) so one address serves both atomics; lanes past
+  // the tile's features have amul = 0 and a private dump slot.
+  if (slot >= 0 && !(A.ablate & 2)) {
+    const int cnt = *c.s_cnt;
+    const uint32_t S = (uint32_t)c.S;
+    constexpr int UB = (NJ <= 2) ? 4 : 2;  // entries per step (register budget)
+    for (int j0 = wave * UB; j0 < cnt; j0 += kHistWaves * UB) {
+      uint4 w[UB];
+      uint32_t bb[UB][NJ];
+#pragma unroll
+      for (int u = 0; u < UB; u++) {
+        const uint4 v = c.s_wl[j0 + u];
+        w[u] = (j0 + u < cnt) ? v : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UB; u++) {
+        const uint32_t i = GINI ? w[u].z : (w[u].w >> 24);
+        const uint32_t rb = __umul24(i, S);
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) bb[u][jj] = c.tile[rb + (uint32_t)posr[jj]];
+      }
+#pragma unroll
+      for (int u = 0; u < UB; u++) {
+        if (GINI) {
+          const uint32_t coff = __umul24(w[u].x, (uint32_t)A.NB * (uint32_t)A.FPH * 4u);
+#pragma unroll
+          for (int jj = 0; jj < NJ; jj++) {
+            const uint32_t addr = (__umul24(bb[u][jj], amul[jj]) + abase[jj]) + (coff & amask[jj]);
+            atomicAdd((uint32_t*)(smem + addr), w[u].y);
+            if (A.ablate & 1) asm volatile("" ::"v"(addr));
+          }
+        } else {
+          const unsigned long long w0 = ((unsigned long long)w[u].y << 32) | w[u].x;
+          const unsigned long long w1 = ((unsigned long long)(w[u].w & 0xffffffu) << 32) | w[u].z;
+#pragma unroll
+          for (int jj = 0; jj < NJ; jj++) {
+            const uint32_t addr = (__umul24(bb[u][jj], amul[jj]) + abase[jj]);
+            unsigned long long* h = (unsigned long long*)(smem + addr);
+            if (A.ablate & 1) {
+              asm volatile("" ::"v"(addr), "v"(w0), "v"(w1));
+            } else {
+              atomicAdd(h, w0);
+              atomicAdd(h + 1, w1);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();  // B3
+}
+
+template <bool GINI, int NJ>
+__global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 128 VGPRs: 2 WGs/CU
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
   const int NB = A.NB, FPH = A.FPH, S = A.S, T = A.T;
   const int ft0 = blockIdx.y * A.FT;
   const bool tile0 = blockIdx.y == 0;
 
-  const size_t hist_bytes = GINI ? (size_t)A.NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
+  // histogram words + one dump slot per lane (targets of masked-off lanes)
+  const size_t words = GINI ? (size_t)A.NS * NB * FPH : (size_t)2 * NB * FPH;
+  const size_t hist_bytes = GINI ? words * 4 + 64 * 4 : words * 8 + 64 * 16;
+  const uint32_t dump = (uint32_t)(GINI ? words * 4 + lane * 4 : words * 8 + lane * 16);
+  HistCtx c;
   size_t off = align16(hist_bytes);
-  uint8_t* tile = smem + off;
+  c.tile = smem + off;
   off += align16((size_t)T * S);
-  uint64_t* s_e0 = (uint64_t*)(smem + off);
-  off += (size_t)T * 8;
-  uint64_t* s_e1 = (uint64_t*)(smem + off);
-  off += (size_t)T * 8;
-  uint4* s_wl = (uint4*)(smem + off);  // compacted histogram entries: weights + tile row
+  c.s_e = (uint64_t*)(smem + off);
+  off += (size_t)T * 8 * 4;
+  c.s_wl = (uint4*)(smem + off);
   off += (size_t)T * 16;
-  uint8_t* s_side = smem + off;
+  c.s_side = smem + off;
   off += align16((size_t)T);
-  int* s_cnt = (int*)(smem + off);
+  c.s_cnt = (int*)(smem + off);
+  c.T = T;
+  c.S = S;
+  const int lpr = S >> 4;
+  c.rpp = kHistThreads / lpr;
+  c.npass = (T + c.rpp - 1) / c.rpp;  // <= 2 (host: T * S <= 32 KB)
+  c.grow = tid / lpr;
+  c.gpart = tid - c.grow * lpr;
+  c.ent_in = A.ent_in;
 
   for (size_t i = (size_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
     *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
-
-  const int lpr = S >> 4;                  // 16-B parts per row
-  const int rpp = kHistThreads / lpr;      // rows per gather pass
-  const int npass = (T + rpp - 1) / rpp;   // <= 2 (host: T * S <= 32 KB)
-  const int grow = tid / lpr, gpart = tid - (tid / lpr) * lpr;
-  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  const int K0 = A.K0, cs = A.cshift;
 
   const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
   int cur_slot = -1, cur_ftn = 0, cur_r = -1;
   int64_t acc = 0;
   int posr[4] = {0, 0, 0, 0};
+  uint32_t amul[4] = {0, 0, 0, 0}, abase[4] = {dump, dump, dump, dump}, amask[4] = {0, 0, 0, 0};
+  HistState st;
   __syncthreads();
 
   for (int p = p0; p < p1; p++) {
@@ -474,153 +660,40 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(HistArgs A) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int fl = lane + 64 * j;
-        posr[j] = (fl < ftn) ? A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0;
+        const bool ok = fl < ftn;
+        posr[j] = ok ? A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0;
+        amul[j] = ok ? (uint32_t)FPH * (GINI ? 4u : 16u) : 0u;
+        abase[j] = ok ? (uint32_t)fl * (GINI ? 4u : 16u) : dump;
+        amask[j] = ok ? 0xffffffffu : 0u;
       }
       cur_r = r;
     }
-    const uint8_t* binsr = A.bins + (int64_t)r * A.bins_rstride;
-    const int ntile = (int)((b - a + T - 1) / T);
-    const int spos = pi.pos, spart = spos >> 4, sbyte = spos & 15;
+    c.binsr = A.bins + (int64_t)r * A.bins_rstride;
+    c.a = a;
+    c.b = b;
+    c.ntile = (int)((b - a + T - 1) / T);
+    c.spos = pi.pos;
+    c.spart = pi.pos >> 4;
+    c.sbyte = pi.pos & 15;
+    c.ssplit = pi.s;
 
-    // prologue: entries of tile 0, gathers of tile 0, entries of tile 1
-    if (tid < T) s_e0[tid] = (a + tid < b) ? A.ent_in[a + tid] : 0ull;
+    // prologue: entries of tiles 0..2 -> LDS; rows of tiles 0..2 and entries of 3..5 in flight
+    if (tid < T)
+#pragma unroll
+      for (int k = 0; k < 3; k++) c.s_e[(size_t)k * T + tid] = load_entry(c, k, tid);
     __syncthreads();
-    uint4 rreg[2];
-    {
-      const int nt0 = (int)min((int64_t)T, b - a);
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const int i = q * rpp + grow;
-        if (q < npass && grow < rpp && i < nt0)
-          rreg[q] = *((const uint4*)(binsr + (int64_t)(uint32_t)s_e0[i] * S) + gpart);
-      }
-    }
-    uint64_t enext = 0;
-    if (tid < T && a + T + tid < b) enext = A.ent_in[a + T + tid];
-
-    for (int t = 0; t < ntile; t++) {
-      uint64_t* s_ec = (t & 1) ? s_e1 : s_e0;
-      uint64_t* s_en = (t & 1) ? s_e0 : s_e1;
-      const int64_t base = a + (int64_t)t * T;
-      const int nt = (int)min((int64_t)T, b - base);
-      // ---- top: commit staged rows (+ split byte), entries of tile t+1
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const int i = q * rpp + grow;
-        if (q < npass && grow < rpp && i < nt) {
-          *((uint4*)(tile + (size_t)i * S) + gpart) = rreg[q];
-          if (spos >= 0 && gpart == spart) {
-            const uint32_t wd = (sbyte < 4) ? rreg[q].x : (sbyte < 8) ? rreg[q].y
-                                : (sbyte < 12) ? rreg[q].z : rreg[q].w;
-            s_side[i] = ((wd >> (8 * (sbyte & 3))) & 0xffu) <= (uint32_t)pi.s ? 0 : 1;
-          }
-        }
-      }
-      if (tid < T) s_en[tid] = enext;
-      if (tid == 0) *s_cnt = 0;
-      __syncthreads();  // B1
-      // ---- prefetch: rows of tile t+1, entries of tile t+2
-      if (t + 1 < ntile) {
-        const int nt1 = (int)min((int64_t)T, b - (base + T));
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-          const int i = q * rpp + grow;
-          if (q < npass && grow < rpp && i < nt1)
-            rreg[q] = *((const uint4*)(binsr + (int64_t)(uint32_t)s_en[i] * S) + gpart);
-        }
-      }
-      enext = 0;
-      if (tid < T && base + 2 * T + tid < b) enext = A.ent_in[base + 2 * T + tid];
-      // ---- route tile t; compact the histogram child's entries with their weights
-      const int ntr = (nt + 63) & ~63;
-      if (tid < ntr) {
-        const bool valid = tid < nt;
-        const int side = (valid && spos >= 0) ? s_side[tid] : 0;
-        const uint64_t e = valid ? s_ec[tid] : 0ull;
-        if (do_write) {
-          const bool wl = valid && side == 0 && pi.write_l;
-          const bool wr = valid && side == 1 && pi.write_r;
-          const uint64_t ml = __ballot(wl), mr = __ballot(wr);
-          unsigned long long bl = 0, br = 0;
-          if (lane == 0) {
-            if (ml) bl = atomicAdd(&A.cursors[2 * pc.parent], (unsigned long long)__popcll(ml));
-            if (mr) {
-              const unsigned long long nr = (unsigned long long)__popcll(mr);
-              br = atomicAdd(&A.cursors[2 * pc.parent + 1], (unsigned long long)(-(long long)nr)) - nr;
-            }
-          }
-          bl = __shfl(bl, 0);
-          br = __shfl(br, 0);
-          if (wl) A.ent_out[bl + __popcll(ml & lt)] = e;
-          if (wr) A.ent_out[br + __popcll(mr & lt)] = e;
-        }
-        if (slot >= 0) {
-          const bool fl = valid && side == pi.hist_side;
-          const uint64_t mf = __ballot(fl);
-          int lbase = 0;
-          if (lane == 0 && mf) lbase = atomicAdd(s_cnt, (int)__popcll(mf));
-          lbase = __shfl(lbase, 0);
-          if (fl) {
-            const int32_t hi = (int32_t)(e >> 32);
-            const uint32_t c = (uint32_t)hi & 0xffu;
-            const int32_t k = hi >> 8;
-            uint4 w;
-            if (GINI) {
-              w = make_uint4(A.count_only ? 0u : (uint32_t)k, c, (uint32_t)tid, 0);
-            } else {
-              const uint64_t w0 = ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)(int64_t)(k + K0);
-              const uint64_t w1 = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);  // < 2^56
-              w = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1,
-                             (uint32_t)(w1 >> 32) | ((uint32_t)tid << 24));
-            }
-            s_wl[lbase + __popcll(mf & lt)] = w;
-          }
-        }
-      }
-      __syncthreads();  // B2
-      // ---- accumulate: 4 entries per wave per step, all reads before the atomics
-      if (slot >= 0) {
-        const int cnt = *s_cnt;
-        for (int j0 = wave * 4; j0 < cnt; j0 += kHistWaves * 4) {
-          uint4 w[4];
-          int bb[4][4];
-#pragma unroll
-          for (int u = 0; u < 4; u++) w[u] = (j0 + u < cnt) ? s_wl[j0 + u] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            const int i = GINI ? (int)w[u].z : (int)(w[u].w >> 24);
-            const uint8_t* row = tile + (size_t)i * S;
-#pragma unroll
-            for (int jj = 0; jj < 4; jj++) bb[u][jj] = (lane + 64 * jj < ftn) ? row[posr[jj]] : 0;
-          }
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            if (j0 + u >= cnt) break;
-            if (GINI) {
-              uint32_t* h32 = (uint32_t*)smem;
-              const size_t cb = (size_t)w[u].x * NB;
-#pragma unroll
-              for (int jj = 0; jj < 4; jj++) {
-                const int fl = lane + 64 * jj;
-                if (fl < ftn) atomicAdd(&h32[(cb + bb[u][jj]) * FPH + fl], w[u].y);
-              }
-            } else {
-              unsigned long long* h64 = (unsigned long long*)smem;
-              const unsigned long long w0 = ((unsigned long long)w[u].y << 32) | w[u].x;
-              const unsigned long long w1 = ((unsigned long long)(w[u].w & 0xffffffu) << 32) | w[u].z;
-#pragma unroll
-              for (int jj = 0; jj < 4; jj++) {
-                const int fl = lane + 64 * jj;
-                if (fl < ftn) {
-                  atomicAdd(&h64[(size_t)bb[u][jj] * FPH + fl], w0);
-                  atomicAdd(&h64[((size_t)NB + bb[u][jj]) * FPH + fl], w1);
-                }
-              }
-            }
-          }
-        }
-      }
-      __syncthreads();  // B3
+    issue_rows(c, 0, c.s_e, st.rreg[0]);
+    issue_rows(c, 1, c.s_e + T, st.rreg[1]);
+    issue_rows(c, 2, c.s_e + 2 * T, st.rreg[2]);
+    st.ereg[0] = load_entry(c, 3, tid);
+    st.ereg[1] = load_entry(c, 4, tid);
+    st.ereg[2] = load_entry(c, 5, tid);
+    for (int t = 0; t < c.ntile; t += 3) {
+      hist_tile<GINI, NJ, 0>(A, c, st, pi, pc.parent, t, posr, amul, abase, amask, do_write, slot, smem);
+      if (t + 1 >= c.ntile) break;
+      hist_tile<GINI, NJ, 1>(A, c, st, pi, pc.parent, t + 1, posr, amul, abase, amask, do_write, slot, smem);
+      if (t + 2 >= c.ntile) break;
+      hist_tile<GINI, NJ, 2>(A, c, st, pi, pc.parent, t + 2, posr, amul, abase, amask, do_write, slot, smem);
     }
   }
   if (cur_slot >= 0) {
@@ -630,25 +703,40 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(HistArgs A) {
 }
 
 size_t hist_lds_bytes(int S, int T, int NB, int NS, int FPH, bool gini) {
-  const size_t hist_bytes = gini ? (size_t)NS * NB * FPH * 4 : (size_t)2 * NB * FPH * 8;
-  return align16(hist_bytes) + align16((size_t)T * S) + (size_t)T * 32 + align16((size_t)T) + 16;
+  const size_t hist_bytes = gini ? (size_t)NS * NB * FPH * 4 + 256 : (size_t)2 * NB * FPH * 8 + 1024;
+  return align16(hist_bytes) + align16((size_t)T * S) + (size_t)T * 48 + align16((size_t)T) + 16;
+}
+
+template <bool GINI, int NJ>
+static void launch_hist_t(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds_bytes) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_hist<GINI, NJ>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((k_hist<GINI, NJ>), grid, dim3(kHistThreads), lds_bytes, st, a);
 }
 
 void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gini,
                  size_t lds_bytes) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_hist<true>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)k_hist<false>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
+  const dim3 grid((unsigned)nwg, (unsigned)ntiles);
+  const int nj = (a.FT + 63) / 64;  // 64-feature lane groups per tile (FT <= 256)
+  if (gini) {
+    switch (nj) {
+      case 1: launch_hist_t<true, 1>(st, a, grid, lds_bytes); break;
+      case 2: launch_hist_t<true, 2>(st, a, grid, lds_bytes); break;
+      case 3: launch_hist_t<true, 3>(st, a, grid, lds_bytes); break;
+      default: launch_hist_t<true, 4>(st, a, grid, lds_bytes); break;
+    }
+  } else {
+    switch (nj) {
+      case 1: launch_hist_t<false, 1>(st, a, grid, lds_bytes); break;
+      case 2: launch_hist_t<false, 2>(st, a, grid, lds_bytes); break;
+      case 3: launch_hist_t<false, 3>(st, a, grid, lds_bytes); break;
+      default: launch_hist_t<false, 4>(st, a, grid, lds_bytes); break;
+    }
   }
-  dim3 grid((unsigned)nwg, (unsigned)ntiles);
-  if (gini)
-    hipLaunchKernelGGL(k_hist<true>, grid, dim3(kHistThreads), lds_bytes, st, a);
-  else
-    hipLaunchKernelGGL(k_hist<false>, grid, dim3(kHistThreads), lds_bytes, st, a);
 }
 
 size_t hist_lds_limit() { return 160 * 1024; }

@@ -296,12 +296,24 @@ class _BaggingEstimator(_BaggingParams):
         est = self.copy(params) if params else self
         return est._train(dataset, bug_compat)
 
-    def _train(self, dataset, bug_compat):
+    def fit_range(self, dataset, learner_begin, learner_end, bug_compat=True, devices=None):
+        """Train only learners [learner_begin, learner_end) of the ensemble (one
+        shard of a multi-process fit, see distributed.py); learner i still uses
+        seed + i, so shards concatenate to exactly the single-process model."""
+        est = self.copy()
+        if devices is not None:
+            est.devices = devices
+        return est._train(dataset, bug_compat, (learner_begin, learner_end))
+
+    def _train(self, dataset, bug_compat, learner_range=None):
         bl = self._base()
         if self.get("weightCol"):
             # DecisionTree has no HasWeightCol in Spark 2.4 (BaggingRegressor.scala:137-144, H10)
             warnings.warn(f"weightCol is ignored, as it is not supported by {type(bl).__name__} now.")
         L = self.get("numBaseLearners")
+        lb0, le0 = learner_range if learner_range is not None else (0, L)
+        if not (0 <= lb0 < le0 <= L):
+            raise nat.IllegalArgumentException(nat.SBAG_EINVAL, f"bad learner range {learner_range}")
         seed = self.get("seed")
         devices = self.devices or [0]
         if isinstance(dataset, Frame):
@@ -315,8 +327,8 @@ class _BaggingEstimator(_BaggingParams):
             make_ds = [lambda ctx, d=dataset: d]
         else:
             X, y = dataset
-            return self._train(Frame(X, y), bug_compat)
-        shards = _learner_shards(L, len(devices))
+            return self._train(Frame(X, y), bug_compat, learner_range)
+        shards = [(lb0 + a, lb0 + b) for a, b in _learner_shards(le0 - lb0, len(devices))]
         results = [None] * len(devices)
         errors = []
 
