@@ -43,9 +43,71 @@ namespace sbag {
 // was written before the batch, so all 5*WB LDS reads are issued up front; the
 // batch then leaves v[i-t] = z3_t (t < WB), v[i-WB] = z4_{WB-1} and the masked
 // v[i-WB-1] -- the same state the sequential recurrence leaves.
+//
+// 624 = 39 * 16: after one prologue step (index 0) every batch of 16 covers the
+// aligned block [16m, 16m+15] (i = 16m+15).  Its five read windows then wrap
+// around the ring end only for m in {0, 10, 27, 34}; every other batch reads each
+// window from one wave-uniform base with immediate offsets (no per-read wrap).
 constexpr int kWB = 16;
 
 __device__ __forceinline__ int wrap624(int x) { return x < 0 ? x + 624 : (x >= 624 ? x - 624 : x); }
+
+struct WellOut {
+  uint32_t o[kWB];  // next(26) of each step
+};
+
+// One batch of kWB steps at ring index i.  FAST: no read window wraps inside the
+// batch (bases wrapped once).  Returns the new ring index.
+template <bool FAST>
+__device__ __forceinline__ int well_batch(uint32_t* __restrict__ st, int lane, int i, uint32_t& v0,
+                                          WellOut& w) {
+  uint32_t m1[kWB], m2[kWB], m3[kWB], hb[kWB], lo[kWB], z3v[kWB];
+  if (FAST) {
+    // lowest address of each window, so every read is a non-negative immediate offset
+    const uint32_t* p1 = st + (wrap624(i + 70) - (kWB - 1)) * 64 + lane;
+    const uint32_t* p2 = st + (wrap624(i + 179) - (kWB - 1)) * 64 + lane;
+    const uint32_t* p3 = st + (wrap624(i - 175) - (kWB - 1)) * 64 + lane;
+    const uint32_t* ph = st + (i - 1 - kWB) * 64 + lane;  // m > 0 here: i - 1 - kWB >= 14
+#pragma unroll
+    for (int t = 0; t < kWB; t++) {
+      m1[t] = p1[(kWB - 1 - t) * 64];
+      m2[t] = p2[(kWB - 1 - t) * 64];
+      m3[t] = p3[(kWB - 1 - t) * 64];
+      hb[t] = ph[(kWB - t) * 64];
+      lo[t] = ph[(kWB - 1 - t) * 64];
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < kWB; t++) {
+      const int j = wrap624(i - t);
+      m1[t] = st[wrap624(j + 70) * 64 + lane];
+      m2[t] = st[wrap624(j + 179) * 64 + lane];
+      m3[t] = st[wrap624(j - 175) * 64 + lane];
+      hb[t] = st[wrap624(j - 1) * 64 + lane];
+      lo[t] = st[wrap624(j - 2) * 64 + lane];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < kWB; t++) {
+    const uint32_t z0 = (0x80000000u & hb[t]) ^ (0x7FFFFFFFu & lo[t]);
+    const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1[t] ^ (m1[t] >> 27));
+    const uint32_t z2 = (m2[t] >> 9) ^ (m3[t] ^ (m3[t] >> 1));
+    const uint32_t z3 = z1 ^ z2;
+    uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
+    z3v[t] = z3;
+    v0 = z4;
+    z4 ^= (z4 << 7) & 0xe46e1700u;
+    z4 ^= (z4 << 15) & 0x9b868000u;
+    w.o[t] = z4 >> 6;  // next(26)
+  }
+  // the written block [i-15, i] never wraps (aligned batches)
+  uint32_t* pw = st + (i - kWB + 1) * 64 + lane;
+#pragma unroll
+  for (int t = 0; t < kWB; t++) pw[(kWB - 1 - t) * 64] = z3v[t];
+  st[wrap624(i - kWB) * 64 + lane] = v0;
+  st[wrap624(i - kWB - 1) * 64 + lane] = lo[kWB - 1] & 0x80000000u;
+  return wrap624(i - kWB);
+}
 
 __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, int64_t N,
                                                 const int64_t* __restrict__ part_off, int P, int R,
@@ -72,74 +134,55 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
   int64_t row = active ? part_off[p] : 0;
   const int64_t row_end = active ? part_off[p + 1] : 0;
   uint8_t* out = counts + (int64_t)r * N;
-  int index = 0;
-  uint32_t v0 = st[lane];
   const double cap = 1000.0 * mean;
   int n = 0, bad = 0;
   double racc = 1.0;
-  uint64_t wbuf = 0;      // counts of rows [wrow0, row), one byte each
-  int64_t wrow0 = row;
+  uint32_t v0 = st[lane];
+  // prologue: the single step at index 0, leaving index 623 = 16*38+15
+  uint32_t pending;  // next(26) of the prologue step, first half of the first double
+  {
+    const uint32_t m1 = st[70 * 64 + lane], m2 = st[179 * 64 + lane], m3 = st[449 * 64 + lane];
+    const uint32_t hb = st[623 * 64 + lane], lo = st[622 * 64 + lane];
+    const uint32_t z0 = (0x80000000u & hb) ^ (0x7FFFFFFFu & lo);
+    const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1 ^ (m1 >> 27));
+    const uint32_t z2 = (m2 >> 9) ^ (m3 ^ (m3 >> 1));
+    const uint32_t z3 = z1 ^ z2;
+    uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
+    st[lane] = z3;
+    st[623 * 64 + lane] = z4;
+    st[622 * 64 + lane] = lo & 0x80000000u;
+    v0 = z4;
+    z4 ^= (z4 << 7) & 0xe46e1700u;
+    z4 ^= (z4 << 15) & 0x9b868000u;
+    pending = z4 >> 6;
+  }
+  int index = 623;
+  WellOut w;
   while (__any(row < row_end)) {
-    uint32_t m1[kWB], m2[kWB], m3[kWB], hb[kWB], lo[kWB], z3v[kWB], o[kWB];
-#pragma unroll
-    for (int t = 0; t < kWB; t++) {
-      const int i = wrap624(index - t);
-      m1[t] = st[wrap624(i + 70) * 64 + lane];
-      m2[t] = st[wrap624(i + 179) * 64 + lane];
-      m3[t] = st[wrap624(i + 449 - 624) * 64 + lane];
-      hb[t] = st[wrap624(i - 1) * 64 + lane];
-      lo[t] = st[wrap624(i - 2) * 64 + lane];
-    }
-#pragma unroll
-    for (int t = 0; t < kWB; t++) {
-      const uint32_t z0 = (0x80000000u & hb[t]) ^ (0x7FFFFFFFu & lo[t]);
-      const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1[t] ^ (m1[t] >> 27));
-      const uint32_t z2 = (m2[t] >> 9) ^ (m3[t] ^ (m3[t] >> 1));
-      const uint32_t z3 = z1 ^ z2;
-      uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
-      z3v[t] = z3;
-      v0 = z4;
-      z4 ^= (z4 << 7) & 0xe46e1700u;
-      z4 ^= (z4 << 15) & 0x9b868000u;
-      o[t] = z4 >> 6;  // next(26)
-    }
-#pragma unroll
-    for (int t = 0; t < kWB; t++) st[wrap624(index - t) * 64 + lane] = z3v[t];
-    st[wrap624(index - kWB) * 64 + lane] = v0;
-    st[wrap624(index - kWB - 1) * 64 + lane] = lo[kWB - 1] & 0x80000000u;
-    index = wrap624(index - kWB);
+    const int m = index >> 4;
+    if (m == 0 || m == 10 || m == 27 || m == 34)
+      index = well_batch<false>(st, lane, index, v0, w);
+    else
+      index = well_batch<true>(st, lane, index, v0, w);
+    // doubles: (pending, o0), (o1, o2), ..., (o13, o14); o15 carries over
 #pragma unroll
     for (int u = 0; u < kWB / 2; u++) {
-      const double x = (double)((((uint64_t)o[2 * u]) << 26) | (uint64_t)o[2 * u + 1]) * 0x1.0p-52;
+      const uint32_t hi = u == 0 ? pending : w.o[2 * u - 1];
+      const double x = (double)((((uint64_t)hi) << 26) | (uint64_t)w.o[2 * u]) * 0x1.0p-52;
       if (row < row_end) {
         racc *= x;
-        bool emit;
-        if (racc >= p_exp) {
-          n++;
-          emit = !((double)n < cap);
-        } else {
-          emit = true;
-        }
-        if (emit) {
-          if (n > 255) bad = 1;
-          wbuf |= (uint64_t)(n > 255 ? 255 : n) << (8 * (int)(row - wrow0));
+        const bool ge = racc >= p_exp;
+        n += ge ? 1 : 0;
+        if (!ge || !((double)n < cap)) {
+          bad |= n > 255;
+          out[row] = (uint8_t)(n > 255 ? 255 : n);
           row++;
           n = 0;
           racc = 1.0;
-          if ((((uintptr_t)(out + row)) & 7) == 0 || row == row_end) {  // flush 8 counts
-            uint8_t* dst = out + wrow0;
-            const int nb = (int)(row - wrow0);
-            if (nb == 8) {
-              *(uint64_t*)dst = wbuf;
-            } else {
-              for (int j = 0; j < nb; j++) dst[j] = (uint8_t)(wbuf >> (8 * j));
-            }
-            wbuf = 0;
-            wrow0 = row;
-          }
         }
       }
     }
+    pending = w.o[kWB - 1];
   }
   if (bad) atomicOr(err, 1);
 }
@@ -405,11 +448,11 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* sme
     const uint64_t MS = (1ull << cs) - 1;
     for (int q = tid; q < ftn * NB; q += blockDim.x) {
       const int b = q % NB, f = q / NB;
-      const uint64_t w0 = h64[((size_t)b * FPH + f) * 2];
+      const uint64_t w0 = h64[(size_t)b * FPH + f];
       if (w0) {
         const uint64_t cnt = w0 >> cs;
         const int64_t sk = (int64_t)(w0 & MS) - (int64_t)A.K0 * (int64_t)cnt;
-        const uint64_t w1 = h64[((size_t)b * FPH + f) * 2 + 1];
+        const uint64_t w1 = h64[((size_t)NB + b) * FPH + f];
         const int64_t gb = ((int64_t)(ft0 + f) * NB + b) * 3;
         atomicAdd(&gh[gb], (unsigned long long)cnt);
         atomicAdd(&gh[gb + 1], (unsigned long long)sk);
@@ -461,6 +504,7 @@ __device__ __forceinline__ void hist_tile(const HistArgs& A, const HistCtx& c, H
                                           const ParentInfo& pi, int parent, int t,
                                           const int (&posr)[4], const uint32_t (&amul)[4],
                                           const uint32_t (&abase)[4], const uint32_t (&amask)[4],
+                                          const uint32_t (&aoff1)[4],
                                           bool do_write, int slot, unsigned char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -567,21 +611,17 @@ __device__ __forceinline__ void hist_tile(const HistArgs& A, const HistCtx& c, H
           for (int jj = 0; jj < NJ; jj++) {
             const uint32_t addr = (__umul24(bb[u][jj], amul[jj]) + abase[jj]) + (coff & amask[jj]);
             atomicAdd((uint32_t*)(smem + addr), w[u].y);
-            if (A.ablate & 1) asm volatile("" ::"v"(addr));
           }
         } else {
           const unsigned long long w0 = ((unsigned long long)w[u].y << 32) | w[u].x;
           const unsigned long long w1 = ((unsigned long long)(w[u].w & 0xffffffu) << 32) | w[u].z;
 #pragma unroll
           for (int jj = 0; jj < NJ; jj++) {
-            const uint32_t addr = (__umul24(bb[u][jj], amul[jj]) + abase[jj]);
-            unsigned long long* h = (unsigned long long*)(smem + addr);
-            if (A.ablate & 1) {
-              asm volatile("" ::"v"(addr), "v"(w0), "v"(w1));
-            } else {
-              atomicAdd(h, w0);
-              atomicAdd(h + 1, w1);
-            }
+            // w0 plane at [bin][FPH], w1 plane `plane1` bytes later: a 16-lane group
+            // of 8-B atomics covers 128 contiguous bytes = all 32 banks
+            const uint32_t addr = __umul24(bb[u][jj], amul[jj]) + abase[jj];
+            atomicAdd((unsigned long long*)(smem + addr), w0);
+            atomicAdd((unsigned long long*)(smem + addr + aoff1[jj]), w1);
           }
         }
       }
@@ -600,8 +640,9 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 1
 
   // histogram words + one dump slot per lane (targets of masked-off lanes)
   const size_t words = GINI ? (size_t)A.NS * NB * FPH : (size_t)2 * NB * FPH;
-  const size_t hist_bytes = GINI ? words * 4 + 64 * 4 : words * 8 + 64 * 16;
-  const uint32_t dump = (uint32_t)(GINI ? words * 4 + lane * 4 : words * 8 + lane * 16);
+  const size_t hist_bytes = GINI ? words * 4 + 64 * 4 : words * 8 + 65 * 8;
+  // dump slots: 4 / 8 B stride so the masked lanes of one instruction hit distinct banks
+  const uint32_t dump = (uint32_t)(GINI ? words * 4 + lane * 4 : words * 8 + lane * 8);
   HistCtx c;
   size_t off = align16(hist_bytes);
   c.tile = smem + off;
@@ -630,6 +671,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 1
   int64_t acc = 0;
   int posr[4] = {0, 0, 0, 0};
   uint32_t amul[4] = {0, 0, 0, 0}, abase[4] = {dump, dump, dump, dump}, amask[4] = {0, 0, 0, 0};
+  uint32_t aoff1[4] = {8, 8, 8, 8};
   HistState st;
   __syncthreads();
 
@@ -662,9 +704,10 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 1
         const int fl = lane + 64 * j;
         const bool ok = fl < ftn;
         posr[j] = ok ? A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0;
-        amul[j] = ok ? (uint32_t)FPH * (GINI ? 4u : 16u) : 0u;
-        abase[j] = ok ? (uint32_t)fl * (GINI ? 4u : 16u) : dump;
+        amul[j] = ok ? (uint32_t)FPH * (GINI ? 4u : 8u) : 0u;
+        abase[j] = ok ? (uint32_t)fl * (GINI ? 4u : 8u) : dump;
         amask[j] = ok ? 0xffffffffu : 0u;
+        aoff1[j] = ok ? (uint32_t)NB * FPH * 8u : 8u;
       }
       cur_r = r;
     }
@@ -689,11 +732,11 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 1
     st.ereg[1] = load_entry(c, 4, tid);
     st.ereg[2] = load_entry(c, 5, tid);
     for (int t = 0; t < c.ntile; t += 3) {
-      hist_tile<GINI, NJ, 0>(A, c, st, pi, pc.parent, t, posr, amul, abase, amask, do_write, slot, smem);
+      hist_tile<GINI, NJ, 0>(A, c, st, pi, pc.parent, t, posr, amul, abase, amask, aoff1, do_write, slot, smem);
       if (t + 1 >= c.ntile) break;
-      hist_tile<GINI, NJ, 1>(A, c, st, pi, pc.parent, t + 1, posr, amul, abase, amask, do_write, slot, smem);
+      hist_tile<GINI, NJ, 1>(A, c, st, pi, pc.parent, t + 1, posr, amul, abase, amask, aoff1, do_write, slot, smem);
       if (t + 2 >= c.ntile) break;
-      hist_tile<GINI, NJ, 2>(A, c, st, pi, pc.parent, t + 2, posr, amul, abase, amask, do_write, slot, smem);
+      hist_tile<GINI, NJ, 2>(A, c, st, pi, pc.parent, t + 2, posr, amul, abase, amask, aoff1, do_write, slot, smem);
     }
   }
   if (cur_slot >= 0) {
