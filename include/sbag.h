@@ -146,6 +146,7 @@ typedef struct {
   double hist_entries;     /* Σ entries processed by hist launches                    */
   double hist_upper_bytes; /* SURVEY §8d upper bound: Σ_r Σ_d inbag_r x (F_r + 4) + 3N */
   int64_t levels;
+  double partition_ms;     /* k_partition: rows of split nodes -> child segments      */
 } sbag_timing;
 int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
 

@@ -493,7 +493,7 @@ struct EventTimer {
     }
   }
 };
-enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_NCAT };
+enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_NCAT };
 
 // ---------------------------------------------------------------- C ABI
 extern "C" {
@@ -778,11 +778,10 @@ struct HistGeom {
 static int roundup(int x, int a) { return (x + a - 1) / a * a; }
 
 static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g) {
-  g.T = std::max(16, std::min(128, 32768 / S));  // npass <= 2 at 512 threads
+  (void)S;
+  g.T = 64;  // piece granularity (entries)
   const int align = gini_layout ? 32 : 16;
-  auto lds_for = [&](int ft) {
-    return hist_lds_bytes(S, g.T, NB, NS, roundup(ft, align), gini_layout);
-  };
+  auto lds_for = [&](int ft) { return hist_lds_bytes(NB, NS, roundup(ft, align), gini_layout); };
   int ft = std::min(256, roundup(Fmax, align));
   const size_t soft = 80 * 1024, hard = 160 * 1024 - 256;
   while (ft > align && lds_for(ft) > soft) ft -= align;
@@ -992,7 +991,6 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     return SBAG_OK;
   };
   HistArgs ha{};
-  if (const char* ab = std::getenv("SBAG_HIST_ABLATE")) ha.ablate = std::atoi(ab);  // timing only
   ha.Fmax = Fmax;
   ha.Fr = d_Fr;
   ha.K0 = (int32_t)K0;
@@ -1009,7 +1007,6 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     ha.chunks = d_pieces;
     ha.wg_piece = d_wg;
     ha.parents = d_par;
-    ha.T = g.T;
     ha.FT = g.FT;
     ha.FPH = g.FPH;
     int h = tm.begin(cat);
@@ -1053,12 +1050,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     ha.S = ds->S;
     ha.pos = d_pos;
     ha.ent_in = entA;
-    ha.ent_out = nullptr;
-    ha.cursors = nullptr;
     ha.hist = hist_cur;
     ha.NB = ncmax;
     ha.NS = NS;
-    ha.do_write = 0;
     ha.count_only = 0;
     TRY(launch(g0, gini, T_HIST, seg, h_par));
     const int64_t words = (int64_t)R * Fmax * ncmax * NS;
@@ -1092,13 +1086,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       ha.S = ds->S;
       ha.pos = d_pos;
       ha.ent_in = entA;
-      ha.ent_out = nullptr;
-      ha.cursors = nullptr;
       ha.hist = d_vch;
       ha.NB = ncmax;
       ha.NS = 1;
-      ha.do_write = 0;
-      ha.count_only = 1;
+        ha.count_only = 1;
       TRY(launch(g, true, T_VC, seg, h_par));
       ha = save;
       std::vector<uint32_t> tmp((size_t)R * slot_words);
@@ -1264,10 +1255,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     TRY(ws_get(c, "histA", (size_t)R * slot_words * word_bytes, &hist_cur));
     HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * slot_words * word_bytes, c->stream));
     ha.ent_in = entA;
-    ha.ent_out = nullptr;
-    ha.cursors = nullptr;
     ha.hist = hist_cur;
-    ha.do_write = 0;
     TRY(launch(g, gini, T_HIST, seg, h_par));
   }
   for (int r = 0; r < R; r++) hist_upper += (double)inbag[r] * (h_Fr[r] + 4) * D + 3.0 * N * D;
@@ -1400,11 +1388,8 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       pseg.push_back(seg[i]);
     }
     if (next_slots.empty()) break;
-    // --- route rows + histograms of level+1
+    // --- partition the rows of every split node into its children
     const int Mn = (int)next_slots.size();
-    void* hist_nxt;
-    TRY(ws_get(c, hist_nxt_name, (size_t)Mn * slot_words * word_bytes, &hist_nxt));
-    HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * slot_words * word_bytes, c->stream));
     const int NP = (int)par.size();
     std::vector<unsigned long long> cur((size_t)2 * NP);
     for (int q = 0; q < NP; q++) {
@@ -1414,18 +1399,21 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     unsigned long long* d_cur;
     TRY(ws_typed(c, "cursors", cur.size(), &d_cur));
     TRY(h2d(c, d_cur, cur.data(), cur.size()));
-    ha.ent_in = ent_cur;
-    ha.ent_out = ent_nxt;
-    ha.cursors = d_cur;
-    ha.hist = hist_nxt;
-    ha.do_write = 1;
-    TRY(launch(g, gini, T_HIST, pseg, par));
-    if (!triples.empty()) {
-      int32_t* d_tri;
-      TRY(ws_typed(c, "triples", triples.size(), &d_tri));
-      TRY(h2d(c, d_tri, triples.data(), triples.size()));
-      int h = tm.begin(T_SUB);
-      launch_subtract(c->stream, hist_nxt, hist_cur, d_tri, (int)triples.size() / 3, slot_words, gini);
+    {
+      build_work(pseg, (int64_t)1 << 40, 256 * 8, 1024, work);
+      TRY(upload_work(par));
+      PartArgs pa{};
+      pa.bins = d_bins;
+      pa.bins_rstride = bins_rstride;
+      pa.S = S;
+      pa.chunks = d_pieces;
+      pa.wg_piece = d_wg;
+      pa.parents = d_par;
+      pa.ent_in = ent_cur;
+      pa.ent_out = ent_nxt;
+      pa.cursors = d_cur;
+      int h = tm.begin(T_PART);
+      launch_partition(c->stream, pa, work.nwg);
       HIP_TRY(hipGetLastError());
       tm.end(h);
     }
@@ -1437,6 +1425,30 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
         nseg[k] = {pseg[pd.parent].first, (int64_t)cur[2 * pd.parent]};
       else
         nseg[k] = {(int64_t)cur[2 * pd.parent + 1], pseg[pd.parent].second};
+    }
+    // --- histograms of level+1: the smaller (or only) child of each split node
+    std::vector<std::pair<int64_t, int64_t>> hseg;
+    std::vector<ParentInfo> hpar;
+    for (int k = 0; k < Mn; k++) {
+      const ParentInfo& pp = par[pend[k].parent];
+      if (pp.hist_slot != k) continue;
+      hseg.push_back(nseg[k]);
+      hpar.push_back(ParentInfo{pp.r, -1, 0, 0, 0, k, 0, 0});
+    }
+    void* hist_nxt;
+    TRY(ws_get(c, hist_nxt_name, (size_t)Mn * slot_words * word_bytes, &hist_nxt));
+    HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * slot_words * word_bytes, c->stream));
+    ha.ent_in = ent_nxt;
+    ha.hist = hist_nxt;
+    TRY(launch(g, gini, T_HIST, hseg, hpar));
+    if (!triples.empty()) {
+      int32_t* d_tri;
+      TRY(ws_typed(c, "triples", triples.size(), &d_tri));
+      TRY(h2d(c, d_tri, triples.data(), triples.size()));
+      int h = tm.begin(T_SUB);
+      launch_subtract(c->stream, hist_nxt, hist_cur, d_tri, (int)triples.size() / 3, slot_words, gini);
+      HIP_TRY(hipGetLastError());
+      tm.end(h);
     }
     seg = nseg;
     slots = next_slots;
@@ -1480,6 +1492,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   T.hist_ms = cats[T_HIST];
   T.split_ms = cats[T_SPLIT];
   T.subtract_ms = cats[T_SUB];
+  T.partition_ms = cats[T_PART];
   T.hist_launches = hist_launches;
   T.hist_alg_bytes = hist_alg_bytes;
   T.hist_entries = hist_entries;

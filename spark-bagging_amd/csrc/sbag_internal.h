@@ -38,22 +38,32 @@ struct HistArgs {
   int32_t Fmax;
   const int16_t* pos;    // [R][Fmax] byte position of local feature fl in a row
   const int32_t* Fr;     // [R]
-  const HistChunk* chunks;   // pieces: slices of parent segments, in parent order
+  const HistChunk* chunks;   // pieces: slices of node segments, in node order
   const int32_t* wg_piece;   // [nwg + 1]: workgroup w walks pieces [wg_piece[w], wg_piece[w+1])
-  const ParentInfo* parents;
+  const ParentInfo* parents; // per segment: replica (r) and histogram slot (hist_slot)
   const uint64_t* ent_in;
-  uint64_t* ent_out;
-  unsigned long long* cursors;  // [2 * parents]: left cursor (grows), right cursor (shrinks)
   void* hist;            // [slot][Fmax][NB][NS] u64 (variance) or u32 (gini / counts)
   int32_t NB, NS;
   int32_t K0;            // label offset for the packed LDS word (variance)
   int32_t cshift;        // bit position of the count field in the packed word
   int64_t flush_limit;   // max entries accumulated in LDS between flushes
-  int32_t FT, FPH, FPW;  // features per tile, LDS pitch, thread-feature width (pow2)
-  int32_t T;             // rows per tile
-  int32_t do_write;      // route + write entries (levels > 0)
+  int32_t FT, FPH;       // features per tile, LDS pitch
   int32_t count_only;    // gini layout with the label ignored (value counts)
-  int32_t ablate;        // timing-only builds: 1 skip atomics, 2 skip accumulate, 4 skip writes
+  int32_t pad;
+};
+
+// k_partition: entries of each split node -> left block (from the segment start,
+// cursors[2p] grows) and right block (from the segment end, cursors[2p+1] shrinks)
+struct PartArgs {
+  const uint8_t* bins;
+  int64_t bins_rstride;
+  int32_t S, pad;
+  const HistChunk* chunks;
+  const int32_t* wg_piece;
+  const ParentInfo* parents;  // r, pos (split column), s (split bin), write_l, write_r
+  const uint64_t* ent_in;
+  uint64_t* ent_out;
+  unsigned long long* cursors;
 };
 
 struct SplitOut {
@@ -97,7 +107,8 @@ void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, con
                     unsigned long long* d_wsum, unsigned int* d_cmax);
 void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gini,
                  size_t lds_bytes);
-size_t hist_lds_bytes(int S, int T, int NB, int NS, int FPH, bool gini);
+size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini);
+void launch_partition(hipStream_t st, const PartArgs& a, int nwg);
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini);
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words);

@@ -7,9 +7,11 @@
 //                 (Rand at sql/bfunctions.scala:62-64)
 //   k_compact     per-replica in-bag row lists (replaces explode/replicate_row,
 //                 sql/bfunctions.scala:42-44, HasSubBag.scala:112-114)
-//   k_hist        fused route-rows + LDS-privatized histogram (the hot loop of
-//                 Spark's RandomForest.findBestSplits, reached via
+//   k_hist        streaming LDS-privatized histogram (the hot loop of Spark's
+//                 RandomForest.findBestSplits, reached via
 //                 ml/ensemble/ensembleParams.scala:113-115)
+//   k_partition   rows of each split node -> its children (RandomForest's
+//                 node-index update of every TreePoint per level)
 //   k_split       prefix scan over bins + fp64 gain + first-max argmax
 //                 (RandomForest.binsToBestSplit / calculateImpurityStats)
 //   k_subtract    sibling histogram = parent - smaller child
@@ -402,57 +404,66 @@ void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, con
 }
 
 // ======================================================================
-// Fused route + histogram (the hot kernel).
+// Histogram (the hot kernel) and the row partition that feeds it.
 //
-// Grid: (workgroups, feature tiles).  Workgroup w walks the pieces
-// [wg_piece[w], wg_piece[w+1]) -- contiguous slices of parent segments, in
-// parent order -- and keeps the histogram of the current parent's child in LDS
-// until the parent changes (or flush_limit entries were added), so a flush of
-// Fr x NB bins happens once per (workgroup, parent run), not per tile.
-// Per tile of T entries the loop is software-pipelined:
-//   top:  staged rows of tile t (registers) -> LDS, split byte captured by the
-//         lane holding it; entries of tile t+1 -> LDS; weights of tile t
-//   B1:   issue the 16-B gathers of tile t+1's rows and the loads of tile t+2's
-//         entries (in flight during the LDS work below)
-//         route tile t: left/right by the parent's split, append to the child
-//         segments (wave ballot, one global atomic per wave and side), compact
-//         the entries of the histogram child into s_list
-//   B2:   wave-per-entry accumulation: lane -> feature, [word][bin][feature]
-//         layout so every lane group hits distinct banks whatever the bins
-//   B3
-// Variance stats are two u64 words per (bin, feature): (count << cshift) +
+// k_hist streams the entries of the nodes being histogrammed; LDS holds only
+// the histogram.  Grid (workgroups, feature tiles): workgroup w walks pieces
+// [wg_piece[w], wg_piece[w+1]) -- contiguous slices of node segments, in node
+// order -- and keeps the current node's histogram in LDS until the node changes
+// (or flush_limit entries were added), so a flush of Fr x NB bins happens once
+// per (workgroup, node run).  Inside a run the waves are independent (no
+// barrier): each takes batches of 64 consecutive entries; lane i loads entry i
+// and computes its stat words, then for every entry of the batch the wave
+// broadcasts row and words (readlane), lane fl loads byte pos[fl] of that row
+// straight from the row's cache line (global_load_ubyte, SGPR row base + VGPR
+// column) one group of 8 entries ahead, and adds the words into
+// [plane][bin][feature] with one LDS atomic per plane.  The LDS atomic pipe is
+// the only shared resource, and it only carries the atomics.
+//
+// Variance stats are two u64 planes per (bin, feature): (count << cshift) +
 // count*(k + K0) and count*k^2 -- integers, so the result is order-independent
-// and bit-exact; the field split `cshift` and flush_limit are chosen on the host
-// from the label range and the largest count.
+// and bit-exact; cshift and flush_limit are chosen on the host from the label
+// range and the largest count.  Gini: one u32 plane per class.  Each plane has
+// 64 trailing dump words: lanes past the tile's features add there (amul = 0),
+// so the accumulation is branch-free.
+//
+// k_partition routes the entries of each split node into its two children
+// (left block grows from the segment start, right block from its end), one
+// cursor atomic per wave and side for 256 entries.
 // ======================================================================
-static __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+constexpr int kHistThreads = 512;  // 8 waves; two workgroups per CU at <= 80 KB of LDS
+constexpr int kHistWaves = kHistThreads / 64;
+constexpr int kG = 8;              // entries per pipeline group
+
+static __host__ __device__ inline uint32_t hist_plane_bytes(int NB, int FPH, bool gini) {
+  return (uint32_t)(NB * FPH + 64) * (gini ? 4u : 8u);
+}
 
 template <bool GINI>
-__device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* smem, int slot,
-                                           int ft0, int ftn) {
+__device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned char* smem,
+                                           uint32_t plane, int slot, int ft0, int ftn) {
   const int tid = threadIdx.x;
   const int NB = A.NB, NS = A.NS, FPH = A.FPH;
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
   if (GINI) {
-    const uint32_t* h32 = (const uint32_t*)smem;
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
     for (int q = tid; q < ftn * NB * NS; q += blockDim.x) {
       const int cls = q % NS, b = (q / NS) % NB, f = q / (NS * NB);
-      const uint32_t v = h32[((size_t)cls * NB + b) * FPH + f];
+      const uint32_t v = *(const uint32_t*)(smem + (size_t)cls * plane + ((size_t)b * FPH + f) * 4);
       if (v) atomicAdd(&gh[((int64_t)(ft0 + f) * NB + b) * NS + cls], v);
     }
   } else {
-    const uint64_t* h64 = (const uint64_t*)smem;
     unsigned long long* gh = (unsigned long long*)A.hist + (int64_t)slot * slot_words;
     const int cs = A.cshift;
     const uint64_t MS = (1ull << cs) - 1;
     for (int q = tid; q < ftn * NB; q += blockDim.x) {
       const int b = q % NB, f = q / NB;
-      const uint64_t w0 = h64[(size_t)b * FPH + f];
+      const size_t o = ((size_t)b * FPH + f) * 8;
+      const uint64_t w0 = *(const uint64_t*)(smem + o);
       if (w0) {
         const uint64_t cnt = w0 >> cs;
         const int64_t sk = (int64_t)(w0 & MS) - (int64_t)A.K0 * (int64_t)cnt;
-        const uint64_t w1 = h64[((size_t)NB + b) * FPH + f];
+        const uint64_t w1 = *(const uint64_t*)(smem + plane + o);
         const int64_t gb = ((int64_t)(ft0 + f) * NB + b) * 3;
         atomicAdd(&gh[gb], (unsigned long long)cnt);
         atomicAdd(&gh[gb + 1], (unsigned long long)sk);
@@ -462,217 +473,81 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, unsigned char* sme
   }
 }
 
-constexpr int kHistThreads = 512;  // 8 waves; two workgroups per CU at <= 80 KB of LDS
-constexpr int kHistWaves = kHistThreads / 64;
-constexpr int kDepth = 3;           // tiles of rows in flight per workgroup (register ring)
-
-struct HistState {  // per-thread pipeline registers
-  uint4 rreg[kDepth][2];
-  uint64_t ereg[kDepth];
-};
-
-struct HistCtx {  // per-piece constants + LDS carve
-  const uint8_t* binsr;
-  const uint64_t* ent_in;
-  int64_t a, b;
-  int ntile, T, S, npass, rpp, grow, gpart, spos, spart, sbyte, ssplit;
-  uint8_t* tile;
-  uint64_t* s_e;  // ring of 4 tiles of entries: tile t at s_e + (t & 3) * T
-  uint4* s_wl;
-  uint8_t* s_side;
-  int* s_cnt;
-};
-
-__device__ __forceinline__ void issue_rows(const HistCtx& c, int t, const uint64_t* se, uint4 (&rr)[2]) {
-  if (t >= c.ntile) return;
-  const int nt = (int)min((int64_t)c.T, c.b - (c.a + (int64_t)t * c.T));
-#pragma unroll
-  for (int q = 0; q < 2; q++) {
-    const int i = q * c.rpp + c.grow;
-    if (q < c.npass && c.grow < c.rpp && i < nt)
-      rr[q] = *((const uint4*)(c.binsr + (int64_t)(uint32_t)se[i] * c.S) + c.gpart);
-  }
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
-__device__ __forceinline__ uint64_t load_entry(const HistCtx& c, int t, int tid) {
-  const int64_t i = c.a + (int64_t)t * c.T + tid;
-  return (tid < c.T && t < c.ntile && i < c.b) ? c.ent_in[i] : 0ull;
-}
-
-template <bool GINI, int NJ, int SLOT>
-__device__ __forceinline__ void hist_tile(const HistArgs& A, const HistCtx& c, HistState& st,
-                                          const ParentInfo& pi, int parent, int t,
-                                          const int (&posr)[4], const uint32_t (&amul)[4],
-                                          const uint32_t (&abase)[4], const uint32_t (&amask)[4],
-                                          const uint32_t (&aoff1)[4],
-                                          bool do_write, int slot, unsigned char* smem) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  const int64_t base = c.a + (int64_t)t * c.T;
-  const int nt = (int)min((int64_t)c.T, c.b - base);
-  uint64_t* s_ec = c.s_e + (size_t)(t & 3) * c.T;
-  uint64_t* s_e3 = c.s_e + (size_t)((t + 3) & 3) * c.T;
-  // ---- top: commit staged rows of tile t (+ split byte); entries of tile t+3 -> LDS
+// bytes of the NJ feature columns of entries [u0, u0 + kG) of the batch
+template <int NJ>
+__device__ __forceinline__ void hist_load_group(const uint8_t* __restrict__ binsr, uint32_t S,
+                                                uint32_t row, int u0, const uint32_t (&posr)[NJ],
+                                                uint32_t (&buf)[kG][NJ]) {
 #pragma unroll
-  for (int q = 0; q < 2; q++) {
-    const int i = q * c.rpp + c.grow;
-    if (q < c.npass && c.grow < c.rpp && i < nt) {
-      const uint4 v = st.rreg[SLOT][q];
-      *((uint4*)(c.tile + (size_t)i * c.S) + c.gpart) = v;
-      if (c.spos >= 0 && c.gpart == c.spart) {
-        const uint32_t wd = (c.sbyte < 4) ? v.x : (c.sbyte < 8) ? v.y : (c.sbyte < 12) ? v.z : v.w;
-        c.s_side[i] = ((wd >> (8 * (c.sbyte & 3))) & 0xffu) <= (uint32_t)c.ssplit ? 0 : 1;
-      }
+  for (int t = 0; t < kG; t++) {
+    const uint8_t* rp = binsr + (size_t)rdlane(row, u0 + t) * S;  // wave-uniform (SGPRs)
+#pragma unroll
+    for (int jj = 0; jj < NJ; jj++) {
+      uint32_t off = posr[jj];
+      asm volatile("" : "+v"(off));  // keep the column a 32-bit VGPR offset: saddr form
+      buf[t][jj] = rp[off];
     }
   }
-  if (tid < c.T) s_e3[tid] = st.ereg[SLOT];
-  if (tid == 0) *c.s_cnt = 0;
-  __syncthreads();  // B1
-  // ---- prefetch: rows of tile t+3 (entries already in LDS), entries of tile t+6
-  issue_rows(c, t + 3, s_e3, st.rreg[SLOT]);
-  st.ereg[SLOT] = load_entry(c, t + 6, tid);
-  // ---- route tile t; compact the histogram child's entries with their weights
-  const int ntr = (nt + 63) & ~63;
-  if (tid < ntr) {
-    const bool valid = tid < nt;
-    const int side = (valid && c.spos >= 0) ? c.s_side[tid] : 0;
-    const uint64_t e = valid ? s_ec[tid] : 0ull;
-    if (do_write && !(A.ablate & 4)) {
-      const bool wl = valid && side == 0 && pi.write_l;
-      const bool wr = valid && side == 1 && pi.write_r;
-      const uint64_t ml = __ballot(wl), mr = __ballot(wr);
-      unsigned long long bl = 0, br = 0;
-      if (lane == 0) {
-        if (ml) bl = atomicAdd(&A.cursors[2 * parent], (unsigned long long)__popcll(ml));
-        if (mr) {
-          const unsigned long long nr = (unsigned long long)__popcll(mr);
-          br = atomicAdd(&A.cursors[2 * parent + 1], (unsigned long long)(-(long long)nr)) - nr;
-        }
-      }
-      bl = __shfl(bl, 0);
-      br = __shfl(br, 0);
-      if (wl) A.ent_out[bl + __popcll(ml & lt)] = e;
-      if (wr) A.ent_out[br + __popcll(mr & lt)] = e;
-    }
-    if (slot >= 0) {
-      const bool fl = valid && side == pi.hist_side;
-      const uint64_t mf = __ballot(fl);
-      int lbase = 0;
-      if (lane == 0 && mf) lbase = atomicAdd(c.s_cnt, (int)__popcll(mf));
-      lbase = __shfl(lbase, 0);
-      if (fl) {
-        const int32_t hi = (int32_t)(e >> 32);
-        const uint32_t cc = (uint32_t)hi & 0xffu;
-        const int32_t k = hi >> 8;
-        uint4 w;
-        if (GINI) {
-          w = make_uint4(A.count_only ? 0u : (uint32_t)k, cc, (uint32_t)tid, 0);
-        } else {
-          const uint64_t w0 = ((uint64_t)cc << A.cshift) + (uint64_t)cc * (uint64_t)(int64_t)(k + A.K0);
-          const uint64_t w1 = (uint64_t)cc * (uint64_t)((int64_t)k * (int64_t)k);  // < 2^56
-          w = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1,
-                         (uint32_t)(w1 >> 32) | ((uint32_t)tid << 24));
-        }
-        c.s_wl[lbase + __popcll(mf & lt)] = w;
-      }
-    }
-  }
-  __syncthreads();  // B2
-  // ---- accumulate: 4 entries per wave per step, branch-free so every LDS read
-  // of the step is issued before the atomics (counted lgkmcnt).  Each lane owns
-  // one feature column per 64-lane group jj; its histogram byte address for bin b
-  // is b * amul[jj] + abase[jj] (one 24-bit mad): variance words (w0, w1) are
-  // interleaved per (bin, feature) so one address serves both atomics; lanes past
-  // the tile's features have amul = 0 and a private dump slot.
-  if (slot >= 0 && !(A.ablate & 2)) {
-    const int cnt = *c.s_cnt;
-    const uint32_t S = (uint32_t)c.S;
-    constexpr int UB = (NJ <= 2) ? 4 : 2;  // entries per step (register budget)
-    for (int j0 = wave * UB; j0 < cnt; j0 += kHistWaves * UB) {
-      uint4 w[UB];
-      uint32_t bb[UB][NJ];
-#pragma unroll
-      for (int u = 0; u < UB; u++) {
-        const uint4 v = c.s_wl[j0 + u];
-        w[u] = (j0 + u < cnt) ? v : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < UB; u++) {
-        const uint32_t i = GINI ? w[u].z : (w[u].w >> 24);
-        const uint32_t rb = __umul24(i, S);
-#pragma unroll
-        for (int jj = 0; jj < NJ; jj++) bb[u][jj] = c.tile[rb + (uint32_t)posr[jj]];
-      }
-#pragma unroll
-      for (int u = 0; u < UB; u++) {
-        if (GINI) {
-          const uint32_t coff = __umul24(w[u].x, (uint32_t)A.NB * (uint32_t)A.FPH * 4u);
-#pragma unroll
-          for (int jj = 0; jj < NJ; jj++) {
-            const uint32_t addr = (__umul24(bb[u][jj], amul[jj]) + abase[jj]) + (coff & amask[jj]);
-            atomicAdd((uint32_t*)(smem + addr), w[u].y);
-          }
-        } else {
-          const unsigned long long w0 = ((unsigned long long)w[u].y << 32) | w[u].x;
-          const unsigned long long w1 = ((unsigned long long)(w[u].w & 0xffffffu) << 32) | w[u].z;
-#pragma unroll
-          for (int jj = 0; jj < NJ; jj++) {
-            // w0 plane at [bin][FPH], w1 plane `plane1` bytes later: a 16-lane group
-            // of 8-B atomics covers 128 contiguous bytes = all 32 banks
-            const uint32_t addr = __umul24(bb[u][jj], amul[jj]) + abase[jj];
-            atomicAdd((unsigned long long*)(smem + addr), w0);
-            atomicAdd((unsigned long long*)(smem + addr + aoff1[jj]), w1);
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();  // B3
 }
 
 template <bool GINI, int NJ>
-__global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 128 VGPRs: 2 WGs/CU
+__device__ __forceinline__ void hist_add_group(unsigned char* smem, uint32_t plane, int u0,
+                                               const uint32_t (&buf)[kG][NJ], uint32_t w0l,
+                                               uint32_t w0h, uint32_t w1l, uint32_t w1h,
+                                               const uint32_t (&amul)[NJ],
+                                               const uint32_t (&abase)[NJ]) {
+#pragma unroll
+  for (int t = 0; t < kG; t++) {
+    const int u = u0 + t;
+    if (GINI) {
+      const uint32_t cu = rdlane(w0l, u), cou = rdlane(w0h, u);
+#pragma unroll
+      for (int jj = 0; jj < NJ; jj++) {
+        const uint32_t addr = __umul24(buf[t][jj], amul[jj]) + abase[jj] + cou;
+        atomicAdd((uint32_t*)(smem + addr), cu);
+      }
+    } else {
+      const unsigned long long a0 = ((unsigned long long)rdlane(w0h, u) << 32) | rdlane(w0l, u);
+      const unsigned long long a1 = ((unsigned long long)rdlane(w1h, u) << 32) | rdlane(w1l, u);
+#pragma unroll
+      for (int jj = 0; jj < NJ; jj++) {
+        const uint32_t addr = __umul24(buf[t][jj], amul[jj]) + abase[jj];
+        atomicAdd((unsigned long long*)(smem + addr), a0);
+        atomicAdd((unsigned long long*)(smem + addr + plane), a1);
+      }
+    }
+  }
+}
+
+template <bool GINI, int NJ>
+__global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int NB = A.NB, FPH = A.FPH, S = A.S, T = A.T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NB = A.NB, FPH = A.FPH;
+  const uint32_t S = (uint32_t)A.S;
   const int ft0 = blockIdx.y * A.FT;
-  const bool tile0 = blockIdx.y == 0;
+  constexpr uint32_t WB = GINI ? 4u : 8u;
+  const uint32_t plane = hist_plane_bytes(NB, FPH, GINI);
+  const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.NS : 2u);
+  const uint32_t dump = (uint32_t)NB * FPH * WB + (uint32_t)lane * WB;  // inside plane 0
 
-  // histogram words + one dump slot per lane (targets of masked-off lanes)
-  const size_t words = GINI ? (size_t)A.NS * NB * FPH : (size_t)2 * NB * FPH;
-  const size_t hist_bytes = GINI ? words * 4 + 64 * 4 : words * 8 + 65 * 8;
-  // dump slots: 4 / 8 B stride so the masked lanes of one instruction hit distinct banks
-  const uint32_t dump = (uint32_t)(GINI ? words * 4 + lane * 4 : words * 8 + lane * 8);
-  HistCtx c;
-  size_t off = align16(hist_bytes);
-  c.tile = smem + off;
-  off += align16((size_t)T * S);
-  c.s_e = (uint64_t*)(smem + off);
-  off += (size_t)T * 8 * 4;
-  c.s_wl = (uint4*)(smem + off);
-  off += (size_t)T * 16;
-  c.s_side = smem + off;
-  off += align16((size_t)T);
-  c.s_cnt = (int*)(smem + off);
-  c.T = T;
-  c.S = S;
-  const int lpr = S >> 4;
-  c.rpp = kHistThreads / lpr;
-  c.npass = (T + c.rpp - 1) / c.rpp;  // <= 2 (host: T * S <= 32 KB)
-  c.grow = tid / lpr;
-  c.gpart = tid - c.grow * lpr;
-  c.ent_in = A.ent_in;
-
-  for (size_t i = (size_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
+  for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
     *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 
   const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
   int cur_slot = -1, cur_ftn = 0, cur_r = -1;
   int64_t acc = 0;
-  int posr[4] = {0, 0, 0, 0};
-  uint32_t amul[4] = {0, 0, 0, 0}, abase[4] = {dump, dump, dump, dump}, amask[4] = {0, 0, 0, 0};
-  uint32_t aoff1[4] = {8, 8, 8, 8};
-  HistState st;
+  uint32_t posr[NJ], amul[NJ], abase[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; j++) {
+    posr[j] = 0;
+    amul[j] = 0;
+    abase[j] = dump;
+  }
   __syncthreads();
 
   for (int p = p0; p < p1; p++) {
@@ -680,18 +555,17 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 1
     const ParentInfo pi = A.parents[pc.parent];
     const int r = pi.r;
     const int ftn = min(A.FT, A.Fr[r] - ft0);
-    if (ftn <= 0) continue;
-    const bool do_write = tile0 && A.do_write;
     const int slot = pi.hist_slot;
-    if (slot < 0 && !do_write) continue;
+    if (ftn <= 0 || slot < 0) continue;
     const int64_t a = pc.a, b = pc.b;
     if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
-        hist_flush<GINI>(A, smem, cur_slot, ft0, cur_ftn);
+        hist_flush<GINI>(A, smem, plane, cur_slot, ft0, cur_ftn);
         __syncthreads();
-        for (size_t i = (size_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
+        for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
           *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+        __syncthreads();
       }
       cur_slot = slot;
       cur_ftn = ftn;
@@ -700,54 +574,66 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {  // <= 1
     acc += b - a;
     if (r != cur_r) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < NJ; j++) {
         const int fl = lane + 64 * j;
         const bool ok = fl < ftn;
-        posr[j] = ok ? A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0;
-        amul[j] = ok ? (uint32_t)FPH * (GINI ? 4u : 8u) : 0u;
-        abase[j] = ok ? (uint32_t)fl * (GINI ? 4u : 8u) : dump;
-        amask[j] = ok ? 0xffffffffu : 0u;
-        aoff1[j] = ok ? (uint32_t)NB * FPH * 8u : 8u;
+        posr[j] = ok ? (uint32_t)A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0u;
+        amul[j] = ok ? (uint32_t)FPH * WB : 0u;
+        abase[j] = ok ? (uint32_t)fl * WB : dump;
       }
       cur_r = r;
     }
-    c.binsr = A.bins + (int64_t)r * A.bins_rstride;
-    c.a = a;
-    c.b = b;
-    c.ntile = (int)((b - a + T - 1) / T);
-    c.spos = pi.pos;
-    c.spart = pi.pos >> 4;
-    c.sbyte = pi.pos & 15;
-    c.ssplit = pi.s;
-
-    // prologue: entries of tiles 0..2 -> LDS; rows of tiles 0..2 and entries of 3..5 in flight
-    if (tid < T)
+    const uint8_t* binsr = A.bins + (int64_t)r * A.bins_rstride;
+    const int cs = A.cshift;
+    const int64_t K0 = A.K0;
+    const uint32_t cstride = A.count_only ? 0u : plane;
+    // entries of the wave's next batch are loaded one batch ahead
+    int64_t q0 = a + (int64_t)wave * 64;
+    uint64_t e_next = (q0 + lane < b) ? A.ent_in[q0 + lane] : 0ull;
+    for (; q0 < b; q0 += (int64_t)kHistWaves * 64) {
+      const int n = (int)min((int64_t)64, b - q0);
+      const uint64_t e = e_next;
+      const int64_t qn = q0 + (int64_t)kHistWaves * 64 + lane;
+      e_next = (qn < b) ? A.ent_in[qn] : 0ull;
+      const uint32_t row = (uint32_t)e;
+      const int32_t hi = (int32_t)(e >> 32);
+      const uint32_t c = (uint32_t)hi & 0xffu;  // 0 for lanes past the piece: they add zeros
+      const int32_t k = hi >> 8;
+      uint32_t w0l, w0h, w1l, w1h;
+      if (GINI) {
+        w0l = c;
+        w0h = (uint32_t)k * cstride;  // class plane offset
+        w1l = w1h = 0;
+      } else {
+        const uint64_t w0 = ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)((int64_t)k + K0);
+        const uint64_t w1 = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);  // < 2^56
+        w0l = (uint32_t)w0;
+        w0h = (uint32_t)(w0 >> 32);
+        w1l = (uint32_t)w1;
+        w1h = (uint32_t)(w1 >> 32);
+      }
+      uint32_t bA[kG][NJ], bB[kG][NJ];
+      hist_load_group<NJ>(binsr, S, row, 0, posr, bA);
 #pragma unroll
-      for (int k = 0; k < 3; k++) c.s_e[(size_t)k * T + tid] = load_entry(c, k, tid);
-    __syncthreads();
-    issue_rows(c, 0, c.s_e, st.rreg[0]);
-    issue_rows(c, 1, c.s_e + T, st.rreg[1]);
-    issue_rows(c, 2, c.s_e + 2 * T, st.rreg[2]);
-    st.ereg[0] = load_entry(c, 3, tid);
-    st.ereg[1] = load_entry(c, 4, tid);
-    st.ereg[2] = load_entry(c, 5, tid);
-    for (int t = 0; t < c.ntile; t += 3) {
-      hist_tile<GINI, NJ, 0>(A, c, st, pi, pc.parent, t, posr, amul, abase, amask, aoff1, do_write, slot, smem);
-      if (t + 1 >= c.ntile) break;
-      hist_tile<GINI, NJ, 1>(A, c, st, pi, pc.parent, t + 1, posr, amul, abase, amask, aoff1, do_write, slot, smem);
-      if (t + 2 >= c.ntile) break;
-      hist_tile<GINI, NJ, 2>(A, c, st, pi, pc.parent, t + 2, posr, amul, abase, amask, aoff1, do_write, slot, smem);
+      for (int g = 0; g < 64 / kG; g += 2) {
+        if ((g + 1) * kG < n) hist_load_group<NJ>(binsr, S, row, (g + 1) * kG, posr, bB);
+        hist_add_group<GINI, NJ>(smem, plane, g * kG, bA, w0l, w0h, w1l, w1h, amul, abase);
+        if ((g + 1) * kG >= n) break;
+        if (g + 2 < 64 / kG && (g + 2) * kG < n)
+          hist_load_group<NJ>(binsr, S, row, (g + 2) * kG, posr, bA);
+        hist_add_group<GINI, NJ>(smem, plane, (g + 1) * kG, bB, w0l, w0h, w1l, w1h, amul, abase);
+        if ((g + 2) * kG >= n) break;
+      }
     }
   }
   if (cur_slot >= 0) {
     __syncthreads();
-    hist_flush<GINI>(A, smem, cur_slot, ft0, cur_ftn);
+    hist_flush<GINI>(A, smem, plane, cur_slot, ft0, cur_ftn);
   }
 }
 
-size_t hist_lds_bytes(int S, int T, int NB, int NS, int FPH, bool gini) {
-  const size_t hist_bytes = gini ? (size_t)NS * NB * FPH * 4 + 256 : (size_t)2 * NB * FPH * 8 + 1024;
-  return align16(hist_bytes) + align16((size_t)T * S) + (size_t)T * 48 + align16((size_t)T) + 16;
+size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini) {
+  return (size_t)hist_plane_bytes(NB, FPH, gini) * (gini ? (size_t)NS : 2u);
 }
 
 template <bool GINI, int NJ>
@@ -783,6 +669,67 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gi
 }
 
 size_t hist_lds_limit() { return 160 * 1024; }
+
+// ---- partition: 4 entries per lane per step, one cursor atomic per wave and side
+constexpr int kPartThreads = 256;
+constexpr int kPartK = 4;
+
+__global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int waves = kPartThreads / 64;
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
+  for (int p = p0; p < p1; p++) {
+    const HistChunk pc = A.chunks[p];
+    const ParentInfo pi = A.parents[pc.parent];
+    const uint8_t* col = A.bins + (int64_t)pi.r * A.bins_rstride + pi.pos;
+    const uint32_t split = (uint32_t)pi.s;
+    const bool wlp = pi.write_l != 0, wrp = pi.write_r != 0;
+    unsigned long long* cur = A.cursors + 2 * (int64_t)pc.parent;
+    for (int64_t base = pc.a + (int64_t)wave * 64 * kPartK; base < pc.b;
+         base += (int64_t)waves * 64 * kPartK) {
+      uint64_t e[kPartK];
+      uint32_t byte[kPartK];
+#pragma unroll
+      for (int k = 0; k < kPartK; k++) {
+        const int64_t i = base + k * 64 + lane;
+        e[k] = i < pc.b ? A.ent_in[i] : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < kPartK; k++) byte[k] = col[(size_t)(uint32_t)e[k] * A.S];
+      uint64_t ml[kPartK], mr[kPartK];
+      int nl = 0, nr = 0;
+#pragma unroll
+      for (int k = 0; k < kPartK; k++) {
+        const bool valid = base + k * 64 + lane < pc.b;
+        const bool right = byte[k] > split;
+        ml[k] = __ballot(valid && !right && wlp);
+        mr[k] = __ballot(valid && right && wrp);
+        nl += __popcll(ml[k]);
+        nr += __popcll(mr[k]);
+      }
+      unsigned long long bl = 0, br = 0;
+      if (lane == 0) {
+        if (nl) bl = atomicAdd(&cur[0], (unsigned long long)nl);
+        if (nr) br = atomicAdd(&cur[1], (unsigned long long)(-(long long)nr)) - (unsigned long long)nr;
+      }
+      bl = (unsigned long long)__shfl((long long)bl, 0);
+      br = (unsigned long long)__shfl((long long)br, 0);
+#pragma unroll
+      for (int k = 0; k < kPartK; k++) {
+        const uint64_t bit = 1ull << lane;
+        if (ml[k] & bit) A.ent_out[bl + __popcll(ml[k] & lt)] = e[k];
+        if (mr[k] & bit) A.ent_out[br + __popcll(mr[k] & lt)] = e[k];
+        bl += __popcll(ml[k]);
+        br += __popcll(mr[k]);
+      }
+    }
+  }
+}
+
+void launch_partition(hipStream_t st, const PartArgs& a, int nwg) {
+  hipLaunchKernelGGL(k_partition, dim3((unsigned)nwg), dim3(kPartThreads), 0, st, a);
+}
 
 // ======================================================================
 // Split search: one workgroup per node slot; thread per local feature does
