@@ -1165,6 +1165,8 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   // ---- 5. bins
   const uint8_t* d_bins;
   int64_t bins_rstride = 0;
+  const uint8_t* d_cols = nullptr;
+  int64_t cols_rstride = 0, npad = 0;
   int32_t S;
   std::vector<int16_t> h_pos((size_t)R * Fmax, 0);
   {
@@ -1225,6 +1227,18 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       for (int r = 0; r < R; r++)
         for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)fl;
     }
+    // column-major copy for k_partition
+    int ncol = 1;
+    for (int r = 0; r < R; r++)
+      for (int fl = 0; fl < h_Fr[r]; fl++) ncol = std::max(ncol, (int)h_pos[(size_t)r * Fmax + fl] + 1);
+    const int Rc = bins_rstride ? R : 1;
+    npad = (N + 63) / 64 * 64;
+    cols_rstride = bins_rstride ? (int64_t)ncol * npad : 0;
+    uint8_t* d_c;
+    TRY(ws_typed(c, "cols", (size_t)Rc * ncol * npad, &d_c));
+    launch_transpose(c->stream, d_bins, N, S, ncol, d_c, npad, Rc, bins_rstride, cols_rstride);
+    HIP_TRY(hipGetLastError());
+    d_cols = d_c;
     tm.end(h);
   }
   int32_t* d_nbins;
@@ -1403,9 +1417,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       build_work(pseg, (int64_t)1 << 40, 256 * 8, 1024, work);
       TRY(upload_work(par));
       PartArgs pa{};
-      pa.bins = d_bins;
-      pa.bins_rstride = bins_rstride;
-      pa.S = S;
+      pa.cols = d_cols;
+      pa.cols_rstride = cols_rstride;
+      pa.npad = npad;
       pa.chunks = d_pieces;
       pa.wg_piece = d_wg;
       pa.parents = d_par;

@@ -55,9 +55,9 @@ struct HistArgs {
 // k_partition: entries of each split node -> left block (from the segment start,
 // cursors[2p] grows) and right block (from the segment end, cursors[2p+1] shrinks)
 struct PartArgs {
-  const uint8_t* bins;
-  int64_t bins_rstride;
-  int32_t S, pad;
+  const uint8_t* cols;   // column-major bins [R?][C][npad] (k_transpose)
+  int64_t cols_rstride;  // bytes between replica copies (0: shared)
+  int64_t npad;          // column stride (rows rounded up to 64)
   const HistChunk* chunks;
   const int32_t* wg_piece;
   const ParentInfo* parents;  // r, pos (split column), s (split bin), write_l, write_r
@@ -109,6 +109,8 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gi
                  size_t lds_bytes);
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini);
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg);
+void launch_transpose(hipStream_t st, const uint8_t* src, int64_t N, int S, int C, uint8_t* dst,
+                      int64_t npad, int R, int64_t src_rstride, int64_t dst_rstride);
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini);
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words);

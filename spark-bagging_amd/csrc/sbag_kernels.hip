@@ -682,7 +682,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
   for (int p = p0; p < p1; p++) {
     const HistChunk pc = A.chunks[p];
     const ParentInfo pi = A.parents[pc.parent];
-    const uint8_t* col = A.bins + (int64_t)pi.r * A.bins_rstride + pi.pos;
+    const uint8_t* col = A.cols + (int64_t)pi.r * A.cols_rstride + (int64_t)pi.pos * A.npad;
     const uint32_t split = (uint32_t)pi.s;
     const bool wlp = pi.write_l != 0, wrp = pi.write_r != 0;
     unsigned long long* cur = A.cursors + 2 * (int64_t)pc.parent;
@@ -696,7 +696,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         e[k] = i < pc.b ? A.ent_in[i] : 0ull;
       }
 #pragma unroll
-      for (int k = 0; k < kPartK; k++) byte[k] = col[(size_t)(uint32_t)e[k] * A.S];
+      for (int k = 0; k < kPartK; k++) byte[k] = col[(uint32_t)e[k]];
       uint64_t ml[kPartK], mr[kPartK];
       int nl = 0, nr = 0;
 #pragma unroll
@@ -725,6 +725,44 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
       }
     }
   }
+}
+
+// ---- column-major copy of a row-major byte matrix (the partition's split column:
+// the sorted rows of a node segment read ~1 byte each instead of a 128-B line)
+__global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ src, int64_t N,
+                                                   int S, int C, uint8_t* __restrict__ dst,
+                                                   int64_t npad, int64_t src_rstride,
+                                                   int64_t dst_rstride) {
+  __shared__ __align__(16) uint8_t t[64][80];
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * 64;
+  const int col0 = blockIdx.y * 64;
+  src += (int64_t)blockIdx.z * src_rstride;
+  dst += (int64_t)blockIdx.z * dst_rstride;
+  {
+    const int r = tid >> 2, part = tid & 3;
+    const int cb = col0 + part * 16;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row0 + r < N && cb < S) v = *(const uint4*)(src + (row0 + r) * S + cb);
+    *(uint4*)&t[r][part * 16] = v;
+  }
+  __syncthreads();
+  const int cl = tid >> 2, rq = tid & 3;
+  if (col0 + cl < C) {
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      w[q] = (uint32_t)t[rq * 16 + 4 * q][cl] | ((uint32_t)t[rq * 16 + 4 * q + 1][cl] << 8) |
+             ((uint32_t)t[rq * 16 + 4 * q + 2][cl] << 16) | ((uint32_t)t[rq * 16 + 4 * q + 3][cl] << 24);
+    *(uint4*)(dst + (int64_t)(col0 + cl) * npad + row0 + rq * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+void launch_transpose(hipStream_t st, const uint8_t* src, int64_t N, int S, int C, uint8_t* dst,
+                      int64_t npad, int R, int64_t src_rstride, int64_t dst_rstride) {
+  const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)R);
+  hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, st, src, N, S, C, dst, npad, src_rstride,
+                     dst_rstride);
 }
 
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg) {
