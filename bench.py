@@ -22,6 +22,25 @@ import sbag_loader  # noqa: E402
 
 SEED_REG = -1395689524  # default seed of BaggingRegressor (class-name hashCode)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
+# ds_add_u64 throughput measured on MI355X by scripts/micro/lds_atomic.hip:
+# 7.16 cycles per wave-instruction per CU (4 x 512-thread workgroups per CU), 256 CUs, 2.4 GHz
+LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "summary.json")
+
+
+def pmc_traffic():
+    """HBM bytes per k_hist launch from the committed rocprofv3 PMC summary of this
+    same command (scripts/profile.sh + scripts/pmc_summary.py): 2 x FETCH_SIZE (gfx950
+    reports half of wide reads) + WRITE_SIZE, in bytes; None if not profiled."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        for k, v in d.items():
+            if k.startswith("sbag::k_hist") and "hbm_bytes_per_launch" in v:
+                return round(v["hbm_bytes_per_launch"])
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def parse():
@@ -112,17 +131,29 @@ def main():
 
     hist_ms = sum(t["hist_ms"] for t in timings)
     hist_launches = sum(t["hist_launches"] for t in timings)
-    alg_bytes = sum(t["hist_alg_bytes"] for t in timings)
-    achieved = alg_bytes / (hist_ms / 1000.0) / 1e9 if hist_ms > 0 else 0.0
-    last = timings[-1]
+    work_bytes = sum(t["hist_work_bytes"] for t in timings)
+    read_bytes = sum(t["hist_alg_bytes"] for t in timings)
+    entries = sum(t["hist_entries"] for t in timings)
+    nl = max(hist_launches, 1)
+    avg_s = hist_ms / 1e3 / nl
+    achieved = work_bytes / nl / avg_s / 1e9 if hist_ms > 0 else 0.0
+    # LDS atomic co-limiter: 2 u64 atomics per entry and 64-feature lane group
+    lds_instr = entries * 2 * ((F + 63) // 64)
+    lds_rate = lds_instr / (hist_ms / 1e3) if hist_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "sbag::k_hist<false>",
-                "avg_launch_ms": round(hist_ms / max(hist_launches, 1), 4),
-                "alg_bytes_per_launch": round(alg_bytes / max(hist_launches, 1)),
-                "upper_bound_GBs_survey": round(last["hist_upper_bytes"] / (last["hist_ms"] / 1e3) / 1e9, 1)
-                if last["hist_ms"] > 0 else None}
-    breakdown = {k: round(v, 3) for k, v in last.items() if k.endswith("_ms")}
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),
+                "kernel": "sbag::k_hist<false,2>",
+                "avg_launch_ms": round(hist_ms / nl, 4),
+                "alg_bytes_per_launch": round(work_bytes / nl),
+                "alg_bytes_def": "SURVEY 8d: sum over histograms built (read or by subtraction) of "
+                                 "n(r,d)*(F_r+4) + 3N",
+                "kernel_read_bytes_per_launch": round(read_bytes / nl),
+                "kernel_read_GBs": round(read_bytes / nl / avg_s / 1e9, 1) if hist_ms > 0 else 0.0,
+                "lds_atomic": {"achieved": round(lds_rate / 1e9, 2),
+                               "peak": round(LDS_ATOMIC_PEAK / 1e9, 2),
+                               "unit": "G wave-instr/s (ds_add_u64)",
+                               "frac": round(lds_rate / LDS_ATOMIC_PEAK, 4)}}
+    breakdown = {k: round(v, 3) for k, v in timings[-1].items() if k.endswith("_ms")}
     out = {
         "metric": "estimator×rows trained/sec", "value": round(value, 1),
         "unit": "estimator*rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

@@ -147,6 +147,9 @@ typedef struct {
   double hist_upper_bytes; /* SURVEY §8d upper bound: Σ_r Σ_d inbag_r x (F_r + 4) + 3N */
   int64_t levels;
   double partition_ms;     /* k_partition: rows of split nodes -> child segments      */
+  double hist_work_bytes;  /* SURVEY §8d algorithmic bytes of all histograms built:
+                              Σ_(r,d) n(r,d) x (F_r + 4) + 3N, n = rows of every node
+                              whose histogram exists (read or obtained by subtraction) */
 } sbag_timing;
 int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
 

@@ -1,5 +1,7 @@
 #!/bin/bash
-# Profile the C3 bench on the GPU box: kernel trace + separate PMC passes.
+# Profile the C3 bench on the GPU box: kernel trace + separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE and the LDS counters each in their own run, never with
+# a trace domain).  Summarise afterwards with scripts/pmc_summary.py.
 # usage: scripts/profile.sh <tag> [bench args...]
 set -u
 TAG=$1; shift

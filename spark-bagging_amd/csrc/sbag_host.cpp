@@ -996,7 +996,17 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   ha.K0 = (int32_t)K0;
   ha.cshift = cshift;
   ha.flush_limit = flush_limit;
-  double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0;
+  double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0, hist_work = 0;
+  // SURVEY §8d work bytes of the histograms of a set of node segments
+  auto add_work = [&](const std::vector<std::pair<int64_t, int64_t>>& segs,
+                      const std::vector<int>& seg_r) {
+    std::vector<char> act(R, 0);
+    for (size_t q = 0; q < segs.size(); q++) {
+      hist_work += (double)(segs[q].second - segs[q].first) * (h_Fr[seg_r[q]] + 4);
+      act[seg_r[q]] = 1;
+    }
+    for (int r = 0; r < R; r++) hist_work += act[r] ? 3.0 * N : 0.0;
+  };
   int64_t hist_launches = 0;
   auto launch = [&](const HistGeom& g, bool gini_layout, int cat,
                     const std::vector<std::pair<int64_t, int64_t>>& segs,
@@ -1273,6 +1283,11 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     TRY(launch(g, gini, T_HIST, seg, h_par));
   }
   for (int r = 0; r < R; r++) hist_upper += (double)inbag[r] * (h_Fr[r] + 4) * D + 3.0 * N * D;
+  {
+    std::vector<int> seg_r(R);
+    for (int r = 0; r < R; r++) seg_r[r] = r;
+    add_work(seg, seg_r);
+  }
   const double inv_scale = std::ldexp(1.0, -ds->shift), inv_scale2 = std::ldexp(1.0, -2 * ds->shift);
   uint64_t* ent_cur = entA;
   uint64_t* ent_nxt = entB;
@@ -1440,6 +1455,11 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       else
         nseg[k] = {(int64_t)cur[2 * pd.parent + 1], pseg[pd.parent].second};
     }
+    {
+      std::vector<int> seg_r(Mn);
+      for (int k = 0; k < Mn; k++) seg_r[k] = next_slots[k].first;
+      add_work(nseg, seg_r);
+    }
     // --- histograms of level+1: the smaller (or only) child of each split node
     std::vector<std::pair<int64_t, int64_t>> hseg;
     std::vector<ParentInfo> hpar;
@@ -1507,6 +1527,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   T.split_ms = cats[T_SPLIT];
   T.subtract_ms = cats[T_SUB];
   T.partition_ms = cats[T_PART];
+  T.hist_work_bytes = hist_work;
   T.hist_launches = hist_launches;
   T.hist_alg_bytes = hist_alg_bytes;
   T.hist_entries = hist_entries;
