@@ -137,8 +137,9 @@ def main():
     nl = max(hist_launches, 1)
     avg_s = hist_ms / 1e3 / nl
     achieved = work_bytes / nl / avg_s / 1e9 if hist_ms > 0 else 0.0
-    # LDS atomic co-limiter: 2 u64 atomics per entry and 64-feature lane group
-    lds_instr = entries * 2 * ((F + 63) // 64)
+    # LDS atomic co-limiter: one u64 atomic per entry and 64-feature lane group
+    # (variance screening: (count, sum) only)
+    lds_instr = entries * ((F + 63) // 64)
     lds_rate = lds_instr / (hist_ms / 1e3) if hist_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),

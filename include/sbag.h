@@ -150,6 +150,8 @@ typedef struct {
   double hist_work_bytes;  /* SURVEY §8d algorithmic bytes of all histograms built:
                               Σ_(r,d) n(r,d) x (F_r + 4) + 3N, n = rows of every node
                               whose histogram exists (read or obtained by subtraction) */
+  double fix_ms;           /* exact-split fallback of screened variance nodes */
+  int64_t exact_fallbacks; /* nodes that needed it                                      */
 } sbag_timing;
 int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
 

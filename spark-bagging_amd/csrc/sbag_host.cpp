@@ -493,7 +493,7 @@ struct EventTimer {
     }
   }
 };
-enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_NCAT };
+enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_FIX, T_NCAT };
 
 // ---------------------------------------------------------------- C ABI
 extern "C" {
@@ -899,18 +899,20 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
   TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
   unsigned long long* d_inbag;
-  TRY(ws_typed(c, "inbag", (size_t)R * 3, &d_inbag));
+  TRY(ws_typed(c, "inbag", (size_t)R * 4, &d_inbag));
   unsigned long long* d_wsum = d_inbag + R;
   unsigned int* d_cmax = (unsigned int*)(d_inbag + 2 * R);
-  HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 24, c->stream));
+  unsigned long long* d_sqsum = d_inbag + 3 * R;
+  HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 32, c->stream));
   {
     int h = tm.begin(T_COMPACT);
-    launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax);
+    launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
+                   d_sqsum);
     HIP_TRY(hipGetLastError());
     tm.end(h);
   }
-  std::vector<unsigned long long> inbag(3 * R);
-  TRY(d2h(c, inbag.data(), d_inbag, (size_t)3 * R));
+  std::vector<unsigned long long> inbag(4 * R);
+  TRY(d2h(c, inbag.data(), d_inbag, (size_t)4 * R));
   std::vector<int64_t> nw(R);
   unsigned int cmax = 1;
   for (int r = 0; r < R; r++) {
@@ -1008,7 +1010,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     for (int r = 0; r < R; r++) hist_work += act[r] ? 3.0 * N : 0.0;
   };
   int64_t hist_launches = 0;
-  auto launch = [&](const HistGeom& g, bool gini_layout, int cat,
+  auto launch = [&](const HistGeom& g, int mode, int cat,
                     const std::vector<std::pair<int64_t, int64_t>>& segs,
                     const std::vector<ParentInfo>& par) -> int {
     const int wpc = std::max(1, std::min(2, (int)((160 * 1024) / g.lds)));  // 16 waves/CU
@@ -1020,7 +1022,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     ha.FT = g.FT;
     ha.FPH = g.FPH;
     int h = tm.begin(cat);
-    launch_hist(c->stream, ha, work.nwg, g.ntiles, gini_layout, g.lds);
+    launch_hist(c->stream, ha, work.nwg, g.ntiles, mode, g.lds);
     HIP_TRY(hipGetLastError());
     tm.end(h);
     if (cat == T_HIST) {
@@ -1064,7 +1066,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     ha.NB = ncmax;
     ha.NS = NS;
     ha.count_only = 0;
-    TRY(launch(g0, gini, T_HIST, seg, h_par));
+    TRY(launch(g0, gini ? kHistGini : kHistVar, T_HIST, seg, h_par));
     const int64_t words = (int64_t)R * Fmax * ncmax * NS;
     std::vector<uint8_t> tmp((size_t)words * word_bytes);
     TRY(d2h(c, tmp.data(), (const uint8_t*)hist_cur, tmp.size()));
@@ -1100,7 +1102,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       ha.NB = ncmax;
       ha.NS = 1;
         ha.count_only = 1;
-      TRY(launch(g, true, T_VC, seg, h_par));
+      TRY(launch(g, kHistGini, T_VC, seg, h_par));
       ha = save;
       std::vector<uint32_t> tmp((size_t)R * slot_words);
       TRY(d2h(c, tmp.data(), d_vch, tmp.size()));
@@ -1280,7 +1282,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * slot_words * word_bytes, c->stream));
     ha.ent_in = entA;
     ha.hist = hist_cur;
-    TRY(launch(g, gini, T_HIST, seg, h_par));
+    TRY(launch(g, gini ? kHistGini : kHistVar, T_HIST, seg, h_par));
   }
   for (int r = 0; r < R; r++) hist_upper += (double)inbag[r] * (h_Fr[r] + 4) * D + 3.0 * N * D;
   {
@@ -1293,6 +1295,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   uint64_t* ent_nxt = entB;
   std::string hist_nxt_name = "histB", hist_cur_name = "histA";
   int levels = 0;
+  // exact sum of count*k^2 of every slot's node (variance screening): root from k_compact
+  std::vector<uint64_t> slot_sq(R);
+  for (int r = 0; r < R; r++) slot_sq[r] = inbag[3 * R + r];
+  int64_t fallbacks = 0;
   for (int level = 0; level <= D; level++) {
     const int M = (int)slots.size();
     if (M == 0) break;
@@ -1321,25 +1327,67 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     sa.inv_scale2 = inv_scale2;
     sa.out = d_sout;
     sa.stats = d_sstats;
+    if (!gini) {
+      uint64_t* d_nsq;
+      TRY(ws_typed(c, "node_sq", (size_t)M, &d_nsq));
+      TRY(h2d(c, d_nsq, slot_sq.data(), (size_t)M));
+      sa.node_sq = d_nsq;
+    }
     {
       int h = tm.begin(T_SPLIT);
-      launch_split(c->stream, sa, M, gini);
+      if (gini)
+        launch_split(c->stream, sa, M, true);
+      else
+        launch_split_screen(c->stream, sa, M);
       HIP_TRY(hipGetLastError());
       tm.end(h);
     }
     std::vector<SplitOut> sout(M);
     std::vector<int64_t> sst((size_t)M * 3 * NS);
     TRY(d2h(c, sout.data(), d_sout, (size_t)M));
+    std::vector<char> exact(M, gini ? 1 : 0);
+    if (!gini) {
+      // nodes the screen could not decide: histogram their sums of squares (word 2)
+      // from their own rows, then the exact Spark-order split
+      std::vector<int32_t> fl_slots;
+      for (int i = 0; i < M; i++)
+        if (sout[i].pad) fl_slots.push_back(i);
+      if (!fl_slots.empty()) {
+        fallbacks += (int64_t)fl_slots.size();
+        int h = tm.begin(T_FIX);
+        int32_t* d_fs;
+        TRY(ws_typed(c, "fix_slots", fl_slots.size(), &d_fs));
+        TRY(h2d(c, d_fs, fl_slots.data(), fl_slots.size()));
+        launch_zero_word(c->stream, (uint64_t*)hist_cur, d_fs, (int)fl_slots.size(), slot_words, 3, 2);
+        HIP_TRY(hipGetLastError());
+        tm.end(h);
+        std::vector<std::pair<int64_t, int64_t>> fseg;
+        std::vector<ParentInfo> fpar;
+        for (int i : fl_slots) {
+          fseg.push_back(seg[i]);
+          fpar.push_back(ParentInfo{slots[i].first, -1, 0, 0, 0, i, 0, 0});
+        }
+        ha.ent_in = ent_cur;
+        ha.hist = hist_cur;
+        TRY(launch(g, kHistSq, T_FIX, fseg, fpar));
+        SplitArgs sx = sa;
+        sx.slot_ids = d_fs;
+        h = tm.begin(T_FIX);
+        launch_split(c->stream, sx, (int)fl_slots.size(), false);
+        HIP_TRY(hipGetLastError());
+        tm.end(h);
+        TRY(d2h(c, sout.data(), d_sout, (size_t)M));
+        for (int i : fl_slots) exact[i] = 1;
+      }
+    }
     TRY(d2h(c, sst.data(), d_sstats, sst.size()));
     // --- node updates (RandomForest.findBestSplits, host part)
+    struct Split {
+      int slot, r, ni, li;
+    };
     std::vector<ParentInfo> par;
     std::vector<std::pair<int64_t, int64_t>> pseg;
-    std::vector<std::pair<int, int>> next_slots;
-    std::vector<int32_t> triples;
-    struct Pending {
-      int side, parent;
-    };
-    std::vector<Pending> pend;
+    std::vector<Split> psplit;
     for (int i = 0; i < M; i++) {
       const int r = slots[i].first;
       const int ni = slots[i].second;
@@ -1371,63 +1419,49 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       HNode L, Rn;
       L.stats.assign(lef, lef + NS);
       Rn.stats.assign(rig, rig + NS);
-      L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
-      Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
-      L.is_leaf = child_leaf || L.impurity == 0.0;
-      Rn.is_leaf = child_leaf || Rn.impurity == 0.0;
+      bool wl = !child_leaf, wr = !child_leaf;
+      if (exact[i]) {  // children stats complete: leaf-by-purity known before routing
+        L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
+        Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
+        wl = wl && L.impurity != 0.0;
+        wr = wr && Rn.impurity != 0.0;
+      }
       const int li = (int)trees[r].size();
       trees[r].push_back(L);
       trees[r].push_back(Rn);
       trees[r][ni].left = li;
       trees[r][ni].right = li + 1;
-      const bool wl = !trees[r][li].is_leaf, wr = !trees[r][li + 1].is_leaf;
-      if (!wl && !wr) continue;
+      if (!wl && !wr && exact[i]) {  // nothing to route, all stats known
+        trees[r][li].is_leaf = trees[r][li + 1].is_leaf = true;
+        continue;
+      }
       ParentInfo p{};
       p.r = r;
       p.pos = h_pos[(size_t)r * Fmax + trees[r][ni].fl];
       p.s = trees[r][ni].s;
       p.write_l = wl;
       p.write_r = wr;
-      const int pidx = (int)par.size();
-      int sl = -1, sr = -1;
-      if (wl) {
-        sl = (int)next_slots.size();
-        next_slots.push_back({r, li});
-        pend.push_back({0, pidx});
-      }
-      if (wr) {
-        sr = (int)next_slots.size();
-        next_slots.push_back({r, li + 1});
-        pend.push_back({1, pidx});
-      }
-      if (wl && wr) {
-        const int64_t lc = Calc{lef, NS, gini, ds->shift}.count();
-        const int64_t rc = Calc{rig, NS, gini, ds->shift}.count();
-        const bool small_left = lc <= rc;
-        p.hist_slot = small_left ? sl : sr;
-        p.hist_side = small_left ? 0 : 1;
-        triples.push_back(small_left ? sr : sl);  // dst (larger child)
-        triples.push_back(i);                     // parent slot (current level)
-        triples.push_back(small_left ? sl : sr);  // small child
-      } else {
-        p.hist_slot = wl ? sl : sr;
-        p.hist_side = wl ? 0 : 1;
-      }
+      p.hist_slot = -1;
       par.push_back(p);
       pseg.push_back(seg[i]);
+      psplit.push_back(Split{i, r, ni, li});
     }
-    if (next_slots.empty()) break;
-    // --- partition the rows of every split node into its children
-    const int Mn = (int)next_slots.size();
+    if (par.empty()) break;
+    // --- partition the rows of every split node into its children (and, for
+    // variance, the exact sum of squares of each left child)
     const int NP = (int)par.size();
-    std::vector<unsigned long long> cur((size_t)2 * NP);
+    std::vector<unsigned long long> cur((size_t)2 * NP), sql(NP, 0);
     for (int q = 0; q < NP; q++) {
       cur[2 * q] = (unsigned long long)pseg[q].first;
       cur[2 * q + 1] = (unsigned long long)pseg[q].second;
     }
-    unsigned long long* d_cur;
+    unsigned long long *d_cur, *d_sql = nullptr;
     TRY(ws_typed(c, "cursors", cur.size(), &d_cur));
     TRY(h2d(c, d_cur, cur.data(), cur.size()));
+    if (!gini) {
+      TRY(ws_typed(c, "sq_left", (size_t)NP, &d_sql));
+      HIP_TRY(hipMemsetAsync(d_sql, 0, (size_t)NP * 8, c->stream));
+    }
     {
       build_work(pseg, (int64_t)1 << 40, 256 * 8, 1024, work);
       TRY(upload_work(par));
@@ -1441,40 +1475,93 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       pa.ent_in = ent_cur;
       pa.ent_out = ent_nxt;
       pa.cursors = d_cur;
+      pa.sq_left = d_sql;
       int h = tm.begin(T_PART);
       launch_partition(c->stream, pa, work.nwg);
       HIP_TRY(hipGetLastError());
       tm.end(h);
     }
     TRY(d2h(c, cur.data(), d_cur, cur.size()));
-    std::vector<std::pair<int64_t, int64_t>> nseg(Mn);
-    for (int k = 0; k < Mn; k++) {
-      const Pending& pd = pend[k];
-      if (pd.side == 0)
-        nseg[k] = {pseg[pd.parent].first, (int64_t)cur[2 * pd.parent]};
-      else
-        nseg[k] = {(int64_t)cur[2 * pd.parent + 1], pseg[pd.parent].second};
+    if (!gini) TRY(d2h(c, sql.data(), d_sql, sql.size()));
+    // --- children: complete stats, purity, the parent's exact gain; next slots
+    std::vector<std::pair<int, int>> next_slots;
+    std::vector<std::pair<int64_t, int64_t>> nseg;
+    std::vector<uint64_t> next_sq;
+    std::vector<int32_t> triples;
+    std::vector<std::pair<int64_t, int64_t>> hseg;
+    std::vector<ParentInfo> hpar;
+    for (int q = 0; q < NP; q++) {
+      const Split& sp = psplit[q];
+      HNode& L = trees[sp.r][sp.li];
+      HNode& Rn = trees[sp.r][sp.li + 1];
+      if (!gini) {
+        const uint64_t psq = (uint64_t)trees[sp.r][sp.ni].stats[2];
+        if (exact[sp.slot]) {
+          if ((uint64_t)L.stats[2] != sql[q])
+            return fail(SBAG_EDEVICE, "internal: left sum of squares differs between histogram "
+                                      "and partition");
+        } else {
+          L.stats[2] = (int64_t)sql[q];
+          Rn.stats[2] = (int64_t)(psq - sql[q]);
+          L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
+          Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
+          // Spark's gain of the chosen split (calculateImpurityStats, operation order)
+          HNode& n = trees[sp.r][sp.ni];
+          const double lc = (double)L.stats[0], rc = (double)Rn.stats[0];
+          const double lw = lc / (lc + rc), rw = rc / (lc + rc);
+          const double gain = n.impurity - lw * L.impurity - rw * Rn.impurity;
+          if (!(gain > 0.0) || gain < tp.min_info_gain)
+            return fail(SBAG_EDEVICE, "internal: screened split fails Spark's gain test");
+          n.gain = gain;
+        }
+      }
+      const bool child_leaf = (level + 1) == D;
+      L.is_leaf = child_leaf || L.impurity == 0.0;
+      Rn.is_leaf = child_leaf || Rn.impurity == 0.0;
+      const bool wl = !L.is_leaf, wr = !Rn.is_leaf;
+      int sl = -1, sr = -1;
+      if (wl) {
+        sl = (int)next_slots.size();
+        next_slots.push_back({sp.r, sp.li});
+        nseg.push_back({pseg[q].first, (int64_t)cur[2 * q]});
+        next_sq.push_back(gini ? 0 : (uint64_t)L.stats[2]);
+      }
+      if (wr) {
+        sr = (int)next_slots.size();
+        next_slots.push_back({sp.r, sp.li + 1});
+        nseg.push_back({(int64_t)cur[2 * q + 1], pseg[q].second});
+        next_sq.push_back(gini ? 0 : (uint64_t)Rn.stats[2]);
+      }
+      int hs = -1;
+      if (wl && wr) {
+        const bool small_left = Calc{L.stats.data(), NS, gini, ds->shift}.count() <=
+                                Calc{Rn.stats.data(), NS, gini, ds->shift}.count();
+        hs = small_left ? sl : sr;
+        triples.push_back(small_left ? sr : sl);  // dst (larger child)
+        triples.push_back(sp.slot);               // parent slot (current level)
+        triples.push_back(hs);                    // small child
+      } else if (wl || wr) {
+        hs = wl ? sl : sr;
+      }
+      if (hs >= 0) {
+        hseg.push_back(nseg[hs]);
+        hpar.push_back(ParentInfo{sp.r, -1, 0, 0, 0, hs, 0, 0});
+      }
     }
+    if (next_slots.empty()) break;
+    const int Mn = (int)next_slots.size();
     {
       std::vector<int> seg_r(Mn);
       for (int k = 0; k < Mn; k++) seg_r[k] = next_slots[k].first;
       add_work(nseg, seg_r);
     }
     // --- histograms of level+1: the smaller (or only) child of each split node
-    std::vector<std::pair<int64_t, int64_t>> hseg;
-    std::vector<ParentInfo> hpar;
-    for (int k = 0; k < Mn; k++) {
-      const ParentInfo& pp = par[pend[k].parent];
-      if (pp.hist_slot != k) continue;
-      hseg.push_back(nseg[k]);
-      hpar.push_back(ParentInfo{pp.r, -1, 0, 0, 0, k, 0, 0});
-    }
     void* hist_nxt;
     TRY(ws_get(c, hist_nxt_name, (size_t)Mn * slot_words * word_bytes, &hist_nxt));
     HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * slot_words * word_bytes, c->stream));
     ha.ent_in = ent_nxt;
     ha.hist = hist_nxt;
-    TRY(launch(g, gini, T_HIST, hseg, hpar));
+    TRY(launch(g, gini ? kHistGini : kHistVar, T_HIST, hseg, hpar));
     if (!triples.empty()) {
       int32_t* d_tri;
       TRY(ws_typed(c, "triples", triples.size(), &d_tri));
@@ -1486,6 +1573,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     }
     seg = nseg;
     slots = next_slots;
+    slot_sq = next_sq;
     std::swap(hist_cur_name, hist_nxt_name);
     hist_cur = hist_nxt;
     std::swap(ent_cur, ent_nxt);
@@ -1528,6 +1616,8 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   T.subtract_ms = cats[T_SUB];
   T.partition_ms = cats[T_PART];
   T.hist_work_bytes = hist_work;
+  T.fix_ms = cats[T_FIX];
+  T.exact_fallbacks = fallbacks;
   T.hist_launches = hist_launches;
   T.hist_alg_bytes = hist_alg_bytes;
   T.hist_entries = hist_entries;

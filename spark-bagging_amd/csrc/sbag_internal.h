@@ -31,6 +31,8 @@ struct ParentInfo {  // a node of level d whose rows are routed to level d+1
   int32_t pad;
 };
 
+enum { kHistGini = 0, kHistVar = 1, kHistSq = 2 };  // k_hist modes
+
 struct HistArgs {
   const uint8_t* bins;   // [R?][N][S] bins (or value codes in count mode)
   int64_t bins_rstride;  // bytes between replica matrices (0: shared)
@@ -64,6 +66,7 @@ struct PartArgs {
   const uint64_t* ent_in;
   uint64_t* ent_out;
   unsigned long long* cursors;
+  unsigned long long* sq_left;  // [parents] sum of count*k^2 of the rows going left (or NULL)
 };
 
 struct SplitOut {
@@ -85,6 +88,8 @@ struct SplitArgs {
   double inv_scale, inv_scale2;  // 2^-s, 2^-2s (fixed-point labels)
   SplitOut* out;                  // [M]
   int64_t* stats;                 // [M][3][NS]: total, left, right (integers)
+  const int32_t* slot_ids;        // block -> slot (NULL: identity)
+  const uint64_t* node_sq;        // screen: [M] exact sum of count*k^2 of each node
 };
 
 struct DevNode {  // packed tree node for predict
@@ -104,14 +109,17 @@ void launch_bernoulli(hipStream_t st, uint8_t* counts, int64_t N, const int64_t*
 void launch_fill(hipStream_t st, uint8_t* p, uint8_t v, int64_t n);
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
-                    unsigned long long* d_wsum, unsigned int* d_cmax);
-void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gini,
+                    unsigned long long* d_wsum, unsigned int* d_cmax, unsigned long long* d_sqsum);
+void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mode,
                  size_t lds_bytes);
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini);
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg);
 void launch_transpose(hipStream_t st, const uint8_t* src, int64_t N, int S, int C, uint8_t* dst,
                       int64_t npad, int R, int64_t src_rstride, int64_t dst_rstride);
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini);
+void launch_split_screen(hipStream_t st, const SplitArgs& a, int M);
+void launch_zero_word(hipStream_t st, uint64_t* hist, const int32_t* d_slots, int nslots,
+                      int64_t slot_words, int stride, int word);
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words);
 void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,

@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
                                                  uint64_t* __restrict__ ent, int64_t cap,
                                                  unsigned long long* cursor,
                                                  unsigned long long* wsum, unsigned int* cmax,
-                                                 int R) {
+                                                 unsigned long long* sqsum, int R) {
   const int r = blockIdx.x % R;
   const int64_t chunk = blockIdx.x / R;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
   __shared__ unsigned int s_max[4];
   const uint8_t* cr = counts + (int64_t)r * N;
   uint64_t* er = ent + (int64_t)r * cap;
-  unsigned long long mysum = 0;
+  unsigned long long mysum = 0, mysq = 0;
   unsigned int mymax = 0;
   for (int it = 0; it < 8; it++) {
     const int64_t row0 = chunk * 8192 + (int64_t)it * 1024 + (int64_t)tid * 4;
@@ -375,32 +375,41 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
     unsigned long long pos = s_base + (unsigned long long)(before + incl - n);
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if (c[j]) er[pos++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
+      if (c[j]) {
+        const int32_t k = labk[row0 + j];
+        mysq += (unsigned long long)c[j] * (unsigned long long)((int64_t)k * k);
+        er[pos++] = pack_entry((uint32_t)(row0 + j), k, c[j]);
+      }
     __syncthreads();
   }
+  __shared__ unsigned long long s_sq[4];
   for (int o = 32; o > 0; o >>= 1) {
     mysum += __shfl_down(mysum, o);
+    mysq += __shfl_down(mysq, o);
     mymax = max(mymax, (unsigned int)__shfl_down((int)mymax, o));
   }
   if (lane == 0) {
     s_red[wave] = mysum;
+    s_sq[wave] = mysq;
     s_max[wave] = mymax;
   }
   __syncthreads();
   if (tid == 0) {
     const unsigned long long s = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    const unsigned long long q = s_sq[0] + s_sq[1] + s_sq[2] + s_sq[3];
     const unsigned int m = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
     if (s) atomicAdd(&wsum[r], s);
+    if (q) atomicAdd(&sqsum[r], q);
     if (m) atomicMax(&cmax[r], m);
   }
 }
 
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
-                    unsigned long long* d_wsum, unsigned int* d_cmax) {
+                    unsigned long long* d_wsum, unsigned int* d_cmax, unsigned long long* d_sqsum) {
   const int64_t chunks = (N + 8191) / 8192;
   hipLaunchKernelGGL(k_compact, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, d_labk,
-                     ent, cap, d_cursor, d_wsum, d_cmax, R);
+                     ent, cap, d_cursor, d_wsum, d_cmax, d_sqsum, R);
 }
 
 // ======================================================================
@@ -439,13 +448,16 @@ static __host__ __device__ inline uint32_t hist_plane_bytes(int NB, int FPH, boo
   return (uint32_t)(NB * FPH + 64) * (gini ? 4u : 8u);
 }
 
-template <bool GINI>
+// MODE: kHistGini  u32 class counts, one plane per class  -> hist[.][cls]
+//       kHistVar   u64 (count << cshift) + count*(k + K0)  -> hist[.][0], hist[.][1]
+//       kHistSq    u64 count*k^2                           -> hist[.][2]
+template <int MODE>
 __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned char* smem,
                                            uint32_t plane, int slot, int ft0, int ftn) {
   const int tid = threadIdx.x;
   const int NB = A.NB, NS = A.NS, FPH = A.FPH;
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
-  if (GINI) {
+  if (MODE == kHistGini) {
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
     for (int q = tid; q < ftn * NB * NS; q += blockDim.x) {
       const int cls = q % NS, b = (q / NS) % NB, f = q / (NS * NB);
@@ -458,16 +470,17 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
     const uint64_t MS = (1ull << cs) - 1;
     for (int q = tid; q < ftn * NB; q += blockDim.x) {
       const int b = q % NB, f = q / NB;
-      const size_t o = ((size_t)b * FPH + f) * 8;
-      const uint64_t w0 = *(const uint64_t*)(smem + o);
-      if (w0) {
-        const uint64_t cnt = w0 >> cs;
-        const int64_t sk = (int64_t)(w0 & MS) - (int64_t)A.K0 * (int64_t)cnt;
-        const uint64_t w1 = *(const uint64_t*)(smem + plane + o);
+      const uint64_t w = *(const uint64_t*)(smem + ((size_t)b * FPH + f) * 8);
+      if (w) {
         const int64_t gb = ((int64_t)(ft0 + f) * NB + b) * 3;
-        atomicAdd(&gh[gb], (unsigned long long)cnt);
-        atomicAdd(&gh[gb + 1], (unsigned long long)sk);
-        atomicAdd(&gh[gb + 2], (unsigned long long)w1);
+        if (MODE == kHistVar) {
+          const uint64_t cnt = w >> cs;
+          const int64_t sk = (int64_t)(w & MS) - (int64_t)A.K0 * (int64_t)cnt;
+          atomicAdd(&gh[gb], (unsigned long long)cnt);
+          atomicAdd(&gh[gb + 1], (unsigned long long)sk);
+        } else {
+          atomicAdd(&gh[gb + 2], (unsigned long long)w);
+        }
       }
     }
   }
@@ -494,45 +507,45 @@ __device__ __forceinline__ void hist_load_group(const uint8_t* __restrict__ bins
   }
 }
 
-template <bool GINI, int NJ>
-__device__ __forceinline__ void hist_add_group(unsigned char* smem, uint32_t plane, int u0,
-                                               const uint32_t (&buf)[kG][NJ], uint32_t w0l,
-                                               uint32_t w0h, uint32_t w1l, uint32_t w1h,
-                                               const uint32_t (&amul)[NJ],
+// one LDS atomic per entry and lane group: GINI adds count wl into class plane
+// (offset wh); the u64 modes add (wh:wl)
+template <int MODE, int NJ>
+__device__ __forceinline__ void hist_add_group(unsigned char* smem, int u0,
+                                               const uint32_t (&buf)[kG][NJ], uint32_t wl,
+                                               uint32_t wh, const uint32_t (&amul)[NJ],
                                                const uint32_t (&abase)[NJ]) {
 #pragma unroll
   for (int t = 0; t < kG; t++) {
     const int u = u0 + t;
-    if (GINI) {
-      const uint32_t cu = rdlane(w0l, u), cou = rdlane(w0h, u);
+    if (MODE == kHistGini) {
+      const uint32_t cu = rdlane(wl, u), cou = rdlane(wh, u);
 #pragma unroll
       for (int jj = 0; jj < NJ; jj++) {
         const uint32_t addr = __umul24(buf[t][jj], amul[jj]) + abase[jj] + cou;
         atomicAdd((uint32_t*)(smem + addr), cu);
       }
     } else {
-      const unsigned long long a0 = ((unsigned long long)rdlane(w0h, u) << 32) | rdlane(w0l, u);
-      const unsigned long long a1 = ((unsigned long long)rdlane(w1h, u) << 32) | rdlane(w1l, u);
+      const unsigned long long a0 = ((unsigned long long)rdlane(wh, u) << 32) | rdlane(wl, u);
 #pragma unroll
       for (int jj = 0; jj < NJ; jj++) {
         const uint32_t addr = __umul24(buf[t][jj], amul[jj]) + abase[jj];
         atomicAdd((unsigned long long*)(smem + addr), a0);
-        atomicAdd((unsigned long long*)(smem + addr + plane), a1);
       }
     }
   }
 }
 
-template <bool GINI, int NJ>
+template <int MODE, int NJ>
 __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
+  constexpr bool GINI = MODE == kHistGini;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NB = A.NB, FPH = A.FPH;
   const uint32_t S = (uint32_t)A.S;
   const int ft0 = blockIdx.y * A.FT;
   constexpr uint32_t WB = GINI ? 4u : 8u;
   const uint32_t plane = hist_plane_bytes(NB, FPH, GINI);
-  const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.NS : 2u);
+  const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.NS : 1u);
   const uint32_t dump = (uint32_t)NB * FPH * WB + (uint32_t)lane * WB;  // inside plane 0
 
   for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
@@ -561,7 +574,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
     if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
-        hist_flush<GINI>(A, smem, plane, cur_slot, ft0, cur_ftn);
+        hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn);
         __syncthreads();
         for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
           *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
@@ -599,73 +612,71 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
       const int32_t hi = (int32_t)(e >> 32);
       const uint32_t c = (uint32_t)hi & 0xffu;  // 0 for lanes past the piece: they add zeros
       const int32_t k = hi >> 8;
-      uint32_t w0l, w0h, w1l, w1h;
-      if (GINI) {
-        w0l = c;
-        w0h = (uint32_t)k * cstride;  // class plane offset
-        w1l = w1h = 0;
+      uint32_t wl, wh;
+      if (MODE == kHistGini) {
+        wl = c;
+        wh = (uint32_t)k * cstride;  // class plane offset
       } else {
-        const uint64_t w0 = ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)((int64_t)k + K0);
-        const uint64_t w1 = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);  // < 2^56
-        w0l = (uint32_t)w0;
-        w0h = (uint32_t)(w0 >> 32);
-        w1l = (uint32_t)w1;
-        w1h = (uint32_t)(w1 >> 32);
+        const uint64_t w = MODE == kHistVar
+                               ? ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)((int64_t)k + K0)
+                               : (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);  // < 2^56
+        wl = (uint32_t)w;
+        wh = (uint32_t)(w >> 32);
       }
       uint32_t bA[kG][NJ], bB[kG][NJ];
       hist_load_group<NJ>(binsr, S, row, 0, posr, bA);
 #pragma unroll
       for (int g = 0; g < 64 / kG; g += 2) {
         if ((g + 1) * kG < n) hist_load_group<NJ>(binsr, S, row, (g + 1) * kG, posr, bB);
-        hist_add_group<GINI, NJ>(smem, plane, g * kG, bA, w0l, w0h, w1l, w1h, amul, abase);
+        hist_add_group<MODE, NJ>(smem, g * kG, bA, wl, wh, amul, abase);
         if ((g + 1) * kG >= n) break;
         if (g + 2 < 64 / kG && (g + 2) * kG < n)
           hist_load_group<NJ>(binsr, S, row, (g + 2) * kG, posr, bA);
-        hist_add_group<GINI, NJ>(smem, plane, (g + 1) * kG, bB, w0l, w0h, w1l, w1h, amul, abase);
+        hist_add_group<MODE, NJ>(smem, (g + 1) * kG, bB, wl, wh, amul, abase);
         if ((g + 2) * kG >= n) break;
       }
     }
   }
   if (cur_slot >= 0) {
     __syncthreads();
-    hist_flush<GINI>(A, smem, plane, cur_slot, ft0, cur_ftn);
+    hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn);
   }
 }
 
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini) {
-  return (size_t)hist_plane_bytes(NB, FPH, gini) * (gini ? (size_t)NS : 2u);
+  return (size_t)hist_plane_bytes(NB, FPH, gini) * (gini ? (size_t)NS : 1u);
 }
 
-template <bool GINI, int NJ>
+template <int MODE, int NJ>
 static void launch_hist_t(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds_bytes) {
   static bool attr_set = false;
   if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_hist<GINI, NJ>,
+    HIPCHK(hipFuncSetAttribute((const void*)k_hist<MODE, NJ>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_hist<GINI, NJ>), grid, dim3(kHistThreads), lds_bytes, st, a);
+  hipLaunchKernelGGL((k_hist<MODE, NJ>), grid, dim3(kHistThreads), lds_bytes, st, a);
 }
 
-void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, bool gini,
+template <int MODE>
+static void launch_hist_m(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds_bytes) {
+  switch ((a.FT + 63) / 64) {  // 64-feature lane groups per tile (FT <= 256)
+    case 1: launch_hist_t<MODE, 1>(st, a, grid, lds_bytes); break;
+    case 2: launch_hist_t<MODE, 2>(st, a, grid, lds_bytes); break;
+    case 3: launch_hist_t<MODE, 3>(st, a, grid, lds_bytes); break;
+    default: launch_hist_t<MODE, 4>(st, a, grid, lds_bytes); break;
+  }
+}
+
+void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mode,
                  size_t lds_bytes) {
   const dim3 grid((unsigned)nwg, (unsigned)ntiles);
-  const int nj = (a.FT + 63) / 64;  // 64-feature lane groups per tile (FT <= 256)
-  if (gini) {
-    switch (nj) {
-      case 1: launch_hist_t<true, 1>(st, a, grid, lds_bytes); break;
-      case 2: launch_hist_t<true, 2>(st, a, grid, lds_bytes); break;
-      case 3: launch_hist_t<true, 3>(st, a, grid, lds_bytes); break;
-      default: launch_hist_t<true, 4>(st, a, grid, lds_bytes); break;
-    }
-  } else {
-    switch (nj) {
-      case 1: launch_hist_t<false, 1>(st, a, grid, lds_bytes); break;
-      case 2: launch_hist_t<false, 2>(st, a, grid, lds_bytes); break;
-      case 3: launch_hist_t<false, 3>(st, a, grid, lds_bytes); break;
-      default: launch_hist_t<false, 4>(st, a, grid, lds_bytes); break;
-    }
-  }
+  if (mode == kHistGini)
+    launch_hist_m<kHistGini>(st, a, grid, lds_bytes);
+  else if (mode == kHistVar)
+    launch_hist_m<kHistVar>(st, a, grid, lds_bytes);
+  else
+    launch_hist_m<kHistSq>(st, a, grid, lds_bytes);
 }
 
 size_t hist_lds_limit() { return 160 * 1024; }
@@ -707,6 +718,20 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         mr[k] = __ballot(valid && right && wrp);
         nl += __popcll(ml[k]);
         nr += __popcll(mr[k]);
+      }
+      if (A.sq_left) {  // exact sum of count*k^2 of the left child (variance stats)
+        unsigned long long q = 0;
+#pragma unroll
+        for (int k = 0; k < kPartK; k++) {
+          const bool valid = base + k * 64 + lane < pc.b;
+          if (valid && byte[k] <= split) {
+            const int32_t hi = (int32_t)(e[k] >> 32);
+            const int64_t kk = hi >> 8;
+            q += (unsigned long long)(hi & 0xff) * (unsigned long long)(kk * kk);
+          }
+        }
+        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+        if (lane == 0 && q) atomicAdd(&A.sq_left[pc.parent], q);
       }
       unsigned long long bl = 0, br = 0;
       if (lane == 0) {
@@ -787,7 +812,7 @@ __device__ __forceinline__ double var_impurity(int64_t cnt, int64_t sk, uint64_t
 template <bool GINI>
 __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int slot = blockIdx.x, tid = threadIdx.x;
+  const int slot = A.slot_ids ? A.slot_ids[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x;
   const int r = A.slot_r[slot];
   const int Fr = A.Fr[r];
   const int NB = A.NB, NS = A.NS;
@@ -995,6 +1020,169 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
     so[NS + c] = l;
     so[2 * NS + c] = s_tot[c] - l;
   }
+}
+
+// ---- variance split screening from (count, sum) only.
+// Spark's gain  impurity - wL*imp(L) - wR*imp(R),  imp = (sumSq - sum^2/n)/n,  equals
+// g = (S1_L^2/n_L + S1_R^2/n_R - S1^2/n)/n exactly in real arithmetic: the sums of
+// squares cancel.  In fp64 both Spark's value G and our g carry rounding errors
+// bounded by a few ulps of sumSq/n (S1^2/n <= sumSq by Cauchy-Schwarz, every term of
+// both formulas is at most sumSq/n), so |G - g| <= delta = 2^-47 * sumSq/n (= 64 u).
+// A candidate whose g beats every other by more than 2*delta is Spark's argmax, and
+// g > delta (g >= minInfoGain + delta) decides G > 0 (G >= minInfoGain).  A node
+// where that does not hold is flagged (SplitOut.pad = 1): the host histograms its
+// sums of squares and reruns the exact k_split on it.
+__global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
+  const int slot = blockIdx.x, tid = threadIdx.x;
+  const int r = A.slot_r[slot];
+  const int Fr = A.Fr[r];
+  const int NB = A.NB;
+  const int64_t slot_words = (int64_t)A.Fmax * NB * 3;
+  __shared__ double s_g[256];
+  __shared__ int s_fl[256], s_s[256], s_cnt[256], s_any[256];
+  __shared__ int64_t s_tot[2];
+  const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
+  const uint64_t* hs = (const uint64_t*)A.hist + (int64_t)slot * slot_words;
+  if (tid < 2) {
+    int64_t t = 0;
+    for (int b = 0; b < NB; b++) t += (int64_t)hs[(int64_t)b * 3 + tid];
+    s_tot[tid] = t;
+  }
+  __syncthreads();
+  const int64_t tc = s_tot[0], tsk = s_tot[1];
+  const uint64_t tsq = A.node_sq[slot];
+  const double is2 = A.inv_scale2;
+  const double n = (double)tc;
+  const double delta = tc > 0 ? ldexp((double)tsq * is2 / n, -47) : 0.0;
+  const double sp = (double)tsk * (double)tsk / n;
+  const double lo_gain = A.min_gain - delta;  // below: invalid in Spark for sure
+  // pass 1: best g per feature (first max), any feature with splits
+  double fgb = -INFINITY;
+  int ffl = INT_MAX, fs = -1, any = INT_MAX;
+  for (int fl = tid; fl < Fr; fl += 256) {
+    const int nsp = nb_r[fl] - 1;
+    if (nsp <= 0) continue;
+    any = min(any, fl);
+    const uint64_t* h = hs + (int64_t)fl * NB * 3;
+    int64_t lc = 0, lsk = 0;
+    for (int s = 0; s < nsp; s++) {
+      lc += (int64_t)h[s * 3];
+      lsk += (int64_t)h[s * 3 + 1];
+      const int64_t rc = tc - lc, rsk = tsk - lsk;
+      if (lc < A.min_inst || rc < A.min_inst) continue;
+      const double g = (((double)lsk * (double)lsk / (double)lc +
+                         (double)rsk * (double)rsk / (double)rc) - sp) / n * is2;
+      if (g < lo_gain) continue;
+      if (g > fgb) {
+        fgb = g;
+        ffl = fl;
+        fs = s;
+      }
+    }
+  }
+  s_g[tid] = fgb;
+  s_fl[tid] = ffl;
+  s_s[tid] = fs;
+  s_any[tid] = any;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const double g2 = s_g[tid + o];
+      const int f2 = s_fl[tid + o];
+      if (g2 > s_g[tid] || (g2 == s_g[tid] && f2 < s_fl[tid])) {
+        s_g[tid] = g2;
+        s_fl[tid] = f2;
+        s_s[tid] = s_s[tid + o];
+      }
+      s_any[tid] = min(s_any[tid], s_any[tid + o]);
+    }
+    __syncthreads();
+  }
+  const double gb = s_g[0];
+  const int bfl = s_fl[0], bs = s_s[0], first_fl = s_any[0];
+  __syncthreads();
+  // pass 2: contenders within 2*delta of the best
+  int cnt = 0;
+  if (bfl != INT_MAX) {
+    const double thr = gb - 2.0 * delta;
+    for (int fl = tid; fl < Fr; fl += 256) {
+      const int nsp = nb_r[fl] - 1;
+      const uint64_t* h = hs + (int64_t)fl * NB * 3;
+      int64_t lc = 0, lsk = 0;
+      for (int s = 0; s < nsp; s++) {
+        lc += (int64_t)h[s * 3];
+        lsk += (int64_t)h[s * 3 + 1];
+        const int64_t rc = tc - lc, rsk = tsk - lsk;
+        if (lc < A.min_inst || rc < A.min_inst) continue;
+        const double g = (((double)lsk * (double)lsk / (double)lc +
+                           (double)rsk * (double)rsk / (double)rc) - sp) / n * is2;
+        if (g >= lo_gain && g >= thr) cnt++;
+      }
+    }
+  }
+  s_cnt[tid] = cnt;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) s_cnt[tid] += s_cnt[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    SplitOut o;
+    int64_t* so = A.stats + (int64_t)slot * 9;
+    so[0] = tc;
+    so[1] = tsk;
+    so[2] = (int64_t)tsq;
+    if (bfl == INT_MAX) {  // every candidate is invalid in Spark: leaf
+      o.gain = -DBL_MAX;
+      o.fl = first_fl == INT_MAX ? -1 : first_fl;
+      o.s = first_fl == INT_MAX ? -1 : 0;
+      o.valid = 0;
+      o.pad = 0;
+      so[3] = so[4] = so[5] = so[6] = so[7] = so[8] = 0;
+    } else {
+      const bool flag = s_cnt[0] > 1 || gb < A.min_gain + delta || gb <= delta;
+      o.gain = gb;
+      o.fl = bfl;
+      o.s = bs;
+      o.valid = 1;
+      o.pad = flag ? 1 : 0;
+      const uint64_t* h = hs + (int64_t)bfl * NB * 3;
+      int64_t lc = 0, lsk = 0;
+      for (int s = 0; s <= bs; s++) {
+        lc += (int64_t)h[s * 3];
+        lsk += (int64_t)h[s * 3 + 1];
+      }
+      so[3] = lc;
+      so[4] = lsk;
+      so[5] = -1;  // left sum of squares: from k_partition
+      so[6] = tc - lc;
+      so[7] = tsk - lsk;
+      so[8] = -1;
+    }
+    A.out[slot] = o;
+  }
+}
+
+void launch_split_screen(hipStream_t st, const SplitArgs& a, int M) {
+  hipLaunchKernelGGL(k_split_screen, dim3(M), dim3(256), 0, st, a);
+}
+
+// zero word `word` of every (feature, bin) cell of the listed slots
+__global__ __launch_bounds__(256) void k_zero_word(uint64_t* __restrict__ hist,
+                                                   const int32_t* __restrict__ slots,
+                                                   int64_t slot_words, int stride, int word) {
+  uint64_t* h = hist + (int64_t)slots[blockIdx.y] * slot_words;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < slot_words / stride;
+       i += (int64_t)gridDim.x * 256)
+    h[i * stride + word] = 0;
+}
+
+void launch_zero_word(hipStream_t st, uint64_t* hist, const int32_t* d_slots, int nslots,
+                      int64_t slot_words, int stride, int word) {
+  if (nslots <= 0) return;
+  const unsigned gx = (unsigned)std::min<int64_t>((slot_words / stride + 255) / 256, 64);
+  hipLaunchKernelGGL(k_zero_word, dim3(gx, (unsigned)nslots), dim3(256), 0, st, hist, d_slots,
+                     slot_words, stride, word);
 }
 
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {

@@ -162,3 +162,26 @@ def test_synthetic_classification_subspace(ctx):
     assert_forest_equal(forest, orf)
     assert (nat.predict_dataset(ctx, forest, ds, nat.AGG_MODE) ==
             oracle.predict(orf, X, classification=True)).all()
+
+
+def test_variance_screen_fallback_on_exact_ties(ctx, cpusmall):
+    """Duplicated feature columns make every split on column 0 tie exactly with its
+    copy: the (count, sum) screen must flag those nodes, and the exact fallback (sums
+    of squares histogram + Spark-order k_split) must pick the first feature like
+    RandomForest.binsToBestSplit's maxBy.  Checked bit-exact against the oracle."""
+    X, y = cpusmall
+    X = np.ascontiguousarray(np.concatenate([X, X[:, :3]], axis=1))
+    forest, orf, _ = _fit_both(ctx, X, y, 4, replacement=True, ratio=1.0, seed=SEED_REG,
+                               depth=6, bins=32, cls=False)
+    assert forest.timing()["exact_fallbacks"] > 0
+    assert_forest_equal(forest, orf)
+
+
+@pytest.mark.parametrize("min_gain", [0.0, 0.5, 25.0])
+def test_variance_min_info_gain(ctx, cpusmall, min_gain):
+    """minInfoGain decides leaves through Spark's fp64 gain: screened nodes near the
+    threshold fall back to the exact split."""
+    X, y = cpusmall
+    forest, orf, _ = _fit_both(ctx, X, y, 4, replacement=True, ratio=0.8, seed=SEED_REG + 3,
+                               depth=8, bins=24, cls=False, min_gain=min_gain, min_inst=3)
+    assert_forest_equal(forest, orf)
