@@ -681,9 +681,9 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mod
 
 size_t hist_lds_limit() { return 160 * 1024; }
 
-// ---- partition: 4 entries per lane per step, one cursor atomic per wave and side
+// ---- partition: 8 entries per lane per step, one cursor atomic per wave and side
 constexpr int kPartThreads = 256;
-constexpr int kPartK = 4;
+constexpr int kPartK = 8;
 
 __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
