@@ -55,8 +55,8 @@ def parse():
     ap.add_argument("--bins", type=int, default=32)
     ap.add_argument("--partitions", type=int, default=128)
     ap.add_argument("--seed", type=int, default=20261015)
-    ap.add_argument("--cpu-rows", type=int, default=200_000)
-    ap.add_argument("--cpu-learners", type=int, default=16)
+    ap.add_argument("--cpu-rows", type=int, default=1_000_000)
+    ap.add_argument("--cpu-learners", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -143,7 +143,7 @@ def main():
     lds_rate = lds_instr / (hist_ms / 1e3) if hist_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),
-                "kernel": "sbag::k_hist<false,2>",
+                "kernel": "sbag::k_hist<1, 2> (kHistVar, 2 lane groups)",
                 "avg_launch_ms": round(hist_ms / nl, 4),
                 "alg_bytes_per_launch": round(work_bytes / nl),
                 "alg_bytes_def": "SURVEY 8d: sum over histograms built (read or by subtraction) of "

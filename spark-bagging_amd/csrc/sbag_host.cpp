@@ -771,25 +771,61 @@ int sbag_dataset_free(sbag_dataset* ds) {
 
 // ---------------------------------------------------------------- fit
 struct HistGeom {
-  int T, FT, FPH, ntiles;
+  int T, FT, FPH, ntf, CT, ntiles;
   size_t lds;
 };
 
 static int roundup(int x, int a) { return (x + a - 1) / a * a; }
 
+// LDS geometry of one k_hist workgroup: FT features (lane groups of 64) and, for
+// gini, CT class planes.  Aim at <= 80 KB (two 512-thread workgroups per CU).
+// Many classes (BASELINE config 5: 64) are split into class tiles first: a class
+// tile re-reads the 8-byte entries but loads the row bytes of its own entries only,
+// whereas a feature tile re-reads every row.
 static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g) {
   (void)S;
   g.T = 64;  // piece granularity (entries)
   const int align = gini_layout ? 32 : 16;
-  auto lds_for = [&](int ft) { return hist_lds_bytes(NB, NS, roundup(ft, align), gini_layout); };
+  size_t soft = 80 * 1024;
+  if (const char* e = getenv("SBAG_HIST_LDS_KB")) soft = (size_t)atoi(e) * 1024;
+  const size_t hard = 160 * 1024 - 256;
+  auto lds_for = [&](int ft, int ct) {
+    size_t b = hist_lds_bytes(NB, gini_layout ? ct : 1, roundup(ft, align), gini_layout);
+    if (gini_layout && ct < NS) b += hist_stage_bytes();
+    return b;
+  };
   int ft = std::min(256, roundup(Fmax, align));
-  const size_t soft = 80 * 1024, hard = 160 * 1024 - 256;
-  while (ft > align && lds_for(ft) > soft) ft -= align;
-  if (lds_for(ft) > hard) return false;
+  int ct = gini_layout ? NS : 1;
+  for (;;) {
+    if (!gini_layout) {
+      if (lds_for(ft, 1) <= soft || ft <= align) break;
+      ft -= align;
+      continue;
+    }
+    const size_t P = hist_lds_bytes(NB, 1, roundup(ft, align), true);
+    if ((size_t)NS * P <= soft) {
+      ct = NS;
+      break;
+    }
+    const long c = soft > hist_stage_bytes() ? (long)((soft - hist_stage_bytes()) / P) : 0;
+    if (c >= 1) {
+      const int nct = (NS + (int)c - 1) / (int)c;
+      ct = (NS + nct - 1) / nct;  // balanced class tiles
+      break;
+    }
+    if (ft <= align) {
+      ct = 1;
+      break;
+    }
+    ft -= align;
+  }
+  if (lds_for(ft, ct) > hard) return false;
   g.FT = std::min(ft, Fmax);
   g.FPH = roundup(g.FT, align);
-  g.ntiles = (Fmax + g.FT - 1) / g.FT;
-  g.lds = lds_for(g.FT);
+  g.CT = ct;
+  g.ntf = (Fmax + g.FT - 1) / g.FT;
+  g.ntiles = g.ntf * ((gini_layout ? (NS + ct - 1) / ct : 1));
+  g.lds = lds_for(g.FT, ct);
   return true;
 }
 
@@ -1021,6 +1057,8 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     ha.parents = d_par;
     ha.FT = g.FT;
     ha.FPH = g.FPH;
+    ha.CT = g.CT;
+    ha.ntf = g.ntf;
     int h = tm.begin(cat);
     launch_hist(c->stream, ha, work.nwg, g.ntiles, mode, g.lds);
     HIP_TRY(hipGetLastError());

@@ -51,6 +51,8 @@ struct HistArgs {
   int64_t flush_limit;   // max entries accumulated in LDS between flushes
   int32_t FT, FPH;       // features per tile, LDS pitch
   int32_t count_only;    // gini layout with the label ignored (value counts)
+  int32_t CT;            // gini: classes per class tile (LDS holds CT class planes)
+  int32_t ntf;           // feature tiles; blockIdx.y = class_tile * ntf + feature_tile
   int32_t pad;
 };
 
@@ -113,6 +115,7 @@ void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, con
 void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mode,
                  size_t lds_bytes);
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini);
+size_t hist_stage_bytes();
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg);
 void launch_transpose(hipStream_t st, const uint8_t* src, int64_t N, int S, int C, uint8_t* dst,
                       int64_t npad, int R, int64_t src_rstride, int64_t dst_rstride);

@@ -453,16 +453,18 @@ static __host__ __device__ inline uint32_t hist_plane_bytes(int NB, int FPH, boo
 //       kHistSq    u64 count*k^2                           -> hist[.][2]
 template <int MODE>
 __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned char* smem,
-                                           uint32_t plane, int slot, int ft0, int ftn) {
+                                           uint32_t plane, int slot, int ft0, int ftn, int c0,
+                                           int nct) {
   const int tid = threadIdx.x;
   const int NB = A.NB, NS = A.NS, FPH = A.FPH;
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
   if (MODE == kHistGini) {
+    // class planes [0, nct) of the LDS hold classes [c0, c0 + nct)
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
-    for (int q = tid; q < ftn * NB * NS; q += blockDim.x) {
-      const int cls = q % NS, b = (q / NS) % NB, f = q / (NS * NB);
-      const uint32_t v = *(const uint32_t*)(smem + (size_t)cls * plane + ((size_t)b * FPH + f) * 4);
-      if (v) atomicAdd(&gh[((int64_t)(ft0 + f) * NB + b) * NS + cls], v);
+    for (int q = tid; q < ftn * NB * nct; q += blockDim.x) {
+      const int cl = q % nct, b = (q / nct) % NB, f = q / (nct * NB);
+      const uint32_t v = *(const uint32_t*)(smem + (size_t)cl * plane + ((size_t)b * FPH + f) * 4);
+      if (v) atomicAdd(&gh[((int64_t)(ft0 + f) * NB + b) * NS + c0 + cl], v);
     }
   } else {
     unsigned long long* gh = (unsigned long long*)A.hist + (int64_t)slot * slot_words;
@@ -542,11 +544,18 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NB = A.NB, FPH = A.FPH;
   const uint32_t S = (uint32_t)A.S;
-  const int ft0 = blockIdx.y * A.FT;
+  const int ft0 = (int)(blockIdx.y % (unsigned)A.ntf) * A.FT;
+  // gini class tiling: this workgroup accumulates classes [c0, c0 + nct) only
+  const int c0 = GINI ? (int)(blockIdx.y / (unsigned)A.ntf) * A.CT : 0;
+  const int nct = GINI ? min(A.CT, A.NS - c0) : 1;
+  const bool ctile = GINI && !A.count_only && A.CT < A.NS;
   constexpr uint32_t WB = GINI ? 4u : 8u;
   const uint32_t plane = hist_plane_bytes(NB, FPH, GINI);
-  const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.NS : 1u);
+  const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.CT : 1u);
   const uint32_t dump = (uint32_t)NB * FPH * WB + (uint32_t)lane * WB;  // inside plane 0
+  // per-wave staging of the batch entries that fall in the class tile
+  uint64_t* stage = (uint64_t*)(smem + hist_bytes) + wave * 64;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 
   for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
     *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
@@ -574,7 +583,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
     if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
-        hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn);
+        hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct);
         __syncthreads();
         for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
           *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
@@ -604,10 +613,23 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
     int64_t q0 = a + (int64_t)wave * 64;
     uint64_t e_next = (q0 + lane < b) ? A.ent_in[q0 + lane] : 0ull;
     for (; q0 < b; q0 += (int64_t)kHistWaves * 64) {
-      const int n = (int)min((int64_t)64, b - q0);
-      const uint64_t e = e_next;
+      int n = (int)min((int64_t)64, b - q0);
+      uint64_t e = e_next;
       const int64_t qn = q0 + (int64_t)kHistWaves * 64 + lane;
       e_next = (qn < b) ? A.ent_in[qn] : 0ull;
+      if (ctile) {  // keep the batch entries of classes [c0, c0 + nct), packed to the front
+        const int32_t eh = (int32_t)(e >> 32);
+        const int kc = eh >> 8;
+        const bool m = ((eh & 0xff) != 0) && kc >= c0 && kc < c0 + nct;  // c = 0 past the piece
+        const uint64_t mask = __ballot(m);
+        if (m) stage[__popcll(mask & lt_mask)] = e;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        n = __popcll(mask);
+        e = (lane < n) ? stage[lane] : 0ull;
+        __builtin_amdgcn_wave_barrier();
+        if (n == 0) continue;
+      }
       const uint32_t row = (uint32_t)e;
       const int32_t hi = (int32_t)(e >> 32);
       const uint32_t c = (uint32_t)hi & 0xffu;  // 0 for lanes past the piece: they add zeros
@@ -615,7 +637,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
       uint32_t wl, wh;
       if (MODE == kHistGini) {
         wl = c;
-        wh = (uint32_t)k * cstride;  // class plane offset
+        wh = c ? (uint32_t)(k - c0) * cstride : 0u;  // class plane offset; c = 0 lanes add 0
       } else {
         const uint64_t w = MODE == kHistVar
                                ? ((uint64_t)c << cs) + (uint64_t)c * (uint64_t)((int64_t)k + K0)
@@ -639,13 +661,14 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   }
   if (cur_slot >= 0) {
     __syncthreads();
-    hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn);
+    hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct);
   }
 }
 
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini) {
   return (size_t)hist_plane_bytes(NB, FPH, gini) * (gini ? (size_t)NS : 1u);
 }
+size_t hist_stage_bytes() { return (size_t)kHistWaves * 64 * 8; }
 
 template <int MODE, int NJ>
 static void launch_hist_t(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds_bytes) {

@@ -185,3 +185,33 @@ def test_variance_min_info_gain(ctx, cpusmall, min_gain):
     forest, orf, _ = _fit_both(ctx, X, y, 4, replacement=True, ratio=0.8, seed=SEED_REG + 3,
                                depth=8, bins=24, cls=False, min_gain=min_gain, min_inst=3)
     assert_forest_equal(forest, orf)
+
+
+def _synthetic_cls(ctx, N, F, C, L, depth, seed_data, ratio=0.5, replacement=False):
+    ds = nat.DeviceDataset.synthetic(N, F, seed=seed_data, num_classes=C, ctx=ctx)
+    X, y = ds.features(), ds.labels()
+    forest = nat.fit(ctx, ds, replacement=replacement, sample_ratio=ratio, seed=SEED_CLS,
+                     learner_begin=0, learner_end=L, max_depth=depth, max_bins=32,
+                     impurity=nat.IMPURITY_GINI)
+    counts = oracle.bag(replacement, ratio, 0, L, SEED_CLS, [0, N], N)
+    subs = [oracle.subspace(ratio, F, SEED_CLS + i) for i in range(L)]
+    orf = oracle_forest(X, y, counts, subs, depth, 32, True)
+    return ds, X, forest, orf
+
+
+def test_many_classes_c5_shape(ctx):
+    """BASELINE config 5 in miniature: 64 classes, without-replacement subsample 0.5,
+    depth 12.  64 class planes do not fit in LDS, so k_hist runs class tiles."""
+    ds, X, forest, orf = _synthetic_cls(ctx, 24000, 100, 64, 3, 12, seed_data=17)
+    assert_forest_equal(forest, orf)
+    assert (nat.predict_dataset(ctx, forest, ds, nat.AGG_MODE) ==
+            oracle.predict(orf, X, classification=True)).all()
+
+
+def test_gini_class_tiles_forced(ctx, monkeypatch):
+    """A tiny LDS budget forces one-class tiles on a 7-class problem (k_hist class
+    tiling + per-wave entry staging), bit-exact against the oracle."""
+    monkeypatch.setenv("SBAG_HIST_LDS_KB", "12")
+    ds, X, forest, orf = _synthetic_cls(ctx, 15000, 80, 7, 4, 7, seed_data=23, ratio=0.8,
+                                        replacement=True)
+    assert_forest_equal(forest, orf)
