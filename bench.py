@@ -21,6 +21,7 @@ sys.path.insert(0, ROOT)
 import sbag_loader  # noqa: E402
 
 SEED_REG = -1395689524  # default seed of BaggingRegressor (class-name hashCode)
+SEED_CLS = 42087812     # default seed of BaggingClassifier
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
 # ds_add_u64 throughput measured on MI355X by scripts/micro/lds_atomic.hip:
 # 7.16 cycles per wave-instruction per CU (4 x 512-thread workgroups per CU), 256 CUs, 2.4 GHz
@@ -43,22 +44,49 @@ def pmc_traffic():
     return None
 
 
+# BASELINE.json configs as bench workloads (per GPU).  c3 is the headline (default);
+# c4 / c5 are the shapes of configs[3] / configs[4] on one GPU's learner shard.
+WORKLOADS = {
+    "c3": dict(rows=10_000_000, features=100, learners=128, depth=8, classes=0,
+               replacement=True, ratio=1.0,
+               name="C3: BaggingRegressor(DecisionTreeRegressor) fit, synthetic {N} rows x {F} "
+                    "features, {L} bootstrap depth-{D} trees per GPU"),
+    "c4": dict(rows=100_000_000, features=256, learners=64, depth=8, classes=0,
+               replacement=True, ratio=1.0,
+               name="C4 shard: BaggingRegressor fit, synthetic {N} rows x {F} features, "
+                    "{L} bootstrap depth-{D} trees per GPU (512 learners over 8 GPUs)"),
+    "c5": dict(rows=50_000_000, features=100, learners=16, depth=12, classes=64,
+               replacement=False, ratio=0.5,
+               name="C5 shard: BaggingClassifier(DecisionTreeClassifier) fit, synthetic {N} rows "
+                    "x {F} features, {C} classes, subsample 0.5 without replacement, {L} depth-{D} "
+                    "trees per GPU (128 learners over 8 GPUs)"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--rows", type=int, default=10_000_000)
-    ap.add_argument("--features", type=int, default=100)
-    ap.add_argument("--learners", type=int, default=128, help="learners per GPU")
-    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--features", type=int, default=None)
+    ap.add_argument("--learners", type=int, default=None, help="learners per GPU")
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--bins", type=int, default=32)
     ap.add_argument("--partitions", type=int, default=128)
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-learners", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    w = WORKLOADS[a.workload]
+    for k in ("rows", "features", "learners", "depth"):
+        if getattr(a, k) is None:
+            setattr(a, k, w[k])
+    a.classes, a.replacement, a.ratio = w["classes"], w["replacement"], w["ratio"]
+    a.workload_name = w["name"].format(N=a.rows, F=a.features, L=a.learners, D=a.depth, C=a.classes)
+    return a
 
 
 def cpu_baseline(args):
@@ -70,12 +98,15 @@ def cpu_baseline(args):
 
     n, L = args.cpu_rows, args.cpu_learners
     cores = min(L, os.cpu_count() or 1, 16)
-    X, y = synthetic.generate(n, args.features, args.seed, 0)
+    cls = args.classes > 0
+    seed = SEED_CLS if cls else SEED_REG
+    X, y = synthetic.generate(n, args.features, args.seed, args.classes)
     part = [int(round(i * n / args.partitions)) for i in range(args.partitions + 1)]
-    counts = oracle.bag(True, 1.0, 0, L, SEED_REG, part, n)
-    subs = [oracle.subspace(1.0, args.features, SEED_REG + i) for i in range(L)]
+    counts = oracle.bag(args.replacement, args.ratio, 0, L, seed, part, n)
+    subs = [oracle.subspace(args.ratio, args.features, seed + i) for i in range(L)]
     t0 = time.perf_counter()
-    oracle.fit(X, y, counts, subs, max_depth=args.depth, max_bins=args.bins, nthreads=cores)
+    oracle.fit(X, y, counts, subs, max_depth=args.depth, max_bins=args.bins, nthreads=cores,
+               classification=cls)
     dt = time.perf_counter() - t0
     return {"value": L * n / dt, "unit": "estimator*rows/s", "cores": cores, "kind": "port",
             "sample": f"{n} rows x {args.features} features, {L} learners, depth {args.depth}, "
@@ -98,14 +129,16 @@ def main():
     nat = sb._native
     ctx = nat.Context(local)
     N, F, L = args.rows, args.features, args.learners
-    ds = nat.DeviceDataset.synthetic(N, F, seed=args.seed, num_classes=0, ctx=ctx)
+    cls = args.classes > 0
+    ds = nat.DeviceDataset.synthetic(N, F, seed=args.seed, num_classes=args.classes, ctx=ctx)
     part = [int(round(i * N / args.partitions)) for i in range(args.partitions + 1)]
     lb = rank * L
 
     def step():
-        return nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG,
-                       learner_begin=lb, learner_end=lb + L, partition_offsets=part,
-                       max_depth=args.depth, max_bins=args.bins)
+        return nat.fit(ctx, ds, replacement=args.replacement, sample_ratio=args.ratio,
+                       seed=SEED_CLS if cls else SEED_REG, learner_begin=lb, learner_end=lb + L,
+                       partition_offsets=part, max_depth=args.depth, max_bins=args.bins,
+                       impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
 
     for _ in range(args.warmup):
         step().free()
@@ -137,22 +170,24 @@ def main():
     nl = max(hist_launches, 1)
     avg_s = hist_ms / 1e3 / nl
     achieved = work_bytes / nl / avg_s / 1e9 if hist_ms > 0 else 0.0
-    # LDS atomic co-limiter: one u64 atomic per entry and 64-feature lane group
-    # (variance screening: (count, sum) only)
+    # LDS atomic co-limiter: one atomic per entry and 64-feature lane group (variance:
+    # ds_add_u64 of (count, sum) after the screening of DESIGN.md §5; gini: ds_add_u32)
     lds_instr = entries * ((F + 63) // 64)
     lds_rate = lds_instr / (hist_ms / 1e3) if hist_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),
-                "kernel": "sbag::k_hist<1, 2> (kHistVar, 2 lane groups)",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic() if args.workload == "c3" else None,
+                "kernel": ("sbag::k_hist<0, NJ> (kHistGini, class tiles)" if cls else
+                           "sbag::k_hist<1, 2> (kHistVar, 2 lane groups)"),
                 "avg_launch_ms": round(hist_ms / nl, 4),
                 "alg_bytes_per_launch": round(work_bytes / nl),
                 "alg_bytes_def": "SURVEY 8d: sum over histograms built (read or by subtraction) of "
-                                 "n(r,d)*(F_r+4) + 3N",
+                                 "n(r,d)*(F_r+s_y) + 3N, s_y = 4 (regression) / 1 (class)",
                 "kernel_read_bytes_per_launch": round(read_bytes / nl),
                 "kernel_read_GBs": round(read_bytes / nl / avg_s / 1e9, 1) if hist_ms > 0 else 0.0,
                 "lds_atomic": {"achieved": round(lds_rate / 1e9, 2),
                                "peak": round(LDS_ATOMIC_PEAK / 1e9, 2),
-                               "unit": "G wave-instr/s (ds_add_u64)",
+                               "unit": "G wave-instr/s (ds_add_u64 peak)",
                                "frac": round(lds_rate / LDS_ATOMIC_PEAK, 4)}}
     breakdown = {k: round(v, 3) for k, v in timings[-1].items() if k.endswith("_ms")}
     out = {
@@ -160,12 +195,13 @@ def main():
         "unit": "estimator*rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64",
-        "data": "synthetic (device generator k_synth: splitmix64 codes mod 32, dyadic labels)",
-        "config": {"workload": "C3: BaggingRegressor(DecisionTreeRegressor) fit, synthetic "
-                               f"{N} rows x {F} features, {L} bootstrap depth-{args.depth} trees per GPU",
+        "data": "synthetic (device generator k_synth: splitmix64 codes mod 32, "
+                + ("class labels)" if cls else "dyadic labels)"),
+        "config": {"workload": args.workload_name,
                    "rows": N, "features": F, "learners_per_gpu": L, "learners_total": L * world,
                    "max_depth": args.depth, "max_bins": args.bins, "partitions": args.partitions,
-                   "replacement": True, "sample_ratio": 1.0, "parallelism": f"learner-shard x{world}"},
+                   "classes": args.classes, "replacement": args.replacement,
+                   "sample_ratio": args.ratio, "parallelism": f"learner-shard x{world}"},
         "roofline": roofline, "breakdown_ms": breakdown,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

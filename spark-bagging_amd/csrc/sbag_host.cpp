@@ -572,7 +572,7 @@ static int run_sampler(sbag_ctx* c, const sbag_sampler_params* p, const std::vec
   TRY(h2d(c, d_poff, poff.data(), poff.size()));
   if (p->replacement) {
     int* d_err;
-    TRY(ws_typed(c, "err", 1, &d_err));
+    TRY(ws_typed(c, "err", 1 + 16, &d_err));  // flag + 64-byte store sink for k_poisson
     HIP_TRY(hipMemsetAsync(d_err, 0, 4, c->stream));
     const double p_exp = std::exp(-p->sample_ratio);  // PoissonDistribution: FastMath.exp(-mean)
     launch_poisson(c->stream, d_counts, N, d_poff, P, R, p->learner_begin, p->seed, p->sample_ratio,
@@ -1035,12 +1035,13 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   ha.cshift = cshift;
   ha.flush_limit = flush_limit;
   double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0, hist_work = 0;
+  const int s_y = gini ? 1 : 4;  // label bytes per row in SURVEY 8d (u8 class / fp32 label)
   // SURVEY §8d work bytes of the histograms of a set of node segments
   auto add_work = [&](const std::vector<std::pair<int64_t, int64_t>>& segs,
                       const std::vector<int>& seg_r) {
     std::vector<char> act(R, 0);
     for (size_t q = 0; q < segs.size(); q++) {
-      hist_work += (double)(segs[q].second - segs[q].first) * (h_Fr[seg_r[q]] + 4);
+      hist_work += (double)(segs[q].second - segs[q].first) * (h_Fr[seg_r[q]] + s_y);
       act[seg_r[q]] = 1;
     }
     for (int r = 0; r < R; r++) hist_work += act[r] ? 3.0 * N : 0.0;
@@ -1068,7 +1069,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       for (size_t q = 0; q < segs.size(); q++) {
         const double ne = (double)(segs[q].second - segs[q].first);
         hist_entries += ne;
-        hist_alg_bytes += ne * (h_Fr[par[q].r] + 4);
+        hist_alg_bytes += ne * (h_Fr[par[q].r] + s_y);
       }
     }
     return SBAG_OK;
@@ -1322,7 +1323,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     ha.hist = hist_cur;
     TRY(launch(g, gini ? kHistGini : kHistVar, T_HIST, seg, h_par));
   }
-  for (int r = 0; r < R; r++) hist_upper += (double)inbag[r] * (h_Fr[r] + 4) * D + 3.0 * N * D;
+  for (int r = 0; r < R; r++) hist_upper += (double)inbag[r] * (h_Fr[r] + s_y) * D + 3.0 * N * D;
   {
     std::vector<int> seg_r(R);
     for (int r = 0; r < R; r++) seg_r[r] = r;

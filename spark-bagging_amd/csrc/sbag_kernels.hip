@@ -91,11 +91,12 @@ __device__ __forceinline__ int well_batch(uint32_t* __restrict__ st, int lane, i
   }
 #pragma unroll
   for (int t = 0; t < kWB; t++) {
-    const uint32_t z0 = (0x80000000u & hb[t]) ^ (0x7FFFFFFFu & lo[t]);
+    const uint32_t z0 = (0x80000000u & hb[t]) | (0x7FFFFFFFu & lo[t]);
     const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1[t] ^ (m1[t] >> 27));
     const uint32_t z2 = (m2[t] >> 9) ^ (m3[t] ^ (m3[t] >> 1));
     const uint32_t z3 = z1 ^ z2;
-    uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
+    // AbstractWell's z4 = z0 ^ (z1 ^ z1<<9) ^ (z2 ^ z2<<21) ^ (z3 ^ z3>>21); z1^z2^z3 == 0
+    uint32_t z4 = z0 ^ (z1 << 9) ^ (z2 << 21) ^ (z3 >> 21);
     z3v[t] = z3;
     v0 = z4;
     z4 ^= (z4 << 7) & 0xe46e1700u;
@@ -136,8 +137,10 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
   int64_t row = active ? part_off[p] : 0;
   const int64_t row_end = active ? part_off[p + 1] : 0;
   uint8_t* out = counts + (int64_t)r * N;
-  const double cap = 1000.0 * mean;
+  // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean)
+  const int icap = (int)ceil(1000.0 * mean);
   int n = 0, bad = 0;
+  uint8_t* const sink = (uint8_t*)(err + 1) + lane;  // stores of lanes that finish no row
   double racc = 1.0;
   uint32_t v0 = st[lane];
   // prologue: the single step at index 0, leaving index 623 = 16*38+15
@@ -166,23 +169,27 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
       index = well_batch<false>(st, lane, index, v0, w);
     else
       index = well_batch<true>(st, lane, index, v0, w);
-    // doubles: (pending, o0), (o1, o2), ..., (o13, o14); o15 carries over
+    // doubles: (pending, o0), (o1, o2), ..., (o13, o14); o15 carries over.
+    // BitsStreamGenerator.nextDouble = (next(26) << 26 | next(26)) * 2^-52, built as
+    // the bits of 1 + m * 2^-52 minus 1 (exact: m < 2^52).  Branch-free row update:
+    // a lane that finishes a row stores its count, the others store to a sink.
 #pragma unroll
     for (int u = 0; u < kWB / 2; u++) {
       const uint32_t hi = u == 0 ? pending : w.o[2 * u - 1];
-      const double x = (double)((((uint64_t)hi) << 26) | (uint64_t)w.o[2 * u]) * 0x1.0p-52;
-      if (row < row_end) {
-        racc *= x;
-        const bool ge = racc >= p_exp;
-        n += ge ? 1 : 0;
-        if (!ge || !((double)n < cap)) {
-          bad |= n > 255;
-          out[row] = (uint8_t)(n > 255 ? 255 : n);
-          row++;
-          n = 0;
-          racc = 1.0;
-        }
-      }
+      const uint32_t lo32 = (hi << 26) | w.o[2 * u];
+      const uint32_t hi32 = 0x3FF00000u | (hi >> 6);
+      const double x = __hiloint2double((int)hi32, (int)lo32) - 1.0;
+      const bool live = row < row_end;
+      racc *= x;
+      const bool ge = racc >= p_exp;
+      n += ge ? 1 : 0;
+      const bool done = live && (!ge || n >= icap);
+      bad |= (done && n > 255) ? 1 : 0;
+      uint8_t* dst = done ? out + row : sink;
+      *dst = (uint8_t)min(n, 255);
+      row += done ? 1 : 0;
+      n = done ? 0 : n;
+      racc = done ? 1.0 : racc;
     }
     pending = w.o[kWB - 1];
   }
