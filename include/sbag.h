@@ -91,6 +91,7 @@ int sbag_dataset_info(const sbag_dataset* ds, int64_t* num_rows, int32_t* num_fe
 int sbag_dataset_labels(const sbag_dataset* ds, double* y_out);
 int sbag_dataset_features(const sbag_dataset* ds, int64_t row_begin, int64_t row_end,
                           double* X_out /* [(row_end-row_begin) x F] */);
+/* datasets reference their context: free every dataset before sbag_ctx_destroy */
 int sbag_dataset_free(sbag_dataset* ds);
 
 /* ---- fit: BaggingRegressor.train / BaggingClassifier.train --------------

@@ -5,6 +5,7 @@ no CPU fallback; if the library is missing or fails to load, importing the
 compute entry points raises.
 """
 import ctypes
+import weakref
 import os
 
 import numpy as np
@@ -144,6 +145,7 @@ class Context:
         self._h = ctypes.c_void_p()
         check(lib().sbag_ctx_create(device, ctypes.byref(self._h)))
         self.device = device
+        self._datasets = weakref.WeakSet()  # freed before the context (sbag.h ownership)
 
     @property
     def handle(self):
@@ -151,6 +153,8 @@ class Context:
 
     def close(self):
         if self._h:
+            for ds in list(self._datasets):
+                ds.free()
             lib().sbag_ctx_destroy(self._h)
             self._h = ctypes.c_void_p()
 
@@ -181,6 +185,7 @@ class DeviceDataset:
 
     def __init__(self, ctx, handle):
         self.ctx, self._h = ctx, handle
+        ctx._datasets.add(self)
 
     @classmethod
     def from_numpy(cls, X, y, ctx=None):

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -57,6 +58,10 @@ struct sbag_ctx {
   hipStream_t stream = nullptr;
   std::unordered_map<std::string, DevBuf> ws;
   uint64_t* d_jump = nullptr;
+  // pinned staging for the per-level uploads (work lists, tables): a bump arena
+  // that is reset whenever the stream is known to be idle (every d2h synchronizes)
+  unsigned char* pin = nullptr;
+  size_t pin_cap = 0, pin_used = 0;
 };
 
 static int ws_get(sbag_ctx* c, const std::string& name, size_t bytes, void** out) {
@@ -96,7 +101,28 @@ static int ws_typed(sbag_ctx* c, const std::string& name, size_t count, T** out)
 template <typename T>
 static int h2d(sbag_ctx* c, T* dst, const T* src, size_t count) {
   if (count == 0) return SBAG_OK;
-  HIP_TRY(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  const size_t bytes = count * sizeof(T);
+  if (bytes <= ((size_t)64 << 20)) {  // through the pinned arena: a true async DMA
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (c->pin_used + need > c->pin_cap) {
+      HIP_TRY(hipStreamSynchronize(c->stream));  // earlier uploads have been consumed
+      c->pin_used = 0;
+      if (need > c->pin_cap) {
+        if (c->pin) HIP_TRY(hipHostFree(c->pin));
+        c->pin = nullptr;
+        c->pin_cap = 0;
+        const size_t cap = std::max<size_t>(need, (size_t)8 << 20);
+        HIP_TRY(hipHostMalloc((void**)&c->pin, cap, hipHostMallocDefault));
+        c->pin_cap = cap;
+      }
+    }
+    unsigned char* stage = c->pin + c->pin_used;
+    c->pin_used += need;
+    memcpy(stage, src, bytes);
+    HIP_TRY(hipMemcpyAsync(dst, stage, bytes, hipMemcpyHostToDevice, c->stream));
+    return SBAG_OK;
+  }
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
   return SBAG_OK;
 }
 template <typename T>
@@ -104,6 +130,7 @@ static int d2h(sbag_ctx* c, T* dst, const T* src, size_t count) {
   if (count == 0) return SBAG_OK;
   HIP_TRY(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  c->pin_used = 0;  // the stream is idle: every staged upload has completed
   return SBAG_OK;
 }
 
@@ -533,6 +560,7 @@ int sbag_ctx_destroy(sbag_ctx* c) {
   for (auto& kv : c->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
   if (c->d_jump) (void)hipFree(c->d_jump);
+  if (c->pin) (void)hipHostFree(c->pin);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return SBAG_OK;
@@ -1338,10 +1366,24 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   std::vector<uint64_t> slot_sq(R);
   for (int r = 0; r < R; r++) slot_sq[r] = inbag[3 * R + r];
   int64_t fallbacks = 0;
+  // host-side phase timing (SBAG_PROFILE_HOST=1 prints it): where the GPU waits
+  const bool hprof = getenv("SBAG_PROFILE_HOST") != nullptr;
+  double hp[8] = {0};
+  auto hnow = [] {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  double ht = hnow();
+  auto hmark = [&](int k) {
+    const double t = hnow();
+    hp[k] += t - ht;
+    ht = t;
+  };
   for (int level = 0; level <= D; level++) {
     const int M = (int)slots.size();
     if (M == 0) break;
     levels++;
+    hmark(7);
     // --- split search on the device
     std::vector<int32_t> h_slot_r(M);
     for (int i = 0; i < M; i++) h_slot_r[i] = slots[i].first;
@@ -1383,7 +1425,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     }
     std::vector<SplitOut> sout(M);
     std::vector<int64_t> sst((size_t)M * 3 * NS);
+    hmark(0);
     TRY(d2h(c, sout.data(), d_sout, (size_t)M));
+    hmark(1);
     std::vector<char> exact(M, gini ? 1 : 0);
     if (!gini) {
       // nodes the screen could not decide: histogram their sums of squares (word 2)
@@ -1485,6 +1529,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       pseg.push_back(seg[i]);
       psplit.push_back(Split{i, r, ni, li});
     }
+    hmark(2);
     if (par.empty()) break;
     // --- partition the rows of every split node into its children (and, for
     // variance, the exact sum of squares of each left child)
@@ -1502,25 +1547,86 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       HIP_TRY(hipMemsetAsync(d_sql, 0, (size_t)NP * 8, c->stream));
     }
     {
-      build_work(pseg, (int64_t)1 << 40, 256 * 8, 1024, work);
-      TRY(upload_work(par));
+      // work order: parents grouped by split column (replica copies apart), pieces of
+      // 8192 entries interleaved round-robin across the parents of a group, so the
+      // concurrent workgroups spread over the group's cursors while the GPU reads
+      // one column
+      const int64_t piece = 8192;
+      std::vector<int32_t> order(NP);
+      for (int q = 0; q < NP; q++) order[q] = q;
+      auto colkey = [&](int q) {
+        return (bins_rstride ? (int64_t)par[q].r * 65536 : 0) + (int64_t)par[q].pos;
+      };
+      std::stable_sort(order.begin(), order.end(),
+                       [&](int x, int y) { return colkey(x) < colkey(y); });
+      // rounds: inside a column group (parents longest first), round k takes piece k
+      // of every parent longer than k pieces; the piece list is written on the device
+      std::vector<PartRound> rounds;
+      std::vector<int64_t> segv((size_t)2 * NP);
+      for (int q = 0; q < NP; q++) {
+        segv[2 * q] = pseg[q].first;
+        segv[2 * q + 1] = pseg[q].second;
+      }
+      int64_t npieces = 0;
+      for (int g0 = 0; g0 < NP;) {
+        int g1 = g0;
+        while (g1 < NP && colkey(order[g1]) == colkey(order[g0])) g1++;
+        std::stable_sort(order.begin() + g0, order.begin() + g1, [&](int x, int y) {
+          return pseg[x].second - pseg[x].first > pseg[y].second - pseg[y].first;
+        });
+        int act = g1 - g0;
+        for (int64_t off = 0;; off += piece) {
+          while (act > 0 && pseg[order[g0 + act - 1]].second - pseg[order[g0 + act - 1]].first <= off)
+            act--;
+          if (act == 0) break;
+          rounds.push_back(PartRound{npieces, g0, act, off});
+          npieces += act;
+        }
+        g0 = g1;
+      }
+      rounds.push_back(PartRound{npieces, NP, 0, 0});  // sentinel
+      PartPiece* d_pp;
+      PartRound* d_rounds;
+      int32_t* d_order;
+      int64_t* d_segv;
+      unsigned long long* d_ctr;
+      // sized once for the whole fit (a regrowth would hipFree = synchronize)
+      TRY(ws_typed(c, "ppieces", (size_t)std::max<int64_t>(npieces, (int64_t)R * cap / piece + 65536),
+                   &d_pp));
+      TRY(ws_typed(c, "prounds", rounds.size(), &d_rounds));
+      TRY(ws_typed(c, "porder", (size_t)NP, &d_order));
+      TRY(ws_typed(c, "psegv", segv.size(), &d_segv));
+      TRY(ws_typed(c, "pctr", 1, &d_ctr));
+      TRY(h2d(c, d_rounds, rounds.data(), rounds.size()));
+      TRY(h2d(c, d_order, order.data(), (size_t)NP));
+      TRY(h2d(c, d_segv, segv.data(), segv.size()));
+      launch_part_pieces(c->stream, d_rounds, (int)rounds.size() - 1, npieces, d_order, d_segv,
+                         piece, d_pp);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemsetAsync(d_ctr, 0, 8, c->stream));
+      TRY(ws_typed(c, "par", std::max<size_t>(par.size(), 1), &d_par));
+      TRY(h2d(c, d_par, par.data(), par.size()));
       PartArgs pa{};
       pa.cols = d_cols;
       pa.cols_rstride = cols_rstride;
       pa.npad = npad;
-      pa.chunks = d_pieces;
-      pa.wg_piece = d_wg;
+      pa.pieces = d_pp;
+      pa.npieces = npieces;
+      pa.counter = d_ctr;
       pa.parents = d_par;
       pa.ent_in = ent_cur;
       pa.ent_out = ent_nxt;
       pa.cursors = d_cur;
       pa.sq_left = d_sql;
+      const int nwg = (int)std::max<int64_t>(1, std::min<int64_t>(npieces, 256 * 8));
+      hmark(3);
       int h = tm.begin(T_PART);
-      launch_partition(c->stream, pa, work.nwg);
+      launch_partition(c->stream, pa, nwg);
       HIP_TRY(hipGetLastError());
       tm.end(h);
     }
     TRY(d2h(c, cur.data(), d_cur, cur.size()));
+    hmark(4);
     if (!gini) TRY(d2h(c, sql.data(), d_sql, sql.size()));
     // --- children: complete stats, purity, the parent's exact gain; next slots
     std::vector<std::pair<int, int>> next_slots;
@@ -1587,6 +1693,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
         hpar.push_back(ParentInfo{sp.r, -1, 0, 0, 0, hs, 0, 0});
       }
     }
+    hmark(5);
     if (next_slots.empty()) break;
     const int Mn = (int)next_slots.size();
     {
@@ -1616,7 +1723,12 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     std::swap(hist_cur_name, hist_nxt_name);
     hist_cur = hist_nxt;
     std::swap(ent_cur, ent_nxt);
+    hmark(6);
   }
+  if (hprof)
+    fprintf(stderr, "host ms: split-prep %.2f split-wait %.2f nodes %.2f part-prep %.2f part-wait %.2f "
+                    "children %.2f hist-prep %.2f loop %.2f\n", hp[0], hp[1], hp[2], hp[3], hp[4], hp[5],
+            hp[6], hp[7]);
   HIP_TRY(hipEventRecord(ev_stop, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
 

@@ -58,13 +58,26 @@ struct HistArgs {
 
 // k_partition: entries of each split node -> left block (from the segment start,
 // cursors[2p] grows) and right block (from the segment end, cursors[2p+1] shrinks)
+struct PartPiece {  // one dynamically scheduled piece of a parent segment
+  int32_t q;         // parent
+  int32_t pad;
+  int64_t a, b;      // entries [a, b)
+};
+
+struct PartRound {   // round k of a column group: order[o0, o0 + m) each give one piece
+  int64_t out0;      // first piece of the round in the piece list
+  int32_t o0, m;     // parents of the group (longest first) that reach this round
+  int64_t off;       // entry offset of the round's pieces inside their parents
+};
+
 struct PartArgs {
   const uint8_t* cols;   // column-major bins [R?][C][npad] (k_transpose)
   int64_t cols_rstride;  // bytes between replica copies (0: shared)
   int64_t npad;          // column stride (rows rounded up to 64)
-  const HistChunk* chunks;
-  const int32_t* wg_piece;
-  const ParentInfo* parents;  // r, pos (split column), s (split bin), write_l, write_r
+  const PartPiece* pieces;  // work order: split-column groups, parents interleaved
+  int64_t npieces;
+  unsigned long long* counter;  // dynamic piece counter (zeroed before the launch)
+  const ParentInfo* parents;    // r, pos (split column), s (split bin), write_l, write_r
   const uint64_t* ent_in;
   uint64_t* ent_out;
   unsigned long long* cursors;
@@ -117,6 +130,8 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mod
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini);
 size_t hist_stage_bytes();
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg);
+void launch_part_pieces(hipStream_t st, const PartRound* rounds, int nrounds, int64_t npieces,
+                        const int32_t* order, const int64_t* seg, int64_t piece, PartPiece* out);
 void launch_transpose(hipStream_t st, const uint8_t* src, int64_t N, int S, int C, uint8_t* dst,
                       int64_t npad, int R, int64_t src_rstride, int64_t dst_rstride);
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini);

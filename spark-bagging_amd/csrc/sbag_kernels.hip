@@ -711,30 +711,50 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mod
 
 size_t hist_lds_limit() { return 160 * 1024; }
 
-// ---- partition: 8 entries per lane per step, one cursor atomic per wave and side
+// ---- partition: 8 entries per lane per step, one cursor atomic per workgroup and
+// side for 2048 entries.  Pieces are handed out dynamically in split-column order
+// (parents of one column interleaved), so at any time the whole GPU gathers from
+// one or two columns of the column-major bins copy: a column (N bytes) stays in
+// the MALL / L2 while every node that splits on it is routed, instead of each
+// sparse 1-byte gather costing its own memory sector.
 constexpr int kPartThreads = 256;
+constexpr int kPartWaves = kPartThreads / 64;
 constexpr int kPartK = 8;
 
 __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int waves = kPartThreads / 64;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
-  for (int p = p0; p < p1; p++) {
-    const HistChunk pc = A.chunks[p];
-    const ParentInfo pi = A.parents[pc.parent];
+  __shared__ int64_t s_a, s_b;
+  __shared__ int s_q;
+  __shared__ int s_n[2][kPartWaves];
+  __shared__ unsigned long long s_base[2];
+  for (;;) {
+    if (tid == 0) {
+      const int64_t p = (int64_t)atomicAdd(A.counter, 1ull);
+      const PartPiece pc = p < A.npieces ? A.pieces[p] : PartPiece{-1, 0, 0, 0};
+      s_q = pc.q;
+      s_a = pc.a;
+      s_b = pc.b;
+    }
+    __syncthreads();
+    const int q = s_q;
+    const int64_t pa = s_a, pb = s_b;
+    __syncthreads();
+    if (q < 0) break;
+    const ParentInfo pi = A.parents[q];
     const uint8_t* col = A.cols + (int64_t)pi.r * A.cols_rstride + (int64_t)pi.pos * A.npad;
     const uint32_t split = (uint32_t)pi.s;
     const bool wlp = pi.write_l != 0, wrp = pi.write_r != 0;
-    unsigned long long* cur = A.cursors + 2 * (int64_t)pc.parent;
-    for (int64_t base = pc.a + (int64_t)wave * 64 * kPartK; base < pc.b;
-         base += (int64_t)waves * 64 * kPartK) {
+    unsigned long long* cur = A.cursors + 2 * (int64_t)q;
+    // every wave runs the same number of steps (barriers inside)
+    for (int64_t step0 = pa; step0 < pb; step0 += (int64_t)kPartWaves * 64 * kPartK) {
+      const int64_t base = step0 + (int64_t)wave * 64 * kPartK;
       uint64_t e[kPartK];
       uint32_t byte[kPartK];
 #pragma unroll
       for (int k = 0; k < kPartK; k++) {
         const int64_t i = base + k * 64 + lane;
-        e[k] = i < pc.b ? A.ent_in[i] : 0ull;
+        e[k] = i < pb ? A.ent_in[i] : 0ull;
       }
 #pragma unroll
       for (int k = 0; k < kPartK; k++) byte[k] = col[(uint32_t)e[k]];
@@ -742,7 +762,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
       int nl = 0, nr = 0;
 #pragma unroll
       for (int k = 0; k < kPartK; k++) {
-        const bool valid = base + k * 64 + lane < pc.b;
+        const bool valid = base + k * 64 + lane < pb;
         const bool right = byte[k] > split;
         ml[k] = __ballot(valid && !right && wlp);
         mr[k] = __ballot(valid && right && wrp);
@@ -750,26 +770,40 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         nr += __popcll(mr[k]);
       }
       if (A.sq_left) {  // exact sum of count*k^2 of the left child (variance stats)
-        unsigned long long q = 0;
+        unsigned long long sq = 0;
 #pragma unroll
         for (int k = 0; k < kPartK; k++) {
-          const bool valid = base + k * 64 + lane < pc.b;
+          const bool valid = base + k * 64 + lane < pb;
           if (valid && byte[k] <= split) {
             const int32_t hi = (int32_t)(e[k] >> 32);
             const int64_t kk = hi >> 8;
-            q += (unsigned long long)(hi & 0xff) * (unsigned long long)(kk * kk);
+            sq += (unsigned long long)(hi & 0xff) * (unsigned long long)(kk * kk);
           }
         }
-        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
-        if (lane == 0 && q) atomicAdd(&A.sq_left[pc.parent], q);
+        for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+        if (lane == 0 && sq) atomicAdd(&A.sq_left[q], sq);
       }
-      unsigned long long bl = 0, br = 0;
       if (lane == 0) {
-        if (nl) bl = atomicAdd(&cur[0], (unsigned long long)nl);
-        if (nr) br = atomicAdd(&cur[1], (unsigned long long)(-(long long)nr)) - (unsigned long long)nr;
+        s_n[0][wave] = nl;
+        s_n[1][wave] = nr;
       }
-      bl = (unsigned long long)__shfl((long long)bl, 0);
-      br = (unsigned long long)__shfl((long long)br, 0);
+      __syncthreads();
+      if (tid == 0) {
+        int tl = 0, tr = 0;
+#pragma unroll
+        for (int w = 0; w < kPartWaves; w++) {
+          tl += s_n[0][w];
+          tr += s_n[1][w];
+        }
+        s_base[0] = tl ? atomicAdd(&cur[0], (unsigned long long)tl) : 0ull;
+        s_base[1] = tr ? atomicAdd(&cur[1], (unsigned long long)(-(long long)tr)) - (unsigned long long)tr : 0ull;
+      }
+      __syncthreads();
+      unsigned long long bl = s_base[0], br = s_base[1];
+      for (int w = 0; w < wave; w++) {
+        bl += (unsigned long long)s_n[0][w];
+        br += (unsigned long long)s_n[1][w];
+      }
 #pragma unroll
       for (int k = 0; k < kPartK; k++) {
         const uint64_t bit = 1ull << lane;
@@ -778,6 +812,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         bl += __popcll(ml[k]);
         br += __popcll(mr[k]);
       }
+      __syncthreads();  // s_n / s_base are rewritten by the next step
     }
   }
 }
@@ -818,6 +853,36 @@ void launch_transpose(hipStream_t st, const uint8_t* src, int64_t N, int S, int 
   const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)R);
   hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, st, src, N, S, C, dst, npad, src_rstride,
                      dst_rstride);
+}
+
+// piece list of k_partition: thread per piece.  A column group's pieces come in
+// rounds (piece k of every parent that is long enough, longest parents first).
+__global__ __launch_bounds__(256) void k_part_pieces(const PartRound* __restrict__ rounds,
+                                                     int nrounds, int64_t npieces,
+                                                     const int32_t* __restrict__ order,
+                                                     const int64_t* __restrict__ seg, int64_t piece,
+                                                     PartPiece* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= npieces) return;
+  int lo = 0, hi = nrounds;  // rounds[lo].out0 <= p < rounds[hi].out0
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (rounds[mid].out0 <= p)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const PartRound rd = rounds[lo];
+  const int q = order[rd.o0 + (int)(p - rd.out0)];
+  const int64_t x = seg[2 * q] + rd.off;
+  out[p] = PartPiece{q, 0, x, min(x + piece, seg[2 * q + 1])};
+}
+
+void launch_part_pieces(hipStream_t st, const PartRound* rounds, int nrounds, int64_t npieces,
+                        const int32_t* order, const int64_t* seg, int64_t piece, PartPiece* out) {
+  if (npieces <= 0) return;
+  hipLaunchKernelGGL(k_part_pieces, dim3((unsigned)((npieces + 255) / 256)), dim3(256), 0, st,
+                     rounds, nrounds, npieces, order, seg, piece, out);
 }
 
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg) {
