@@ -27,6 +27,7 @@
 #include <climits>
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "sbag_internal.h"
 
@@ -196,12 +197,222 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
   if (bad) atomicOr(err, 1);
 }
 
+// ---- two-wave pipeline: wave 0 runs the Well19937c recurrence, wave 1 the
+// Poisson parse.  With 64 streams per CU (the state fills the LDS) one wave used
+// one SIMD and ran both chains back to back; split, the two chains overlap on two
+// SIMDs.  Wave 0 writes the untempered z4 of each batch of kPB steps into a
+// double-buffered LDS ring (the last 4 KB of the 160 KB); wave 1 tempers, builds
+// the doubles and draws.  One s_barrier per batch; the parser reports "all rows
+// done" in the ring slot it has just consumed, which the generator reads before
+// refilling it.
+constexpr int kPB = 8;  // 624 = 78 * 8: batches cover aligned blocks after the prologue step
+
+template <bool FAST>
+__device__ __forceinline__ int well_batch_raw(uint32_t* __restrict__ st, int lane, int i,
+                                              uint32_t& v0, uint32_t (&z4o)[kPB]) {
+  uint32_t m1[kPB], m2[kPB], m3[kPB], hb[kPB], lo[kPB], z3v[kPB];
+  if (FAST) {
+    const uint32_t* p1 = st + (wrap624(i + 70) - (kPB - 1)) * 64 + lane;
+    const uint32_t* p2 = st + (wrap624(i + 179) - (kPB - 1)) * 64 + lane;
+    const uint32_t* p3 = st + (wrap624(i - 175) - (kPB - 1)) * 64 + lane;
+    const uint32_t* ph = st + (i - 1 - kPB) * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < kPB; t++) {
+      m1[t] = p1[(kPB - 1 - t) * 64];
+      m2[t] = p2[(kPB - 1 - t) * 64];
+      m3[t] = p3[(kPB - 1 - t) * 64];
+      hb[t] = ph[(kPB - t) * 64];
+      lo[t] = ph[(kPB - 1 - t) * 64];
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < kPB; t++) {
+      const int j = wrap624(i - t);
+      m1[t] = st[wrap624(j + 70) * 64 + lane];
+      m2[t] = st[wrap624(j + 179) * 64 + lane];
+      m3[t] = st[wrap624(j - 175) * 64 + lane];
+      hb[t] = st[wrap624(j - 1) * 64 + lane];
+      lo[t] = st[wrap624(j - 2) * 64 + lane];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < kPB; t++) {
+    const uint32_t z0 = (0x80000000u & hb[t]) | (0x7FFFFFFFu & lo[t]);
+    const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1[t] ^ (m1[t] >> 27));
+    const uint32_t z2 = (m2[t] >> 9) ^ (m3[t] ^ (m3[t] >> 1));
+    const uint32_t z3 = z1 ^ z2;
+    const uint32_t z4 = z0 ^ (z1 << 9) ^ (z2 << 21) ^ (z3 >> 21);  // z1 ^ z2 ^ z3 == 0
+    z3v[t] = z3;
+    z4o[t] = z4;
+    v0 = z4;
+  }
+  uint32_t* pw = st + (i - kPB + 1) * 64 + lane;  // [i-7, i] never wraps (aligned batches)
+#pragma unroll
+  for (int t = 0; t < kPB; t++) pw[(kPB - 1 - t) * 64] = z3v[t];
+  st[wrap624(i - kPB) * 64 + lane] = v0;
+  st[wrap624(i - kPB - 1) * 64 + lane] = lo[kPB - 1] & 0x80000000u;
+  return wrap624(i - kPB);
+}
+
+__device__ __forceinline__ bool well_window_ok(int x) {  // [x-kPB+1, x] inside the ring
+  const int lo = wrap624(x) - (kPB - 1);
+  return lo >= 0;
+}
+
+__device__ __forceinline__ uint32_t well_temper26(uint32_t z4) {
+  z4 ^= (z4 << 7) & 0xe46e1700u;
+  z4 ^= (z4 << 15) & 0x9b868000u;
+  return z4 >> 6;  // next(26)
+}
+
+__global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, int64_t N,
+                                                  const int64_t* __restrict__ part_off, int P,
+                                                  int R, int learner0, int64_t seed, double mean,
+                                                  double p_exp, int* err, int dbg) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  uint32_t* st = sm;                    // [624][64] state
+  uint32_t* ring = sm + 624 * 64;       // [2][kPB][64] untempered z4
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t sid = (int64_t)blockIdx.x * 64 + lane;
+  const bool active = sid < (int64_t)R * P;
+  const int r = active ? (int)(sid / P) : 0;
+  const int p = active ? (int)(sid % P) : 0;
+  if (wave == 0) {
+    // PoissonDistribution.reseedRandomGenerator(seed + i + partitionIndex) -> AbstractWell.setSeed
+    const uint64_t s64 = (uint64_t)seed + (uint64_t)(int64_t)(learner0 + r) + (uint64_t)(int64_t)p;
+    uint32_t vm2 = (uint32_t)(s64 >> 32), vm1 = (uint32_t)s64;
+    st[0 * 64 + lane] = vm2;
+    st[1 * 64 + lane] = vm1;
+    for (int i = 2; i < 624; i++) {
+      const int64_t l = (int64_t)(int32_t)vm2;
+      const uint32_t v = (uint32_t)(1812433253ull * (uint64_t)(l ^ (l >> 30)) + (uint64_t)i);
+      st[i * 64 + lane] = v;
+      vm2 = vm1;
+      vm1 = v;
+    }
+    uint32_t v0 = st[lane];
+    // prologue: the single step at index 0 (leaves index 623 = 8*77 + 7); its output
+    // goes to ring slot 1, step kPB-1, where the parser picks up its pending half
+    {
+      const uint32_t m1 = st[70 * 64 + lane], m2 = st[179 * 64 + lane], m3 = st[449 * 64 + lane];
+      const uint32_t hb = st[623 * 64 + lane], lo = st[622 * 64 + lane];
+      const uint32_t z0 = (0x80000000u & hb) | (0x7FFFFFFFu & lo);
+      const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1 ^ (m1 >> 27));
+      const uint32_t z2 = (m2 >> 9) ^ (m3 ^ (m3 >> 1));
+      const uint32_t z3 = z1 ^ z2;
+      const uint32_t z4 = z0 ^ (z1 << 9) ^ (z2 << 21) ^ (z3 >> 21);
+      st[lane] = z3;
+      st[623 * 64 + lane] = z4;
+      st[622 * 64 + lane] = lo & 0x80000000u;
+      v0 = z4;
+      ring[(1 * kPB + kPB - 1) * 64 + lane] = z4;
+    }
+    __syncthreads();  // the parser takes the prologue output
+    int index = 623;
+    for (int k = 0;; k++) {
+      // the parser's verdict after batch k-2 (its last barrier matched batch k-1's)
+      if (k >= 2 && ring[((k & 1) * kPB) * 64] != 0u) break;
+      uint32_t z4o[kPB];
+      if (dbg & 2) {  // ablation: no generator work
+        uint32_t* slot = ring + (k & 1) * kPB * 64 + lane;
+#pragma unroll
+        for (int t = 0; t < kPB; t++) slot[t * 64] = v0 + t * 77777u;
+        __syncthreads();
+        continue;
+      }
+      const bool fast = well_window_ok(index + 70) && well_window_ok(index + 179) &&
+                        well_window_ok(index - 175) && index - 1 - kPB >= 0;
+      if (fast)
+        index = well_batch_raw<true>(st, lane, index, v0, z4o);
+      else
+        index = well_batch_raw<false>(st, lane, index, v0, z4o);
+      uint32_t* slot = ring + (k & 1) * kPB * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < kPB; t++) slot[t * 64] = z4o[t];
+      __syncthreads();
+    }
+  } else {
+    int64_t row = active ? part_off[p] : 0;
+    const int64_t row_end = active ? part_off[p + 1] : 0;
+    uint8_t* out = counts + (int64_t)r * N;
+    // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean)
+    const int icap = (int)ceil(1000.0 * mean);
+    uint8_t* const sink = (uint8_t*)(err + 1) + lane;  // stores of lanes that finish no row
+    int n = 0, bad = 0;
+    double racc = 1.0;
+    __syncthreads();  // the prologue output: first half of the first double
+    uint32_t pending = well_temper26(ring[(1 * kPB + kPB - 1) * 64 + lane]);
+    for (int k = 0;; k++) {
+      __syncthreads();  // batch k is in ring slot k & 1
+      uint32_t* slot = ring + (k & 1) * kPB * 64;
+      uint32_t o[kPB];
+#pragma unroll
+      for (int t = 0; t < kPB; t++) o[t] = well_temper26(slot[t * 64 + lane]);
+      // doubles: (pending, o0), (o1, o2), (o3, o4), (o5, o6); o7 carries over.
+      // BitsStreamGenerator.nextDouble = (next(26) << 26 | next(26)) * 2^-52, built as
+      // the bits of 1 + m * 2^-52 minus 1 (exact: m < 2^52).
+      if (dbg & 1) {  // ablation: no parse, one row per double
+        row = min(row + kPB / 2, row_end);
+        if (lane == 0) slot[0] = !__any(row < row_end) ? 1u : 0u;
+        if (!__any(row < row_end)) {
+          __syncthreads();
+          break;
+        }
+        continue;
+      }
+#pragma unroll
+      for (int u = 0; u < kPB / 2; u++) {
+        const uint32_t hi = u == 0 ? pending : o[2 * u - 1];
+        const uint32_t lo32 = (hi << 26) | o[2 * u];
+        const uint32_t hi32 = 0x3FF00000u | (hi >> 6);
+        const double x = __hiloint2double((int)hi32, (int)lo32) - 1.0;
+        const bool live = row < row_end;
+        racc *= x;
+        const bool ge = racc >= p_exp;
+        n += ge ? 1 : 0;
+        const bool done = live && (!ge || n >= icap);
+        bad |= (done && n > 255) ? 1 : 0;
+        uint8_t* dst = done ? out + row : sink;
+        *dst = (uint8_t)min(n, 255);
+        row += done ? 1 : 0;
+        n = done ? 0 : n;
+        racc = done ? 1.0 : racc;
+      }
+      pending = o[kPB - 1];
+      const bool all_done = !__any(row < row_end);
+      // report in the consumed slot: the generator reads it before refilling the slot
+      if (lane == 0) slot[0] = all_done ? 1u : 0u;
+      if (all_done) {
+        __syncthreads();  // matches the generator's next barrier
+        break;
+      }
+    }
+    if (bad) atomicOr(err, 1);
+  }
+}
+
 void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
                     int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err) {
   const int64_t streams = (int64_t)R * P;
   const int blocks = (int)((streams + 63) / 64);
-  hipLaunchKernelGGL(k_poisson, dim3(blocks), dim3(64), 0, st, counts, N, d_part_off, P, R,
-                     learner0, seed, mean, p_exp, d_err);
+  static int v1 = -1;
+  if (v1 < 0) v1 = getenv("SBAG_POISSON_V1") ? 1 : 0;
+  if (v1) {
+    hipLaunchKernelGGL(k_poisson, dim3(blocks), dim3(64), 0, st, counts, N, d_part_off, P, R,
+                       learner0, seed, mean, p_exp, d_err);
+    return;
+  }
+  const size_t lds = (size_t)(624 + 2 * kPB) * 64 * 4;  // 163840 = the whole LDS
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_poisson2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    attr_set = true;
+  }
+  static int dbg = -1;
+  if (dbg < 0) dbg = getenv("SBAG_POISSON_DBG") ? atoi(getenv("SBAG_POISSON_DBG")) : 0;
+  hipLaunchKernelGGL(k_poisson2, dim3(blocks), dim3(128), lds, st, counts, N, d_part_off, P, R,
+                     learner0, seed, mean, p_exp, d_err, dbg);
 }
 
 // ======================================================================
