@@ -370,12 +370,29 @@ struct Calc {  // ImpurityCalculator over exact integer stats
   }
 };
 
+struct NodeStats {  // exact integer stats of a node: inline up to 8 words (no allocation)
+  int64_t inl[8];
+  std::vector<int64_t> heap;
+  int n = 0;
+  int64_t* data() { return n <= 8 ? inl : heap.data(); }
+  const int64_t* data() const { return n <= 8 ? inl : heap.data(); }
+  int64_t& operator[](size_t i) { return data()[i]; }
+  int64_t operator[](size_t i) const { return data()[i]; }
+  void assign(const int64_t* a, const int64_t* b) {
+    n = (int)(b - a);
+    if (n > 8)
+      heap.assign(a, b);
+    else
+      std::copy(a, b, inl);
+  }
+};
+
 struct HNode {  // LearningNode
   int left = -1, right = -1;
   bool is_leaf = false, has_split = false;
   int fl = -1, s = -1;
   double thr = 0.0;
-  std::vector<int64_t> stats;
+  NodeStats stats;
   double impurity = 0.0, gain = NAN;
   bool valid = true;
 };
@@ -1334,6 +1351,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   std::vector<std::vector<HNode>> trees(R);
   std::vector<std::pair<int, int>> slots(R);  // (replica, node index)
   for (int r = 0; r < R; r++) {
+    trees[r].reserve((size_t)std::min<int64_t>((int64_t)1 << std::min(D + 1, 20), 2 * (int64_t)inbag[r] + 1));
     trees[r].push_back(HNode{});
     slots[r] = {r, 0};
   }
