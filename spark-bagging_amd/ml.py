@@ -24,6 +24,7 @@ import warnings
 import numpy as np
 
 from . import _native as nat
+from . import persistence as sp
 
 
 def java_string_hash(s):
@@ -124,24 +125,66 @@ class _DecisionTreeParams(Params):
         return self.get("impurity")
 
 
-class DecisionTreeRegressor(_DecisionTreeParams):
+class _DecisionTreeEstimator(_DecisionTreeParams):
+    _spark_class = None
+    _spark_model_class = None
+    _spark_defaults = None
+    _uid_prefix = None
+
+    def __init__(self, uid=None):
+        super().__init__(uid or f"{self._uid_prefix}_{uuid.uuid4().hex[-12:]}")
+        self._other_params = {}  # Spark params the engine does not use (round-tripped)
+
+    def setImpurity(self, v):
+        return self.set("impurity", v)
+
+    def save(self, path):
+        """DefaultParamsWritable: metadata only (explicitly set params)."""
+        sp.save_metadata(path, self._spark_class, self.uid, dict(self._other_params, **self._values),
+                         self._spark_defaults)
+
+    @staticmethod
+    def load(path):
+        meta = sp.load_metadata(path)
+        cls = {sp.DTR_CLASS: DecisionTreeRegressor, sp.DTC_CLASS: DecisionTreeClassifier}.get(meta["class"])
+        if cls is None:
+            raise nat.IllegalArgumentException(
+                nat.SBAG_EINVAL, f"the MI355X engine accelerates DecisionTree base learners only, "
+                                 f"found {meta['class']}")
+        bl = cls(uid=meta["uid"])
+        for k, v in meta["paramMap"].items():
+            if k in bl._defaults:
+                bl.set(k, v)
+            else:
+                bl._other_params[k] = v
+        return bl
+
+    def copy(self, extra=None):
+        other = super().copy(extra)
+        other._other_params = dict(self._other_params)
+        return other
+
+
+class DecisionTreeRegressor(_DecisionTreeEstimator):
     _defaults = dict(_DecisionTreeParams._defaults, impurity="variance",
                      seed=java_string_hash("org.apache.spark.ml.regression.DecisionTreeRegressor"))
     _validators = dict(_DecisionTreeParams._validators, impurity=lambda x: x == "variance")
     impurity_code = nat.IMPURITY_VARIANCE
+    _spark_class = sp.DTR_CLASS
+    _spark_model_class = sp.DTR_MODEL_CLASS
+    _spark_defaults = sp.DTR_DEFAULTS
+    _uid_prefix = "dtr"
 
-    def setImpurity(self, v):
-        return self.set("impurity", v)
 
-
-class DecisionTreeClassifier(_DecisionTreeParams):
+class DecisionTreeClassifier(_DecisionTreeEstimator):
     _defaults = dict(_DecisionTreeParams._defaults, impurity="gini",
                      seed=java_string_hash("org.apache.spark.ml.classification.DecisionTreeClassifier"))
     _validators = dict(_DecisionTreeParams._validators, impurity=lambda x: x == "gini")
     impurity_code = nat.IMPURITY_GINI
-
-    def setImpurity(self, v):
-        return self.set("impurity", v)
+    _spark_class = sp.DTC_CLASS
+    _spark_model_class = sp.DTC_MODEL_CLASS
+    _spark_defaults = sp.DTC_DEFAULTS
+    _uid_prefix = "dtc"
 
 
 class Frame:
@@ -282,6 +325,29 @@ class _BaggingEstimator(_BaggingParams):
             other._values["baseLearner"] = other.get("baseLearner").copy()
         return other
 
+    # ---- persistence: BaggingRegressor.write (BaggingRegressorParams.saveImpl,
+    # BaggingRegressor.scala:50-66): metadata without baseLearner + learner/
+    def save(self, path):
+        if os.path.exists(path):
+            raise nat.IllegalArgumentException(
+                nat.SBAG_EINVAL, f"Path {path} already exists. To overwrite it, please use "
+                                 "write.overwrite().save(path) for Scala and use "
+                                 "write().overwrite().save(path) for Java and Python.")
+        params = {k: v for k, v in self.extractParamMap().items() if k != "baseLearner"}
+        defaults = {k: v for k, v in self._defaults.items() if v is not None and k != "baseLearner"}
+        sp.save_metadata(path, self._spark_class, self.uid, params, defaults)
+        self._base().save(os.path.join(path, "learner"))
+
+    @classmethod
+    def load(cls, path):
+        meta = sp.load_metadata(path, cls._spark_class)
+        est = cls(uid=meta["uid"])
+        for k, v in meta["paramMap"].items():
+            if k in est._defaults:
+                est._values[k] = v
+        est._values["baseLearner"] = _DecisionTreeEstimator.load(os.path.join(path, "learner"))
+        return est
+
     def _base(self):
         bl = self.get("baseLearner")
         if bl is None:
@@ -416,62 +482,72 @@ class _BaggingModel(_BaggingParams):
         """Single-vector predict (BaggingRegressor.scala:248-256 / BaggingClassifier.scala:248-257)."""
         return float(self.transform(np.asarray(features, np.float64)[None, :])[0])
 
-    # ---- persistence (MLWritable / MLReadable), Spark directory layout -------------
+    # ---- persistence (MLWritable / MLReadable), Spark 2.4.3 directory layout -------
+    def _bagging_defaults(self):
+        d = {k: v for k, v in _BaggingParams._defaults.items() if v is not None}
+        d["seed"] = self._estimator_seed_default
+        return d
+
     def save(self, path):
-        """metadata (params + numBaseModels), learner/ (base learner params),
-        model-$idx (nodes), data-$idx (subspace) -- BaggingRegressor.scala:273-295."""
-        os.makedirs(path, exist_ok=False)
+        """BaggingRegressionModelWriter.saveImpl (BaggingRegressor.scala:273-295):
+        metadata (+ numBaseModels), learner/, model-$idx (tree), data-$idx (subspace)."""
+        if os.path.exists(path):
+            raise nat.IllegalArgumentException(
+                nat.SBAG_EINVAL, f"Path {path} already exists. To overwrite it, please use "
+                                 "write.overwrite().save(path) for Scala and use "
+                                 "write().overwrite().save(path) for Java and Python.")
         params = {k: v for k, v in self.extractParamMap().items() if k != "baseLearner"}
-        meta = {"class": self._spark_class, "uid": self.uid, "paramMap": params,
-                "numBaseModels": self.numBaseModels, "sparkVersion": "2.4.3"}
-        with open(os.path.join(path, "metadata.json"), "w") as fh:
-            json.dump(meta, fh)
+        sp.save_metadata(path, self._spark_class, self.uid, params, self._bagging_defaults(),
+                         {"numBaseModels": self.numBaseModels})
         bl = self.get("baseLearner")
-        os.makedirs(os.path.join(path, "learner"))
-        with open(os.path.join(path, "learner", "metadata.json"), "w") as fh:
-            json.dump({"class": type(bl).__name__ if bl else None,
-                       "paramMap": bl.extractParamMap() if bl else {}}, fh)
+        if bl is None:
+            bl = (DecisionTreeClassifier() if self._agg == nat.AGG_MODE else DecisionTreeRegressor())
+        bl.save(os.path.join(path, "learner"))
+        # fitBaseLearner sets labelCol / featuresCol / predictionCol explicitly
+        # (ensembleParams.scala:105-108); the tree model keeps the estimator's uid
+        tree_params = dict(bl._other_params, **bl._values)
+        tree_params.update(labelCol=self.get("labelCol"), featuresCol=self.get("featuresCol"),
+                           predictionCol=self.get("predictionCol"))
         for i, (m, s) in enumerate(zip(self.models, self.subspaces)):
-            os.makedirs(os.path.join(path, f"model-{i}"))
-            np.savez(os.path.join(path, f"model-{i}", "nodes.npz"), nodes=m.nodes, stats=m.stats,
-                     impurity=np.int32(m.impurity))
-            os.makedirs(os.path.join(path, f"data-{i}"))
-            with open(os.path.join(path, f"data-{i}", "part-00000.json"), "w") as fh:
-                json.dump({"subspace": [int(x) for x in s]}, fh)
+            mp = os.path.join(path, f"model-{i}")
+            extra = {"numFeatures": int(len(s))}
+            if m.impurity == nat.IMPURITY_GINI:
+                extra["numClasses"] = int(m.stats.shape[1])
+            sp.save_metadata(mp, bl._spark_model_class, bl.uid, tree_params, bl._spark_defaults,
+                             extra)
+            sp.write_tree_data(mp, m.nodes, m.stats)
+            sp.write_subspace(os.path.join(path, f"data-{i}"), s)
 
     @classmethod
     def load(cls, path):
-        with open(os.path.join(path, "metadata.json")) as fh:
-            meta = json.load(fh)
-        if meta["class"] != cls._spark_class:
-            raise nat.IllegalArgumentException(
-                nat.SBAG_EINVAL, f"Error loading metadata: Expected class name {cls._spark_class} "
-                                 f"but found class name {meta['class']}")
+        """Bagging*ModelReader.load (BaggingRegressor.scala:297-318; classifier: the
+        model count comes from metadata numBaseModels, BaggingClassifier.scala:307)."""
+        meta = sp.load_metadata(path, cls._spark_class)
+        bl = _DecisionTreeEstimator.load(os.path.join(path, "learner"))
+        if cls._agg == nat.AGG_MEAN:
+            n = int(meta["paramMap"]["numBaseLearners"])
+        else:
+            n = int(meta["numBaseModels"])
         models, subs = [], []
-        for i in range(meta["numBaseModels"]):
-            z = np.load(os.path.join(path, f"model-{i}", "nodes.npz"), allow_pickle=False)
-            models.append(DecisionTreeModel(z["nodes"], z["stats"], int(z["impurity"])))
-            with open(os.path.join(path, f"data-{i}", "part-00000.json")) as fh:
-                subs.append(json.load(fh)["subspace"])
+        for i in range(n):
+            mp = os.path.join(path, f"model-{i}")
+            mm = sp.load_metadata(mp)
+            imp = nat.IMPURITY_GINI if mm["class"] == sp.DTC_MODEL_CLASS else nat.IMPURITY_VARIANCE
+            nodes, stats = sp.read_tree_data(mp)
+            models.append(DecisionTreeModel(nodes, stats, imp))
+            subs.append(sp.read_subspace(os.path.join(path, f"data-{i}")))
         m = cls(subs, models, uid=meta["uid"])
-        for k, v in meta["paramMap"].items():
-            if v is not None:
+        for k, v in meta["paramMap"].items():  # DefaultParamsReader.getAndSetParams
+            if k in m._defaults:
                 m._values[k] = v
-        with open(os.path.join(path, "learner", "metadata.json")) as fh:
-            lm = json.load(fh)
-        if lm["class"]:
-            bl = {"DecisionTreeRegressor": DecisionTreeRegressor,
-                  "DecisionTreeClassifier": DecisionTreeClassifier}[lm["class"]]()
-            for k, v in lm["paramMap"].items():
-                if v is not None:
-                    bl._values[k] = v
-            m._values["baseLearner"] = bl
+        m._values["baseLearner"] = bl
         return m
 
 
 class BaggingRegressionModel(_BaggingModel):
     _agg = nat.AGG_MEAN
     _spark_class = "org.apache.spark.ml.regression.BaggingRegressionModel"
+    _estimator_seed_default = java_string_hash("org.apache.spark.ml.regression.BaggingRegressor")
     _defaults = dict(_BaggingParams._defaults,
                      seed=java_string_hash("org.apache.spark.ml.regression.BaggingRegressionModel"))
 
@@ -479,17 +555,20 @@ class BaggingRegressionModel(_BaggingModel):
 class BaggingClassificationModel(_BaggingModel):
     _agg = nat.AGG_MODE
     _spark_class = "org.apache.spark.ml.classification.BaggingClassificationModel"
+    _estimator_seed_default = java_string_hash("org.apache.spark.ml.classification.BaggingClassifier")
     _defaults = dict(_BaggingParams._defaults,
                      seed=java_string_hash("org.apache.spark.ml.classification.BaggingClassificationModel"))
 
 
 class BaggingRegressor(_BaggingEstimator):
     _model_cls = BaggingRegressionModel
+    _spark_class = "org.apache.spark.ml.regression.BaggingRegressor"
     _defaults = dict(_BaggingParams._defaults,
                      seed=java_string_hash("org.apache.spark.ml.regression.BaggingRegressor"))
 
 
 class BaggingClassifier(_BaggingEstimator):
     _model_cls = BaggingClassificationModel
+    _spark_class = "org.apache.spark.ml.classification.BaggingClassifier"
     _defaults = dict(_BaggingParams._defaults,
                      seed=java_string_hash("org.apache.spark.ml.classification.BaggingClassifier"))
