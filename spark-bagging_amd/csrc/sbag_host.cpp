@@ -1898,6 +1898,101 @@ static int check_agg(const sbag_forest* f, int agg) {
   return SBAG_OK;
 }
 
+}  // extern "C" (host helpers of the predict entry points)
+
+// ---- LDS-tiled predict plan: trees relaid breadth first (children adjacent),
+// thresholds compiled to code space by `tc_of(g, thr)` = the largest code whose
+// value is <= thr, trees chunked to the LDS budget.  false: a tree does not fit
+// (very deep trees / very wide rows) -> the global-memory walk.
+struct TiledPlan {
+  std::vector<PNode> pn;
+  std::vector<double> lv;
+  std::vector<int64_t> tn, tl;
+  std::vector<PredictChunk> chunks;
+};
+
+template <typename TC>
+static bool plan_tiled(const sbag_forest* f, PredictArgs& pa, int F, TC tc_of, TiledPlan& P) {
+  const int L = (int)f->trees.size();
+  pa.L = L;
+  pa.nclasses = std::max(f->nclasses, 1);
+  pa.chunk_bytes = 0;
+  const size_t fixed = predict_tiled_lds(pa);
+  const size_t lds_cap = 160 * 1024 - 512;
+  if (F >= 32768 || fixed + 4096 > lds_cap) return false;
+  const int budget = (int)std::min<size_t>(64 * 1024, lds_cap - fixed) & ~15;
+  pa.chunk_bytes = budget;
+  P.tn.assign(L, 0);
+  P.tl.assign(L, 0);
+  for (int t = 0; t < L; t++) {
+    const HTree& h = f->trees[t];
+    P.tn[t] = (int64_t)P.pn.size();
+    P.tl[t] = (int64_t)P.lv.size();
+    std::vector<int> order{0}, pos(h.nodes.size(), -1);
+    pos[0] = 0;
+    for (size_t k = 0; k < order.size(); k++) {
+      const sbag_node& n = h.nodes[order[k]];
+      if (n.left >= 0) {
+        pos[n.left] = (int)order.size();
+        order.push_back(n.left);
+        pos[n.right] = (int)order.size();
+        order.push_back(n.right);
+      }
+    }
+    for (int k : order) {
+      const sbag_node& n = h.nodes[k];
+      PNode q{};
+      if (n.left >= 0) {
+        const int g = h.sub[n.feature];
+        const int64_t tc = tc_of(g, n.threshold);
+        if (tc + 1 >= (1 << 17)) return false;
+        q.a = (uint32_t)pos[n.left];
+        q.b = ((uint32_t)g << 17) | (uint32_t)(tc + 1);
+      } else {
+        q.a = 0x80000000u | (uint32_t)(P.lv.size() - P.tl[t]);
+        P.lv.push_back(n.prediction);
+      }
+      P.pn.push_back(q);
+    }
+    const int64_t tb = (int64_t)(P.pn.size() - P.tn[t]) * 8 + (int64_t)(P.lv.size() - P.tl[t]) * 8;
+    if (tb > budget) return false;
+    if (P.chunks.empty() ||
+        (P.chunks.back().n1 - P.chunks.back().n0 + P.chunks.back().l1 - P.chunks.back().l0) * 8 + tb > budget)
+      P.chunks.push_back(PredictChunk{t, t, P.tn[t], P.tn[t], P.tl[t], P.tl[t]});
+    PredictChunk& ch = P.chunks.back();
+    ch.t1 = t + 1;
+    ch.n1 = (int64_t)P.pn.size();
+    ch.l1 = (int64_t)P.lv.size();
+  }
+  return true;
+}
+
+static int upload_plan(sbag_ctx* c, const TiledPlan& P, PredictArgs& pa) {
+  PNode* d_pn;
+  double* d_lv;
+  int64_t *d_tn, *d_tl;
+  PredictChunk* d_ch;
+  TRY(ws_typed(c, "pd_nodes", P.pn.size(), &d_pn));
+  TRY(ws_typed(c, "pd_leaves", std::max<size_t>(P.lv.size(), 1), &d_lv));
+  TRY(ws_typed(c, "pd_tn", P.tn.size(), &d_tn));
+  TRY(ws_typed(c, "pd_tl", P.tl.size(), &d_tl));
+  TRY(ws_typed(c, "pd_chunks", P.chunks.size(), &d_ch));
+  TRY(h2d(c, d_pn, P.pn.data(), P.pn.size()));
+  TRY(h2d(c, d_lv, P.lv.data(), P.lv.size()));
+  TRY(h2d(c, d_tn, P.tn.data(), P.tn.size()));
+  TRY(h2d(c, d_tl, P.tl.data(), P.tl.size()));
+  TRY(h2d(c, d_ch, P.chunks.data(), P.chunks.size()));
+  pa.nodes = d_pn;
+  pa.leaves = d_lv;
+  pa.tree_node = d_tn;
+  pa.tree_leaf = d_tl;
+  pa.chunks = d_ch;
+  pa.nchunks = (int)P.chunks.size();
+  return SBAG_OK;
+}
+
+extern "C" {
+
 int sbag_predict(sbag_ctx* c, const sbag_forest* f, const double* X, int64_t N, int32_t F, int32_t agg,
                  double* out, double* per_tree) {
   if (!c || !f || !X || !out || N < 0 || F <= 0) return fail(SBAG_EINVAL, "bad arguments");
@@ -1907,11 +2002,65 @@ int sbag_predict(sbag_ctx* c, const sbag_forest* f, const double* X, int64_t N, 
       if (g >= F) return fail(SBAG_EINVAL, "feature vector shorter than a subspace index");
   if (N == 0) return SBAG_OK;
   HIP_TRY(hipSetDevice(c->device));
-  TRY(upload_forest(c, f));
   const int L = (int)f->trees.size();
-  double *d_X, *d_out, *d_pt = nullptr;
-  TRY(ws_typed(c, "pX", (size_t)N * F, &d_X));
+  double *d_out, *d_pt = nullptr;
   TRY(ws_typed(c, "pout", (size_t)N, &d_out));
+  // batched transform: rows go up in batches, are binned on the device against the
+  // forest's own thresholds (code = #{thresholds of the feature < x}, so
+  // x <= threshold_k <=> code <= k, exact; NaN -> past every threshold) and walk
+  // the LDS-tiled forest
+  std::vector<std::vector<double>> T(F);
+  for (const HTree& t : f->trees)
+    for (const sbag_node& n : t.nodes)
+      if (n.left >= 0) T[t.sub[n.feature]].push_back(n.threshold);
+  std::vector<int64_t> toff(F + 1, 0);
+  for (int g = 0; g < F; g++) {
+    std::sort(T[g].begin(), T[g].end());
+    T[g].erase(std::unique(T[g].begin(), T[g].end()), T[g].end());
+    toff[g + 1] = toff[g] + (int64_t)T[g].size();
+  }
+  const int32_t Sq = (F + 15) / 16 * 16;
+  PredictArgs pa{};
+  pa.code_bytes = 2;
+  pa.S = Sq;
+  pa.agg = agg;
+  TiledPlan P;
+  const bool tiled = per_tree == nullptr &&
+                     plan_tiled(f, pa, F, [&](int g, double thr) {
+                       return (int64_t)(std::lower_bound(T[g].begin(), T[g].end(), thr) - T[g].begin());
+                     }, P);
+  if (tiled) {
+    std::vector<double> tv((size_t)std::max<int64_t>(toff[F], 1));
+    for (int g = 0; g < F; g++) std::copy(T[g].begin(), T[g].end(), tv.begin() + toff[g]);
+    double* d_T;
+    int64_t* d_toff;
+    TRY(ws_typed(c, "pq_thr", tv.size(), &d_T));
+    TRY(ws_typed(c, "pq_off", toff.size(), &d_toff));
+    TRY(h2d(c, d_T, tv.data(), tv.size()));
+    TRY(h2d(c, d_toff, toff.data(), toff.size()));
+    TRY(upload_plan(c, P, pa));
+    int64_t batch = std::max<int64_t>(1, std::min<int64_t>(N, ((int64_t)2 << 30) / (8 * (int64_t)F)));
+    if (const char* e = getenv("SBAG_PREDICT_BATCH_ROWS")) batch = std::max<int64_t>(1, std::min<int64_t>(batch, atoll(e)));
+    double* d_X;
+    uint16_t* d_codes;
+    TRY(ws_typed(c, "pX", (size_t)batch * F, &d_X));
+    TRY(ws_typed(c, "pq_codes", (size_t)batch * Sq, &d_codes));
+    for (int64_t r0 = 0; r0 < N; r0 += batch) {
+      const int64_t n = std::min(batch, N - r0);
+      HIP_TRY(hipMemcpyAsync(d_X, X + r0 * F, (size_t)n * F * 8, hipMemcpyHostToDevice, c->stream));
+      launch_quantize(c->stream, d_X, n, F, d_T, d_toff, d_codes, Sq);
+      pa.codes = d_codes;
+      pa.N = n;
+      pa.out = d_out + r0;
+      launch_predict_tiled(c->stream, pa);
+      HIP_TRY(hipGetLastError());
+    }
+    TRY(d2h(c, out, d_out, (size_t)N));
+    return SBAG_OK;
+  }
+  TRY(upload_forest(c, f));
+  double* d_X;
+  TRY(ws_typed(c, "pX", (size_t)N * F, &d_X));
   if (per_tree) TRY(ws_typed(c, "ppt", (size_t)N * L, &d_pt));
   TRY(h2d(c, d_X, X, (size_t)N * F));
   launch_predict(c->stream, d_X, nullptr, 1, nullptr, nullptr, N, F, F, f->d_nodes, f->d_off, L, agg,
@@ -1930,12 +2079,31 @@ int sbag_predict_dataset(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* 
     for (int32_t g : t.sub)
       if (g >= ds->F) return fail(SBAG_EINVAL, "dataset has fewer features than the model");
   HIP_TRY(hipSetDevice(c->device));
-  TRY(upload_forest(c, f));
   double* d_out;
   TRY(ws_typed(c, "pout", (size_t)ds->N, &d_out));
-  launch_predict(c->stream, nullptr, ds->d_codes, ds->code_bytes, ds->d_dict, ds->d_dict_off, ds->N,
-                 ds->F, ds->S, f->d_nodes, f->d_off, (int)f->trees.size(), agg,
-                 std::max(f->nclasses, 1), d_out, nullptr);
+  if (ds->N == 0) return SBAG_OK;
+  const int L = (int)f->trees.size();
+  PredictArgs pa{};
+  pa.code_bytes = ds->code_bytes;
+  pa.S = ds->S;
+  pa.N = ds->N;
+  pa.agg = agg;
+  TiledPlan P;
+  // TreePoint's `value <= threshold` in the dataset's code space (dict sorted ascending)
+  const bool tiled = plan_tiled(f, pa, ds->F, [&](int g, double thr) {
+    const std::vector<double>& d = ds->dict[g];
+    return (int64_t)(std::upper_bound(d.begin(), d.end(), thr) - d.begin()) - 1;
+  }, P);
+  if (tiled) {
+    TRY(upload_plan(c, P, pa));
+    pa.codes = ds->d_codes;
+    pa.out = d_out;
+    launch_predict_tiled(c->stream, pa);
+  } else {  // very deep trees or very wide rows: node walk from global memory
+    TRY(upload_forest(c, f));
+    launch_predict(c->stream, nullptr, ds->d_codes, ds->code_bytes, ds->d_dict, ds->d_dict_off, ds->N,
+                   ds->F, ds->S, f->d_nodes, f->d_off, L, agg, std::max(f->nclasses, 1), d_out, nullptr);
+  }
   HIP_TRY(hipGetLastError());
   TRY(d2h(c, out, d_out, (size_t)ds->N));
   return SBAG_OK;

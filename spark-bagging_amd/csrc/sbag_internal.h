@@ -115,6 +115,36 @@ struct DevNode {  // packed tree node for predict
   int32_t pad;
 };
 
+// Packed tree for the LDS-tiled predict: children adjacent (right = left + 1).
+// internal: a = left child, b = (global feature << 17) | (tc + 1), go left iff
+//           code <= tc, tc = largest code whose value <= threshold (-1: none)
+// leaf:     a = 0x80000000 | leaf index (prediction in the chunk's leaf values)
+struct PNode {
+  uint32_t a, b;
+};
+
+struct PredictChunk {  // consecutive trees whose nodes + leaves fit the LDS budget
+  int32_t t0, t1;      // trees [t0, t1)
+  int64_t n0, n1;      // packed nodes [n0, n1)
+  int64_t l0, l1;      // leaf values [l0, l1)
+};
+
+struct PredictArgs {
+  const void* codes;   // [N][S] u8 / u16
+  int32_t code_bytes, S;
+  int64_t N;
+  const PNode* nodes;
+  const double* leaves;
+  const int64_t* tree_node;  // [L] first packed node of each tree
+  const int64_t* tree_leaf;  // [L] first leaf value of each tree
+  const PredictChunk* chunks;
+  int32_t nchunks, L;
+  int32_t agg, nclasses;
+  int32_t chunk_bytes;       // LDS bytes reserved for one chunk
+  int32_t pad;
+  double* out;
+};
+
 // ---- launchers (sbag_kernels.hip) ----
 void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
                     int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err);
@@ -151,6 +181,10 @@ void launch_predict(hipStream_t st, const double* X, const void* codes, int code
                     double* out, double* per_tree);
 void launch_aggregate(hipStream_t st, const double* votes, int L, int64_t N, int agg, int nclasses,
                       double* out);
+size_t predict_tiled_lds(const PredictArgs& a);
+void launch_quantize(hipStream_t st, const double* X, int64_t n, int32_t F, const double* thr,
+                     const int64_t* toff, uint16_t* codes, int32_t S);
+void launch_predict_tiled(hipStream_t st, const PredictArgs& a);
 void launch_vc_global(hipStream_t st, const void* codes, int code_bytes, int32_t S, const uint64_t* ent,
                       int64_t cap, const unsigned long long* d_inbag, const int32_t* d_sub,
                       const int32_t* d_Fr, int32_t Fmax, int R, const int64_t* d_off, uint32_t* vc);

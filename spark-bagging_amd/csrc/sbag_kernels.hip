@@ -1721,6 +1721,150 @@ void launch_predict(hipStream_t st, const double* X, const void* codes, int code
                      per_tree);
 }
 
+// ---- LDS-tiled predict over device-resident rows (transform of large scoring
+// sets).  A workgroup stages kPredRows rows of codes (pitch
+// S + 4 bytes: rows on distinct banks) and walks them through the forest chunk by
+// chunk (packed nodes + leaf values in LDS), trees in learner order: the sum is
+// breeze's sequential sum (BaggingRegressor.scala:249-255), the vote breeze's
+// mode (first class to reach the final max count, BaggingClassifier.scala:249-257).
+// Thresholds are precompiled to code space (code <= tc  <=>  value <= threshold,
+// the dictionary being sorted), so a level is two LDS reads and no fp64 compare.
+constexpr int kPredRows = 512;  // 2 rows per thread (two independent walks in flight)
+constexpr int kPredThreads = 256;
+
+size_t predict_tiled_lds(const PredictArgs& a) {
+  const size_t pitch = (size_t)a.S * a.code_bytes + 4;
+  size_t b = (size_t)kPredRows * pitch + (size_t)a.chunk_bytes;
+  if (a.agg == 1) b += (size_t)a.nclasses * kPredRows * 2;
+  return (b + 15) & ~(size_t)15;
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kPredThreads) void k_predict_tiled(PredictArgs A) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int pitch = A.S * (int)sizeof(CT) + 4;
+  unsigned char* rows = smem;
+  unsigned char* chunk = smem + (size_t)kPredRows * pitch;
+  uint16_t* cnt = (uint16_t*)(chunk + A.chunk_bytes);  // [nclasses][kPredRows]
+  const int64_t row0 = (int64_t)blockIdx.x * kPredRows;
+  const int rb = A.S * (int)sizeof(CT);  // bytes of one row
+  for (int q = tid; q < kPredRows * (rb >> 2); q += kPredThreads) {
+    const int r = q / (rb >> 2), w = q - r * (rb >> 2);
+    uint32_t v = 0;
+    if (row0 + r < A.N) v = *(const uint32_t*)((const unsigned char*)A.codes + (row0 + r) * rb + w * 4);
+    *(uint32_t*)(rows + r * pitch + w * 4) = v;
+  }
+  if (A.agg == 1)
+    for (int i = tid; i < A.nclasses * kPredRows; i += kPredThreads) cnt[i] = 0;
+  double sum0 = 0.0, sum1 = 0.0, mode0 = 0.0, mode1 = 0.0;
+  int max0 = 0, max1 = 0;
+  const unsigned char* r0p = rows + tid * pitch;
+  const unsigned char* r1p = rows + (tid + kPredThreads) * pitch;
+  for (int c = 0; c < A.nchunks; c++) {
+    const PredictChunk ch = A.chunks[c];
+    __syncthreads();  // previous chunk done (and the row tile written)
+    const int nb = (int)(ch.n1 - ch.n0) * 8, lb = (int)(ch.l1 - ch.l0) * 8;
+    for (int i = tid; i < (nb >> 3); i += kPredThreads)
+      ((PNode*)chunk)[i] = A.nodes[ch.n0 + i];
+    for (int i = tid; i < (lb >> 3); i += kPredThreads)
+      ((double*)(chunk + nb))[i] = A.leaves[ch.l0 + i];
+    __syncthreads();
+    for (int t = ch.t0; t < ch.t1; t++) {
+      const PNode* tn = (const PNode*)chunk + (A.tree_node[t] - ch.n0);
+      const double* tl = (const double*)(chunk + nb) + (A.tree_leaf[t] - ch.l0);
+      uint32_t i0 = 0, i1 = 0;
+      PNode a0 = tn[0], a1 = tn[0];
+      while (!((a0.a & a1.a) & 0x80000000u)) {  // until both walks reach a leaf
+        if (!(a0.a & 0x80000000u)) {
+          const uint32_t code = ((const CT*)r0p)[a0.b >> 17];
+          i0 = a0.a + (code < (a0.b & 0x1ffffu) ? 0u : 1u);
+          a0 = tn[i0];
+        }
+        if (!(a1.a & 0x80000000u)) {
+          const uint32_t code = ((const CT*)r1p)[a1.b >> 17];
+          i1 = a1.a + (code < (a1.b & 0x1ffffu) ? 0u : 1u);
+          a1 = tn[i1];
+        }
+      }
+      const double p0 = tl[a0.a & 0x7fffffffu], p1 = tl[a1.a & 0x7fffffffu];
+      if (A.agg == 0) {
+        sum0 += p0;
+        sum1 += p1;
+      } else {
+        const int k0 = ++cnt[(int)p0 * kPredRows + tid];
+        if (k0 > max0) {
+          max0 = k0;
+          mode0 = p0;
+        }
+        const int k1 = ++cnt[(int)p1 * kPredRows + tid + kPredThreads];
+        if (k1 > max1) {
+          max1 = k1;
+          mode1 = p1;
+        }
+      }
+    }
+  }
+  if (row0 + tid < A.N) A.out[row0 + tid] = A.agg == 0 ? sum0 / (double)A.L : mode0;
+  if (row0 + tid + kPredThreads < A.N)
+    A.out[row0 + tid + kPredThreads] = A.agg == 0 ? sum1 / (double)A.L : mode1;
+}
+
+// rows -> u16 codes against the forest's thresholds of each feature:
+// code = #{t < x} (binary search), so x <= t_k <=> code <= k; NaN compares false
+// with everything in Spark (goes right) -> the code past every threshold
+__global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ X, int64_t n, int32_t F,
+                                                  const double* __restrict__ thr,
+                                                  const int64_t* __restrict__ toff,
+                                                  uint16_t* __restrict__ codes, int32_t S) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * S) return;
+  const int64_t row = i / S;
+  const int g = (int)(i - row * S);
+  uint32_t code = 0;
+  if (g < F) {
+    const double x = X[row * F + g];
+    int64_t lo = toff[g], hi = toff[g + 1];
+    if (x != x) {
+      lo = hi;
+    } else {
+      while (lo < hi) {  // first threshold >= x
+        const int64_t mid = (lo + hi) >> 1;
+        if (thr[mid] < x)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+    }
+    code = (uint32_t)(lo - toff[g]);
+  }
+  codes[i] = (uint16_t)code;
+}
+
+void launch_quantize(hipStream_t st, const double* X, int64_t n, int32_t F, const double* thr,
+                     const int64_t* toff, uint16_t* codes, int32_t S) {
+  const int64_t total = n * S;
+  hipLaunchKernelGGL(k_quantize, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, X, n, F,
+                     thr, toff, codes, S);
+}
+
+void launch_predict_tiled(hipStream_t st, const PredictArgs& a) {
+  const size_t lds = predict_tiled_lds(a);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_predict_tiled<uint8_t>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)k_predict_tiled<uint16_t>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const dim3 grid((unsigned)((a.N + kPredRows - 1) / kPredRows));
+  if (a.code_bytes == 1)
+    hipLaunchKernelGGL(k_predict_tiled<uint8_t>, grid, dim3(kPredThreads), lds, st, a);
+  else
+    hipLaunchKernelGGL(k_predict_tiled<uint16_t>, grid, dim3(kPredThreads), lds, st, a);
+}
+
 __global__ __launch_bounds__(256) void k_aggregate(const double* __restrict__ votes, int L,
                                                    int64_t N, int agg, int nclasses,
                                                    double* __restrict__ out) {

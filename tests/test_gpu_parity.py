@@ -215,3 +215,21 @@ def test_gini_class_tiles_forced(ctx, monkeypatch):
     ds, X, forest, orf = _synthetic_cls(ctx, 15000, 80, 7, 4, 7, seed_data=23, ratio=0.8,
                                         replacement=True)
     assert_forest_equal(forest, orf)
+
+
+def test_transform_batches_nan_and_signed_zero(ctx, cpusmall, monkeypatch):
+    """Batched host-row transform (rows binned on the device against the forest's
+    thresholds): several upload batches, NaN (Spark: `NaN <= t` is false -> right),
+    -0.0 == 0.0 and +-inf, bit-exact against the oracle's tree walk."""
+    X, y = cpusmall
+    forest, orf, _ = _fit_both(ctx, X, y, 7, replacement=True, ratio=0.9, seed=SEED_REG,
+                               depth=7, bins=32, cls=False)
+    Z = X.copy()
+    rng = np.random.default_rng(3)
+    Z[rng.random(Z.shape) < 0.05] = np.nan
+    Z[rng.random(Z.shape) < 0.05] = -0.0
+    Z[rng.random(Z.shape) < 0.01] = np.inf
+    Z[rng.random(Z.shape) < 0.01] = -np.inf
+    monkeypatch.setenv("SBAG_PREDICT_BATCH_ROWS", "1000")
+    got = nat.predict(ctx, forest, Z, nat.AGG_MEAN)
+    np.testing.assert_array_equal(got, oracle.predict(orf, Z))
