@@ -18,6 +18,7 @@
 #include <limits>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -965,6 +966,19 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   HIP_TRY(hipEventCreate(&ev_start));
   HIP_TRY(hipEventCreate(&ev_stop));
   HIP_TRY(hipEventRecord(ev_start, c->stream));
+  // host-side phase timing (SBAG_PROFILE_HOST=1 prints it): where the GPU waits
+  const bool hprof = getenv("SBAG_PROFILE_HOST") != nullptr;
+  double hp[16] = {0};
+  auto hnow = [] {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  double ht = hnow();
+  auto hmark = [&](int k) {
+    const double t = hnow();
+    hp[k] += t - ht;
+    ht = t;
+  };
 
   // ---- 1. bag: counts [R][N]
   uint8_t* d_counts;
@@ -992,8 +1006,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     HIP_TRY(hipGetLastError());
     tm.end(h);
   }
+  hmark(8);
   std::vector<unsigned long long> inbag(4 * R);
   TRY(d2h(c, inbag.data(), d_inbag, (size_t)4 * R));
+  hmark(9);
   std::vector<int64_t> nw(R);
   unsigned int cmax = 1;
   for (int r = 0; r < R; r++) {
@@ -1212,6 +1228,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     tm.end(h);
   }
 
+  hmark(10);
   // ---- 4. thresholds, LUTs (code -> bin), numSplits per (replica, feature)
   std::vector<std::vector<double>> thr((size_t)R * Fmax);
   std::vector<int32_t> h_nbins((size_t)R * Fmax, 1);
@@ -1219,23 +1236,39 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   std::vector<int32_t> exact(R, 1);
   bool identity = ds->code_bytes == 1;
   int NB = 1;
-  for (int r = 0; r < R; r++) {
-    const int64_t required = std::max<int64_t>((int64_t)tp.max_bins * tp.max_bins, 10000);
-    if (required < nw[r]) exact[r] = 0;  // reference samples for split finding
-    for (int fl = 0; fl < h_Fr[r]; fl++) {
-      const int g = sub[r][fl];
-      const size_t o = (size_t)vcoff[(size_t)r * Fmax + fl];
-      std::vector<double>& t = thr[(size_t)r * Fmax + fl];
-      const int nt = find_splits(ds->dict[g], vc.data() + o, ds->zero_code[g], nw[r], tp.max_bins, t);
-      h_nbins[(size_t)r * Fmax + fl] = nt + 1;
-      NB = std::max(NB, nt + 1);
-      const auto& d = ds->dict[g];
-      for (size_t k = 0; k < d.size(); k++) {
-        const int b = (int)(std::lower_bound(t.begin(), t.end(), d[k]) - t.begin());  // #{t < v}
-        lut[o + k] = (uint8_t)b;
-        if (b != (int)k) identity = false;
+  {
+    // replicas are independent: split finding runs on host threads
+    const int nth = std::max(1, std::min<int>(R, std::min(16, (int)std::thread::hardware_concurrency())));
+    std::vector<int> t_nb(nth, 1);
+    std::vector<char> t_id(nth, 1);
+    auto work = [&](int w) {
+      for (int r = w; r < R; r += nth) {
+        const int64_t required = std::max<int64_t>((int64_t)tp.max_bins * tp.max_bins, 10000);
+        if (required < nw[r]) exact[r] = 0;  // reference samples for split finding
+        for (int fl = 0; fl < h_Fr[r]; fl++) {
+          const int g = sub[r][fl];
+          const size_t o = (size_t)vcoff[(size_t)r * Fmax + fl];
+          std::vector<double>& t = thr[(size_t)r * Fmax + fl];
+          const int nt = find_splits(ds->dict[g], vc.data() + o, ds->zero_code[g], nw[r], tp.max_bins, t);
+          h_nbins[(size_t)r * Fmax + fl] = nt + 1;
+          t_nb[w] = std::max(t_nb[w], nt + 1);
+          const auto& d = ds->dict[g];
+          for (size_t k = 0; k < d.size(); k++) {
+            const int b = (int)(std::lower_bound(t.begin(), t.end(), d[k]) - t.begin());  // #{t < v}
+            lut[o + k] = (uint8_t)b;
+            if (b != (int)k) t_id[w] = 0;
+          }
+          if ((int)d.size() > nt + 1) t_id[w] = 0;
+        }
       }
-      if ((int)d.size() > nt + 1) identity = false;
+    };
+    std::vector<std::thread> pool;
+    for (int w = 1; w < nth; w++) pool.emplace_back(work, w);
+    work(0);
+    for (auto& th : pool) th.join();
+    for (int w = 0; w < nth; w++) {
+      NB = std::max(NB, t_nb[w]);
+      identity = identity && t_id[w];
     }
   }
   if (optimistic && identity) {
@@ -1258,6 +1291,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
         }
       }
   }
+  hmark(11);
   // ---- 5. bins
   const uint8_t* d_bins;
   int64_t bins_rstride = 0;
@@ -1343,6 +1377,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   TRY(h2d(c, d_pos, h_pos.data(), h_pos.size()));
   TRY(h2d(c, d_nbins, h_nbins.data(), h_nbins.size()));
 
+  hmark(12);
   // ---- 6. level-wise growth
   HistGeom g;
   if (!hist_geometry(S, Fmax, NB, NS, gini, g))
@@ -1384,19 +1419,6 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   std::vector<uint64_t> slot_sq(R);
   for (int r = 0; r < R; r++) slot_sq[r] = inbag[3 * R + r];
   int64_t fallbacks = 0;
-  // host-side phase timing (SBAG_PROFILE_HOST=1 prints it): where the GPU waits
-  const bool hprof = getenv("SBAG_PROFILE_HOST") != nullptr;
-  double hp[8] = {0};
-  auto hnow = [] {
-    return std::chrono::duration<double, std::milli>(
-               std::chrono::steady_clock::now().time_since_epoch()).count();
-  };
-  double ht = hnow();
-  auto hmark = [&](int k) {
-    const double t = hnow();
-    hp[k] += t - ht;
-    ht = t;
-  };
   for (int level = 0; level <= D; level++) {
     const int M = (int)slots.size();
     if (M == 0) break;
@@ -1564,19 +1586,32 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       TRY(ws_typed(c, "sq_left", (size_t)NP, &d_sql));
       HIP_TRY(hipMemsetAsync(d_sql, 0, (size_t)NP * 8, c->stream));
     }
+    hmark(13);
     {
       // work order: parents grouped by split column (replica copies apart), pieces of
       // 8192 entries interleaved round-robin across the parents of a group, so the
       // concurrent workgroups spread over the group's cursors while the GPU reads
       // one column
       const int64_t piece = 8192;
-      std::vector<int32_t> order(NP);
-      for (int q = 0; q < NP; q++) order[q] = q;
       auto colkey = [&](int q) {
         return (bins_rstride ? (int64_t)par[q].r * 65536 : 0) + (int64_t)par[q].pos;
       };
-      std::stable_sort(order.begin(), order.end(),
-                       [&](int x, int y) { return colkey(x) < colkey(y); });
+      // counting sort of the parents by column (pos < 65536; per replica when bins are)
+      std::vector<int32_t> order(NP);
+      {
+        const int64_t nkeys = bins_rstride ? (int64_t)R * 65536 : 65536;
+        std::vector<int32_t> start;
+        if (nkeys <= ((int64_t)1 << 24)) {
+          start.assign((size_t)nkeys + 1, 0);
+          for (int q = 0; q < NP; q++) start[(size_t)colkey(q) + 1]++;
+          for (int64_t k = 0; k < nkeys; k++) start[(size_t)k + 1] += start[(size_t)k];
+          for (int q = 0; q < NP; q++) order[start[(size_t)colkey(q)]++] = q;
+        } else {
+          for (int q = 0; q < NP; q++) order[q] = q;
+          std::stable_sort(order.begin(), order.end(),
+                           [&](int x, int y) { return colkey(x) < colkey(y); });
+        }
+      }
       // rounds: inside a column group (parents longest first), round k takes piece k
       // of every parent longer than k pieces; the piece list is written on the device
       std::vector<PartRound> rounds;
@@ -1589,8 +1624,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       for (int g0 = 0; g0 < NP;) {
         int g1 = g0;
         while (g1 < NP && colkey(order[g1]) == colkey(order[g0])) g1++;
-        std::stable_sort(order.begin() + g0, order.begin() + g1, [&](int x, int y) {
-          return pseg[x].second - pseg[x].first > pseg[y].second - pseg[y].first;
+        std::sort(order.begin() + g0, order.begin() + g1, [&](int x, int y) {
+          const int64_t lx = pseg[x].second - pseg[x].first, ly = pseg[y].second - pseg[y].first;
+          return lx != ly ? lx > ly : x < y;
         });
         int act = g1 - g0;
         for (int64_t off = 0;; off += piece) {
@@ -1603,6 +1639,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
         g0 = g1;
       }
       rounds.push_back(PartRound{npieces, NP, 0, 0});  // sentinel
+      hmark(14);
       PartPiece* d_pp;
       PartRound* d_rounds;
       int32_t* d_order;
@@ -1744,9 +1781,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     hmark(6);
   }
   if (hprof)
-    fprintf(stderr, "host ms: split-prep %.2f split-wait %.2f nodes %.2f part-prep %.2f part-wait %.2f "
-                    "children %.2f hist-prep %.2f loop %.2f\n", hp[0], hp[1], hp[2], hp[3], hp[4], hp[5],
-            hp[6], hp[7]);
+    fprintf(stderr, "host ms: setup+sample-launch %.2f compact-wait %.2f valuecounts %.2f thresholds %.2f "
+                    "bins %.2f | split-prep %.2f split-wait %.2f nodes %.2f part-cursors %.2f part-sort %.2f "
+                    "part-upload %.2f part-wait %.2f children %.2f hist-prep %.2f loop %.2f\n", hp[8], hp[9],
+            hp[10], hp[11], hp[12], hp[0], hp[1], hp[2], hp[13], hp[14], hp[3], hp[4], hp[5], hp[6], hp[7]);
   HIP_TRY(hipEventRecord(ev_stop, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
 
