@@ -1491,6 +1491,157 @@ void launch_zero_word(hipStream_t st, uint64_t* hist, const int32_t* d_slots, in
                      slot_words, stride, word);
 }
 
+// ---- gini split search with every thread on a candidate.  k_split<true> ran one
+// thread per feature (100 of 256 busy) through 31 splits x 2C fp64 divisions each;
+// with 64 classes (BASELINE config 5) that dominated a level.  Here a block stages
+// the bin-prefix counts of a group of G features in LDS ([f][bin][class] u32) and
+// gives each thread one (feature, split) candidate; the arithmetic of a candidate is
+// k_split<true>'s, in Spark's operation order (ImpurityCalculator.count = sequential
+// class sum, Gini.calculate = 1 - sum freq^2 in class order), and the block argmax
+// keeps Spark's first max (maxBy over splits, then over features).
+__global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int slot = A.slot_ids ? A.slot_ids[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x;
+  const int r = A.slot_r[slot];
+  const int Fr = A.Fr[r];
+  const int NB = A.NB, NS = A.NS;
+  const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
+  const uint32_t* hs = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
+  const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
+  int64_t* s_tot = (int64_t*)smem;                      // [NS]
+  double* s_gain = (double*)(s_tot + NS);               // [256]
+  int* s_key = (int*)(s_gain + 256);                    // [256] fl * 65536 + s (INT_MAX: none)
+  int* s_valid = s_key + 256;                           // [256]
+  uint32_t* pre = (uint32_t*)(s_valid + 256);           // [G][NB][NS] prefix over bins
+  for (int c = tid; c < NS; c += 256) {
+    int64_t t = 0;
+    for (int b = 0; b < NB; b++) t += hs[(int64_t)b * NS + c];
+    s_tot[c] = t;
+  }
+  __syncthreads();
+  double ttot = 0.0;
+  for (int c = 0; c < NS; c++) ttot += (double)s_tot[c];
+  double imp = 0.0;
+  if (ttot != 0) {
+    imp = 1.0;
+    for (int c = 0; c < NS; c++) {
+      const double f = (double)s_tot[c] / ttot;
+      imp -= f * f;
+    }
+  }
+  const int64_t tcount = (int64_t)ttot;
+  double bgain = -INFINITY;
+  int bkey = INT_MAX, bvalid = 0;
+  for (int f0 = 0; f0 < Fr; f0 += G) {
+    const int g = min(G, Fr - f0);
+    __syncthreads();  // previous group's prefix no longer read
+    for (int q = tid; q < g * NS; q += 256) {
+      const int fl = q / NS, c = q - fl * NS;
+      const uint32_t* h = hs + (int64_t)(f0 + fl) * NB * NS + c;
+      uint32_t* o = pre + (size_t)fl * NB * NS + c;
+      uint32_t acc = 0;
+      for (int b = 0; b < NB; b++) {
+        acc += h[(int64_t)b * NS];
+        o[(size_t)b * NS] = acc;
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < g * (NB - 1); q += 256) {
+      const int fl = q / (NB - 1), sp = q - fl * (NB - 1);
+      const int nsp = nb_r[f0 + fl] - 1;
+      if (sp >= nsp) continue;
+      const uint32_t* left = pre + ((size_t)fl * NB + sp) * NS;
+      double lt = 0.0;
+      for (int c = 0; c < NS; c++) lt += (double)left[c];
+      const int64_t lc = (int64_t)lt;
+      const int64_t rc = tcount - lc;
+      double gain;
+      int valid;
+      if (lc < A.min_inst || rc < A.min_inst) {
+        gain = -DBL_MAX;
+        valid = 0;
+      } else {
+        double li = 0.0, ri = 0.0;
+        if (lt != 0) {
+          li = 1.0;
+          for (int c = 0; c < NS; c++) {
+            const double fq = (double)left[c] / lt;
+            li -= fq * fq;
+          }
+        }
+        double rt = 0.0;
+        for (int c = 0; c < NS; c++) rt += (double)(s_tot[c] - (int64_t)left[c]);
+        if (rt != 0) {
+          ri = 1.0;
+          for (int c = 0; c < NS; c++) {
+            const double fq = (double)(s_tot[c] - (int64_t)left[c]) / rt;
+            ri -= fq * fq;
+          }
+        }
+        const double lw = (double)lc / (double)(lc + rc);
+        const double rw = (double)rc / (double)(lc + rc);
+        gain = imp - lw * li - rw * ri;
+        valid = 1;
+        if (gain < A.min_gain) {
+          gain = -DBL_MAX;
+          valid = 0;
+        }
+      }
+      const int key = (f0 + fl) * 65536 + sp;
+      if (gain > bgain || (gain == bgain && key < bkey)) {
+        bgain = gain;
+        bkey = key;
+        bvalid = valid;
+      }
+    }
+  }
+  s_gain[tid] = bgain;
+  s_key[tid] = bkey;
+  s_valid[tid] = bvalid;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const double g2 = s_gain[tid + o];
+      const int k2 = s_key[tid + o];
+      if (g2 > s_gain[tid] || (g2 == s_gain[tid] && k2 < s_key[tid])) {
+        s_gain[tid] = g2;
+        s_key[tid] = k2;
+        s_valid[tid] = s_valid[tid + o];
+      }
+    }
+    __syncthreads();
+  }
+  const int key = s_key[0];
+  const int bf = key == INT_MAX ? -1 : key / 65536, bsp = key == INT_MAX ? -1 : key % 65536;
+  int64_t* so = A.stats + (int64_t)slot * 3 * NS;
+  if (tid == 0) {
+    SplitOut o;
+    if (key == INT_MAX) {
+      o.gain = -DBL_MAX;
+      o.fl = -1;
+      o.s = -1;
+      o.valid = 0;
+    } else {
+      o.gain = s_gain[0];
+      o.fl = bf;
+      o.s = bsp;
+      o.valid = s_valid[0];
+    }
+    o.pad = 0;
+    A.out[slot] = o;
+  }
+  for (int c = tid; c < NS; c += 256) {
+    int64_t l = 0;
+    if (bf >= 0) {
+      const uint32_t* h = hs + (int64_t)bf * NB * NS;
+      for (int sb = 0; sb <= bsp; sb++) l += h[(int64_t)sb * NS + c];
+    }
+    so[c] = s_tot[c];
+    so[NS + c] = l;
+    so[2 * NS + c] = s_tot[c] - l;
+  }
+}
+
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
   const size_t lds = 256 * (8 + 4 + 4 + 4) + 8 * (size_t)a.NS + (gini ? (size_t)a.NS * 256 * 4 : 0);
   static bool attr_set = false;
@@ -1501,10 +1652,26 @@ void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  if (gini)
+  if (gini) {
+    // feature group: <= 64 KB of u32 prefix counts and about one candidate per thread
+    const size_t per_f = (size_t)a.NB * a.NS * 4;
+    int G = (int)std::max<size_t>(1, std::min<size_t>((64 * 1024) / per_f, (size_t)(256 / std::max(1, a.NB - 1))));
+    G = std::max(1, std::min(G, a.Fmax));
+    const size_t lds_g = (size_t)a.NS * 8 + 256 * (8 + 4 + 4) + (size_t)G * per_f;
+    static bool attr_g = false;
+    if (!attr_g) {
+      HIPCHK(hipFuncSetAttribute((const void*)k_split_gini, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024));
+      attr_g = true;
+    }
+    if (lds_g <= 160 * 1024 && !getenv("SBAG_SPLIT_GINI_V1")) {
+      hipLaunchKernelGGL(k_split_gini, dim3(M), dim3(256), lds_g, st, a, G);
+      return;
+    }
     hipLaunchKernelGGL(k_split<true>, dim3(M), dim3(256), lds, st, a);
-  else
+  } else {
     hipLaunchKernelGGL(k_split<false>, dim3(M), dim3(256), lds, st, a);
+  }
 }
 
 // sibling = parent - smaller child  (triples: dst slot, parent slot, small slot)
