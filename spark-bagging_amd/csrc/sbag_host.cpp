@@ -371,6 +371,8 @@ struct Calc {  // ImpurityCalculator over exact integer stats
   }
 };
 
+constexpr int kMaxHostNS = 4096;  // classes + 1 (check_agg's bound on nclasses)
+
 struct NodeStats {  // exact integer stats of a node: inline up to 8 words (no allocation)
   int64_t inl[8];
   std::vector<int64_t> heap;
@@ -1075,6 +1077,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     seg[r] = {(int64_t)r * cap, (int64_t)r * cap + (int64_t)inbag[r]};
   }
   const int NS = gini ? (int)ds->kmax + 1 : 3;
+  if (NS > kMaxHostNS) return fail(SBAG_EUNSUPPORTED, "more than 4095 classes");
   const size_t word_bytes = gini ? 4 : 8;
   HistWork work;
   ParentInfo* d_par;
@@ -1448,6 +1451,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     sa.inv_scale2 = inv_scale2;
     sa.out = d_sout;
     sa.stats = d_sstats;
+    sa.plane = (int64_t)M * NS;
     if (!gini) {
       uint64_t* d_nsq;
       TRY(ws_typed(c, "node_sq", (size_t)M, &d_nsq));
@@ -1464,6 +1468,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       tm.end(h);
     }
     std::vector<SplitOut> sout(M);
+    // stats planes [total][left][right] x [M][NS]; the host needs the left plane (a
+    // node's total is known from its parent's split, right = total - left) and, at the
+    // root, the totals
     std::vector<int64_t> sst((size_t)M * 3 * NS);
     hmark(0);
     TRY(d2h(c, sout.data(), d_sout, (size_t)M));
@@ -1503,7 +1510,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
         for (int i : fl_slots) exact[i] = 1;
       }
     }
-    TRY(d2h(c, sst.data(), d_sstats, sst.size()));
+    if (level == 0)
+      TRY(d2h(c, sst.data(), d_sstats, (size_t)2 * M * NS));
+    else
+      TRY(d2h(c, sst.data() + (size_t)M * NS, d_sstats + (size_t)M * NS, (size_t)M * NS));
     // --- node updates (RandomForest.findBestSplits, host part)
     struct Split {
       int slot, r, ni, li;
@@ -1514,15 +1524,16 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     for (int i = 0; i < M; i++) {
       const int r = slots[i].first;
       const int ni = slots[i].second;
-      const int64_t* tot = &sst[(size_t)i * 3 * NS];
-      const int64_t* lef = tot + NS;
-      const int64_t* rig = tot + 2 * NS;
+      const int64_t* lef = &sst[(size_t)M * NS + (size_t)i * NS];
+      int64_t rig[kMaxHostNS];
       {
         HNode& n = trees[r][ni];
         if (level == 0) {
+          const int64_t* tot = &sst[(size_t)i * NS];
           n.stats.assign(tot, tot + NS);
           n.impurity = Calc{n.stats.data(), NS, gini, ds->shift}.impurity();
         }
+        for (int k = 0; k < NS; k++) rig[k] = n.stats[k] - lef[k];
         const SplitOut& so = sout[i];
         if (so.fl < 0) {  // no feature has splits: invalid stats on the parent aggregate
           n.gain = kDoubleMinValue;
@@ -1544,14 +1555,19 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       Rn.stats.assign(rig, rig + NS);
       bool wl = !child_leaf, wr = !child_leaf;
       if (exact[i]) {  // children stats complete: leaf-by-purity known before routing
-        L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
-        Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
+        if (gini && (sout[i].pad & 2)) {  // computed by k_split_gini
+          L.impurity = sout[i].imp_l;
+          Rn.impurity = sout[i].imp_r;
+        } else {
+          L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
+          Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
+        }
         wl = wl && L.impurity != 0.0;
         wr = wr && Rn.impurity != 0.0;
       }
       const int li = (int)trees[r].size();
-      trees[r].push_back(L);
-      trees[r].push_back(Rn);
+      trees[r].push_back(std::move(L));
+      trees[r].push_back(std::move(Rn));
       trees[r][ni].left = li;
       trees[r][ni].right = li + 1;
       if (!wl && !wr && exact[i]) {  // nothing to route, all stats known
@@ -1780,30 +1796,37 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     std::swap(ent_cur, ent_nxt);
     hmark(6);
   }
-  if (hprof)
-    fprintf(stderr, "host ms: setup+sample-launch %.2f compact-wait %.2f valuecounts %.2f thresholds %.2f "
-                    "bins %.2f | split-prep %.2f split-wait %.2f nodes %.2f part-cursors %.2f part-sort %.2f "
-                    "part-upload %.2f part-wait %.2f children %.2f hist-prep %.2f loop %.2f\n", hp[8], hp[9],
-            hp[10], hp[11], hp[12], hp[0], hp[1], hp[2], hp[13], hp[14], hp[3], hp[4], hp[5], hp[6], hp[7]);
   HIP_TRY(hipEventRecord(ev_stop, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
 
-  // ---- 7. models (toNode(prune = true)) + subspaces
+  // ---- 7. models (toNode(prune = true)) + subspaces, trees on host threads
   forest->trees.resize(R);
   int nclasses = 0;
+  std::vector<int> ns_of(R, 3);
   for (int r = 0; r < R; r++) {
-    HTree& t = forest->trees[r];
-    t.sub = sub[r];
-    t.exact = exact[r];
-    int ns_out = 3;
     if (gini) {  // Classifier.getNumClasses on the subbag: max label + 1
-      ns_out = 0;
+      int ns_out = 0;
       for (int k = 0; k < NS; k++)
         if (trees[r][0].stats[k] > 0) ns_out = k + 1;
+      ns_of[r] = ns_out;
       nclasses = std::max(nclasses, ns_out);
     }
-    t.ns = ns_out;
-    emit(trees[r], 0, t, NS, gini, ds->shift, ns_out);
+  }
+  {
+    const int nth = std::max(1, std::min<int>(R, std::min(16, (int)std::thread::hardware_concurrency())));
+    auto work = [&](int w) {
+      for (int r = w; r < R; r += nth) {
+        HTree& t = forest->trees[r];
+        t.sub = sub[r];
+        t.exact = exact[r];
+        t.ns = ns_of[r];
+        emit(trees[r], 0, t, NS, gini, ds->shift, ns_of[r]);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int w = 1; w < nth; w++) pool.emplace_back(work, w);
+    work(0);
+    for (auto& th : pool) th.join();
   }
   forest->nclasses = gini ? std::max(nclasses, (int)ds->kmax + 1) : 0;
   double cats[T_NCAT] = {0};
@@ -1830,6 +1853,13 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   T.hist_entries = hist_entries;
   T.hist_upper_bytes = hist_upper;
   T.levels = levels;
+  hmark(15);
+  if (hprof)
+    fprintf(stderr, "host ms: setup+sample-launch %.2f compact-wait %.2f valuecounts %.2f thresholds %.2f "
+                    "bins %.2f | split-prep %.2f split-wait %.2f nodes %.2f part-cursors %.2f part-sort %.2f "
+                    "part-upload %.2f part-wait %.2f children %.2f hist-prep %.2f loop %.2f | emit %.2f\n",
+            hp[8], hp[9], hp[10], hp[11], hp[12], hp[0], hp[1], hp[2], hp[13], hp[14], hp[3], hp[4], hp[5],
+            hp[6], hp[7], hp[15]);
   *out = forest.release();
   return SBAG_OK;
 }

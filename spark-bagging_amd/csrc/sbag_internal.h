@@ -89,7 +89,8 @@ struct SplitOut {
   int32_t fl;   // best local feature, -1 when no feature has splits
   int32_t s;    // best split bin
   int32_t valid;
-  int32_t pad;
+  int32_t pad;  // bit 0: variance screen undecided; bit 1: imp_l / imp_r are set
+  double imp_l, imp_r;  // Gini.calculate of the chosen split's children (k_split_gini)
 };
 
 struct SplitArgs {
@@ -102,7 +103,8 @@ struct SplitArgs {
   double min_gain;
   double inv_scale, inv_scale2;  // 2^-s, 2^-2s (fixed-point labels)
   SplitOut* out;                  // [M]
-  int64_t* stats;                 // [M][3][NS]: total, left, right (integers)
+  int64_t* stats;                 // [3][M][NS] planes: total, left, right (integers)
+  int64_t plane;                  // M * NS
   const int32_t* slot_ids;        // block -> slot (NULL: identity)
   const uint64_t* node_sq;        // screen: [M] exact sum of count*k^2 of each node
 };

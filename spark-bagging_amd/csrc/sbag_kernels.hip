@@ -1292,7 +1292,7 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
     }
     __syncthreads();
   }
-  int64_t* so = A.stats + (int64_t)slot * 3 * NS;
+  int64_t* so = A.stats + (int64_t)slot * NS;  // so[k * plane + c]: total, left, right
   if (tid == 0) {
     SplitOut o;
     const int fl = s_fl[0];
@@ -1323,8 +1323,8 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
       }
     }
     so[c] = s_tot[c];
-    so[NS + c] = l;
-    so[2 * NS + c] = s_tot[c] - l;
+    so[A.plane + c] = l;
+    so[2 * A.plane + c] = s_tot[c] - l;
   }
 }
 
@@ -1434,7 +1434,8 @@ __global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
   }
   if (tid == 0) {
     SplitOut o;
-    int64_t* so = A.stats + (int64_t)slot * 9;
+    int64_t* so = A.stats + (int64_t)slot * 3;  // NS = 3; so[k * plane + c]
+    const int64_t P = A.plane;
     so[0] = tc;
     so[1] = tsk;
     so[2] = (int64_t)tsq;
@@ -1444,7 +1445,7 @@ __global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
       o.s = first_fl == INT_MAX ? -1 : 0;
       o.valid = 0;
       o.pad = 0;
-      so[3] = so[4] = so[5] = so[6] = so[7] = so[8] = 0;
+      so[P] = so[P + 1] = so[P + 2] = so[2 * P] = so[2 * P + 1] = so[2 * P + 2] = 0;
     } else {
       const bool flag = s_cnt[0] > 1 || gb < A.min_gain + delta || gb <= delta;
       o.gain = gb;
@@ -1458,12 +1459,12 @@ __global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
         lc += (int64_t)h[s * 3];
         lsk += (int64_t)h[s * 3 + 1];
       }
-      so[3] = lc;
-      so[4] = lsk;
-      so[5] = -1;  // left sum of squares: from k_partition
-      so[6] = tc - lc;
-      so[7] = tsk - lsk;
-      so[8] = -1;
+      so[P] = lc;
+      so[P + 1] = lsk;
+      so[P + 2] = -1;  // left sum of squares: from k_partition
+      so[2 * P] = tc - lc;
+      so[2 * P + 1] = tsk - lsk;
+      so[2 * P + 2] = -1;
     }
     A.out[slot] = o;
   }
@@ -1613,7 +1614,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   }
   const int key = s_key[0];
   const int bf = key == INT_MAX ? -1 : key / 65536, bsp = key == INT_MAX ? -1 : key % 65536;
-  int64_t* so = A.stats + (int64_t)slot * 3 * NS;
+  int64_t* so = A.stats + (int64_t)slot * NS;  // so[k * plane + c]: total, left, right
   if (tid == 0) {
     SplitOut o;
     if (key == INT_MAX) {
@@ -1637,8 +1638,29 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
       for (int sb = 0; sb <= bsp; sb++) l += h[(int64_t)sb * NS + c];
     }
     so[c] = s_tot[c];
-    so[NS + c] = l;
-    so[2 * NS + c] = s_tot[c] - l;
+    so[A.plane + c] = l;
+    so[2 * A.plane + c] = s_tot[c] - l;
+  }
+  __syncthreads();
+  if (tid == 0 && bf >= 0) {  // the children's Gini.calculate, as the host's Calc would
+    double imp2[2];
+    for (int side = 0; side < 2; side++) {
+      const int64_t* st = so + (1 + side) * A.plane;
+      double total = 0.0;
+      for (int c = 0; c < NS; c++) total += (double)st[c];
+      double im = 0.0;
+      if (total != 0) {
+        im = 1.0;
+        for (int c = 0; c < NS; c++) {
+          const double fq = (double)st[c] / total;
+          im -= fq * fq;
+        }
+      }
+      imp2[side] = im;
+    }
+    A.out[slot].imp_l = imp2[0];
+    A.out[slot].imp_r = imp2[1];
+    A.out[slot].pad = 2;
   }
 }
 
