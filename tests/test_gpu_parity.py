@@ -233,3 +233,18 @@ def test_transform_batches_nan_and_signed_zero(ctx, cpusmall, monkeypatch):
     monkeypatch.setenv("SBAG_PREDICT_BATCH_ROWS", "1000")
     got = nat.predict(ctx, forest, Z, nat.AGG_MEAN)
     np.testing.assert_array_equal(got, oracle.predict(orf, Z))
+
+
+def test_wide_rows_four_lane_groups(ctx):
+    """200 features: 256-byte rows and four 64-feature lane groups in k_hist (the C4
+    shape has 256), with a partial last group and a 0.6 feature subspace."""
+    ds = nat.DeviceDataset.synthetic(12000, 200, seed=29, num_classes=0, ctx=ctx)
+    X, y = ds.features(), ds.labels()
+    forest = nat.fit(ctx, ds, replacement=True, sample_ratio=0.6, seed=SEED_REG, learner_begin=0,
+                     learner_end=3, max_depth=6, max_bins=32)
+    counts = oracle.bag(True, 0.6, 0, 3, SEED_REG, [0, 12000], 12000)
+    subs = [oracle.subspace(0.6, 200, SEED_REG + i) for i in range(3)]
+    orf = oracle_forest(X, y, counts, subs, 6, 32, False)
+    assert_forest_equal(forest, orf)
+    np.testing.assert_array_equal(nat.predict_dataset(ctx, forest, ds, nat.AGG_MEAN),
+                                  oracle.predict(orf, X))
