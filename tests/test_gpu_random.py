@@ -1,0 +1,80 @@
+"""GPU: randomized parity sweep -- small random datasets and parameter draws
+(depth 0..9, maxBins 2..64, F 1..70, 1..6 learners, both samplers, random
+partition layouts, minInstancesPerNode / minInfoGain, 2..9 classes), every tree
+bit-exact against the CPU oracle and every prediction equal.  Seeds are fixed so a
+failure replays."""
+import numpy as np
+import pytest
+
+import oracle
+from parity_utils import assert_forest_equal, oracle_forest
+
+import spark_bagging_amd as sb
+from spark_bagging_amd import _native as nat
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return sb.default_context(0)
+
+
+def _case(seed):
+    rng = np.random.default_rng(seed)
+    N = int(rng.integers(40, 2500))
+    F = int(rng.integers(1, 71))
+    cls = bool(rng.integers(0, 2))
+    # feature values: a mix of few-level and many-level columns, zeros included
+    X = np.empty((N, F))
+    for f in range(F):
+        levels = int(rng.choice([2, 3, 7, 31, 200, 5000]))
+        X[:, f] = np.round(rng.normal(size=N) * levels) / 8.0
+        X[rng.random(N) < 0.1, f] = 0.0
+    if cls:
+        C = int(rng.integers(2, 10))
+        y = rng.integers(0, C, size=N).astype(np.float64)
+    else:
+        y = rng.integers(-400, 400, size=N) / 16.0  # dyadic
+    P = int(rng.integers(1, 5))
+    cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
+    part = [0] + [int(c) for c in cuts] + [N]
+    params = dict(L=int(rng.integers(1, 7)), replacement=bool(rng.integers(0, 2)),
+                  ratio=float(rng.choice([1.0, 0.9, 0.63, 0.35])), depth=int(rng.integers(0, 10)),
+                  bins=int(rng.choice([2, 3, 8, 16, 32, 64])),
+                  min_inst=int(rng.choice([1, 1, 2, 7])),
+                  min_gain=float(rng.choice([0.0, 0.0, 0.01, 0.2])))
+    if not params["replacement"] and params["ratio"] == 1.0:
+        params["ratio"] = 0.8  # all-ones bags are covered elsewhere
+    return X, y, cls, part, params
+
+
+@pytest.mark.parametrize("seed", list(range(24)))
+def test_random_parity(ctx, seed):
+    X, y, cls, part, p = _case(1000 + seed)
+    sd = oracle.DEFAULT_SEED_CLASSIFIER if cls else oracle.DEFAULT_SEED_REGRESSOR
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        forest = nat.fit(ctx, ds, replacement=p["replacement"], sample_ratio=p["ratio"], seed=sd,
+                         learner_begin=0, learner_end=p["L"], partition_offsets=part,
+                         max_depth=p["depth"], max_bins=p["bins"],
+                         min_instances_per_node=p["min_inst"], min_info_gain=p["min_gain"],
+                         impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    except sb.SparkException:
+        # an empty bag: the oracle must agree that some learner drew no row
+        counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, len(y))
+        assert (counts.sum(axis=1) == 0).any()
+        return
+    except sb.IllegalArgumentException as e:
+        # mkSubspace drew no feature: VectorSlicer's requirement
+        assert "at least one feature" in str(e)
+        assert any(len(oracle.subspace(p["ratio"], X.shape[1], sd + i)) == 0 for i in range(p["L"]))
+        return
+    counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, len(y))
+    subs = [oracle.subspace(p["ratio"], X.shape[1], sd + i) for i in range(p["L"])]
+    orf = oracle_forest(X, y, counts, subs, p["depth"], p["bins"], cls, p["min_inst"], p["min_gain"])
+    assert_forest_equal(forest, orf)
+    agg = nat.AGG_MODE if cls else nat.AGG_MEAN
+    want = oracle.predict(orf, X, classification=cls)
+    np.testing.assert_array_equal(nat.predict(ctx, forest, X, agg), want)
+    np.testing.assert_array_equal(nat.predict_dataset(ctx, forest, ds, agg), want)
