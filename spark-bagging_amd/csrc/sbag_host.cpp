@@ -910,6 +910,17 @@ static void build_work(const std::vector<std::pair<int64_t, int64_t>>& segs, int
     run += len;
   }
   while (cur < w.nwg) w.wg[++cur] = np;
+  // a segment whose pieces all fall in one workgroup is flushed with plain stores
+  std::vector<int> wg_of(np);
+  for (int g = 0; g < w.nwg; g++)
+    for (int p = w.wg[g]; p < w.wg[g + 1]; p++) wg_of[p] = g;
+  for (int p0 = 0; p0 < np;) {
+    int p1 = p0;
+    while (p1 < np && w.pieces[p1].parent == w.pieces[p0].parent) p1++;
+    const int ex = wg_of[p0] == wg_of[p1 - 1] ? 1 : 0;
+    for (int p = p0; p < p1; p++) w.pieces[p].excl = ex;
+    p0 = p1;
+  }
   w.entries = (double)tot;
 }
 

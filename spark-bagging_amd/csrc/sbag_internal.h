@@ -16,7 +16,7 @@ __host__ __device__ inline uint64_t pack_entry(uint32_t row, int32_t k, uint32_t
 
 struct HistChunk {  // one workgroup: entries [a, b) of one parent segment
   int32_t parent;
-  int32_t pad;
+  int32_t excl;      // the whole segment lies in this workgroup's pieces: flush with stores
   int64_t a, b;
 };
 

@@ -672,7 +672,7 @@ static __host__ __device__ inline uint32_t hist_plane_bytes(int NB, int FPH, boo
 template <int MODE>
 __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned char* smem,
                                            uint32_t plane, int slot, int ft0, int ftn, int c0,
-                                           int nct) {
+                                           int nct, bool store) {
   const int tid = threadIdx.x;
   const int NB = A.NB, NS = A.NS, FPH = A.FPH;
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
@@ -682,7 +682,13 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
     for (int q = tid; q < ftn * NB * nct; q += blockDim.x) {
       const int cl = q % nct, b = (q / nct) % NB, f = q / (nct * NB);
       const uint32_t v = *(const uint32_t*)(smem + (size_t)cl * plane + ((size_t)b * FPH + f) * 4);
-      if (v) atomicAdd(&gh[((int64_t)(ft0 + f) * NB + b) * NS + c0 + cl], v);
+      if (v) {
+        uint32_t* dst = &gh[((int64_t)(ft0 + f) * NB + b) * NS + c0 + cl];
+        if (store)
+          *dst = v;
+        else
+          atomicAdd(dst, v);
+      }
     }
   } else {
     unsigned long long* gh = (unsigned long long*)A.hist + (int64_t)slot * slot_words;
@@ -696,8 +702,15 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
         if (MODE == kHistVar) {
           const uint64_t cnt = w >> cs;
           const int64_t sk = (int64_t)(w & MS) - (int64_t)A.K0 * (int64_t)cnt;
-          atomicAdd(&gh[gb], (unsigned long long)cnt);
-          atomicAdd(&gh[gb + 1], (unsigned long long)sk);
+          if (store) {
+            gh[gb] = (unsigned long long)cnt;
+            gh[gb + 1] = (unsigned long long)sk;
+          } else {
+            atomicAdd(&gh[gb], (unsigned long long)cnt);
+            atomicAdd(&gh[gb + 1], (unsigned long long)sk);
+          }
+        } else if (store) {
+          gh[gb + 2] = (unsigned long long)w;
         } else {
           atomicAdd(&gh[gb + 2], (unsigned long long)w);
         }
@@ -780,6 +793,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
 
   const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
   int cur_slot = -1, cur_ftn = 0, cur_r = -1;
+  bool cur_store = false;  // the current node run is this workgroup's alone and not yet flushed
   int64_t acc = 0;
   uint32_t posr[NJ], amul[NJ], abase[NJ];
 #pragma unroll
@@ -801,12 +815,14 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
     if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
-        hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct);
+        hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
         __syncthreads();
         for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
           *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
         __syncthreads();
       }
+      // a node split over several flushes by this workgroup adds from the second on
+      cur_store = (slot != cur_slot) && pc.excl != 0;
       cur_slot = slot;
       cur_ftn = ftn;
       acc = 0;
@@ -879,7 +895,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   }
   if (cur_slot >= 0) {
     __syncthreads();
-    hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct);
+    hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
   }
 }
 
