@@ -1311,6 +1311,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   int64_t bins_rstride = 0;
   const uint8_t* d_cols = nullptr;
   int64_t cols_rstride = 0, npad = 0;
+  const uint32_t* d_planes = nullptr;
+  int64_t plane_nw32 = 0;
+  int plane_nsp = 0;
   int32_t S;
   std::vector<int16_t> h_pos((size_t)R * Fmax, 0);
   {
@@ -1383,6 +1386,18 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     launch_transpose(c->stream, d_bins, N, S, ncol, d_c, npad, Rc, bins_rstride, cols_rstride);
     HIP_TRY(hipGetLastError());
     d_cols = d_c;
+    // side-bit planes (bin > s) of the shared bins for the partition's gather, when
+    // they fit in 8 GB (NB - 1 planes of N/8 bytes per column)
+    plane_nw32 = (N + 31) / 32;
+    plane_nsp = NB - 1;
+    if (bins_rstride == 0 && plane_nsp >= 1 &&
+        (double)ncol * plane_nsp * plane_nw32 * 4 <= 8.0 * (1ull << 30) && !getenv("SBAG_NO_PLANES")) {
+      uint32_t* d_pl;
+      TRY(ws_typed(c, "planes", (size_t)ncol * plane_nsp * plane_nw32, &d_pl));
+      launch_planes(c->stream, d_c, npad, ncol, plane_nsp, plane_nw32, d_pl);
+      HIP_TRY(hipGetLastError());
+      d_planes = d_pl;
+    }
     tm.end(h);
   }
   int32_t* d_nbins;
@@ -1620,13 +1635,19 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       // concurrent workgroups spread over the group's cursors while the GPU reads
       // one column
       const int64_t piece = 8192;
+      // the gathered object: a side-bit plane (column, split) once parents are many (with
+      // few parents, finer groups would crowd the workgroups onto fewer cursors), else a
+      // column byte array
+      const bool lvl_planes = d_planes != nullptr && NP >= 1024;
       auto colkey = [&](int q) {
+        if (lvl_planes) return (int64_t)par[q].pos * plane_nsp + par[q].s;
         return (bins_rstride ? (int64_t)par[q].r * 65536 : 0) + (int64_t)par[q].pos;
       };
       // counting sort of the parents by column (pos < 65536; per replica when bins are)
       std::vector<int32_t> order(NP);
       {
-        const int64_t nkeys = bins_rstride ? (int64_t)R * 65536 : 65536;
+        int64_t nkeys = 1;
+        for (int q = 0; q < NP; q++) nkeys = std::max<int64_t>(nkeys, colkey(q) + 1);
         std::vector<int32_t> start;
         if (nkeys <= ((int64_t)1 << 24)) {
           start.assign((size_t)nkeys + 1, 0);
@@ -1692,6 +1713,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       pa.cols = d_cols;
       pa.cols_rstride = cols_rstride;
       pa.npad = npad;
+      pa.planes = lvl_planes ? d_planes : nullptr;
+      pa.nw32 = plane_nw32;
+      pa.nsp = plane_nsp;
       pa.pieces = d_pp;
       pa.npieces = npieces;
       pa.counter = d_ctr;

@@ -74,6 +74,10 @@ struct PartArgs {
   const uint8_t* cols;   // column-major bins [R?][C][npad] (k_transpose)
   int64_t cols_rstride;  // bytes between replica copies (0: shared)
   int64_t npad;          // column stride (rows rounded up to 64)
+  const uint32_t* planes;   // [ncol][nsp][nw32] side bits (bin > s) of shared bins, or NULL
+  int64_t nw32;             // words per plane = ceil(N / 32)
+  int32_t nsp;              // planes per column (maxBins - 1)
+  int32_t pad2;
   const PartPiece* pieces;  // work order: split-column groups, parents interleaved
   int64_t npieces;
   unsigned long long* counter;  // dynamic piece counter (zeroed before the launch)
@@ -162,6 +166,8 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mod
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini);
 size_t hist_stage_bytes();
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg);
+void launch_planes(hipStream_t st, const uint8_t* cols, int64_t npad, int ncol, int nsp, int64_t nw32,
+                   uint32_t* planes);
 void launch_part_pieces(hipStream_t st, const PartRound* rounds, int nrounds, int64_t npieces,
                         const int32_t* order, const int64_t* seg, int64_t piece, PartPiece* out);
 void launch_transpose(hipStream_t st, const uint8_t* src, int64_t N, int S, int C, uint8_t* dst,

@@ -948,6 +948,7 @@ constexpr int kPartThreads = 256;
 constexpr int kPartWaves = kPartThreads / 64;
 constexpr int kPartK = 8;
 
+template <bool PLANES>
 __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -970,6 +971,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
     if (q < 0) break;
     const ParentInfo pi = A.parents[q];
     const uint8_t* col = A.cols + (int64_t)pi.r * A.cols_rstride + (int64_t)pi.pos * A.npad;
+    const uint32_t* plane = PLANES ? A.planes + ((int64_t)pi.pos * A.nsp + pi.s) * A.nw32 : nullptr;
     const uint32_t split = (uint32_t)pi.s;
     const bool wlp = pi.write_l != 0, wrp = pi.write_r != 0;
     unsigned long long* cur = A.cursors + 2 * (int64_t)q;
@@ -984,13 +986,21 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         e[k] = i < pb ? A.ent_in[i] : 0ull;
       }
 #pragma unroll
-      for (int k = 0; k < kPartK; k++) byte[k] = col[(uint32_t)e[k]];
+      for (int k = 0; k < kPartK; k++) {
+        // 1 = goes right (bin > split): one bit of an L2-sized plane, or the column byte
+        if (PLANES) {
+          const uint32_t row = (uint32_t)e[k];
+          byte[k] = (plane[row >> 5] >> (row & 31u)) & 1u;
+        } else {
+          byte[k] = col[(uint32_t)e[k]] > split ? 1u : 0u;
+        }
+      }
       uint64_t ml[kPartK], mr[kPartK];
       int nl = 0, nr = 0;
 #pragma unroll
       for (int k = 0; k < kPartK; k++) {
         const bool valid = base + k * 64 + lane < pb;
-        const bool right = byte[k] > split;
+        const bool right = byte[k] != 0u;
         ml[k] = __ballot(valid && !right && wlp);
         mr[k] = __ballot(valid && right && wrp);
         nl += __popcll(ml[k]);
@@ -1001,7 +1011,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
 #pragma unroll
         for (int k = 0; k < kPartK; k++) {
           const bool valid = base + k * 64 + lane < pb;
-          if (valid && byte[k] <= split) {
+          if (valid && byte[k] == 0u) {
             const int32_t hi = (int32_t)(e[k] >> 32);
             const int64_t kk = hi >> 8;
             sq += (unsigned long long)(hi & 0xff) * (unsigned long long)(kk * kk);
@@ -1112,8 +1122,57 @@ void launch_part_pieces(hipStream_t st, const PartRound* rounds, int nrounds, in
                      rounds, nrounds, npieces, order, seg, piece, out);
 }
 
+// side-bit planes of the shared bins for k_partition: bit (row & 31) of word
+// row >> 5 of plane (f, s) = bins[row][f] > s.  A plane is N/8 bytes (1.25 MB for C3),
+// small enough for an XCD's L2 while the whole GPU routes the nodes split at (f, s).
+__global__ __launch_bounds__(256) void k_planes(const uint8_t* __restrict__ cols, int64_t npad,
+                                                int nsp, int64_t nw32, uint32_t* __restrict__ planes) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int f = blockIdx.y;
+  if (w >= nw32) return;
+  const uint32_t* src = (const uint32_t*)(cols + (int64_t)f * npad + w * 32);
+  uint32_t v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = src[i];
+  uint32_t* dst = planes + (int64_t)f * nsp * nw32 + w;
+  if (nsp <= 127) {
+    // bins < 128: per 4 bytes, (b | 0x80) - (s + 1) keeps bit 7 iff b > s; the four
+    // bit-7s are gathered into a nibble with one multiply (no carries collide)
+    for (int sp = 0; sp < nsp; sp++) {
+      const uint32_t sub = (uint32_t)(sp + 1) * 0x01010101u;
+      uint32_t word = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint32_t t = (((v[i] | 0x80808080u) - sub) & 0x80808080u) >> 7;
+        word |= ((t * 0x00204081u) >> 21 & 0xfu) << (4 * i);
+      }
+      dst[(int64_t)sp * nw32] = word;
+    }
+    return;
+  }
+  for (int sp = 0; sp < nsp; sp++) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+      const uint32_t b = (v[i >> 2] >> ((i & 3) * 8)) & 0xffu;
+      word |= (b > (uint32_t)sp ? 1u : 0u) << i;
+    }
+    dst[(int64_t)sp * nw32] = word;
+  }
+}
+
+void launch_planes(hipStream_t st, const uint8_t* cols, int64_t npad, int ncol, int nsp, int64_t nw32,
+                   uint32_t* planes) {
+  if (ncol <= 0 || nsp <= 0) return;
+  const dim3 grid((unsigned)((nw32 + 255) / 256), (unsigned)ncol);
+  hipLaunchKernelGGL(k_planes, grid, dim3(256), 0, st, cols, npad, nsp, nw32, planes);
+}
+
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg) {
-  hipLaunchKernelGGL(k_partition, dim3((unsigned)nwg), dim3(kPartThreads), 0, st, a);
+  if (a.planes)
+    hipLaunchKernelGGL(k_partition<true>, dim3((unsigned)nwg), dim3(kPartThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_partition<false>, dim3((unsigned)nwg), dim3(kPartThreads), 0, st, a);
 }
 
 // ======================================================================
