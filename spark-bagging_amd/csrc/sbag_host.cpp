@@ -72,12 +72,13 @@ static int ws_get(sbag_ctx* c, const std::string& name, size_t bytes, void** out
     if (b.p) HIP_TRY(hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
-    size_t want = bytes + bytes / 8;
+    // 256 bytes of slack past every buffer: row-wise kernels may over-read the last row
+    size_t want = bytes + bytes / 8 + 256;
     hipError_t e = hipMalloc(&b.p, want);
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      e = hipMalloc(&b.p, bytes);
-      want = bytes;
+      want = bytes + 256;
+      e = hipMalloc(&b.p, want);
     }
     if (e != hipSuccess) {
       (void)hipGetLastError();
@@ -708,7 +709,8 @@ int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, cons
     return fail(SBAG_EUNSUPPORTED, "a feature has more than 65536 distinct values");
   ds->code_bytes = maxd <= 256 ? 1 : 2;
   const size_t bytes = (size_t)N * ds->S * ds->code_bytes;
-  HIP_TRY(hipMalloc(&ds->d_codes, bytes));
+  HIP_TRY(hipMalloc(&ds->d_codes, bytes + 256));  // zero slack: k_hist_rl over-reads rows
+  HIP_TRY(hipMemset((uint8_t*)ds->d_codes + bytes, 0, 256));
   {
     std::vector<uint8_t> buf(bytes, 0);
     for (int f = 0; f < F; f++) {
@@ -749,7 +751,8 @@ int sbag_dataset_synthetic(sbag_ctx* c, int64_t N, int32_t F, uint64_t seed, int
   for (int f = 0; f < F; f++)
     for (int v = 0; v < 32; v++) ds->dict[f][v] = (double)v;
   ds->zero_code.assign(F, 0);
-  HIP_TRY(hipMalloc(&ds->d_codes, (size_t)N * ds->S));
+  HIP_TRY(hipMalloc(&ds->d_codes, (size_t)N * ds->S + 256));
+  HIP_TRY(hipMemset((uint8_t*)ds->d_codes + (size_t)N * ds->S, 0, 256));
   HIP_TRY(hipMalloc(&ds->d_labk, (size_t)N * 4));
   launch_synth(c->stream, (uint8_t*)ds->d_codes, ds->S, N, F, seed, num_classes, ds->d_labk);
   HIP_TRY(hipGetLastError());
@@ -820,6 +823,7 @@ int sbag_dataset_free(sbag_dataset* ds) {
 // ---------------------------------------------------------------- fit
 struct HistGeom {
   int T, FT, FPH, ntf, CT, ntiles;
+  int rl;  // row-lane kernel (k_hist_rl)
   size_t lds;
 };
 
@@ -830,7 +834,8 @@ static int roundup(int x, int a) { return (x + a - 1) / a * a; }
 // Many classes (BASELINE config 5: 64) are split into class tiles first: a class
 // tile re-reads the 8-byte entries but loads the row bytes of its own entries only,
 // whereas a feature tile re-reads every row.
-static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g) {
+static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g,
+                          int rl_mode = 0) {
   (void)S;
   g.T = 64;  // piece granularity (entries)
   const int align = gini_layout ? 32 : 16;
@@ -874,6 +879,15 @@ static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, His
   g.ntf = (Fmax + g.FT - 1) / g.FT;
   g.ntiles = g.ntf * ((gini_layout ? (NS + ct - 1) / ct : 1));
   g.lds = lds_for(g.FT, ct);
+  g.rl = 0;
+  // row lanes when they carry fewer dump lanes than 64-feature lane groups
+  if (rl_mode && roundup(g.FT, hist_rl_lanes()) < roundup(g.FT, 64)) {
+    const size_t b = hist_rl_lds_bytes(NB, ct, g.FPH, gini_layout);
+    if (b <= hard) {
+      g.rl = rl_mode;
+      g.lds = b;
+    }
+  }
   return true;
 }
 
@@ -1052,6 +1066,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     const int cbits = 64 - cshift;
     if (cbits >= 1 && std::ldexp(1.0, cbits) > wmax && wmax * kabs * kabs < 1.8e19) break;
   }
+  // the row-lane histogram builds the word as (c << cshift) + c*(k + K0) with a 32-bit
+  // low half: raise cshift to 32 when the count field keeps room for flush_limit * cmax
+  if (!gini && cshift < 32 && (double)flush_limit * cmax < 4294967296.0) cshift = 32;
   if (!gini && (double)N * cmax * kabs * kabs >= std::ldexp(1.0, 53))
     return fail(SBAG_EUNSUPPORTED, "sum of squared labels would exceed 2^53 (not exact in fp64)");
 
@@ -1135,6 +1152,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     ha.FPH = g.FPH;
     ha.CT = g.CT;
     ha.ntf = g.ntf;
+    ha.rl = g.rl;
     int h = tm.begin(cat);
     launch_hist(c->stream, ha, work.nwg, g.ntiles, mode, g.lds);
     HIP_TRY(hipGetLastError());
@@ -1353,6 +1371,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_lut,
                          d_lutoff, d_b, S);
       HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemsetAsync(d_b + (size_t)N * S, 0, 256, c->stream));  // zero slack
       d_bins = d_b;
       h_pos = h_pos_codes;
     } else {
@@ -1369,6 +1388,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
                          d_lut, d_lutoff, d_b, S);
       HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemsetAsync(d_b + (size_t)R * N * S, 0, 256, c->stream));  // zero slack
       d_bins = d_b;
       bins_rstride = (int64_t)N * S;
       for (int r = 0; r < R; r++)
@@ -1409,7 +1429,19 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   hmark(12);
   // ---- 6. level-wise growth
   HistGeom g;
-  if (!hist_geometry(S, Fmax, NB, NS, gini, g))
+  // row-lane histogram: identity byte layout, packed variance words with cshift >= 32
+  // (SBAG_HIST_RL: 0 = never, 1 = always 64-bit row addresses; tests pin both paths)
+  const int rl_env = getenv("SBAG_HIST_RL") ? atoi(getenv("SBAG_HIST_RL")) : -1;
+  bool rl_ok = rl_env != 0 && (gini || cshift >= 32);
+  for (int r = 0; r < R && rl_ok; r++)
+    for (int fl = 0; fl < h_Fr[r]; fl++)
+      if (h_pos[(size_t)r * Fmax + fl] != fl) {
+        rl_ok = false;
+        break;
+      }
+  const int rl_mode = !rl_ok ? 0
+                      : (rl_env != 1 && N < (1 << 24) && (double)N * S + S < 4294967296.0) ? 2 : 1;
+  if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode))
     return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
   const int64_t slot_words = (int64_t)Fmax * NB * NS;
   std::vector<std::vector<HNode>> trees(R);

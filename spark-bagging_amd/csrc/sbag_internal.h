@@ -53,7 +53,7 @@ struct HistArgs {
   int32_t count_only;    // gini layout with the label ignored (value counts)
   int32_t CT;            // gini: classes per class tile (LDS holds CT class planes)
   int32_t ntf;           // feature tiles; blockIdx.y = class_tile * ntf + feature_tile
-  int32_t pad;
+  int32_t rl;            // k_hist_rl (identity byte layout): 1 = 64-bit row addresses, 2 = 32-bit
 };
 
 // k_partition: entries of each split node -> left block (from the segment start,
@@ -165,6 +165,8 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mod
                  size_t lds_bytes);
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini);
 size_t hist_stage_bytes();
+size_t hist_rl_lds_bytes(int NB, int CT, int FPH, bool gini);
+int hist_rl_lanes();
 void launch_partition(hipStream_t st, const PartArgs& a, int nwg);
 void launch_planes(hipStream_t st, const uint8_t* cols, int64_t npad, int ncol, int nsp, int64_t nw32,
                    uint32_t* planes);

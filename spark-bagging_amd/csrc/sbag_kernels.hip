@@ -899,6 +899,276 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   }
 }
 
+// ----------------------------------------------------------------------
+// k_hist_rl: the row-lane layout, for feature tiles that would leave lane groups
+// idle (F = 100 fills 100 of k_hist's 128 lanes).  kRlG lanes share an entry and
+// 64 / kRlG entries share a wave-instruction; lane (e, s) adds features
+// [s*K, s*K + K) of entry e, K = ceil(FT / kRlG), so one wave-instruction carries
+// roundup(FT, 16) useful-or-dump lanes per 4 entries instead of roundup(FT, 64) per
+// entry (F = 100: 112 vs 128 LDS atomics per 4 entries).  Four lanes share a
+// feature in each instruction; at 4 the bank conflicts of skewed bins stay at
+// k_hist's level (scripts/micro/lds_rl.hip; 8 or 16 lanes per feature double them).
+// A lane reads its K bytes with aligned dword loads realigned by v_alignbyte.
+// Lanes past the tile add into the LDS row's pad columns [ftn, FPH), which the flush
+// never reads: they read row padding or the next features' bins, all < NB (row
+// padding and the buffers' slack are zero).  Requires the identity byte layout
+// (pos[r][f] = f) and, for variance, cshift >= 32.
+// ----------------------------------------------------------------------
+constexpr int kRlG = 16;                 // lanes per entry
+constexpr int kRlEP = 64 / kRlG;         // entries per wave-instruction
+
+// raw dwords covering a lane's byte range [off, off + K) of one row (the buffers
+// carry >= 64 bytes of slack, so the last row's over-read stays in bounds)
+template <int K>
+struct RlRaw {
+  static constexpr int KW = (K + 3) / 4;
+  uint32_t d[KW + 1];
+};
+
+// OFF32: rows * S < 2^32 and rows < 2^24, so the row offset is one v_mad_u32_u24 off an
+// SGPR base; otherwise a 64-bit address per lane
+template <int K, bool OFF32>
+__device__ __forceinline__ void rl_load(const uint8_t* __restrict__ binsr, uint32_t loff,
+                                        uint32_t S, uint32_t row, RlRaw<K>& r) {
+  const uint32_t* p = OFF32 ? (const uint32_t*)(binsr + (uint32_t)(__umul24(row, S) + loff))
+                            : (const uint32_t*)(binsr + (size_t)row * S + loff);
+#pragma unroll
+  for (int d = 0; d <= RlRaw<K>::KW; d++) r.d[d] = p[d];
+}
+
+// one pass: K LDS atomics of the lane's entry (weights wl/wh, LDS base lb)
+template <int MODE, int K>
+__device__ __forceinline__ void rl_add(unsigned char* smem, const RlRaw<K>& r, uint32_t sh,
+                                       uint32_t amul, uint32_t lb, uint32_t wl, uint32_t wh) {
+  constexpr int KW = RlRaw<K>::KW;
+  constexpr uint32_t WB = MODE == kHistGini ? 4u : 8u;
+  uint32_t w[KW];
+#pragma unroll
+  for (int q = 0; q < KW; q++) w[q] = __builtin_amdgcn_alignbyte(r.d[q + 1], r.d[q], sh);
+  const unsigned long long a64 = ((unsigned long long)wh << 32) | wl;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    const uint32_t bin = __builtin_amdgcn_ubfe(w[j >> 2], 8 * (j & 3), 8);
+    const uint32_t addr = __umul24(bin, amul) + lb + (uint32_t)j * WB;
+    if (MODE == kHistGini)
+      atomicAdd((uint32_t*)(smem + addr), wl);
+    else
+      atomicAdd((unsigned long long*)(smem + addr), a64);
+  }
+}
+
+// stat words of one entry: u64 modes add (wh:wl); gini adds the count wl into its class
+// plane (lb offset).  Variance: (c << cshift) + c*(k + K0) with cshift >= 32 and
+// c*(k + K0) < 2^32, i.e. wh = c << (cshift - 32), wl = c*(k + K0).
+template <int MODE>
+__device__ __forceinline__ void rl_words(uint64_t e, int csh, int32_t K0, int c0, uint32_t cstride,
+                                         uint32_t& wl, uint32_t& wh, uint32_t& lb) {
+  const int32_t hi = (int32_t)(e >> 32);
+  const uint32_t c = (uint32_t)hi & 0xffu;
+  const int32_t k = hi >> 8;
+  if (MODE == kHistGini) {
+    wl = c;
+    wh = 0;
+    lb += c ? (uint32_t)(k - c0) * cstride : 0u;
+  } else if (MODE == kHistVar) {
+    wl = __umul24(c, (uint32_t)(k + K0));
+    wh = c << csh;
+  } else {
+    const uint64_t w = (uint64_t)c * (uint64_t)((int64_t)k * (int64_t)k);
+    wl = (uint32_t)w;
+    wh = (uint32_t)(w >> 32);
+  }
+}
+
+struct RlLane {  // per-lane constants of the current (replica, tile)
+  const uint8_t* binsr;  // bins of the replica (wave-uniform)
+  uint32_t loff;         // off & ~3: the lane's first aligned byte in a row
+  uint32_t sh;           // off & 3
+  uint32_t lb;           // LDS byte offset of feature s*K
+};
+
+// one batch of n <= 64 entries (16 passes of 4 entries), row bytes two passes ahead and
+// entries three passes ahead.  FULL: n == 64 from global memory, no bounds checks.
+// src: the batch's entries, global (ent_in + q0) or the wave's LDS stage.
+template <int MODE, int K, bool OFF32, bool FULL>
+__device__ __forceinline__ void rl_batch(unsigned char* smem, const uint64_t* src, int n,
+                                         int eo, const RlLane& L, uint32_t S, uint32_t amul,
+                                         int csh, int32_t K0, int c0, uint32_t cstride) {
+  const int npass = FULL ? 16 : (n + kRlEP - 1) / kRlEP;
+  auto fetch = [&](int t) -> uint64_t {
+    const int i = t * kRlEP + eo;
+    if (FULL) return src[i];
+    return i < n ? src[i] : 0ull;
+  };
+  // rows two passes ahead, entries three
+  uint64_t e0 = fetch(0), e1 = 0, e2 = 0, e3 = 0;
+  if (FULL || 1 < npass) e1 = fetch(1);
+  if (FULL || 2 < npass) e2 = fetch(2);
+  RlRaw<K> r0, r1, r2;
+  rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)e0, r0);
+  if (FULL || 1 < npass) rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)e1, r1);
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    if (!FULL && t >= npass) break;
+    if (FULL ? t + 3 < 16 : t + 3 < npass) e3 = fetch(t + 3);
+    if (FULL ? t + 2 < 16 : t + 2 < npass) rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)e2, r2);
+    uint32_t wl, wh, lb = L.lb;
+    rl_words<MODE>(e0, csh, K0, c0, cstride, wl, wh, lb);
+    rl_add<MODE, K>(smem, r0, L.sh, amul, lb, wl, wh);
+    e0 = e1;
+    e1 = e2;
+    e2 = e3;
+    r0 = r1;
+    r1 = r2;
+  }
+}
+
+template <int MODE, int K, bool OFF32>
+__global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr bool GINI = MODE == kHistGini;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s = lane % kRlG, eo = lane / kRlG;
+  const int NB = A.NB, FPH = A.FPH;
+  const uint32_t S = (uint32_t)A.S;
+  const int ft0 = (int)(blockIdx.y % (unsigned)A.ntf) * A.FT;
+  const int c0 = GINI ? (int)(blockIdx.y / (unsigned)A.ntf) * A.CT : 0;
+  const int nct = GINI ? min(A.CT, A.NS - c0) : 1;
+  const bool ctile = GINI && A.CT < A.NS;
+  constexpr uint32_t WB = GINI ? 4u : 8u;
+  const uint32_t plane = hist_plane_bytes(NB, FPH, GINI);
+  const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.CT : 1u);
+  uint64_t* stage = (uint64_t*)(smem + hist_bytes) + wave * 64;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  const uint32_t amul = (uint32_t)FPH * WB;
+  const int csh = A.cshift - 32;
+  const int32_t K0 = A.K0;
+
+  for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
+    *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+
+  const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
+  int cur_slot = -1, cur_ftn = 0, cur_ftn_lane = -1;
+  bool cur_store = false;
+  int64_t acc = 0;
+  // this lane's byte range of the tile: [off, off + K)
+  RlLane L{A.bins, 0u, 0u, (uint32_t)(s * K) * WB};
+  __syncthreads();
+
+  for (int p = p0; p < p1; p++) {
+    const HistChunk pc = A.chunks[p];
+    const ParentInfo pi = A.parents[pc.parent];
+    const int r = pi.r;
+    const int ftn = min(A.FT, A.Fr[r] - ft0);
+    const int slot = pi.hist_slot;
+    if (ftn <= 0 || slot < 0) continue;
+    const int64_t a = pc.a, b = pc.b;
+    if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
+      if (cur_slot >= 0) {
+        __syncthreads();
+        hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
+        __syncthreads();
+        for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
+          *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+      }
+      cur_store = (slot != cur_slot) && pc.excl != 0;
+      cur_slot = slot;
+      cur_ftn = ftn;
+      acc = 0;
+    }
+    acc += b - a;
+    if (ftn != cur_ftn_lane) {
+      // lanes wholly past the tile read its first bytes (into pad columns)
+      const uint32_t off = (uint32_t)(ft0 + (s * K < ftn ? s * K : 0));
+      L.loff = off & ~3u;
+      L.sh = off & 3u;
+      cur_ftn_lane = ftn;
+    }
+    L.binsr = A.bins + (int64_t)r * A.bins_rstride;
+    for (int64_t q0 = a + (int64_t)wave * 64; q0 < b; q0 += (int64_t)kHistWaves * 64) {
+      const int n = (int)min((int64_t)64, b - q0);
+      if (ctile) {  // keep the batch entries of classes [c0, c0 + nct), packed to the front
+        const uint64_t e = (lane < n) ? A.ent_in[q0 + lane] : 0ull;
+        const int32_t eh = (int32_t)(e >> 32);
+        const int kc = eh >> 8;
+        const bool m = ((eh & 0xff) != 0) && kc >= c0 && kc < c0 + nct;
+        const uint64_t mask = __ballot(m);
+        const int nm = __popcll(mask);
+        __builtin_amdgcn_wave_barrier();
+        if (m) stage[__popcll(mask & lt_mask)] = e;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (nm > 0)
+          rl_batch<MODE, K, OFF32, false>(smem, stage, nm, eo, L, S, amul, csh, K0, c0, plane);
+        __builtin_amdgcn_wave_barrier();
+      } else if (n == 64) {
+        rl_batch<MODE, K, OFF32, true>(smem, A.ent_in + q0, 64, eo, L, S, amul, csh, K0, c0, plane);
+      } else {
+        rl_batch<MODE, K, OFF32, false>(smem, A.ent_in + q0, n, eo, L, S, amul, csh, K0, c0, plane);
+      }
+    }
+  }
+  if (cur_slot >= 0) {
+    __syncthreads();
+    hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
+  }
+}
+
+template <int K, bool OFF32>
+static void launch_hist_rl_ko(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (const void* f : {(const void*)k_hist_rl<kHistGini, K, OFF32>,
+                          (const void*)k_hist_rl<kHistVar, K, OFF32>,
+                          (const void*)k_hist_rl<kHistSq, K, OFF32>})
+      HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  if (mode == kHistGini)
+    hipLaunchKernelGGL((k_hist_rl<kHistGini, K, OFF32>), grid, dim3(kHistThreads), lds, st, a);
+  else if (mode == kHistVar)
+    hipLaunchKernelGGL((k_hist_rl<kHistVar, K, OFF32>), grid, dim3(kHistThreads), lds, st, a);
+  else
+    hipLaunchKernelGGL((k_hist_rl<kHistSq, K, OFF32>), grid, dim3(kHistThreads), lds, st, a);
+}
+
+template <int K>
+static void launch_hist_rl_k(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
+  if (a.rl == 2)
+    launch_hist_rl_ko<K, true>(st, a, grid, lds, mode);
+  else
+    launch_hist_rl_ko<K, false>(st, a, grid, lds, mode);
+}
+
+static void launch_hist_rl(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
+  switch ((a.FT + kRlG - 1) / kRlG) {
+    case 1: launch_hist_rl_k<1>(st, a, grid, lds, mode); break;
+    case 2: launch_hist_rl_k<2>(st, a, grid, lds, mode); break;
+    case 3: launch_hist_rl_k<3>(st, a, grid, lds, mode); break;
+    case 4: launch_hist_rl_k<4>(st, a, grid, lds, mode); break;
+    case 5: launch_hist_rl_k<5>(st, a, grid, lds, mode); break;
+    case 6: launch_hist_rl_k<6>(st, a, grid, lds, mode); break;
+    case 7: launch_hist_rl_k<7>(st, a, grid, lds, mode); break;
+    case 8: launch_hist_rl_k<8>(st, a, grid, lds, mode); break;
+    case 9: launch_hist_rl_k<9>(st, a, grid, lds, mode); break;
+    case 10: launch_hist_rl_k<10>(st, a, grid, lds, mode); break;
+    case 11: launch_hist_rl_k<11>(st, a, grid, lds, mode); break;
+    case 12: launch_hist_rl_k<12>(st, a, grid, lds, mode); break;
+    case 13: launch_hist_rl_k<13>(st, a, grid, lds, mode); break;
+    case 14: launch_hist_rl_k<14>(st, a, grid, lds, mode); break;
+    case 15: launch_hist_rl_k<15>(st, a, grid, lds, mode); break;
+    default: launch_hist_rl_k<16>(st, a, grid, lds, mode); break;
+  }
+}
+
+size_t hist_rl_lds_bytes(int NB, int CT, int FPH, bool gini) {
+  return (size_t)hist_plane_bytes(NB, FPH, gini) * (gini ? (size_t)CT : 1u) +
+         (size_t)kHistWaves * 64 * 8;
+}
+int hist_rl_lanes() { return kRlG; }
+
 size_t hist_lds_bytes(int NB, int NS, int FPH, bool gini) {
   return (size_t)hist_plane_bytes(NB, FPH, gini) * (gini ? (size_t)NS : 1u);
 }
@@ -928,6 +1198,10 @@ static void launch_hist_m(hipStream_t st, const HistArgs& a, dim3 grid, size_t l
 void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mode,
                  size_t lds_bytes) {
   const dim3 grid((unsigned)nwg, (unsigned)ntiles);
+  if (a.rl) {
+    launch_hist_rl(st, a, grid, lds_bytes, mode);
+    return;
+  }
   if (mode == kHistGini)
     launch_hist_m<kHistGini>(st, a, grid, lds_bytes);
   else if (mode == kHistVar)

@@ -248,3 +248,28 @@ def test_wide_rows_four_lane_groups(ctx):
     assert_forest_equal(forest, orf)
     np.testing.assert_array_equal(nat.predict_dataset(ctx, forest, ds, nat.AGG_MEAN),
                                   oracle.predict(orf, X))
+
+
+@pytest.mark.parametrize("rl", ["0", "1", "auto"])
+def test_row_lane_histogram_modes(ctx, cpusmall, monkeypatch, rl):
+    """k_hist_rl (16 lanes per entry, 4 entries per LDS atomic) against k_hist: off,
+    forced 64-bit row addresses, and the automatic choice (32-bit offsets here), on
+    variance (with the exact-tie Sq fallback), gini and a 100-feature tail tile."""
+    if rl != "auto":
+        monkeypatch.setenv("SBAG_HIST_RL", rl)
+    X, y = cpusmall
+    X2 = np.ascontiguousarray(np.concatenate([X, X[:, :3]], axis=1))
+    forest, orf, _ = _fit_both(ctx, X2, y, 3, replacement=True, ratio=1.0, seed=SEED_REG,
+                               depth=6, bins=32, cls=False)
+    assert forest.timing()["exact_fallbacks"] > 0
+    assert_forest_equal(forest, orf)
+    ds, Xs, forest, orf = _synthetic_cls(ctx, 12000, 100, 9, 3, 8, seed_data=29, ratio=1.0,
+                                         replacement=True)
+    assert_forest_equal(forest, orf)
+    ds = nat.DeviceDataset.synthetic(16000, 100, seed=31, num_classes=0, ctx=ctx)
+    Xr, yr = ds.features(), ds.labels()
+    forest = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                     learner_end=3, max_depth=7, max_bins=32)
+    counts = oracle.bag(True, 1.0, 0, 3, SEED_REG, [0, 16000], 16000)
+    subs = [oracle.subspace(1.0, 100, SEED_REG + i) for i in range(3)]
+    assert_forest_equal(forest, oracle_forest(Xr, yr, counts, subs, 7, 32, False))
