@@ -63,6 +63,19 @@ WORKLOADS = {
 }
 
 
+def hist_kernel_name(F, cls, N):
+    """The k_hist variant the host picks for an F-feature tile (sbag_host.cpp
+    hist_geometry): row lanes when roundup(F, 16) < roundup(F, 64)."""
+    ft = min(F, 256)
+    mode = "0" if cls else "1"
+    tag = "kHistGini, class tiles" if cls else "kHistVar"
+    if -(-ft // 16) * 16 < -(-ft // 64) * 64:
+        k = -(-ft // 16)
+        off32 = "true" if N < (1 << 24) else "false"
+        return f"sbag::k_hist_rl<{mode}, {k}, {off32}> ({tag}, row lanes)"
+    return f"sbag::k_hist<{mode}, {-(-ft // 64)}> ({tag}, {-(-ft // 64)} lane groups)"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,19 +179,17 @@ def main():
     hist_launches = sum(t["hist_launches"] for t in timings)
     work_bytes = sum(t["hist_work_bytes"] for t in timings)
     read_bytes = sum(t["hist_alg_bytes"] for t in timings)
-    entries = sum(t["hist_entries"] for t in timings)
     nl = max(hist_launches, 1)
     avg_s = hist_ms / 1e3 / nl
     achieved = work_bytes / nl / avg_s / 1e9 if hist_ms > 0 else 0.0
-    # LDS atomic co-limiter: one atomic per entry and 64-feature lane group (variance:
-    # ds_add_u64 of (count, sum) after the screening of DESIGN.md §5; gini: ds_add_u32)
-    lds_instr = entries * ((F + 63) // 64)
+    # LDS atomic co-limiter, counted by the host per launch (variance: ds_add_u64 of the
+    # packed (count, sum) word after the screening of DESIGN.md §5; gini: ds_add_u32)
+    lds_instr = sum(t["hist_lds_atomics"] for t in timings)
     lds_rate = lds_instr / (hist_ms / 1e3) if hist_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic() if args.workload == "c3" else None,
-                "kernel": ("sbag::k_hist<0, NJ> (kHistGini, class tiles)" if cls else
-                           "sbag::k_hist<1, 2> (kHistVar, 2 lane groups)"),
+                "kernel": hist_kernel_name(F, cls, N),
                 "avg_launch_ms": round(hist_ms / nl, 4),
                 "alg_bytes_per_launch": round(work_bytes / nl),
                 "alg_bytes_def": "SURVEY 8d: sum over histograms built (read or by subtraction) of "

@@ -153,6 +153,7 @@ typedef struct {
                               whose histogram exists (read or obtained by subtraction) */
   double fix_ms;           /* exact-split fallback of screened variance nodes */
   int64_t exact_fallbacks; /* nodes that needed it                                      */
+  double hist_lds_atomics; /* LDS atomic wave-instructions issued by the hist launches   */
 } sbag_timing;
 int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
 

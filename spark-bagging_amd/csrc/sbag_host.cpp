@@ -1126,7 +1126,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   ha.K0 = (int32_t)K0;
   ha.cshift = cshift;
   ha.flush_limit = flush_limit;
-  double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0, hist_work = 0;
+  double hist_entries = 0, hist_alg_bytes = 0, hist_upper = 0, hist_work = 0, hist_lds = 0;
   const int s_y = gini ? 1 : 4;  // label bytes per row in SURVEY 8d (u8 class / fp32 label)
   // SURVEY §8d work bytes of the histograms of a set of node segments
   auto add_work = [&](const std::vector<std::pair<int64_t, int64_t>>& segs,
@@ -1159,9 +1159,15 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     tm.end(h);
     if (cat == T_HIST) {
       hist_launches++;
+      // LDS atomic wave-instructions per entry: per feature tile, k_hist one per 64-lane
+      // group, k_hist_rl K/4 (16 lanes of K features per entry, 4 entries per instruction)
+      const double per_entry =
+          g.ntf * (g.rl ? (double)((g.FT + hist_rl_lanes() - 1) / hist_rl_lanes()) * hist_rl_lanes() / 64.0
+                        : (double)((g.FT + 63) / 64));
       for (size_t q = 0; q < segs.size(); q++) {
         const double ne = (double)(segs[q].second - segs[q].first);
         hist_entries += ne;
+        hist_lds += ne * per_entry;
         hist_alg_bytes += ne * (h_Fr[par[q].r] + s_y);
       }
     }
@@ -1183,10 +1189,20 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   TRY(h2d(c, d_pos, h_pos_codes.data(), h_pos_codes.size()));
   std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1), 0);
   const bool optimistic = ds->code_bytes == 1 && ncmax <= tp.max_bins;
+  // row-lane histogram: identity byte layout, packed variance words with cshift >= 32
+  // (SBAG_HIST_RL: 0 = never, 1 = always 64-bit row addresses; tests pin both paths)
+  const int rl_env = getenv("SBAG_HIST_RL") ? atoi(getenv("SBAG_HIST_RL")) : -1;
+  auto rl_mode_for = [&](const std::vector<int16_t>& pos, int32_t S_) {
+    if (rl_env == 0 || !(gini || cshift >= 32)) return 0;
+    for (int r = 0; r < R; r++)
+      for (int fl = 0; fl < h_Fr[r]; fl++)
+        if (pos[(size_t)r * Fmax + fl] != fl) return 0;
+    return (rl_env != 1 && N < (1 << 24) && (double)N * S_ + S_ < 4294967296.0) ? 2 : 1;
+  };
   bool root_done = false;
   HistGeom g0{};
   if (optimistic) {
-    if (!hist_geometry(ds->S, Fmax, ncmax, NS, gini, g0))
+    if (!hist_geometry(ds->S, Fmax, ncmax, NS, gini, g0, rl_mode_for(h_pos_codes, ds->S)))
       return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
     HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * Fmax * ncmax * NS * word_bytes, c->stream));
     ha.bins = (const uint8_t*)ds->d_codes;
@@ -1429,19 +1445,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   hmark(12);
   // ---- 6. level-wise growth
   HistGeom g;
-  // row-lane histogram: identity byte layout, packed variance words with cshift >= 32
-  // (SBAG_HIST_RL: 0 = never, 1 = always 64-bit row addresses; tests pin both paths)
-  const int rl_env = getenv("SBAG_HIST_RL") ? atoi(getenv("SBAG_HIST_RL")) : -1;
-  bool rl_ok = rl_env != 0 && (gini || cshift >= 32);
-  for (int r = 0; r < R && rl_ok; r++)
-    for (int fl = 0; fl < h_Fr[r]; fl++)
-      if (h_pos[(size_t)r * Fmax + fl] != fl) {
-        rl_ok = false;
-        break;
-      }
-  const int rl_mode = !rl_ok ? 0
-                      : (rl_env != 1 && N < (1 << 24) && (double)N * S + S < 4294967296.0) ? 2 : 1;
-  if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode))
+  if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode_for(h_pos, S)))
     return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
   const int64_t slot_words = (int64_t)Fmax * NB * NS;
   std::vector<std::vector<HNode>> trees(R);
@@ -1918,6 +1922,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   T.hist_launches = hist_launches;
   T.hist_alg_bytes = hist_alg_bytes;
   T.hist_entries = hist_entries;
+  T.hist_lds_atomics = hist_lds;
   T.hist_upper_bytes = hist_upper;
   T.levels = levels;
   hmark(15);
