@@ -1849,12 +1849,61 @@ void launch_zero_word(hipStream_t st, uint64_t* hist, const int32_t* d_slots, in
 // k_split<true>'s, in Spark's operation order (ImpurityCalculator.count = sequential
 // class sum, Gini.calculate = 1 - sum freq^2 in class order), and the block argmax
 // keeps Spark's first max (maxBy over splits, then over features).
+// stage the raw [g][NB][NS] u32 histogram of features [f0, f0 + g) (contiguous in the
+// slot) into LDS rows of NS + 1 words (odd pitch: the candidate threads of a wave read
+// rows (fl, sp) at one class c without bank conflicts), 16-byte loads with several in
+// flight per thread, then prefix sums over bins in place (a thread per (feature, class))
+__device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ hs, int f0, int g,
+                                                   int NB, int NS, uint32_t* pre) {
+  const int tid = threadIdx.x;
+  const int NSP = NS + 1;
+  const int64_t words = (int64_t)g * NB * NS;
+  const uint32_t* src = hs + (int64_t)f0 * NB * NS;
+  if ((NS & 3) == 0) {
+    const int n4 = (int)(words >> 2), ns4 = NS >> 2;
+    const uint4* s4 = (const uint4*)src;
+    auto put = [&](int q, const uint4& v) {
+      const int row = q / ns4, c = (q - row * ns4) * 4;
+      uint32_t* d = pre + (size_t)row * NSP + c;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    };
+    int q = tid;
+    for (; q + 3 * 256 < n4; q += 4 * 256) {
+      const uint4 v0 = s4[q], v1 = s4[q + 256], v2 = s4[q + 512], v3 = s4[q + 768];
+      put(q, v0);
+      put(q + 256, v1);
+      put(q + 512, v2);
+      put(q + 768, v3);
+    }
+    for (; q < n4; q += 256) put(q, s4[q]);
+  } else {
+    for (int64_t q = tid; q < words; q += 256) {
+      const int row = (int)(q / NS), c = (int)(q - (int64_t)row * NS);
+      pre[(size_t)row * NSP + c] = src[q];
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < g * NS; q += 256) {
+    const int fl = q / NS, c = q - fl * NS;
+    uint32_t* o = pre + (size_t)fl * NB * NSP + c;
+    uint32_t acc = 0;
+    for (int b = 0; b < NB; b++) {
+      acc += o[(size_t)b * NSP];
+      o[(size_t)b * NSP] = acc;
+    }
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int slot = A.slot_ids ? A.slot_ids[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x;
   const int r = A.slot_r[slot];
   const int Fr = A.Fr[r];
-  const int NB = A.NB, NS = A.NS;
+  const int NB = A.NB, NS = A.NS, NSP = NS + 1;
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
   const uint32_t* hs = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
   const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
@@ -1862,12 +1911,10 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   double* s_gain = (double*)(s_tot + NS);               // [256]
   int* s_key = (int*)(s_gain + 256);                    // [256] fl * 65536 + s (INT_MAX: none)
   int* s_valid = s_key + 256;                           // [256]
-  uint32_t* pre = (uint32_t*)(s_valid + 256);           // [G][NB][NS] prefix over bins
-  for (int c = tid; c < NS; c += 256) {
-    int64_t t = 0;
-    for (int b = 0; b < NB; b++) t += hs[(int64_t)b * NS + c];
-    s_tot[c] = t;
-  }
+  uint32_t* pre = (uint32_t*)(s_valid + 256);           // [G][NB][NS + 1] prefix over bins
+  // group 0 first: the node totals are feature 0's last prefix
+  split_stage_prefix(hs, 0, min(G, Fr), NB, NS, pre);
+  for (int c = tid; c < NS; c += 256) s_tot[c] = (int64_t)pre[(size_t)(NB - 1) * NSP + c];
   __syncthreads();
   double ttot = 0.0;
   for (int c = 0; c < NS; c++) ttot += (double)s_tot[c];
@@ -1884,25 +1931,23 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   int bkey = INT_MAX, bvalid = 0;
   for (int f0 = 0; f0 < Fr; f0 += G) {
     const int g = min(G, Fr - f0);
-    __syncthreads();  // previous group's prefix no longer read
-    for (int q = tid; q < g * NS; q += 256) {
-      const int fl = q / NS, c = q - fl * NS;
-      const uint32_t* h = hs + (int64_t)(f0 + fl) * NB * NS + c;
-      uint32_t* o = pre + (size_t)fl * NB * NS + c;
-      uint32_t acc = 0;
-      for (int b = 0; b < NB; b++) {
-        acc += h[(int64_t)b * NS];
-        o[(size_t)b * NS] = acc;
-      }
+    if (f0 > 0) {
+      __syncthreads();  // previous group's prefix no longer read
+      split_stage_prefix(hs, f0, g, NB, NS, pre);
     }
-    __syncthreads();
     for (int q = tid; q < g * (NB - 1); q += 256) {
       const int fl = q / (NB - 1), sp = q - fl * (NB - 1);
       const int nsp = nb_r[f0 + fl] - 1;
       if (sp >= nsp) continue;
-      const uint32_t* left = pre + ((size_t)fl * NB + sp) * NS;
-      double lt = 0.0;
-      for (int c = 0; c < NS; c++) lt += (double)left[c];
+      const uint32_t* left = pre + ((size_t)fl * NB + sp) * NSP;
+      // class sums of integers: exact in any order
+      double lt = 0.0, rt = 0.0;
+#pragma unroll 8
+      for (int c = 0; c < NS; c++) {
+        const uint32_t l = left[c];
+        lt += (double)l;
+        rt += (double)(s_tot[c] - (int64_t)l);
+      }
       const int64_t lc = (int64_t)lt;
       const int64_t rc = tcount - lc;
       double gain;
@@ -1911,22 +1956,15 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
         gain = -DBL_MAX;
         valid = 0;
       } else {
-        double li = 0.0, ri = 0.0;
-        if (lt != 0) {
-          li = 1.0;
-          for (int c = 0; c < NS; c++) {
-            const double fq = (double)left[c] / lt;
-            li -= fq * fq;
-          }
-        }
-        double rt = 0.0;
-        for (int c = 0; c < NS; c++) rt += (double)(s_tot[c] - (int64_t)left[c]);
-        if (rt != 0) {
-          ri = 1.0;
-          for (int c = 0; c < NS; c++) {
-            const double fq = (double)(s_tot[c] - (int64_t)left[c]) / rt;
-            ri -= fq * fq;
-          }
+        // Gini.calculate of both children: 1 - sum freq^2 in class order
+        double li = lt != 0 ? 1.0 : 0.0, ri = rt != 0 ? 1.0 : 0.0;
+#pragma unroll 8
+        for (int c = 0; c < NS; c++) {
+          const uint32_t l = left[c];
+          const double fl_ = (double)l / lt;
+          const double fr_ = (double)(s_tot[c] - (int64_t)l) / rt;
+          if (lt != 0) li -= fl_ * fl_;
+          if (rt != 0) ri -= fr_ * fr_;
         }
         const double lw = (double)lc / (double)(lc + rc);
         const double rw = (double)rc / (double)(lc + rc);
@@ -1980,11 +2018,20 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
     o.pad = 0;
     A.out[slot] = o;
   }
+  // left stats of the best split: bins [0, bsp] of feature bf, 8 loads in flight
   for (int c = tid; c < NS; c += 256) {
     int64_t l = 0;
     if (bf >= 0) {
-      const uint32_t* h = hs + (int64_t)bf * NB * NS;
-      for (int sb = 0; sb <= bsp; sb++) l += h[(int64_t)sb * NS + c];
+      const uint32_t* h = hs + (int64_t)bf * NB * NS + c;
+      int sb = 0;
+      for (; sb + 8 <= bsp + 1; sb += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = h[(int64_t)(sb + u) * NS];
+#pragma unroll
+        for (int u = 0; u < 8; u++) l += v[u];
+      }
+      for (; sb <= bsp; sb++) l += h[(int64_t)sb * NS];
     }
     so[c] = s_tot[c];
     so[A.plane + c] = l;
@@ -2025,7 +2072,7 @@ void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
   }
   if (gini) {
     // feature group: <= 64 KB of u32 prefix counts and about one candidate per thread
-    const size_t per_f = (size_t)a.NB * a.NS * 4;
+    const size_t per_f = (size_t)a.NB * (a.NS + 1) * 4;
     int G = (int)std::max<size_t>(1, std::min<size_t>((64 * 1024) / per_f, (size_t)(256 / std::max(1, a.NB - 1))));
     G = std::max(1, std::min(G, a.Fmax));
     const size_t lds_g = (size_t)a.NS * 8 + 256 * (8 + 4 + 4) + (size_t)G * per_f;
