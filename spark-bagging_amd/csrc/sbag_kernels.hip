@@ -207,32 +207,60 @@ __global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, in
 // refilling it.
 constexpr int kPB = 8;  // 624 = 78 * 8: batches cover aligned blocks after the prologue step
 
+// The state is a ring of z3 words: AbstractWell's writes of z4 (at index - 1) and of
+// the `&= 0x80000000` (at index - 2) are overwritten by z3 one or two steps later and
+// read in between only as v0 (kept in a register) or through their top bit (z0's hb,
+// which the mask leaves alone), so a batch writes only its 8 z3 words.
+// LDS layout: quads of 4 consecutive ring positions per lane, [pos / 4][lane][pos % 4],
+// so a batch reads each of its windows (8 or 9 consecutive positions) with 2-3
+// conflict-free ds_read_b128 and writes its z3 words with 2 ds_write_b128.
+__device__ __forceinline__ int wq(int pos, int lane) { return ((pos >> 2) * 64 + lane) * 4 + (pos & 3); }
+
+// 12 words of positions [p0, p0 + 12), p0 a multiple of 4 inside the ring
+__device__ __forceinline__ void well_read12(const uint32_t* __restrict__ st, int lane, int p0,
+                                            uint32_t (&w)[12]) {
+  const uint4* q = (const uint4*)st + (p0 >> 2) * 64 + lane;
+#pragma unroll
+  for (int u = 0; u < 3; u++) {
+    const uint4 v = q[u * 64];
+    w[4 * u] = v.x;
+    w[4 * u + 1] = v.y;
+    w[4 * u + 2] = v.z;
+    w[4 * u + 3] = v.w;
+  }
+}
+
+// batch of kPB = 8 steps at ring index i (i = 8k + 7): steps j = i, i-1, ..., i-7.
+// FAST: no read window straddles the ring end.  Returns the new index i - 8.
 template <bool FAST>
 __device__ __forceinline__ int well_batch_raw(uint32_t* __restrict__ st, int lane, int i,
                                               uint32_t& v0, uint32_t (&z4o)[kPB]) {
   uint32_t m1[kPB], m2[kPB], m3[kPB], hb[kPB], lo[kPB], z3v[kPB];
   if (FAST) {
-    const uint32_t* p1 = st + (wrap624(i + 70) - (kPB - 1)) * 64 + lane;
-    const uint32_t* p2 = st + (wrap624(i + 179) - (kPB - 1)) * 64 + lane;
-    const uint32_t* p3 = st + (wrap624(i - 175) - (kPB - 1)) * 64 + lane;
-    const uint32_t* ph = st + (i - 1 - kPB) * 64 + lane;
+    // windows (start mod 4): m1 [i+63, i+70] (2), m2 [i+172, i+179] (3),
+    // m3 [i-182, i-175] (1), hb/lo [i-9, i-1] (2); word 7-t of a window is step t's
+    uint32_t w1[12], w2[12], w3[12], wh[12];
+    well_read12(st, lane, wrap624(i + 63) - 2, w1);
+    well_read12(st, lane, wrap624(i + 172) - 3, w2);
+    well_read12(st, lane, wrap624(i - 182) - 1, w3);
+    well_read12(st, lane, wrap624(i - 9) - 2, wh);
 #pragma unroll
     for (int t = 0; t < kPB; t++) {
-      m1[t] = p1[(kPB - 1 - t) * 64];
-      m2[t] = p2[(kPB - 1 - t) * 64];
-      m3[t] = p3[(kPB - 1 - t) * 64];
-      hb[t] = ph[(kPB - t) * 64];
-      lo[t] = ph[(kPB - 1 - t) * 64];
+      m1[t] = w1[2 + 7 - t];
+      m2[t] = w2[3 + 7 - t];
+      m3[t] = w3[1 + 7 - t];
+      hb[t] = wh[2 + 8 - t];
+      lo[t] = wh[2 + 7 - t];
     }
   } else {
 #pragma unroll
     for (int t = 0; t < kPB; t++) {
-      const int j = wrap624(i - t);
-      m1[t] = st[wrap624(j + 70) * 64 + lane];
-      m2[t] = st[wrap624(j + 179) * 64 + lane];
-      m3[t] = st[wrap624(j - 175) * 64 + lane];
-      hb[t] = st[wrap624(j - 1) * 64 + lane];
-      lo[t] = st[wrap624(j - 2) * 64 + lane];
+      const int j = i - t;
+      m1[t] = st[wq(wrap624(j + 70), lane)];
+      m2[t] = st[wq(wrap624(j + 179), lane)];
+      m3[t] = st[wq(wrap624(j - 175), lane)];
+      hb[t] = st[wq(wrap624(j - 1), lane)];
+      lo[t] = st[wq(wrap624(j - 2), lane)];
     }
   }
 #pragma unroll
@@ -246,17 +274,16 @@ __device__ __forceinline__ int well_batch_raw(uint32_t* __restrict__ st, int lan
     z4o[t] = z4;
     v0 = z4;
   }
-  uint32_t* pw = st + (i - kPB + 1) * 64 + lane;  // [i-7, i] never wraps (aligned batches)
-#pragma unroll
-  for (int t = 0; t < kPB; t++) pw[(kPB - 1 - t) * 64] = z3v[t];
-  st[wrap624(i - kPB) * 64 + lane] = v0;
-  st[wrap624(i - kPB - 1) * 64 + lane] = lo[kPB - 1] & 0x80000000u;
+  // positions [i-7, i] (a multiple of 4 apart from the ring start): step t wrote i - t
+  uint4* q = (uint4*)st + ((i - 7) >> 2) * 64 + lane;
+  q[0] = make_uint4(z3v[7], z3v[6], z3v[5], z3v[4]);
+  q[64] = make_uint4(z3v[3], z3v[2], z3v[1], z3v[0]);
   return wrap624(i - kPB);
 }
 
-__device__ __forceinline__ bool well_window_ok(int x) {  // [x-kPB+1, x] inside the ring
-  const int lo = wrap624(x) - (kPB - 1);
-  return lo >= 0;
+__device__ __forceinline__ bool well_window_ok(int p, int len) {  // [p, p+len) inside the ring
+  const int w = wrap624(p);
+  return w + len <= 624;
 }
 
 __device__ __forceinline__ uint32_t well_temper26(uint32_t z4) {
@@ -281,31 +308,29 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
     // PoissonDistribution.reseedRandomGenerator(seed + i + partitionIndex) -> AbstractWell.setSeed
     const uint64_t s64 = (uint64_t)seed + (uint64_t)(int64_t)(learner0 + r) + (uint64_t)(int64_t)p;
     uint32_t vm2 = (uint32_t)(s64 >> 32), vm1 = (uint32_t)s64;
-    st[0 * 64 + lane] = vm2;
-    st[1 * 64 + lane] = vm1;
+    st[wq(0, lane)] = vm2;
+    st[wq(1, lane)] = vm1;
     for (int i = 2; i < 624; i++) {
       const int64_t l = (int64_t)(int32_t)vm2;
       const uint32_t v = (uint32_t)(1812433253ull * (uint64_t)(l ^ (l >> 30)) + (uint64_t)i);
-      st[i * 64 + lane] = v;
+      st[wq(i, lane)] = v;
       vm2 = vm1;
       vm1 = v;
     }
-    uint32_t v0 = st[lane];
+    uint32_t v0 = st[wq(0, lane)];
     // prologue: the single step at index 0 (leaves index 623 = 8*77 + 7); its output
     // goes to ring slot 1, step kPB-1, where the parser picks up its pending half
     {
-      const uint32_t m1 = st[70 * 64 + lane], m2 = st[179 * 64 + lane], m3 = st[449 * 64 + lane];
-      const uint32_t hb = st[623 * 64 + lane], lo = st[622 * 64 + lane];
+      const uint32_t m1 = st[wq(70, lane)], m2 = st[wq(179, lane)], m3 = st[wq(449, lane)];
+      const uint32_t hb = st[wq(623, lane)], lo = st[wq(622, lane)];
       const uint32_t z0 = (0x80000000u & hb) | (0x7FFFFFFFu & lo);
       const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1 ^ (m1 >> 27));
       const uint32_t z2 = (m2 >> 9) ^ (m3 ^ (m3 >> 1));
       const uint32_t z3 = z1 ^ z2;
       const uint32_t z4 = z0 ^ (z1 << 9) ^ (z2 << 21) ^ (z3 >> 21);
-      st[lane] = z3;
-      st[623 * 64 + lane] = z4;
-      st[622 * 64 + lane] = lo & 0x80000000u;
+      st[wq(0, lane)] = z3;
       v0 = z4;
-      ring[(1 * kPB + kPB - 1) * 64 + lane] = z4;
+      ring[kPB * 64 + lane * 4 + (kPB - 1 - 4) + 256] = z4;  // slot 1, half 1, word 3
     }
     __syncthreads();  // the parser takes the prologue output
     int index = 623;
@@ -314,21 +339,22 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
       if (k >= 2 && ring[((k & 1) * kPB) * 64] != 0u) break;
       uint32_t z4o[kPB];
       if (dbg & 2) {  // ablation: no generator work
-        uint32_t* slot = ring + (k & 1) * kPB * 64 + lane;
+        uint32_t* slot = ring + (k & 1) * kPB * 64 + lane * 4;
 #pragma unroll
-        for (int t = 0; t < kPB; t++) slot[t * 64] = v0 + t * 77777u;
+        for (int t = 0; t < kPB; t++) slot[(t >> 2) * 256 + (t & 3)] = v0 + t * 77777u;
         __syncthreads();
         continue;
       }
-      const bool fast = well_window_ok(index + 70) && well_window_ok(index + 179) &&
-                        well_window_ok(index - 175) && index - 1 - kPB >= 0;
+      const bool fast = well_window_ok(index + 63 - 2, 12) && well_window_ok(index + 172 - 3, 12) &&
+                        well_window_ok(index - 182 - 1, 12) && well_window_ok(index - 9 - 2, 12);
       if (fast)
         index = well_batch_raw<true>(st, lane, index, v0, z4o);
       else
         index = well_batch_raw<false>(st, lane, index, v0, z4o);
-      uint32_t* slot = ring + (k & 1) * kPB * 64 + lane;
-#pragma unroll
-      for (int t = 0; t < kPB; t++) slot[t * 64] = z4o[t];
+      // ring slot: [half][lane][4] words, steps 0-3 then 4-7
+      uint4* slot = (uint4*)(ring + (k & 1) * kPB * 64) + lane;
+      slot[0] = make_uint4(z4o[0], z4o[1], z4o[2], z4o[3]);
+      slot[64] = make_uint4(z4o[4], z4o[5], z4o[6], z4o[7]);
       __syncthreads();
     }
   } else {
@@ -341,13 +367,22 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
     int n = 0, bad = 0;
     double racc = 1.0;
     __syncthreads();  // the prologue output: first half of the first double
-    uint32_t pending = well_temper26(ring[(1 * kPB + kPB - 1) * 64 + lane]);
+    uint32_t pending = well_temper26(ring[kPB * 64 + lane * 4 + (kPB - 1 - 4) + 256]);
     for (int k = 0;; k++) {
       __syncthreads();  // batch k is in ring slot k & 1
       uint32_t* slot = ring + (k & 1) * kPB * 64;
       uint32_t o[kPB];
-#pragma unroll
-      for (int t = 0; t < kPB; t++) o[t] = well_temper26(slot[t * 64 + lane]);
+      {
+        const uint4 a0 = ((const uint4*)slot)[lane], a1 = ((const uint4*)slot)[64 + lane];
+        o[0] = well_temper26(a0.x);
+        o[1] = well_temper26(a0.y);
+        o[2] = well_temper26(a0.z);
+        o[3] = well_temper26(a0.w);
+        o[4] = well_temper26(a1.x);
+        o[5] = well_temper26(a1.y);
+        o[6] = well_temper26(a1.z);
+        o[7] = well_temper26(a1.w);
+      }
       // doubles: (pending, o0), (o1, o2), (o3, o4), (o5, o6); o7 carries over.
       // BitsStreamGenerator.nextDouble = (next(26) << 26 | next(26)) * 2^-52, built as
       // the bits of 1 + m * 2^-52 minus 1 (exact: m < 2^52).
