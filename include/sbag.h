@@ -105,6 +105,9 @@ typedef struct {
   int32_t min_instances_per_node; /* default 1                                    */
   int32_t impurity;               /* SBAG_IMPURITY_*                              */
   double min_info_gain;           /* default 0.0                                  */
+  int64_t seed;                   /* the base learner's seed param (HasSeed; default the
+                                     class-name hashCode): seeds RandomForest.findSplits'
+                                     split-finding sample of subbags > max(maxBins^2, 1e4) */
 } sbag_tree_params;
 
 typedef struct {
@@ -128,6 +131,8 @@ typedef struct { /* DecisionTreeModelReadWrite.NodeData, pre-order ids */
 } sbag_node;
 
 int sbag_forest_num_trees(const sbag_forest* f, int32_t* n);
+/* exact_splits: 1 when the tree's thresholds are Spark's (always, since the split-finding
+   sample of large subbags is replayed; kept for ABI compatibility) */
 int sbag_forest_tree_info(const sbag_forest* f, int32_t t, int32_t* num_nodes, int32_t* num_stats,
                           int32_t* subspace_len, int32_t* exact_splits);
 int sbag_forest_subspace(const sbag_forest* f, int32_t t, int32_t* idx_out);

@@ -15,12 +15,17 @@ LIB_PATH = os.path.join(HERE, "lib", "liboracle.so")
 
 DEFAULT_SEED_REGRESSOR = -1395689524   # "org.apache.spark.ml.regression.BaggingRegressor".hashCode
 DEFAULT_SEED_CLASSIFIER = 42087812     # "org.apache.spark.ml.classification.BaggingClassifier".hashCode
+# base learners' HasSeed defaults (class-name hashCode): seed of the split-finding sample
+DT_SEED_REGRESSOR = 926680331          # "org.apache.spark.ml.regression.DecisionTreeRegressor"
+DT_SEED_CLASSIFIER = 159147643         # "org.apache.spark.ml.classification.DecisionTreeClassifier"
 
 
 class TreeParams(ctypes.Structure):
     _fields_ = [("max_depth", ctypes.c_int32), ("max_bins", ctypes.c_int32),
                 ("min_instances_per_node", ctypes.c_int32), ("impurity", ctypes.c_int32),
-                ("min_info_gain", ctypes.c_double)]
+                ("min_info_gain", ctypes.c_double), ("seed", ctypes.c_int64),
+                ("part_off", ctypes.c_void_p), ("num_partitions", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
 
 
 NODE_DTYPE = np.dtype([("id", "<i4"), ("left", "<i4"), ("right", "<i4"), ("feature", "<i4"),
@@ -55,6 +60,11 @@ def lib():
         L.or_fit.argtypes = [P, P, i64, i32, P, i32, P, P, ctypes.POINTER(TreeParams), i32,
                              P, i32, P, i32, P, P, P]
         L.or_predict.argtypes = [P, i64, i32, i32, P, P, P, i32, i32, P, P]
+        L.or_split_sample_fraction.restype = dbl
+        L.or_split_sample_fraction.argtypes = [i64, i32]
+        L.or_split_sample_seeds.argtypes = [i64, i32, P]
+        L.or_split_sample.restype = i64
+        L.or_split_sample.argtypes = [P, P, i32, i64, dbl, P]
         _lib = L
     return _lib
 
@@ -137,8 +147,29 @@ class Forest:
         return self.nodes[l, :n], self.stats[l, :n, : int(self.num_stats[l])]
 
 
+def split_sample_fraction(num_examples, max_bins):
+    return lib().or_split_sample_fraction(int(num_examples), int(max_bins))
+
+
+def split_sample_seeds(dt_seed, P):
+    out = np.zeros(P, np.int64)
+    lib().or_split_sample_seeds(int(dt_seed), int(P), _p(out))
+    return out
+
+
+def split_sample(counts_row, part_off, dt_seed, fraction):
+    """Multiplicity of each row of one replica's subbag in RandomForest.findSplits'
+    sample (sbag_oracle.c or_split_sample)."""
+    c = np.ascontiguousarray(counts_row, np.uint8)
+    off = np.ascontiguousarray(part_off, np.int64)
+    mult = np.zeros(len(c), np.uint16)
+    lib().or_split_sample(_p(c), _p(off), len(off) - 1, int(dt_seed), float(fraction), _p(mult))
+    return mult
+
+
 def fit(X, y, counts, subspaces, max_depth=5, max_bins=32, min_instances_per_node=1,
-        min_info_gain=0.0, classification=False, nthreads=None, max_stats=None):
+        min_info_gain=0.0, classification=False, nthreads=None, max_stats=None, part=None,
+        dt_seed=None):
     X = np.ascontiguousarray(X, np.float64)
     y = np.ascontiguousarray(y, np.float64)
     counts = np.ascontiguousarray(counts, np.uint8)
@@ -157,8 +188,11 @@ def fit(X, y, counts, subspaces, max_depth=5, max_bins=32, min_instances_per_nod
     num_nodes = np.zeros(L, np.int32)
     num_stats = np.zeros(L, np.int32)
     exact = np.zeros(L, np.int32)
+    if dt_seed is None:
+        dt_seed = DT_SEED_CLASSIFIER if classification else DT_SEED_REGRESSOR
+    off = np.ascontiguousarray(part if part is not None else [0, N], np.int64)
     p = TreeParams(max_depth, max_bins, min_instances_per_node, 1 if classification else 0,
-                   min_info_gain)
+                   min_info_gain, int(dt_seed), off.ctypes.data, len(off) - 1, 0)
     rc = lib().or_fit(_p(X), _p(y), N, F, _p(counts), L, _p(sub), _p(nsub), ctypes.byref(p),
                       nthreads or os.cpu_count() or 1, _p(nodes), max_nodes, _p(stats), max_stats,
                       _p(num_nodes), _p(num_stats), _p(exact))

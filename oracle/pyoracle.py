@@ -195,8 +195,59 @@ def subspace(ratio, nfeat, seed):
     return [f for f in range(nfeat) if rng.next_double() < ratio]
 
 
+# ---------------------------------------------------------------- split-finding sample
+class JavaRandom:
+    """java.util.Random (48-bit LCG)."""
+
+    def __init__(self, seed):
+        self.s = (seed ^ 0x5DEECE66D) & ((1 << 48) - 1)
+
+    def next(self, bits):
+        self.s = (self.s * 0x5DEECE66D + 0xB) & ((1 << 48) - 1)
+        return _i32(self.s >> (48 - bits))
+
+    def next_long(self):
+        return _i64((self.next(32) << 32) + self.next(32))
+
+
+def split_sample_fraction(num_examples, max_bins):
+    """RandomForest.samplesFractionForFindSplits (metadata.maxBins = min(maxBins, n))."""
+    mpb = min(max_bins, num_examples)
+    required = max(mpb * mpb, 10000)
+    return required / num_examples if required < num_examples else 1.0
+
+
+def split_sample(counts_row, part_off, dt_seed, fraction):
+    """RDD.sample(false, fraction, new XORShiftRandom(seed).nextInt()) over the exploded
+    subbag: per-partition java.util.Random seeds, BernoulliSampler with GapSampling
+    (fraction <= 0.4) or a nextDouble test per item.  Returns the multiplicity per row."""
+    import math
+    jr = JavaRandom(XORShiftRandom(dt_seed).next_int())
+    mult = [0] * len(counts_row)
+    for p in range(len(part_off) - 1):
+        rng = XORShiftRandom(jr.next_long())
+        if fraction <= 0.4:
+            lnq = math.log1p(-fraction)
+            cfd = None
+            for r in range(part_off[p], part_off[p + 1]):
+                for _ in range(int(counts_row[r])):
+                    if cfd is None:  # lazy GapSampling: construction draws the first gap
+                        cfd = int(math.log(max(rng.next_double(), 5e-11)) / lnq)
+                    if cfd > 0:
+                        cfd -= 1
+                    else:
+                        cfd = int(math.log(max(rng.next_double(), 5e-11)) / lnq)
+                        mult[r] += 1
+        else:
+            for r in range(part_off[p], part_off[p + 1]):
+                for _ in range(int(counts_row[r])):
+                    if rng.next_double() <= fraction:
+                        mult[r] += 1
+    return mult
+
+
 # ---------------------------------------------------------------- DecisionTree
-def find_splits(values_with_mult, n, max_bins):
+def find_splits(values_with_mult, n, max_bins, num_samples=None):
     """RandomForest.findSplitsForContinuousFeature on the whole subbag.
 
     values_with_mult: dict value -> multiplicity over the replicated subbag (all values).
@@ -205,7 +256,8 @@ def find_splits(values_with_mult, n, max_bins):
     if not nonzero:
         return []
     num_splits = min(max_bins, n) - 1
-    num_samples = n
+    if num_samples is None:
+        num_samples = n
     part = sum(nonzero.values())
     vc = dict(nonzero)
     if num_samples - part > 0:

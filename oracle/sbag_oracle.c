@@ -268,14 +268,16 @@ static int cmp_double(const void* a, const void* b) {
   return (x < y) ? -1 : (x > y) ? 1 : 0;
 }
 
+/* Spark 2.4.3 RandomForest.findSplitsForContinuousFeature.  vals: the nonzero values of
+   the split-finding sample with multiplicity (findSplitsBySorting drops zeros); n =
+   metadata.numExamples; num_samples = (samplesFractionForFindSplits * numExamples).toInt,
+   the expected sample size whose shortfall over nnz is the implied zero count. */
 static int find_splits_values(double* vals /*nonzero values with multiplicity, sorted in place*/,
-                              int64_t nnz, int64_t n, int64_t max_bins, double* thr, int* exact) {
-  const int64_t required = (max_bins * max_bins > 10000) ? max_bins * max_bins : 10000;
-  *exact = !(required < n);
+                              int64_t nnz, int64_t n, int64_t num_samples, int64_t max_bins,
+                              double* thr) {
   if (nnz == 0) return 0; /* featureSamples.isEmpty */
   const int64_t max_possible_bins = (max_bins < n) ? max_bins : n;
   const int64_t num_splits = max_possible_bins - 1;
-  const int64_t num_samples = n; /* fraction treated as 1 (see header) */
   qsort(vals, (size_t)nnz, sizeof(double), cmp_double);
   vc_t* vc = (vc_t*)malloc(sizeof(vc_t) * (size_t)(nnz + 1));
   int64_t k = 0;
@@ -328,6 +330,93 @@ static int find_splits_values(double* vals /*nonzero values with multiplicity, s
   return nt;
 }
 
+/* ======================================================================
+ * The split-finding sample (Spark 2.4.3 RandomForest.findSplits):
+ *   fraction = samplesFractionForFindSplits = required / numExamples when
+ *     required = max(maxPossibleBins^2, 10000) < numExamples, else 1;
+ *   input.sample(withReplacement = false, fraction, new XORShiftRandom(seed).nextInt())
+ *   -> PartitionwiseSampledRDD: java.util.Random(sampleSeed).nextLong() per partition, in
+ *      partition order, seeds that partition's BernoulliSampler (XORShiftRandom.setSeed);
+ *   -> BernoulliSampler.sample per item: GapSampling when fraction <= 0.4
+ *      (countForDropping = (log(max(u, 5e-11)) / log1p(-f)).toInt, first gap drawn at
+ *      construction), else nextDouble() <= fraction.
+ * The items are the replica's subbag rows in partition order, each row repeated `count`
+ * times consecutively (replicate_row = explode(array_repeat), sql/bfunctions.scala:42-44).
+ * `seed` is the base learner's seed param (HasSeed default: class-name hashCode).
+ * Math.log / log1p are libm here (the JVM's may differ by 1 ulp; a draw flips only if the
+ * quotient lands within that of an integer).
+ * ==================================================================== */
+typedef struct {
+  uint64_t s;
+} jr_t; /* java.util.Random */
+static void jr_init(jr_t* r, int64_t seed) { r->s = ((uint64_t)seed ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
+static int32_t jr_next(jr_t* r, int bits) {
+  r->s = (r->s * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+  return (int32_t)(uint32_t)(r->s >> (48 - bits));
+}
+static int64_t jr_next_long(jr_t* r) {
+  const int64_t hi = (int64_t)jr_next(r, 32), lo = (int64_t)jr_next(r, 32);
+  return (int64_t)((uint64_t)hi << 32) + lo;
+}
+
+double or_split_sample_fraction(int64_t num_examples, int max_bins) {
+  const int64_t mpb = (max_bins < num_examples) ? max_bins : num_examples;
+  const int64_t required = (mpb * mpb > 10000) ? mpb * mpb : 10000;
+  return (required < num_examples) ? (double)required / (double)num_examples : 1.0;
+}
+
+void or_split_sample_seeds(int64_t dt_seed, int P, int64_t* part_seed) {
+  xs_t x;
+  xs_init(&x, dt_seed);
+  const int64_t sample_seed = (int64_t)xs_next(&x, 32); /* XORShiftRandom.nextInt */
+  jr_t j;
+  jr_init(&j, sample_seed);
+  for (int p = 0; p < P; p++) part_seed[p] = jr_next_long(&j);
+}
+
+int64_t or_split_sample(const uint8_t* cnt, const int64_t* off, int P, int64_t dt_seed,
+                        double fraction, uint16_t* mult) {
+  int64_t* ps = (int64_t*)malloc(sizeof(int64_t) * (size_t)(P > 0 ? P : 1));
+  or_split_sample_seeds(dt_seed, P, ps);
+  int64_t taken = 0;
+  const double lnq = log1p(-fraction);
+  for (int p = 0; p < P; p++) {
+    for (int64_t r = off[p]; r < off[p + 1]; r++) mult[r] = 0;
+    xs_t x;
+    xs_init(&x, ps[p]);
+    if (fraction <= 0.4) {
+      int32_t cfd = 0, started = 0;
+      for (int64_t r = off[p]; r < off[p + 1]; r++)
+        for (int c = 0; c < cnt[r]; c++) {
+          if (!started) { /* lazy GapSampling: its constructor draws the first gap */
+            double u = xs_next_double(&x);
+            if (u < 5e-11) u = 5e-11;
+            cfd = (int32_t)(log(u) / lnq);
+            started = 1;
+          }
+          if (cfd > 0) {
+            cfd--;
+          } else {
+            double u = xs_next_double(&x);
+            if (u < 5e-11) u = 5e-11;
+            cfd = (int32_t)(log(u) / lnq);
+            mult[r]++;
+            taken++;
+          }
+        }
+    } else {
+      for (int64_t r = off[p]; r < off[p + 1]; r++)
+        for (int c = 0; c < cnt[r]; c++)
+          if (xs_next_double(&x) <= fraction) {
+            mult[r]++;
+            taken++;
+          }
+    }
+  }
+  free(ps);
+  return taken;
+}
+
 int or_find_splits(const double* X, int64_t N, int F, int feature, const uint8_t* counts,
                    int max_bins, double* thr_out, int* exact_out) {
   int64_t n = 0, nnz = 0;
@@ -342,7 +431,8 @@ int or_find_splits(const double* X, int64_t N, int F, int feature, const uint8_t
     if (x != 0.0)
       for (int c = 0; c < counts[r]; c++) vals[k++] = x;
   }
-  int nt = find_splits_values(vals, nnz, n, max_bins, thr_out, exact_out);
+  *exact_out = or_split_sample_fraction(n, max_bins) >= 1.0;
+  int nt = find_splits_values(vals, nnz, n, n, max_bins, thr_out);
   free(vals);
   return nt;
 }
@@ -546,21 +636,32 @@ static int fit_one(const double* X, const double* y, int64_t N, int F, const uin
   int* nthr = (int*)malloc(sizeof(int) * (size_t)Fr);
   uint16_t* bins = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)nrows * (size_t)Fr);
   int all_exact = 1;
+  /* RandomForest.findSplits: the split-finding sample of the subbag */
+  const double fraction = or_split_sample_fraction(n, p->max_bins);
+  uint16_t* mult = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)N);
+  int64_t num_samples = n;
+  if (fraction < 1.0) {
+    const int64_t one[2] = {0, N};
+    const int64_t* off = p->part_off ? p->part_off : one;
+    const int P = p->part_off ? p->num_partitions : 1;
+    or_split_sample(cnt, off, P, p->seed, fraction, mult);
+    num_samples = (int64_t)(int32_t)(fraction * (double)n); /* (fraction * numExamples).toInt */
+  } else {
+    for (int64_t r = 0; r < N; r++) mult[r] = cnt[r];
+  }
   for (int fl = 0; fl < Fr; fl++) {
     const int fg = sub[fl];
     int64_t nnz = 0;
     for (int64_t k = 0; k < nrows; k++)
-      if (X[rows[k] * F + fg] != 0.0) nnz += cnt[rows[k]];
+      if (X[rows[k] * F + fg] != 0.0) nnz += mult[rows[k]];
     double* vals = (double*)malloc(sizeof(double) * (size_t)(nnz + 1));
     int64_t q = 0;
     for (int64_t k = 0; k < nrows; k++) {
       const double x = X[rows[k] * F + fg];
       if (x != 0.0)
-        for (int c = 0; c < cnt[rows[k]]; c++) vals[q++] = x;
+        for (int c = 0; c < mult[rows[k]]; c++) vals[q++] = x;
     }
-    int ex;
-    nthr[fl] = find_splits_values(vals, nnz, n, p->max_bins, thr + (int64_t)fl * p->max_bins, &ex);
-    all_exact &= ex;
+    nthr[fl] = find_splits_values(vals, nnz, n, num_samples, p->max_bins, thr + (int64_t)fl * p->max_bins);
     free(vals);
     const double* t = thr + (int64_t)fl * p->max_bins;
     for (int64_t k = 0; k < nrows; k++) {
@@ -750,6 +851,7 @@ static int fit_one(const double* X, const double* y, int64_t N, int F, const uin
   to_node(ln, 1, &e, gini, &rid);
   *out_num_nodes = e.count;
   *out_ns = ns;
+  free(mult);
   *out_exact = all_exact;
   free(ln);
   free(node_of);

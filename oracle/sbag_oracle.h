@@ -35,7 +35,17 @@ int or_subspace(double ratio, int F, int64_t seed, int32_t* idx, int32_t* n_out)
 typedef struct {
   int32_t max_depth, max_bins, min_instances_per_node, impurity; /* 0 variance, 1 gini */
   double min_info_gain;
+  int64_t seed;             /* the base learner's seed param (split-finding sample)       */
+  const int64_t* part_off;  /* [num_partitions + 1] subbag partitions, NULL: one          */
+  int32_t num_partitions, pad_;
 } or_tree_params;
+
+/* RandomForest.findSplits' sample: fraction for numExamples rows, the per-partition
+   sampler seeds, and the multiplicity of each subbag row in the sample.            */
+double or_split_sample_fraction(int64_t num_examples, int max_bins);
+void or_split_sample_seeds(int64_t dt_seed, int P, int64_t* part_seed);
+int64_t or_split_sample(const uint8_t* counts, const int64_t* part_off, int P, int64_t dt_seed,
+                        double fraction, uint16_t* mult /*[N]*/);
 
 typedef struct { /* pre-order NodeData layout (DecisionTreeModelReadWrite.NodeData) */
   int32_t id, left, right, feature; /* feature: subspace-local index, -1 for a leaf */
@@ -43,8 +53,8 @@ typedef struct { /* pre-order NodeData layout (DecisionTreeModelReadWrite.NodeDa
   double threshold, prediction, impurity, gain;
 } or_node;
 
-/* thresholds of one feature from a replica's subbag; returns #thresholds.
-   exact_out = 1 when Spark's split-finding sample is the whole subbag.   */
+/* thresholds of one feature from a replica's whole subbag (no sample); returns
+   #thresholds.  exact_out = 1 when Spark's split-finding sample is the whole subbag. */
 int or_find_splits(const double* X, int64_t N, int F, int feature, const uint8_t* counts,
                    int max_bins, double* thr_out, int* exact_out);
 

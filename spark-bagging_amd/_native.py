@@ -51,7 +51,13 @@ class SamplerParams(ctypes.Structure):
 class TreeParams(ctypes.Structure):
     _fields_ = [("max_depth", ctypes.c_int32), ("max_bins", ctypes.c_int32),
                 ("min_instances_per_node", ctypes.c_int32), ("impurity", ctypes.c_int32),
-                ("min_info_gain", ctypes.c_double)]
+                ("min_info_gain", ctypes.c_double), ("seed", ctypes.c_int64)]
+
+
+# base learners' HasSeed defaults (class-name hashCode): seed of RandomForest.findSplits'
+# split-finding sample
+DT_SEED_REGRESSOR = 926680331     # "org.apache.spark.ml.regression.DecisionTreeRegressor"
+DT_SEED_CLASSIFIER = 159147643    # "org.apache.spark.ml.classification.DecisionTreeClassifier"
 
 
 class FitParams(ctypes.Structure):
@@ -327,7 +333,10 @@ def subspace(ratio, num_features, seed):
 
 def fit(ctx, dataset, *, replacement, sample_ratio, seed, learner_begin, learner_end,
         subspace_ratio=1.0, subspace_bug_compat=True, partition_offsets=None, max_depth=5,
-        max_bins=32, min_instances_per_node=1, min_info_gain=0.0, impurity=IMPURITY_VARIANCE):
+        max_bins=32, min_instances_per_node=1, min_info_gain=0.0, impurity=IMPURITY_VARIANCE,
+        tree_seed=None):
+    if tree_seed is None:
+        tree_seed = DT_SEED_CLASSIFIER if impurity == IMPURITY_GINI else DT_SEED_REGRESSOR
     off = None
     P = 1
     if partition_offsets is not None:
@@ -338,7 +347,7 @@ def fit(ctx, dataset, *, replacement, sample_ratio, seed, learner_begin, learner
                    float(subspace_ratio), int(subspace_bug_compat), P,
                    off.ctypes.data if off is not None else None,
                    TreeParams(max_depth, max_bins, min_instances_per_node, impurity,
-                              float(min_info_gain)))
+                              float(min_info_gain), int(tree_seed)))
     h = ctypes.c_void_p()
     check(lib().sbag_fit(ctx.handle, dataset.handle, ctypes.byref(fp), ctypes.byref(h)))
     return NativeForest(h, impurity)

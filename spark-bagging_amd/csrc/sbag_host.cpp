@@ -466,9 +466,11 @@ static ToNodeRet emit(const std::vector<HNode>& nodes, int idx, HTree& t, int ns
 // ---------------------------------------------------------------- split finding (host)
 // RandomForest.findSplitsForContinuousFeature over a replica's weighted value
 // counts (the subbag replicates each row `count` times).  `cnt[c]` is the
-// weighted count of dictionary value `vals[c]` among in-bag rows.
+// weighted count of dictionary value `vals[c]` among the in-bag rows, or among the
+// split-finding sample; n = numExamples, num_samples = n or (fraction * n).toInt, whose
+// shortfall over the nonzero count is the implied count of 0.0.
 static int find_splits(const std::vector<double>& vals, const uint32_t* cnt, int zero_code, int64_t n,
-                       int max_bins, std::vector<double>& thr) {
+                       int64_t num_samples, int max_bins, std::vector<double>& thr) {
   thr.clear();
   int64_t nnz = 0;
   for (size_t c = 0; c < vals.size(); c++)
@@ -476,7 +478,6 @@ static int find_splits(const std::vector<double>& vals, const uint32_t* cnt, int
   if (nnz == 0) return 0;  // featureSamples.isEmpty
   const int64_t max_possible_bins = std::min<int64_t>(max_bins, n);
   const int64_t num_splits = max_possible_bins - 1;
-  const int64_t num_samples = n;
   std::vector<std::pair<double, int64_t>> vc;
   vc.reserve(vals.size());
   const int64_t zeros = num_samples - nnz;
@@ -488,7 +489,7 @@ static int find_splits(const std::vector<double>& vals, const uint32_t* cnt, int
     if (cnt[c] == 0) continue;
     vc.emplace_back(vals[c], (int64_t)cnt[c]);
   }
-  if (zero_code < 0 && zeros > 0) {  // zeros implied although no 0.0 code (cannot happen here)
+  if (zero_code < 0 && zeros > 0) {  // zeros implied by a sample short of numSamples
     vc.emplace_back(0.0, zeros);
     std::sort(vc.begin(), vc.end());
   }
@@ -1277,6 +1278,74 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   }
 
   hmark(10);
+  // ---- 3b. RandomForest.findSplits' split-finding sample: a subbag of more than
+  // required = max(min(maxBins, n)^2, 10^4) rows is thresholded on
+  // RDD.sample(false, required / n, new XORShiftRandom(seed).nextInt()) (k_split_sample);
+  // findSplitsForContinuousFeature then sees numSamples = (fraction * n).toInt
+  std::vector<double> sfrac(R, 1.0);
+  std::vector<uint32_t> vcs;
+  {
+    std::vector<int32_t> reps;
+    std::vector<double> fl2;
+    for (int r = 0; r < R; r++) {
+      const int64_t mpb = std::min<int64_t>(tp.max_bins, nw[r]);
+      const int64_t required = std::max<int64_t>(mpb * mpb, 10000);
+      if (required < nw[r]) {
+        sfrac[r] = (double)required / (double)nw[r];
+        reps.push_back(r);
+        fl2.push_back(sfrac[r]);
+        fl2.push_back(std::log1p(-sfrac[r]));
+      }
+    }
+    if (!reps.empty()) {
+      const int P = (int)poff.size() - 1;
+      // PartitionwiseSampledRDD: java.util.Random(sampleSeed).nextLong() per partition
+      uint64_t js = ((uint64_t)(int64_t)HostXS(tp.seed).next(32) ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1);
+      auto jnext = [&]() {
+        js = (js * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+        return (int64_t)(int32_t)(uint32_t)(js >> 16);
+      };
+      std::vector<uint64_t> pst(P);
+      for (int q = 0; q < P; q++) {
+        const int64_t hi = jnext(), lo = jnext();
+        pst[q] = h_hash_seed((int64_t)((uint64_t)hi << 32) + lo);
+      }
+      int32_t* d_reps;
+      double* d_frac;
+      uint64_t* d_pst;
+      int64_t *d_spoff, *d_svcoff;
+      uint32_t* d_vcs;
+      TRY(ws_typed(c, "ss_reps", reps.size(), &d_reps));
+      TRY(ws_typed(c, "ss_frac", fl2.size(), &d_frac));
+      TRY(ws_typed(c, "ss_pst", pst.size(), &d_pst));
+      TRY(ws_typed(c, "ss_poff", poff.size(), &d_spoff));
+      TRY(ws_typed(c, "ss_vcoff", vcoff.size(), &d_svcoff));
+      TRY(ws_typed(c, "ss_vc", (size_t)std::max<int64_t>(vc_total, 1), &d_vcs));
+      TRY(h2d(c, d_reps, reps.data(), reps.size()));
+      TRY(h2d(c, d_frac, fl2.data(), fl2.size()));
+      TRY(h2d(c, d_pst, pst.data(), pst.size()));
+      TRY(h2d(c, d_spoff, poff.data(), poff.size()));
+      TRY(h2d(c, d_svcoff, vcoff.data(), vcoff.size()));
+      HIP_TRY(hipMemsetAsync(d_vcs, 0, (size_t)std::max<int64_t>(vc_total, 1) * 4, c->stream));
+      int h = tm.begin(T_VC);
+      launch_split_sample(c->stream, d_counts, N, d_spoff, P, d_reps, (int)reps.size(), d_pst, d_frac,
+                          ds->d_codes, ds->code_bytes, ds->S, d_sub, d_Fr, Fmax, d_svcoff, d_vcs);
+      HIP_TRY(hipGetLastError());
+      tm.end(h);
+      vcs.assign((size_t)std::max<int64_t>(vc_total, 1), 0);
+      TRY(d2h(c, vcs.data(), d_vcs, vcs.size()));
+      if (getenv("SBAG_DEBUG_SAMPLE")) {
+        for (int r : reps) {
+          int64_t tot = 0;
+          for (int64_t k = vcoff[(size_t)r * Fmax]; k < vcoff[(size_t)r * Fmax + 1]; k++) tot += vcs[k];
+          fprintf(stderr, "split sample r=%d n=%lld frac=%.17g sampled=%lld seed=%lld pst0=%llx\n", r,
+                  (long long)nw[r], sfrac[r], (long long)tot, (long long)tp.seed,
+                  (unsigned long long)pst[0]);
+        }
+      }
+    }
+  }
+
   // ---- 4. thresholds, LUTs (code -> bin), numSplits per (replica, feature)
   std::vector<std::vector<double>> thr((size_t)R * Fmax);
   std::vector<int32_t> h_nbins((size_t)R * Fmax, 1);
@@ -1291,13 +1360,15 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     std::vector<char> t_id(nth, 1);
     auto work = [&](int w) {
       for (int r = w; r < R; r += nth) {
-        const int64_t required = std::max<int64_t>((int64_t)tp.max_bins * tp.max_bins, 10000);
-        if (required < nw[r]) exact[r] = 0;  // reference samples for split finding
+        const bool sampled = sfrac[r] < 1.0;
+        // (fraction * numExamples).toInt
+        const int64_t nsamp = sampled ? (int64_t)(int32_t)(sfrac[r] * (double)nw[r]) : nw[r];
         for (int fl = 0; fl < h_Fr[r]; fl++) {
           const int g = sub[r][fl];
           const size_t o = (size_t)vcoff[(size_t)r * Fmax + fl];
           std::vector<double>& t = thr[(size_t)r * Fmax + fl];
-          const int nt = find_splits(ds->dict[g], vc.data() + o, ds->zero_code[g], nw[r], tp.max_bins, t);
+          const int nt = find_splits(ds->dict[g], (sampled ? vcs.data() : vc.data()) + o, ds->zero_code[g],
+                                     nw[r], nsamp, tp.max_bins, t);
           h_nbins[(size_t)r * Fmax + fl] = nt + 1;
           t_nb[w] = std::max(t_nb[w], nt + 1);
           const auto& d = ds->dict[g];

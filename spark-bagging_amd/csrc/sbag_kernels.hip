@@ -451,6 +451,101 @@ void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d
 }
 
 // ======================================================================
+// RandomForest.findSplits' split-finding sample (Spark 2.4.3): for subbags of more than
+// max(maxBins^2, 10^4) rows, thresholds come from RDD.sample(false, fraction, seed') over
+// the exploded subbag: partition p's BernoulliSampler is an XORShiftRandom seeded with
+// the p-th java.util.Random(seed').nextLong() (part_state = its hashed state, host);
+// GapSampling when fraction <= 0.4 (countForDropping = (log(max(u, 5e-11)) / log1p(-f))
+// .toInt, the first gap drawn at the first item), else one nextDouble() <= f per item.
+// A thread walks one (replica, partition) in row order, each row standing for `count`
+// consecutive items, and adds every sampled item's value codes to the replica's value
+// counts (vcoff layout), as findSplitsBySorting's groupByKey would see them.
+// ======================================================================
+__device__ __forceinline__ uint64_t xs_step_s(uint64_t s) {
+  s ^= s << 21;
+  s ^= s >> 35;
+  s ^= s << 4;
+  return s;
+}
+
+__global__ __launch_bounds__(64) void k_split_sample(
+    const uint8_t* __restrict__ counts, int64_t N, const int64_t* __restrict__ part_off, int P,
+    const int32_t* __restrict__ reps, int nrep, const uint64_t* __restrict__ part_state,
+    const double* __restrict__ frac, const uint8_t* __restrict__ codes, int code_bytes, int32_t S,
+    const int32_t* __restrict__ sub, const int32_t* __restrict__ Fr, int32_t Fmax,
+    const int64_t* __restrict__ vcoff, uint32_t* __restrict__ vc) {
+  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (t >= (int64_t)nrep * P) return;
+  const int ri = (int)(t / P), p = (int)(t % P);
+  const int r = reps[ri];
+  // per replica: fraction = required / numExamples and log1p(-fraction) (host libm, as the
+  // oracle computes it)
+  const double fraction = frac[2 * ri], lnq = frac[2 * ri + 1];
+  uint64_t s = part_state[p];
+  auto next_double = [&]() {
+    s = xs_step_s(s);
+    const int64_t a = (int64_t)(s & ((1ull << 26) - 1));
+    s = xs_step_s(s);
+    const int64_t b = (int64_t)(s & ((1ull << 27) - 1));
+    return (double)((a << 27) + b) * 0x1.0p-53;
+  };
+  auto gap = [&]() {
+    const double u = fmax(next_double(), 5e-11);
+    return (int32_t)(log(u) / lnq);
+  };
+  const int fr = Fr[r];
+  const int32_t* sr = sub + (int64_t)r * Fmax;
+  const int64_t* vo = vcoff + (int64_t)r * Fmax;
+  auto take = [&](int64_t row) {
+    for (int fl = 0; fl < fr; fl++) {
+      const int64_t pos = row * S + sr[fl];
+      const uint32_t code = code_bytes == 1 ? (uint32_t)codes[pos]
+                                            : (uint32_t)((const uint16_t*)codes)[pos];
+      atomicAdd(&vc[vo[fl] + code], 1u);
+    }
+  };
+  const uint8_t* cr = counts + (int64_t)r * N;
+  const int64_t r0 = part_off[p], r1 = part_off[p + 1];
+  if (fraction <= 0.4) {
+    int32_t cfd = 0;
+    bool started = false;
+    for (int64_t row = r0; row < r1; row++) {
+      int c = cr[row];
+      while (c > 0) {
+        if (!started) {  // the lazy GapSampling is built at the partition's first item
+          cfd = gap();
+          started = true;
+        }
+        if (cfd >= c) {
+          cfd -= c;
+          c = 0;
+        } else {
+          c -= cfd + 1;
+          cfd = gap();
+          take(row);
+        }
+      }
+    }
+  } else {
+    for (int64_t row = r0; row < r1; row++)
+      for (int k = cr[row]; k > 0; k--)
+        if (next_double() <= fraction) take(row);
+  }
+}
+
+void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, const int64_t* d_part_off,
+                         int P, const int32_t* d_reps, int nrep, const uint64_t* d_part_state,
+                         const double* d_frac, const void* codes, int code_bytes, int32_t S,
+                         const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax,
+                         const int64_t* d_vcoff, uint32_t* vc) {
+  const int64_t threads = (int64_t)nrep * P;
+  if (threads == 0) return;
+  hipLaunchKernelGGL(k_split_sample, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st, counts,
+                     N, d_part_off, P, d_reps, nrep, d_part_state, d_frac, (const uint8_t*)codes,
+                     code_bytes, S, d_sub, d_Fr, Fmax, d_vcoff, vc);
+}
+
+// ======================================================================
 // Bernoulli sampler: XORShiftRandom is GF(2)-linear; a thread jumps its
 // stream to row j0 with precomputed M^(2^k) matrices and then steps 256 rows.
 // ======================================================================

@@ -105,9 +105,12 @@ class _DecisionTreeParams(Params):
         return self.set("minInfoGain", float(v))
 
     def setSeed(self, v):
-        # DecisionTree's seed only drives split-finding sampling for subbags larger
-        # than max(maxBins^2, 10000) rows, which the engine replaces.
+        # DecisionTree's seed drives RandomForest.findSplits' split-finding sample of
+        # subbags larger than max(maxBins^2, 10000) rows (k_split_sample).
         return self.set("seed", int(v))
+
+    def getSeed(self):
+        return self.get("seed")
 
     def getMaxDepth(self):
         return self.get("maxDepth")
@@ -410,7 +413,8 @@ class _BaggingEstimator(_BaggingParams):
                     subspace_bug_compat=bug_compat, partition_offsets=part,
                     max_depth=bl.getMaxDepth(), max_bins=bl.getMaxBins(),
                     min_instances_per_node=bl.getMinInstancesPerNode(),
-                    min_info_gain=bl.getMinInfoGain(), impurity=bl.impurity_code)
+                    min_info_gain=bl.getMinInfoGain(), impurity=bl.impurity_code,
+                    tree_seed=bl.getSeed())
             except Exception as e:  # surfaced like ThreadUtils.awaitResult (BaggingRegressor.scala:191)
                 errors.append(e)
 

@@ -7,10 +7,11 @@ import oracle
 FIELDS = ("id", "left", "right", "feature", "threshold", "prediction", "impurity", "gain")
 
 
-def oracle_forest(X, y, counts, subspaces, depth, bins, classification, min_inst=1, min_gain=0.0):
+def oracle_forest(X, y, counts, subspaces, depth, bins, classification, min_inst=1, min_gain=0.0,
+                  part=None, dt_seed=None):
     return oracle.fit(X, y, counts, subspaces, max_depth=depth, max_bins=bins,
                       min_instances_per_node=min_inst, min_info_gain=min_gain,
-                      classification=classification)
+                      classification=classification, part=part, dt_seed=dt_seed)
 
 
 def assert_forest_equal(native, orf, rel_tol_pred=0.0):

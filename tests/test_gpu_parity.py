@@ -273,3 +273,28 @@ def test_row_lane_histogram_modes(ctx, cpusmall, monkeypatch, rl):
     counts = oracle.bag(True, 1.0, 0, 3, SEED_REG, [0, 16000], 16000)
     subs = [oracle.subspace(1.0, 100, SEED_REG + i) for i in range(3)]
     assert_forest_equal(forest, oracle_forest(Xr, yr, counts, subs, 7, 32, False))
+
+
+@pytest.mark.parametrize("n_rows,cls,P", [(30000, False, 3), (16000, True, 2), (40000, False, 1)])
+def test_sampled_split_finding(ctx, n_rows, cls, P):
+    """Subbags larger than max(maxBins^2, 10^4) rows: thresholds from RandomForest.findSplits'
+    RDD.sample (k_split_sample: per-partition BernoulliSampler seeded through
+    java.util.Random, GapSampling at fraction <= 0.4, per-item draws above), continuous
+    features with zeros, bit-exact against the oracle's restatement."""
+    rng = np.random.default_rng(n_rows + P)
+    F = 5
+    X = np.round(rng.normal(size=(n_rows, F)), 2)
+    X[rng.random((n_rows, F)) < 0.15] = 0.0
+    y = (rng.integers(0, 5, n_rows) if cls else rng.integers(-256, 256, n_rows) / 16).astype(np.float64)
+    part = [int(round(i * n_rows / P)) for i in range(P + 1)]
+    L = 3
+    seed = SEED_CLS if cls else SEED_REG
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    forest = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=seed, learner_begin=0,
+                     learner_end=L, partition_offsets=part, max_depth=6, max_bins=32,
+                     impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    counts = oracle.bag(True, 1.0, 0, L, seed, part, n_rows)
+    assert oracle.split_sample_fraction(int(counts[0].sum()), 32) < 1.0
+    subs = [oracle.subspace(1.0, F, seed + i) for i in range(L)]
+    orf = oracle_forest(X, y, counts, subs, 6, 32, cls, part=part)
+    assert_forest_equal(forest, orf)

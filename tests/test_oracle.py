@@ -234,3 +234,61 @@ def test_synthetic_generator_shape_and_levels():
     assert (np.ldexp(y, 6) == np.floor(np.ldexp(y, 6))).all()
     Xc, yc = synthetic.generate(4000, 20, seed=9, num_classes=7)
     assert (X == Xc).all() and set(np.unique(yc)) <= set(range(7))
+
+
+# ---------------------------------------------------------------- split-finding sample
+def test_java_random_known_answers():
+    """java.util.Random(42): nextLong() = -5025562857975149833, -5843495416241995736."""
+    jr = po.JavaRandom(42)
+    assert jr.next_long() == -5025562857975149833
+    assert jr.next_long() == -5843495416241995736
+    seeds = oracle.split_sample_seeds(oracle.DT_SEED_REGRESSOR, 3)
+    jr = po.JavaRandom(po.XORShiftRandom(oracle.DT_SEED_REGRESSOR).next_int())
+    assert list(seeds) == [jr.next_long() for _ in range(3)]
+
+
+@pytest.mark.parametrize("n_rows,P", [(30000, 3), (13000, 2)])
+def test_split_sample_matches_python_twin(n_rows, P):
+    """RandomForest.findSplits' sample (GapSampling at fraction <= 0.4, per-item
+    nextDouble above): C oracle == pure-Python twin, row multiplicities exact."""
+    rng = np.random.default_rng(n_rows)
+    counts = rng.poisson(1.0, n_rows).astype(np.uint8)
+    off = [int(round(i * n_rows / P)) for i in range(P + 1)]
+    n = int(counts.sum())
+    f = oracle.split_sample_fraction(n, 32)
+    assert f == po.split_sample_fraction(n, 32) and f < 1.0
+    assert (f <= 0.4) == (n_rows == 30000)
+    got = oracle.split_sample(counts, off, oracle.DT_SEED_REGRESSOR, f)
+    want = po.split_sample(counts, off, oracle.DT_SEED_REGRESSOR, f)
+    assert list(got) == want
+    assert (got <= counts).all()
+    # the expected size is f * n = 10000; a Bernoulli(f) sample lands within a few sigma
+    assert abs(int(got.sum()) - 10000) < 500
+
+
+def test_sampled_split_finding_in_fit():
+    """A subbag larger than max(maxBins^2, 10^4) with continuous features: the oracle's
+    thresholds are those of findSplitsForContinuousFeature over the sample (zeros implied
+    by numSamples = (fraction * n).toInt), not over the whole subbag."""
+    rng = np.random.default_rng(5)
+    N, F = 24000, 3
+    X = np.round(rng.normal(size=(N, F)), 3)
+    X[rng.random((N, F)) < 0.2] = 0.0
+    y = rng.integers(0, 64, N).astype(np.float64) / 8
+    counts = rng.poisson(1.0, (1, N)).astype(np.uint8)
+    off = [0, 9000, 24000]
+    orf = oracle.fit(X, y, counts, [np.arange(F)], max_depth=2, max_bins=16, part=off)
+    n = int(counts.sum())
+    frac = po.split_sample_fraction(n, 16)
+    mult = po.split_sample(counts[0], off, oracle.DT_SEED_REGRESSOR, frac)
+    ns = int(frac * n)
+    nodes, _ = orf.tree(0)
+    root = nodes[0]
+    assert root["feature"] >= 0
+    f = int(root["feature"])
+    vm = {}
+    for r in range(N):
+        if mult[r] and X[r, f] != 0.0:
+            vm[X[r, f]] = vm.get(X[r, f], 0) + mult[r]
+    thr = po.find_splits(vm, n, 16, num_samples=ns)
+    assert root["threshold"] in thr
