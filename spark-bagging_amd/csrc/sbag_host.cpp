@@ -1328,10 +1328,32 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       TRY(h2d(c, d_svcoff, vcoff.data(), vcoff.size()));
       HIP_TRY(hipMemsetAsync(d_vcs, 0, (size_t)std::max<int64_t>(vc_total, 1) * 4, c->stream));
       int h = tm.begin(T_VC);
+      // a replica's value counts accumulate in LDS when they fit in 64 KB
+      int64_t maxw = 0, maxreq = 0;
+      for (int r : reps) {
+        maxw = std::max(maxw, vcoff[(size_t)r * Fmax + h_Fr[r]] - vcoff[(size_t)r * Fmax]);
+        const int64_t mpb = std::min<int64_t>(tp.max_bins, nw[r]);
+        maxreq = std::max(maxreq, std::max<int64_t>(mpb * mpb, 10000));
+      }
+      const int lds_words = maxw <= 16384 ? (int)maxw : 0;
+      // sampled rows per replica: Binomial(n, required / n), capacity 8 sigma above
+      const int64_t cap = maxreq + 8 * (int64_t)std::ceil(std::sqrt((double)maxreq)) + 1024;
+      uint32_t *d_srows, *d_snr;
+      TRY(ws_typed(c, "ss_rows", (size_t)reps.size() * cap, &d_srows));
+      TRY(ws_typed(c, "ss_nrows", reps.size(), &d_snr));
+      HIP_TRY(hipMemsetAsync(d_snr, 0, reps.size() * 4, c->stream));
       launch_split_sample(c->stream, d_counts, N, d_spoff, P, d_reps, (int)reps.size(), d_pst, d_frac,
-                          ds->d_codes, ds->code_bytes, ds->S, d_sub, d_Fr, Fmax, d_svcoff, d_vcs);
+                          d_srows, cap, d_snr);
+      HIP_TRY(hipGetLastError());
+      launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, (int)reps.size(), ds->d_codes,
+                             ds->code_bytes, ds->S, d_sub, d_Fr, Fmax, d_svcoff, d_vcs, lds_words);
       HIP_TRY(hipGetLastError());
       tm.end(h);
+      std::vector<uint32_t> snr(reps.size());
+      TRY(d2h(c, snr.data(), d_snr, snr.size()));
+      for (uint32_t k : snr)
+        if ((int64_t)k > cap)
+          return fail(SBAG_EDEVICE, "split-finding sample exceeds its capacity");
       vcs.assign((size_t)std::max<int64_t>(vc_total, 1), 0);
       TRY(d2h(c, vcs.data(), d_vcs, vcs.size()));
       if (getenv("SBAG_DEBUG_SAMPLE")) {

@@ -161,9 +161,12 @@ void launch_fill(hipStream_t st, uint8_t* p, uint8_t v, int64_t n);
 void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, const int64_t* d_part_off,
                          int P, const int32_t* d_reps, int nrep, const uint64_t* d_part_state,
                          const double* d_frac /*[nrep][2]: fraction, log1p(-fraction)*/,
-                         const void* codes, int code_bytes, int32_t S,
-                         const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax,
-                         const int64_t* d_vcoff, uint32_t* vc);
+                         uint32_t* d_rows /*[nrep][cap]*/, int64_t cap, uint32_t* d_nrows);
+void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
+                            const uint32_t* d_nrows, const int32_t* d_reps, int nrep,
+                            const void* codes, int code_bytes, int32_t S, const int32_t* d_sub,
+                            const int32_t* d_Fr, int32_t Fmax, const int64_t* d_vcoff, uint32_t* vc,
+                            int lds_words);
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
                     unsigned long long* d_wsum, unsigned int* d_cmax, unsigned long long* d_sqsum);

@@ -468,16 +468,25 @@ __device__ __forceinline__ uint64_t xs_step_s(uint64_t s) {
   return s;
 }
 
+// Phase 1, a thread per (replica, partition): the walk appends every sampled item's row
+// to the replica's list (order is irrelevant to the counts).  It skips whole 64-row
+// chunks (one cache line of counts) while the current gap covers them.  Phase 2
+// (k_split_sample_vc) gathers the sampled rows' value codes with every lane busy: the
+// walk's lanes sample at different times, so gathering inside it serialised the wave.
+__device__ __forceinline__ uint32_t bytesum4(uint32_t x) {
+  x = (x & 0x00ff00ffu) + ((x >> 8) & 0x00ff00ffu);
+  return (x & 0xffffu) + (x >> 16);
+}
+
 __global__ __launch_bounds__(64) void k_split_sample(
     const uint8_t* __restrict__ counts, int64_t N, const int64_t* __restrict__ part_off, int P,
-    const int32_t* __restrict__ reps, int nrep, const uint64_t* __restrict__ part_state,
-    const double* __restrict__ frac, const uint8_t* __restrict__ codes, int code_bytes, int32_t S,
-    const int32_t* __restrict__ sub, const int32_t* __restrict__ Fr, int32_t Fmax,
-    const int64_t* __restrict__ vcoff, uint32_t* __restrict__ vc) {
-  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (t >= (int64_t)nrep * P) return;
-  const int ri = (int)(t / P), p = (int)(t % P);
+    const int32_t* __restrict__ reps, const uint64_t* __restrict__ part_state,
+    const double* __restrict__ frac, uint32_t* __restrict__ rows_out, int64_t cap,
+    uint32_t* __restrict__ nrows) {
+  const int ri = blockIdx.y;
   const int r = reps[ri];
+  const int p = (int)blockIdx.x * 64 + (int)threadIdx.x;
+  if (p >= P) return;
   // per replica: fraction = required / numExamples and log1p(-fraction) (host libm, as the
   // oracle computes it)
   const double fraction = frac[2 * ri], lnq = frac[2 * ri + 1];
@@ -493,24 +502,17 @@ __global__ __launch_bounds__(64) void k_split_sample(
     const double u = fmax(next_double(), 5e-11);
     return (int32_t)(log(u) / lnq);
   };
-  const int fr = Fr[r];
-  const int32_t* sr = sub + (int64_t)r * Fmax;
-  const int64_t* vo = vcoff + (int64_t)r * Fmax;
+  uint32_t* out = rows_out + (int64_t)ri * cap;
   auto take = [&](int64_t row) {
-    for (int fl = 0; fl < fr; fl++) {
-      const int64_t pos = row * S + sr[fl];
-      const uint32_t code = code_bytes == 1 ? (uint32_t)codes[pos]
-                                            : (uint32_t)((const uint16_t*)codes)[pos];
-      atomicAdd(&vc[vo[fl] + code], 1u);
-    }
+    const uint32_t k = atomicAdd(&nrows[ri], 1u);
+    if (k < (uint64_t)cap) out[k] = (uint32_t)row;
   };
   const uint8_t* cr = counts + (int64_t)r * N;
   const int64_t r0 = part_off[p], r1 = part_off[p + 1];
   if (fraction <= 0.4) {
     int32_t cfd = 0;
     bool started = false;
-    for (int64_t row = r0; row < r1; row++) {
-      int c = cr[row];
+    auto row_items = [&](int64_t row, int c) {
       while (c > 0) {
         if (!started) {  // the lazy GapSampling is built at the partition's first item
           cfd = gap();
@@ -525,6 +527,33 @@ __global__ __launch_bounds__(64) void k_split_sample(
           take(row);
         }
       }
+    };
+    int64_t row = r0;
+    while (row < r1) {
+      if ((((uintptr_t)(cr + row)) & 63) == 0 && row + 64 <= r1) {
+        const uint4* q = (const uint4*)(cr + row);
+        uint32_t w[16];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint4 v = q[u];
+          w[4 * u] = v.x;
+          w[4 * u + 1] = v.y;
+          w[4 * u + 2] = v.z;
+          w[4 * u + 3] = v.w;
+        }
+        uint32_t sum = 0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) sum += bytesum4(w[u]);
+        if (started ? (uint32_t)cfd >= sum : sum == 0u) {
+          if (started) cfd -= (int32_t)sum;
+        } else {
+          for (int k = 0; k < 64; k++) row_items(row + k, (int)((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
+        }
+        row += 64;
+      } else {
+        row_items(row, cr[row]);
+        row++;
+      }
     }
   } else {
     for (int64_t row = r0; row < r1; row++)
@@ -533,16 +562,73 @@ __global__ __launch_bounds__(64) void k_split_sample(
   }
 }
 
+// Phase 2, grid (sample chunks of 256, replicas): a thread per sampled item adds its value
+// codes to the replica's counts, in LDS when they fit (`lds_words`), flushed once.
+__global__ __launch_bounds__(256) void k_split_sample_vc(
+    const uint32_t* __restrict__ rows, int64_t cap, const uint32_t* __restrict__ nrows,
+    const int32_t* __restrict__ reps, const uint8_t* __restrict__ codes, int code_bytes, int32_t S,
+    const int32_t* __restrict__ sub, const int32_t* __restrict__ Fr, int32_t Fmax,
+    const int64_t* __restrict__ vcoff, uint32_t* __restrict__ vc, int lds_words) {
+  extern __shared__ uint32_t s_vc[];
+  const int ri = blockIdx.y;
+  const int r = reps[ri];
+  const int64_t n = min((int64_t)nrows[ri], cap);
+  const int64_t k0 = (int64_t)blockIdx.x * 256;
+  if (k0 >= n) return;  // whole block
+  const int fr = Fr[r];
+  const int32_t* sr = sub + (int64_t)r * Fmax;
+  const int64_t* vo = vcoff + (int64_t)r * Fmax;
+  const int64_t vbase = vo[0];
+  const int nw = (int)(vcoff[(int64_t)r * Fmax + fr] - vbase);
+  const bool use_lds = nw <= lds_words;
+  if (use_lds)
+    for (int i = threadIdx.x; i < nw; i += 256) s_vc[i] = 0u;
+  __syncthreads();
+  const int64_t k = k0 + threadIdx.x;
+  if (k < n) {
+    const int64_t row = rows[(int64_t)ri * cap + k];
+    for (int fl = 0; fl < fr; fl++) {
+      const int64_t pos = row * S + sr[fl];
+      const uint32_t code = code_bytes == 1 ? (uint32_t)codes[pos]
+                                            : (uint32_t)((const uint16_t*)codes)[pos];
+      if (use_lds)
+        atomicAdd(&s_vc[vo[fl] - vbase + code], 1u);
+      else
+        atomicAdd(&vc[vo[fl] + code], 1u);
+    }
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nw; i += 256)
+      if (s_vc[i]) atomicAdd(&vc[vbase + i], s_vc[i]);
+  }
+}
+
 void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, const int64_t* d_part_off,
                          int P, const int32_t* d_reps, int nrep, const uint64_t* d_part_state,
-                         const double* d_frac, const void* codes, int code_bytes, int32_t S,
-                         const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax,
-                         const int64_t* d_vcoff, uint32_t* vc) {
-  const int64_t threads = (int64_t)nrep * P;
-  if (threads == 0) return;
-  hipLaunchKernelGGL(k_split_sample, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st, counts,
-                     N, d_part_off, P, d_reps, nrep, d_part_state, d_frac, (const uint8_t*)codes,
-                     code_bytes, S, d_sub, d_Fr, Fmax, d_vcoff, vc);
+                         const double* d_frac, uint32_t* d_rows, int64_t cap, uint32_t* d_nrows) {
+  if (nrep == 0 || P == 0) return;
+  const dim3 grid((unsigned)((P + 63) / 64), (unsigned)nrep);
+  hipLaunchKernelGGL(k_split_sample, grid, dim3(64), 0, st, counts, N, d_part_off, P, d_reps,
+                     d_part_state, d_frac, d_rows, cap, d_nrows);
+}
+
+void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
+                            const uint32_t* d_nrows, const int32_t* d_reps, int nrep,
+                            const void* codes, int code_bytes, int32_t S, const int32_t* d_sub,
+                            const int32_t* d_Fr, int32_t Fmax, const int64_t* d_vcoff, uint32_t* vc,
+                            int lds_words) {
+  if (nrep == 0) return;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_split_sample_vc,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    attr_set = true;
+  }
+  const dim3 grid((unsigned)((cap + 255) / 256), (unsigned)nrep);
+  hipLaunchKernelGGL(k_split_sample_vc, grid, dim3(256), (size_t)lds_words * 4, st, d_rows, cap,
+                     d_nrows, d_reps, (const uint8_t*)codes, code_bytes, S, d_sub, d_Fr, Fmax,
+                     d_vcoff, vc, lds_words);
 }
 
 // ======================================================================
