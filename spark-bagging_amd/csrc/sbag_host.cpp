@@ -1342,8 +1342,10 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       TRY(ws_typed(c, "ss_rows", (size_t)reps.size() * cap, &d_srows));
       TRY(ws_typed(c, "ss_nrows", reps.size(), &d_snr));
       HIP_TRY(hipMemsetAsync(d_snr, 0, reps.size() * 4, c->stream));
-      launch_split_sample(c->stream, d_counts, N, d_spoff, P, d_reps, (int)reps.size(), d_pst, d_frac,
-                          d_srows, cap, d_snr);
+      uint16_t* d_gsums;
+      TRY(ws_typed(c, "ss_gsums", (size_t)split_sample_groups((int64_t)R * N), &d_gsums));
+      launch_split_sample(c->stream, d_counts, N, R, d_spoff, P, d_reps, (int)reps.size(), d_pst,
+                          d_frac, d_gsums, d_srows, cap, d_snr);
       HIP_TRY(hipGetLastError());
       launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, (int)reps.size(), ds->d_codes,
                              ds->code_bytes, ds->S, d_sub, d_Fr, Fmax, d_svcoff, d_vcs, lds_words);

@@ -158,9 +158,13 @@ void launch_bernoulli(hipStream_t st, uint8_t* counts, int64_t N, const int64_t*
                       const int64_t* d_chunk_pre, int P, int64_t chunks_total, int R,
                       int learner0, int64_t seed, double ratio, const uint64_t* d_jump);
 void launch_fill(hipStream_t st, uint8_t* p, uint8_t v, int64_t n);
-void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, const int64_t* d_part_off,
-                         int P, const int32_t* d_reps, int nrep, const uint64_t* d_part_state,
+// 256-byte groups of a counts buffer of `bytes` bytes, padded to whole 8-group chunks
+inline int64_t split_sample_groups(int64_t bytes) { return ((bytes + 255) / 256 + 7) / 8 * 8; }
+void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, int64_t R,
+                         const int64_t* d_part_off, int P, const int32_t* d_reps, int nrep,
+                         const uint64_t* d_part_state,
                          const double* d_frac /*[nrep][2]: fraction, log1p(-fraction)*/,
+                         uint16_t* d_gsums /*[split_sample_groups(R * N)]*/,
                          uint32_t* d_rows /*[nrep][cap]*/, int64_t cap, uint32_t* d_nrows);
 void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                             const uint32_t* d_nrows, const int32_t* d_reps, int nrep,

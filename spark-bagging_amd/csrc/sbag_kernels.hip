@@ -481,8 +481,9 @@ __device__ __forceinline__ uint32_t bytesum4(uint32_t x) {
 __global__ __launch_bounds__(64) void k_split_sample(
     const uint8_t* __restrict__ counts, int64_t N, const int64_t* __restrict__ part_off, int P,
     const int32_t* __restrict__ reps, const uint64_t* __restrict__ part_state,
-    const double* __restrict__ frac, uint32_t* __restrict__ rows_out, int64_t cap,
-    uint32_t* __restrict__ nrows) {
+    const double* __restrict__ frac, const uint16_t* __restrict__ gsums,
+    uint32_t* __restrict__ rows_out, int64_t cap, uint32_t* __restrict__ nrows) {
+  __shared__ uint32_t s_take[64 * 33];
   const int ri = blockIdx.y;
   const int r = reps[ri];
   const int p = (int)blockIdx.x * 64 + (int)threadIdx.x;
@@ -503,56 +504,147 @@ __global__ __launch_bounds__(64) void k_split_sample(
     return (int32_t)(log(u) / lnq);
   };
   uint32_t* out = rows_out + (int64_t)ri * cap;
+  // sampled rows wait in the thread's LDS buffer: one returning atomic per 32 samples
+  // (lanes sample at different times, so per-sample atomics serialised the wave)
+  uint32_t* tb = s_take + threadIdx.x * 33;
+  int nt = 0;
+  auto flush = [&]() {
+    if (nt == 0) return;
+    const uint32_t k = atomicAdd(&nrows[ri], (uint32_t)nt);
+    for (int i = 0; i < nt; i++)
+      if ((int64_t)k + i < cap) out[k + i] = tb[i];
+    nt = 0;
+  };
   auto take = [&](int64_t row) {
-    const uint32_t k = atomicAdd(&nrows[ri], 1u);
-    if (k < (uint64_t)cap) out[k] = (uint32_t)row;
+    tb[nt++] = (uint32_t)row;
+    if (nt == 32) flush();
   };
   const uint8_t* cr = counts + (int64_t)r * N;
   const int64_t r0 = part_off[p], r1 = part_off[p + 1];
   if (fraction <= 0.4) {
-    int32_t cfd = 0;
-    bool started = false;
-    auto row_items = [&](int64_t row, int c) {
-      while (c > 0) {
-        if (!started) {  // the lazy GapSampling is built at the partition's first item
-          cfd = gap();
-          started = true;
-        }
-        if (cfd >= c) {
-          cfd -= c;
-          c = 0;
-        } else {
-          c -= cfd + 1;
-          cfd = gap();
-          take(row);
-        }
-      }
-    };
-    int64_t row = r0;
-    while (row < r1) {
-      if ((((uintptr_t)(cr + row)) & 63) == 0 && row + 64 <= r1) {
-        const uint4* q = (const uint4*)(cr + row);
-        uint32_t w[16];
+    // Item positions: the partition's rows in order, row i standing for counts[i] items.
+    // GapSampling takes items g1, g1 + 1 + g2, ... (the gaps are drawn in order, the
+    // first at the first item; an empty partition takes nothing either way), so the lanes
+    // step in lockstep from one taken item to the next.  A lane finds the 256-row group
+    // holding its target from the group sums (8 per 16-byte chunk, k_group_sums; the
+    // partition's head and tail groups are summed here with the rows outside it masked),
+    // then the word and the byte inside the group's counts.
+    const int64_t off0 = (int64_t)r * N + r0, off1 = (int64_t)r * N + r1;  // byte offsets
+    if (off1 > off0) {
+      const int64_t G0 = off0 >> 8, G1 = (off1 - 1) >> 8;
+      uint4 v[16];
+      auto load_group = [&](int64_t G) {
+        const uint4* q = (const uint4*)(counts + (G << 8));
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint4 v = q[u];
-          w[4 * u] = v.x;
-          w[4 * u + 1] = v.y;
-          w[4 * u + 2] = v.z;
-          w[4 * u + 3] = v.w;
-        }
-        uint32_t sum = 0;
+        for (int u = 0; u < 16; u++) v[u] = q[u];
+        if ((G << 8) < off0 || (G << 8) + 256 > off1) {
 #pragma unroll
-        for (int u = 0; u < 16; u++) sum += bytesum4(w[u]);
-        if (started ? (uint32_t)cfd >= sum : sum == 0u) {
-          if (started) cfd -= (int32_t)sum;
-        } else {
-          for (int k = 0; k < 64; k++) row_items(row + k, (int)((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
+          for (int u = 0; u < 16; u++) {
+            uint32_t* w = (uint32_t*)&v[u];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              const int64_t a0 = (G << 8) + 16 * u + 4 * e;
+              uint32_t m = 0;
+#pragma unroll
+              for (int bb = 0; bb < 4; bb++)
+                m |= (a0 + bb >= off0 && a0 + bb < off1) ? (0xffu << (8 * bb)) : 0u;
+              w[e] &= m;
+            }
+          }
         }
-        row += 64;
-      } else {
-        row_items(row, cr[row]);
-        row++;
+      };
+      auto vsum = [&]() {
+        uint32_t t = 0;
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+          t += bytesum4(v[u].x) + bytesum4(v[u].y) + bytesum4(v[u].z) + bytesum4(v[u].w);
+        return t;
+      };
+      load_group(G0);
+      const uint32_t head = vsum();
+      load_group(G1);
+      const uint32_t tail = vsum();
+      int64_t vg = G1;  // the group held in v
+      uint32_t cs[8];
+      const int64_t K1 = G1 >> 3;
+      int64_t K = G0 >> 3;
+      auto load_chunk = [&]() {
+        const uint4 q = ((const uint4*)gsums)[K];
+        const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int64_t G = K * 8 + j;
+          const uint32_t gsv = (qq[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+          cs[j] = (G < G0 || G > G1) ? 0u : G == G0 ? head : G == G1 ? tail : gsv;
+        }
+      };
+      auto csum = [&]() {
+        uint32_t t = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) t += cs[j];
+        return t;
+      };
+      load_chunk();
+      uint32_t ksum = csum();
+      int64_t base = 0;  // items before chunk K
+      int64_t target = gap();
+      while (true) {
+        while (base + ksum <= target) {
+          base += ksum;
+          if (++K > K1) break;
+          load_chunk();
+          ksum = csum();
+        }
+        if (K > K1) break;
+        int gsel = 0;
+        int64_t gb = base;
+        {
+          int64_t acc = base;
+          bool found = false;
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            const bool hit = !found && target < acc + cs[j];
+            gsel = hit ? j : gsel;
+            gb = hit ? acc : gb;
+            found = found || hit;
+            acc += cs[j];
+          }
+        }
+        const int64_t G = K * 8 + gsel;
+        if (G != vg) {
+          load_group(G);
+          vg = G;
+        }
+        uint32_t o = (uint32_t)(target - gb);  // item offset inside the group
+        int widx = 0;
+        uint32_t wsel = 0;
+        {
+          uint32_t acc = 0;
+          bool found = false;
+#pragma unroll
+          for (int u = 0; u < 16; u++) {
+            const uint32_t ww[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              const uint32_t ws = bytesum4(ww[e]);
+              const bool hit = !found && o < acc + ws;
+              widx = hit ? 4 * u + e : widx;
+              wsel = hit ? ww[e] : wsel;
+              o = hit ? o - acc : o;
+              found = found || hit;
+              acc += found ? 0u : ws;
+            }
+          }
+        }
+        int bsel = 3;
+#pragma unroll
+        for (int bb = 2; bb >= 0; bb--) {
+          uint32_t pre = 0;
+          for (int t = 0; t <= bb; t++) pre += (wsel >> (8 * t)) & 0xffu;
+          bsel = o < pre ? bb : bsel;
+        }
+        take((G << 8) + 4 * widx + bsel - (int64_t)r * N);
+        target += 1 + (int64_t)gap();
       }
     }
   } else {
@@ -560,10 +652,12 @@ __global__ __launch_bounds__(64) void k_split_sample(
       for (int k = cr[row]; k > 0; k--)
         if (next_double() <= fraction) take(row);
   }
+  flush();
 }
 
-// Phase 2, grid (sample chunks of 256, replicas): a thread per sampled item adds its value
-// codes to the replica's counts, in LDS when they fit (`lds_words`), flushed once.
+// Phase 2, grid (sample chunks of kSvcRows, replicas): each sampled row adds its value codes
+// to the replica's counts, in LDS when they fit (`lds_words`), flushed once.
+constexpr int kSvcRows = 1024;  // sampled rows per k_split_sample_vc workgroup
 __global__ __launch_bounds__(256) void k_split_sample_vc(
     const uint32_t* __restrict__ rows, int64_t cap, const uint32_t* __restrict__ nrows,
     const int32_t* __restrict__ reps, const uint8_t* __restrict__ codes, int code_bytes, int32_t S,
@@ -573,7 +667,7 @@ __global__ __launch_bounds__(256) void k_split_sample_vc(
   const int ri = blockIdx.y;
   const int r = reps[ri];
   const int64_t n = min((int64_t)nrows[ri], cap);
-  const int64_t k0 = (int64_t)blockIdx.x * 256;
+  const int64_t k0 = (int64_t)blockIdx.x * kSvcRows;
   if (k0 >= n) return;  // whole block
   const int fr = Fr[r];
   const int32_t* sr = sub + (int64_t)r * Fmax;
@@ -584,17 +678,26 @@ __global__ __launch_bounds__(256) void k_split_sample_vc(
   if (use_lds)
     for (int i = threadIdx.x; i < nw; i += 256) s_vc[i] = 0u;
   __syncthreads();
-  const int64_t k = k0 + threadIdx.x;
-  if (k < n) {
-    const int64_t row = rows[(int64_t)ri * cap + k];
-    for (int fl = 0; fl < fr; fl++) {
-      const int64_t pos = row * S + sr[fl];
-      const uint32_t code = code_bytes == 1 ? (uint32_t)codes[pos]
-                                            : (uint32_t)((const uint16_t*)codes)[pos];
-      if (use_lds)
-        atomicAdd(&s_vc[vo[fl] - vbase + code], 1u);
-      else
-        atomicAdd(&vc[vo[fl] + code], 1u);
+  // lane = feature within a 64-feature group, wave = every 4th sampled row: a row's
+  // codes are read by one wave from its cache line
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t k1 = min(n, k0 + kSvcRows);
+  for (int fg = 0; fg < fr; fg += 64) {
+    const int fl = fg + lane;
+    if (fl >= fr) break;
+    const int64_t col = sr[fl];
+    const uint32_t* rr = rows + (int64_t)ri * cap;
+    auto code_at = [&](int64_t k) {
+      const int64_t pos = (int64_t)rr[k] * S + col;
+      return code_bytes == 1 ? (uint32_t)codes[pos] : (uint32_t)((const uint16_t*)codes)[pos];
+    };
+    if (use_lds) {
+      uint32_t* dst = s_vc + (vo[fl] - vbase);
+#pragma unroll 4
+      for (int64_t k = k0 + wv; k < k1; k += 4) atomicAdd(&dst[code_at(k)], 1u);
+    } else {
+      uint32_t* dst = vc + vo[fl];
+      for (int64_t k = k0 + wv; k < k1; k += 4) atomicAdd(&dst[code_at(k)], 1u);
     }
   }
   if (use_lds) {
@@ -604,13 +707,36 @@ __global__ __launch_bounds__(256) void k_split_sample_vc(
   }
 }
 
-void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, const int64_t* d_part_off,
-                         int P, const int32_t* d_reps, int nrep, const uint64_t* d_part_state,
-                         const double* d_frac, uint32_t* d_rows, int64_t cap, uint32_t* d_nrows) {
+// byte sums of the counts buffer's 256-byte groups (k_split_sample's skip index); groups
+// past the buffer (the padding to whole 8-group chunks) are 0
+__global__ __launch_bounds__(256) void k_group_sums(const uint8_t* __restrict__ counts,
+                                                    int64_t bytes, uint16_t* __restrict__ gsums,
+                                                    int64_t ngroups) {
+  const int64_t G = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (G >= ngroups) return;
+  uint32_t t = 0;
+  if ((G << 8) < bytes) {
+    const uint4* q = (const uint4*)(counts + (G << 8));
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const uint4 v = q[u];
+      t += bytesum4(v.x) + bytesum4(v.y) + bytesum4(v.z) + bytesum4(v.w);
+    }
+  }
+  gsums[G] = (uint16_t)t;
+}
+
+void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, int64_t R,
+                         const int64_t* d_part_off, int P, const int32_t* d_reps, int nrep,
+                         const uint64_t* d_part_state, const double* d_frac, uint16_t* d_gsums,
+                         uint32_t* d_rows, int64_t cap, uint32_t* d_nrows) {
   if (nrep == 0 || P == 0) return;
+  const int64_t ng = split_sample_groups(R * N);
+  hipLaunchKernelGGL(k_group_sums, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, st, counts,
+                     R * N, d_gsums, ng);
   const dim3 grid((unsigned)((P + 63) / 64), (unsigned)nrep);
   hipLaunchKernelGGL(k_split_sample, grid, dim3(64), 0, st, counts, N, d_part_off, P, d_reps,
-                     d_part_state, d_frac, d_rows, cap, d_nrows);
+                     d_part_state, d_frac, d_gsums, d_rows, cap, d_nrows);
 }
 
 void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
@@ -625,7 +751,7 @@ void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                                hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
     attr_set = true;
   }
-  const dim3 grid((unsigned)((cap + 255) / 256), (unsigned)nrep);
+  const dim3 grid((unsigned)((cap + kSvcRows - 1) / kSvcRows), (unsigned)nrep);
   hipLaunchKernelGGL(k_split_sample_vc, grid, dim3(256), (size_t)lds_words * 4, st, d_rows, cap,
                      d_nrows, d_reps, (const uint8_t*)codes, code_bytes, S, d_sub, d_Fr, Fmax,
                      d_vcoff, vc, lds_words);

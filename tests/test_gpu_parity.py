@@ -275,7 +275,8 @@ def test_row_lane_histogram_modes(ctx, cpusmall, monkeypatch, rl):
     assert_forest_equal(forest, oracle_forest(Xr, yr, counts, subs, 7, 32, False))
 
 
-@pytest.mark.parametrize("n_rows,cls,P", [(30000, False, 3), (16000, True, 2), (40000, False, 1)])
+@pytest.mark.parametrize("n_rows,cls,P", [(30000, False, 3), (16000, True, 2), (40000, False, 1),
+                                           (400000, False, 7), (250000, True, 5)])
 def test_sampled_split_finding(ctx, n_rows, cls, P):
     """Subbags larger than max(maxBins^2, 10^4) rows: thresholds from RandomForest.findSplits'
     RDD.sample (k_split_sample: per-partition BernoulliSampler seeded through
