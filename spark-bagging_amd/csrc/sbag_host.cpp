@@ -939,8 +939,67 @@ static void build_work(const std::vector<std::pair<int64_t, int64_t>>& segs, int
   w.entries = (double)tot;
 }
 
+// fit_range's request to be called again on halves of its learner range: per-replica bins
+// (thresholds that differ across replicas) of all its replicas exceed the device budget
+static constexpr int kSplitRange = -1000;
+
+// device bytes per-replica bins may take: SBAG_BINS_BUDGET_MB, else 40 % of the device
+static double bins_budget(sbag_ctx* c) {
+  if (const char* e = getenv("SBAG_BINS_BUDGET_MB")) return atof(e) * (1 << 20);
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return 48.0 * (1ull << 30);
+  }
+  return 0.4 * (double)tot;
+}
+
+static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out);
+
+// Learners are independent (seed + i per learner), so a range whose per-replica
+// bins do not fit is fitted as two halves and the trees concatenated in learner order.
 int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
   if (!c || !ds || !fp || !out) return fail(SBAG_EINVAL, "bad arguments");
+  const int st = fit_range(c, ds, fp, out);
+  if (st != kSplitRange) return st;
+  const int lb = fp->sampler.learner_begin, le = fp->sampler.learner_end, mid = lb + (le - lb) / 2;
+  sbag_fit_params h = *fp;
+  h.sampler.learner_end = mid;
+  sbag_forest* a = nullptr;
+  TRY(sbag_fit(c, ds, &h, &a));
+  std::unique_ptr<sbag_forest> fa(a);
+  h.sampler.learner_begin = mid;
+  h.sampler.learner_end = le;
+  sbag_forest* b = nullptr;
+  TRY(sbag_fit(c, ds, &h, &b));
+  std::unique_ptr<sbag_forest> fb(b);
+  for (auto& t : fb->trees) fa->trees.push_back(std::move(t));
+  fa->nclasses = std::max(fa->nclasses, fb->nclasses);
+  sbag_timing& T = fa->timing;
+  const sbag_timing& U = fb->timing;
+  T.total_ms += U.total_ms;
+  T.sample_ms += U.sample_ms;
+  T.valuecount_ms += U.valuecount_ms;
+  T.bin_ms += U.bin_ms;
+  T.compact_ms += U.compact_ms;
+  T.hist_ms += U.hist_ms;
+  T.split_ms += U.split_ms;
+  T.subtract_ms += U.subtract_ms;
+  T.hist_launches += U.hist_launches;
+  T.hist_alg_bytes += U.hist_alg_bytes;
+  T.hist_entries += U.hist_entries;
+  T.hist_upper_bytes += U.hist_upper_bytes;
+  T.levels = std::max(T.levels, U.levels);
+  T.partition_ms += U.partition_ms;
+  T.hist_work_bytes += U.hist_work_bytes;
+  T.fix_ms += U.fix_ms;
+  T.exact_fallbacks += U.exact_fallbacks;
+  T.hist_lds_atomics += U.hist_lds_atomics;
+  *out = fa.release();
+  return SBAG_OK;
+}
+
+static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
   const sbag_tree_params& tp = fp->tree;
   TRY(check_sampler(&fp->sampler));
   if (tp.max_depth < 0 || tp.max_depth > 30)
@@ -1487,9 +1546,16 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
       h_pos = h_pos_codes;
     } else {
       S = row_stride(Fmax);
-      if ((double)R * N * S > 48.0 * (1ull << 30))
-        return fail(SBAG_EUNSUPPORTED, "per-replica binning of this size is not implemented "
-                                       "(thresholds differ across replicas)");
+      // the bins and their column copy, per replica
+      const double need = (double)R * N * S + (double)R * Fmax * ((N + 63) / 64 * 64);
+      if (need > bins_budget(c)) {
+        if (R > 1) {
+          (void)hipEventDestroy(ev_start);
+          (void)hipEventDestroy(ev_stop);
+          return kSplitRange;
+        }
+        return fail(SBAG_EUNSUPPORTED, "per-replica bins of one learner exceed the device budget");
+      }
       TRY(ws_typed(c, "lut", lut.size(), &d_lut));
       TRY(ws_typed(c, "lutoff", vcoff.size(), &d_lutoff));
       TRY(h2d(c, d_lut, lut.data(), lut.size()));

@@ -100,6 +100,25 @@ def test_cpusmall_c1_parity(ctx, cpusmall):
     np.testing.assert_allclose(pred, oracle.predict(orf, X), rtol=1e-5, atol=0)
 
 
+@pytest.mark.parametrize("budget_mb", ["1.5", "0.3"])
+def test_per_replica_bins_over_budget_split_learner_range(ctx, cpusmall, monkeypatch, budget_mb):
+    """cpusmall's thresholds differ across replicas, so bins are per replica; over the
+    device budget (SBAG_BINS_BUDGET_MB) the learner range is fitted in halves (down to one
+    learner per fit at 0.3 MB) and the trees concatenated in learner order."""
+    X, y = cpusmall
+    whole, _, _ = _fit_both(ctx, X, y, 10, replacement=True, ratio=1.0, seed=SEED_REG,
+                            depth=5, bins=32, cls=False)
+    monkeypatch.setenv("SBAG_BINS_BUDGET_MB", budget_mb)
+    forest, orf, _ = _fit_both(ctx, X, y, 10, replacement=True, ratio=1.0, seed=SEED_REG,
+                               depth=5, bins=32, cls=False)
+    assert len(forest) == 10
+    # every sub-range ran its own level loop
+    assert forest.timing()["hist_launches"] > whole.timing()["hist_launches"]
+    assert_forest_equal(forest, orf)
+    np.testing.assert_allclose(nat.predict(ctx, forest, X, nat.AGG_MEAN), oracle.predict(orf, X),
+                               rtol=1e-5, atol=0)
+
+
 def test_cpusmall_reference_grid_point(ctx, cpusmall):
     """One CV grid point of BaggingRegressorSuite.scala:30-38 (depth 10, bins 30, ratio 0.7)."""
     X, y = cpusmall
