@@ -79,7 +79,8 @@ int sbag_subspace(double ratio, int32_t num_features, int64_t seed, int32_t* idx
 
 /* ---- datasets (the DataFrame's label + features columns) ---------------- */
 /* X row-major [num_rows x num_features] fp64, y [num_rows]; copied to HBM as
-   per-feature value codes (exact distinct-value dictionaries) + labels.       */
+   per-feature value codes (exact distinct-value dictionaries; u8, u16 or u32
+   codes by the widest feature) + labels.                                      */
 int sbag_dataset_create(sbag_ctx* ctx, int64_t num_rows, int32_t num_features, const double* X,
                         const double* y, sbag_dataset** out);
 /* Deterministic synthetic data generated directly in HBM (bench workload):

@@ -217,8 +217,9 @@ struct sbag_dataset {
   sbag_ctx* ctx = nullptr;
   int64_t N = 0;
   int32_t F = 0, S = 0;     // S: row stride in code elements
-  int code_bytes = 1;
+  int code_bytes = 1;                     // 4: "wide" (a feature with > 65536 distinct values)
   void* d_codes = nullptr;
+  std::vector<uint32_t> h_codes;          // wide datasets: the codes on the host too [N][S]
   std::vector<std::vector<double>> dict;  // sorted distinct values per feature (-0.0 == 0.0)
   std::vector<int32_t> zero_code;         // code of 0.0, -1 when absent
   std::vector<double> y;
@@ -706,9 +707,7 @@ int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, cons
       if (d[k] == 0.0) ds->zero_code[f] = (int)k;
     ds->dict[f] = std::move(d);
   }
-  if (maxd > 65536)
-    return fail(SBAG_EUNSUPPORTED, "a feature has more than 65536 distinct values");
-  ds->code_bytes = maxd <= 256 ? 1 : 2;
+  ds->code_bytes = maxd <= 256 ? 1 : maxd <= 65536 ? 2 : 4;
   const size_t bytes = (size_t)N * ds->S * ds->code_bytes;
   HIP_TRY(hipMalloc(&ds->d_codes, bytes + 256));  // zero slack: k_hist_rl over-reads rows
   HIP_TRY(hipMemset((uint8_t*)ds->d_codes + bytes, 0, 256));
@@ -722,11 +721,17 @@ int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, cons
         const size_t k = (size_t)(std::lower_bound(d.begin(), d.end(), v) - d.begin());
         if (ds->code_bytes == 1)
           buf[(size_t)i * ds->S + f] = (uint8_t)k;
-        else
+        else if (ds->code_bytes == 2)
           ((uint16_t*)buf.data())[(size_t)i * ds->S + f] = (uint16_t)k;
+        else
+          ((uint32_t*)buf.data())[(size_t)i * ds->S + f] = (uint32_t)k;
       }
     }
     HIP_TRY(hipMemcpy(ds->d_codes, buf.data(), bytes, hipMemcpyHostToDevice));
+    if (ds->code_bytes == 4) {  // split finding gathers the sampled rows' codes on the host
+      ds->h_codes.resize((size_t)N * ds->S);
+      std::memcpy(ds->h_codes.data(), buf.data(), bytes);
+    }
   }
   ds->y.assign(y, y + N);
   analyze_labels(ds.get());
@@ -802,8 +807,9 @@ int sbag_dataset_features(const sbag_dataset* ds, int64_t r0, int64_t r1, double
                     buf.size(), hipMemcpyDeviceToHost));
   for (int64_t i = 0; i < n; i++)
     for (int f = 0; f < ds->F; f++) {
-      const size_t k = ds->code_bytes == 1 ? buf[(size_t)i * ds->S + f]
-                                           : ((uint16_t*)buf.data())[(size_t)i * ds->S + f];
+      const size_t k = ds->code_bytes == 1   ? buf[(size_t)i * ds->S + f]
+                       : ds->code_bytes == 2 ? ((uint16_t*)buf.data())[(size_t)i * ds->S + f]
+                                             : ((uint32_t*)buf.data())[(size_t)i * ds->S + f];
       X[i * ds->F + f] = ds->dict[f][k];
     }
   return SBAG_OK;
@@ -1024,6 +1030,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   HIP_TRY(hipSetDevice(c->device));
   const int64_t N = ds->N;
   const int F = ds->F;
+  // wide datasets (u32 codes): value counts are sparse (code, count) lists built on the
+  // host from the subbag's rows or the split-finding sample's rows, bins are per replica
+  const bool wide = ds->code_bytes == 4;
   const int lb = fp->sampler.learner_begin;
   const int R = fp->sampler.learner_end - lb;
   const int D = tp.max_depth;
@@ -1149,13 +1158,14 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     for (int r = 0; r < R; r++)
       for (int fl = 0; fl < Fmax; fl++) {
         vcoff[(size_t)r * Fmax + fl] = o;
-        if (fl < h_Fr[r]) o += (int64_t)ds->dict[sub[r][fl]].size();
+        if (fl < h_Fr[r] && !wide) o += (int64_t)ds->dict[sub[r][fl]].size();
       }
     vcoff[(size_t)R * Fmax] = o;
   }
   const int64_t vc_total = vcoff[(size_t)R * Fmax];
   int ncmax = 0;
-  for (int f = 0; f < F; f++) ncmax = std::max(ncmax, (int)ds->dict[f].size());
+  if (!wide)
+    for (int f = 0; f < F; f++) ncmax = std::max(ncmax, (int)ds->dict[f].size());
 
   // root "parents": one per replica, no routing, histogram slot = replica
   std::vector<ParentInfo> h_par(R);
@@ -1292,7 +1302,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
           vc[vcoff[(size_t)r * Fmax + fl] + k] = (uint32_t)cnt;
         }
       }
-  } else {
+  } else if (!wide) {
     int h = tm.begin(T_VC);
     HistGeom g;
     if (ds->code_bytes == 1 && hist_geometry(ds->S, Fmax, ncmax, 1, true, g)) {
@@ -1343,6 +1353,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   // findSplitsForContinuousFeature then sees numSamples = (fraction * n).toInt
   std::vector<double> sfrac(R, 1.0);
   std::vector<uint32_t> vcs;
+  // wide datasets: per replica the (row, weight) items split finding counts
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> items(wide ? R : 0);
   {
     std::vector<int32_t> reps;
     std::vector<double> fl2;
@@ -1406,8 +1418,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       launch_split_sample(c->stream, d_counts, N, R, d_spoff, P, d_reps, (int)reps.size(), d_pst,
                           d_frac, d_gsums, d_srows, cap, d_snr);
       HIP_TRY(hipGetLastError());
-      launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, (int)reps.size(), ds->d_codes,
-                             ds->code_bytes, ds->S, d_sub, d_Fr, Fmax, d_svcoff, d_vcs, lds_words);
+      if (!wide)
+        launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, (int)reps.size(), ds->d_codes,
+                               ds->code_bytes, ds->S, d_sub, d_Fr, Fmax, d_svcoff, d_vcs, lds_words);
       HIP_TRY(hipGetLastError());
       tm.end(h);
       std::vector<uint32_t> snr(reps.size());
@@ -1415,6 +1428,15 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       for (uint32_t k : snr)
         if ((int64_t)k > cap)
           return fail(SBAG_EDEVICE, "split-finding sample exceeds its capacity");
+      if (wide) {
+        std::vector<uint32_t> rows((size_t)reps.size() * cap);
+        TRY(d2h(c, rows.data(), d_srows, rows.size()));
+        for (size_t ri = 0; ri < reps.size(); ri++) {
+          auto& it = items[reps[ri]];
+          it.clear();
+          for (uint32_t k = 0; k < snr[ri]; k++) it.emplace_back(rows[ri * cap + k], 1u);
+        }
+      }
       vcs.assign((size_t)std::max<int64_t>(vc_total, 1), 0);
       TRY(d2h(c, vcs.data(), d_vcs, vcs.size()));
       if (getenv("SBAG_DEBUG_SAMPLE")) {
@@ -1436,6 +1458,16 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   std::vector<int32_t> exact(R, 1);
   bool identity = ds->code_bytes == 1;
   int NB = 1;
+  if (wide) {  // subbags within the split-finding limit: their in-bag rows with counts
+    for (int r = 0; r < R; r++) {
+      if (sfrac[r] < 1.0) continue;
+      std::vector<uint64_t> e((size_t)inbag[r]);
+      TRY(d2h(c, e.data(), entA + (size_t)r * cap, e.size()));
+      items[r].resize(e.size());
+      for (size_t k = 0; k < e.size(); k++)
+        items[r][k] = {(uint32_t)e[k], (uint32_t)(e[k] >> 32) & 0xffu};
+    }
+  }
   {
     // replicas are independent: split finding runs on host threads
     const int nth = std::max(1, std::min<int>(R, std::min(16, (int)std::thread::hardware_concurrency())));
@@ -1446,6 +1478,37 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         const bool sampled = sfrac[r] < 1.0;
         // (fraction * numExamples).toInt
         const int64_t nsamp = sampled ? (int64_t)(int32_t)(sfrac[r] * (double)nw[r]) : nw[r];
+        if (wide) {
+          // sparse value counts: the items' codes sorted and merged
+          std::vector<std::pair<uint32_t, uint32_t>> cw;
+          std::vector<double> sv;
+          std::vector<uint32_t> sc;
+          t_id[w] = 0;
+          for (int fl = 0; fl < h_Fr[r]; fl++) {
+            const int g = sub[r][fl];
+            cw.clear();
+            for (const auto& it : items[r])
+              cw.emplace_back(ds->h_codes[(size_t)it.first * ds->S + g], it.second);
+            std::sort(cw.begin(), cw.end());
+            sv.clear();
+            sc.clear();
+            int szero = -1;
+            for (size_t k = 0; k < cw.size(); k++) {
+              if (k > 0 && cw[k].first == cw[k - 1].first) {
+                sc.back() += cw[k].second;
+                continue;
+              }
+              if ((int64_t)cw[k].first == ds->zero_code[g]) szero = (int)sv.size();
+              sv.push_back(ds->dict[g][cw[k].first]);
+              sc.push_back(cw[k].second);
+            }
+            std::vector<double>& t = thr[(size_t)r * Fmax + fl];
+            const int nt = find_splits(sv, sc.data(), szero, nw[r], nsamp, tp.max_bins, t);
+            h_nbins[(size_t)r * Fmax + fl] = nt + 1;
+            t_nb[w] = std::max(t_nb[w], nt + 1);
+          }
+          continue;
+        }
         for (int fl = 0; fl < h_Fr[r]; fl++) {
           const int g = sub[r][fl];
           const size_t o = (size_t)vcoff[(size_t)r * Fmax + fl];
@@ -1478,8 +1541,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     root_done = true;
   }
   // per global feature: is the LUT the same for every replica that uses it?
-  bool shared = true;
-  {
+  bool shared = !wide;
+  if (shared) {
     std::vector<int64_t> first_off(F, -1);
     for (int r = 0; r < R && shared; r++)
       for (int fl = 0; fl < h_Fr[r] && shared; fl++) {
@@ -1556,14 +1619,33 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         }
         return fail(SBAG_EUNSUPPORTED, "per-replica bins of one learner exceed the device budget");
       }
-      TRY(ws_typed(c, "lut", lut.size(), &d_lut));
-      TRY(ws_typed(c, "lutoff", vcoff.size(), &d_lutoff));
-      TRY(h2d(c, d_lut, lut.data(), lut.size()));
-      TRY(h2d(c, d_lutoff, vcoff.data(), vcoff.size()));
       uint8_t* d_b;
       TRY(ws_typed(c, "bins", (size_t)R * N * S, &d_b));
-      launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
-                         d_lut, d_lutoff, d_b, S);
+      if (wide) {
+        // bin(code) = #{t < dict[code]} = #{j : cut_j <= code}, cut_j = #{dict values <= t_j}
+        const int nc = std::max(NB - 1, 1);
+        std::vector<uint32_t> cut((size_t)R * Fmax * nc, 0xffffffffu);
+        for (int r = 0; r < R; r++)
+          for (int fl = 0; fl < h_Fr[r]; fl++) {
+            const auto& d = ds->dict[sub[r][fl]];
+            const auto& t = thr[(size_t)r * Fmax + fl];
+            for (size_t j = 0; j < t.size(); j++)
+              cut[((size_t)r * Fmax + fl) * nc + j] =
+                  (uint32_t)(std::upper_bound(d.begin(), d.end(), t[j]) - d.begin());
+          }
+        uint32_t* d_cut;
+        TRY(ws_typed(c, "cut", cut.size(), &d_cut));
+        TRY(h2d(c, d_cut, cut.data(), cut.size()));
+        launch_materialize_cut(c->stream, (const uint32_t*)ds->d_codes, N, ds->S, d_sub, d_Fr, Fmax,
+                               R, d_cut, nc, d_b, S);
+      } else {
+        TRY(ws_typed(c, "lut", lut.size(), &d_lut));
+        TRY(ws_typed(c, "lutoff", vcoff.size(), &d_lutoff));
+        TRY(h2d(c, d_lut, lut.data(), lut.size()));
+        TRY(h2d(c, d_lutoff, vcoff.data(), vcoff.size()));
+        launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
+                           d_lut, d_lutoff, d_b, S);
+      }
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemsetAsync(d_b + (size_t)R * N * S, 0, 256, c->stream));  // zero slack
       d_bins = d_b;
@@ -2391,7 +2473,7 @@ int sbag_predict_dataset(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* 
   pa.agg = agg;
   TiledPlan P;
   // TreePoint's `value <= threshold` in the dataset's code space (dict sorted ascending)
-  const bool tiled = plan_tiled(f, pa, ds->F, [&](int g, double thr) {
+  const bool tiled = ds->code_bytes != 4 && plan_tiled(f, pa, ds->F, [&](int g, double thr) {
     const std::vector<double>& d = ds->dict[g];
     return (int64_t)(std::upper_bound(d.begin(), d.end(), thr) - d.begin()) - 1;
   }, P);

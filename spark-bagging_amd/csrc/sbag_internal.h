@@ -171,6 +171,10 @@ void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                             const void* codes, int code_bytes, int32_t S, const int32_t* d_sub,
                             const int32_t* d_Fr, int32_t Fmax, const int64_t* d_vcoff, uint32_t* vc,
                             int lds_words);
+// per-replica bins of u32 codes: bin = #{j < nc : cut[r][fl][j] <= code} (cut padded with ~0u)
+void launch_materialize_cut(hipStream_t st, const uint32_t* codes, int64_t N, int32_t S_codes,
+                            const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
+                            const uint32_t* d_cut, int nc, uint8_t* out, int32_t S_out);
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
                     unsigned long long* d_wsum, unsigned int* d_cmax, unsigned long long* d_sqsum);

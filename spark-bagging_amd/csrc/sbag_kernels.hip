@@ -2499,6 +2499,48 @@ void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64
                        S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
 }
 
+// Per-replica bins of a wide (u32-coded) dataset: the bin of a code is the number of the
+// feature's thresholds below its value, i.e. of code cuts (#{dict values <= t}) at or
+// below the code; a binary search over the replica's cuts (padded with ~0u).
+__global__ __launch_bounds__(256) void k_materialize_cut(const uint32_t* __restrict__ codes,
+                                                         int64_t N, int32_t S_codes,
+                                                         const int32_t* __restrict__ sub,
+                                                         const int32_t* __restrict__ Fr, int32_t Fmax,
+                                                         const uint32_t* __restrict__ cut, int nc,
+                                                         uint8_t* __restrict__ out, int32_t S_out) {
+  const int r = blockIdx.y;
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= N) return;
+  const int fr = Fr[r];
+  uint8_t* o = out + ((int64_t)r * N + row) * S_out;
+  const uint32_t* cr = codes + row * S_codes;
+  for (int fl = 0; fl < S_out; fl++) {
+    uint32_t b = 0;
+    if (fl < fr) {
+      const uint32_t code = cr[sub[(int64_t)r * Fmax + fl]];
+      const uint32_t* cu = cut + ((int64_t)r * Fmax + fl) * nc;
+      int lo = 0, hi = nc;  // first j with cu[j] > code
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cu[mid] <= code)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      b = (uint32_t)lo;
+    }
+    o[fl] = (uint8_t)b;
+  }
+}
+
+void launch_materialize_cut(hipStream_t st, const uint32_t* codes, int64_t N, int32_t S_codes,
+                            const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
+                            const uint32_t* d_cut, int nc, uint8_t* out, int32_t S_out) {
+  dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
+  hipLaunchKernelGGL(k_materialize_cut, grid, dim3(256), 0, st, codes, N, S_codes, d_sub, d_Fr, Fmax,
+                     d_cut, nc, out, S_out);
+}
+
 // Value counts with global atomics (u16 codes / dictionaries too large for LDS)
 template <typename CT>
 __global__ __launch_bounds__(256) void k_vc_global(const CT* __restrict__ codes, int32_t S,
@@ -2610,8 +2652,9 @@ __global__ __launch_bounds__(256) void k_predict(const double* __restrict__ X,
       if (X) {
         v = X[row * F + g];
       } else {
-        const int64_t c = (code_bytes == 1) ? (int64_t)((const uint8_t*)codes)[row * S + g]
-                                            : (int64_t)((const uint16_t*)codes)[row * S + g];
+        const int64_t c = code_bytes == 1   ? (int64_t)((const uint8_t*)codes)[row * S + g]
+                          : code_bytes == 2 ? (int64_t)((const uint16_t*)codes)[row * S + g]
+                                            : (int64_t)((const uint32_t*)codes)[row * S + g];
         v = dict[dict_off[g] + c];
       }
       id = (v <= t[id].value) ? t[id].left : t[id].right;

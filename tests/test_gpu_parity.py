@@ -318,3 +318,37 @@ def test_sampled_split_finding(ctx, n_rows, cls, P):
     subs = [oracle.subspace(1.0, F, seed + i) for i in range(L)]
     orf = oracle_forest(X, y, counts, subs, 6, 32, cls, part=part)
     assert_forest_equal(forest, orf)
+
+
+@pytest.mark.parametrize("cls,replacement,ratio", [(False, True, 1.0), (True, True, 1.0),
+                                                  (False, False, 0.1)])
+def test_wide_features_more_than_65536_values(ctx, cls, replacement, ratio):
+    """Features with more than 65536 distinct values (u32 value codes): split finding
+    counts the sampled rows' (or, for small subbags, the in-bag rows') values sparsely,
+    bins are materialized per replica from code cuts; trees, predictions on host rows and
+    on the device dataset bit-exact against the oracle."""
+    rng = np.random.default_rng(7 + int(cls) + int(replacement))
+    n_rows, F, P, L = 90000, 3, 3, 3
+    X = np.round(rng.normal(size=(n_rows, F)), 6)
+    X[:, 1] = np.round(X[:, 1], 1)  # one narrow feature next to the wide ones
+    X[rng.random((n_rows, F)) < 0.05] = 0.0
+    assert len(np.unique(X[:, 0])) > 65536
+    y = (rng.integers(0, 4, n_rows) if cls else rng.integers(-512, 512, n_rows) / 8).astype(np.float64)
+    part = [int(round(i * n_rows / P)) for i in range(P + 1)]
+    seed = SEED_CLS if cls else SEED_REG
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    # subspaceRatio 1 (not the sample ratio of H1): a 0.1 subspace of 3 features is empty
+    forest = nat.fit(ctx, ds, replacement=replacement, sample_ratio=ratio, seed=seed,
+                     learner_begin=0, learner_end=L, partition_offsets=part, max_depth=5,
+                     max_bins=32, subspace_ratio=1.0, subspace_bug_compat=False,
+                     impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    counts = oracle.bag(replacement, ratio, 0, L, seed, part, n_rows)
+    assert (counts.sum(axis=1) > 10000).all() == replacement  # sampled / whole-subbag paths
+    subs = [oracle.subspace(1.0, F, seed + i) for i in range(L)]
+    orf = oracle_forest(X, y, counts, subs, 5, 32, cls, part=part)
+    assert_forest_equal(forest, orf)
+    agg = nat.AGG_MODE if cls else nat.AGG_MEAN
+    want = oracle.predict(orf, X, classification=cls)
+    np.testing.assert_array_equal(nat.predict(ctx, forest, X, agg), want)
+    np.testing.assert_array_equal(nat.predict_dataset(ctx, forest, ds, agg), want)
+    np.testing.assert_array_equal(ds.features(0, 1000), np.where(X[:1000] == 0.0, 0.0, X[:1000]))
