@@ -12,6 +12,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -54,7 +57,72 @@ struct DevBuf {
   size_t cap = 0;
 };
 
+// Persistent host workers for the per-level bookkeeping: run(n, f) calls f(0) on the
+// caller and f(1..n-1) on workers, and returns when all are done (a per-level thread
+// spawn cost about as much as the work it split).
+struct HostPool {
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv, done;
+  const std::function<void(int)>* job = nullptr;
+  int n = 0, pending = 0;
+  uint64_t gen = 0;
+  bool stop = false;
+  static int width() {
+    return std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+  }
+  void run(int nw, const std::function<void(int)>& f) {
+    nw = std::max(1, std::min(nw, width()));
+    if (nw == 1) {
+      f(0);
+      return;
+    }
+    {
+      std::unique_lock<std::mutex> lk(m);
+      while ((int)th.size() < nw - 1) {
+        const int id = (int)th.size() + 1;
+        th.emplace_back([this, id] { loop(id); });
+      }
+      job = &f;
+      n = nw;
+      pending = nw - 1;
+      gen++;
+    }
+    cv.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(m);
+    done.wait(lk, [&] { return pending == 0; });
+    job = nullptr;
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        if (id >= n) continue;
+        f = job;
+      }
+      (*f)(id);
+      std::lock_guard<std::mutex> lk(m);
+      if (--pending == 0) done.notify_all();
+    }
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+};
+
 struct sbag_ctx {
+  HostPool pool;
   int device = 0;
   hipStream_t stream = nullptr;
   std::unordered_map<std::string, DevBuf> ws;
@@ -1470,7 +1538,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   }
   {
     // replicas are independent: split finding runs on host threads
-    const int nth = std::max(1, std::min<int>(R, std::min(16, (int)std::thread::hardware_concurrency())));
+    const int nth = std::max(1, std::min<int>(R, HostPool::width()));
     std::vector<int> t_nb(nth, 1);
     std::vector<char> t_id(nth, 1);
     auto work = [&](int w) {
@@ -1527,10 +1595,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         }
       }
     };
-    std::vector<std::thread> pool;
-    for (int w = 1; w < nth; w++) pool.emplace_back(work, w);
-    work(0);
-    for (auto& th : pool) th.join();
+    c->pool.run(nth, work);
     for (int w = 0; w < nth; w++) {
       NB = std::max(NB, t_nb[w]);
       identity = identity && t_id[w];
@@ -1823,10 +1888,25 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     struct Split {
       int slot, r, ni, li;
     };
-    std::vector<ParentInfo> par;
-    std::vector<std::pair<int64_t, int64_t>> pseg;
-    std::vector<Split> psplit;
-    for (int i = 0; i < M; i++) {
+    // a replica's slots are contiguous (slots keep replica order), so chunks of whole
+    // replicas update their trees on host workers; concatenated in chunk order, the
+    // parent lists are those of one sequential pass
+    const int nch = M < 256 ? 1 : std::min(HostPool::width(), M / 128);
+    std::vector<int> cb(nch + 1, M);
+    cb[0] = 0;
+    for (int w = 1; w < nch; w++) {
+      int k = std::max(cb[w - 1], (int)((int64_t)M * w / nch));
+      while (k > 0 && k < M && slots[k].first == slots[k - 1].first) k++;
+      cb[w] = k;
+    }
+    std::vector<std::vector<ParentInfo>> cpar(nch);
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> cpseg(nch);
+    std::vector<std::vector<Split>> cpsplit(nch);
+    const std::function<void(int)> node_work = [&](int w) {
+    std::vector<ParentInfo>& par = cpar[w];
+    std::vector<std::pair<int64_t, int64_t>>& pseg = cpseg[w];
+    std::vector<Split>& psplit = cpsplit[w];
+    for (int i = cb[w]; i < cb[w + 1]; i++) {
       const int r = slots[i].first;
       const int ni = slots[i].second;
       const int64_t* lef = &sst[(size_t)M * NS + (size_t)i * NS];
@@ -1889,6 +1969,16 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       par.push_back(p);
       pseg.push_back(seg[i]);
       psplit.push_back(Split{i, r, ni, li});
+    }
+    };
+    c->pool.run(nch, node_work);
+    std::vector<ParentInfo> par;
+    std::vector<std::pair<int64_t, int64_t>> pseg;
+    std::vector<Split> psplit;
+    for (int w = 0; w < nch; w++) {
+      par.insert(par.end(), cpar[w].begin(), cpar[w].end());
+      pseg.insert(pseg.end(), cpseg[w].begin(), cpseg[w].end());
+      psplit.insert(psplit.end(), cpsplit[w].begin(), cpsplit[w].end());
     }
     hmark(2);
     if (par.empty()) break;
@@ -2127,8 +2217,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     }
   }
   {
-    const int nth = std::max(1, std::min<int>(R, std::min(16, (int)std::thread::hardware_concurrency())));
-    auto work = [&](int w) {
+    const int nth = std::max(1, std::min<int>(R, HostPool::width()));
+    const std::function<void(int)> work = [&](int w) {
       for (int r = w; r < R; r += nth) {
         HTree& t = forest->trees[r];
         t.sub = sub[r];
@@ -2137,10 +2227,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         emit(trees[r], 0, t, NS, gini, ds->shift, ns_of[r]);
       }
     };
-    std::vector<std::thread> pool;
-    for (int w = 1; w < nth; w++) pool.emplace_back(work, w);
-    work(0);
-    for (auto& th : pool) th.join();
+    c->pool.run(nth, work);
   }
   forest->nclasses = gini ? std::max(nclasses, (int)ds->kmax + 1) : 0;
   double cats[T_NCAT] = {0};
