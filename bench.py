@@ -26,7 +26,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
 # ds_add_u64 throughput measured on MI355X by scripts/micro/lds_atomic.hip:
 # 7.16 cycles per wave-instruction per CU (4 x 512-thread workgroups per CU), 256 CUs, 2.4 GHz
 LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01g", "summary.json")
 
 
 def pmc_traffic():
