@@ -66,6 +66,10 @@ WORKLOADS = {
 def hist_kernel_name(F, cls, N):
     """The k_hist variant the host picks for an F-feature tile (sbag_host.cpp
     hist_geometry): row lanes when roundup(F, 16) < roundup(F, 64)."""
+    if cls:
+        # gini tiles shrink features and classes to fit the LDS target; the variant is
+        # not predicted here (C5 runs sbag::k_hist<0, 1>: profiles/r01g_c5/)
+        return "sbag::k_hist* (kHistGini, class tiles; variant per hist_geometry)"
     ft = min(F, 256)
     mode = "0" if cls else "1"
     tag = "kHistGini, class tiles" if cls else "kHistVar"
