@@ -65,6 +65,11 @@ def lib():
         L.or_split_sample_seeds.argtypes = [i64, i32, P]
         L.or_split_sample.restype = i64
         L.or_split_sample.argtypes = [P, P, i32, i64, dbl, P]
+        L.or_fit_x.argtypes = [P, i32, P, i64, i32, P, i32, P, P, ctypes.POINTER(TreeParams), i32,
+                               P, i32, P, i32, P, P, P]
+        L.or_synth.argtypes = [i64, i64, i32, ctypes.c_uint64, i32, i32, P, P]
+        L.or_mm3_bytes_hash.restype = ctypes.c_uint32
+        L.or_mm3_bytes_hash.argtypes = [P, i32, ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -167,10 +172,28 @@ def split_sample(counts_row, part_off, dt_seed, fraction):
     return mult
 
 
+def mm3_bytes_hash(data, seed):
+    """scala.util.hashing.MurmurHash3.bytesHash (= MurmurHash3_x86_32) of a bytes object."""
+    buf = np.frombuffer(bytes(data), np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
+    return int(lib().or_mm3_bytes_hash(_p(buf), len(data), seed & 0xFFFFFFFF))
+
+
+def synth(num_rows, num_features, seed=20261015, num_classes=0, row_begin=0, nthreads=None):
+    """The synthetic bench rows as u8 codes [N][F] + fp64 labels."""
+    X = np.empty((num_rows, num_features), np.uint8)
+    y = np.empty(num_rows, np.float64)
+    lib().or_synth(row_begin, num_rows, num_features, seed, num_classes,
+                   nthreads or os.cpu_count() or 1, _p(X), _p(y))
+    return X, y
+
+
 def fit(X, y, counts, subspaces, max_depth=5, max_bins=32, min_instances_per_node=1,
         min_info_gain=0.0, classification=False, nthreads=None, max_stats=None, part=None,
         dt_seed=None):
-    X = np.ascontiguousarray(X, np.float64)
+    """Fit one tree per row of counts.  X is fp64 [N][F], or u8 value codes whose fp64 value
+    is the code (the synthetic workload)."""
+    xkind = 1 if np.asarray(X).dtype == np.uint8 else 0
+    X = np.ascontiguousarray(X, np.uint8 if xkind else np.float64)
     y = np.ascontiguousarray(y, np.float64)
     counts = np.ascontiguousarray(counts, np.uint8)
     L, N = counts.shape
@@ -193,9 +216,9 @@ def fit(X, y, counts, subspaces, max_depth=5, max_bins=32, min_instances_per_nod
     off = np.ascontiguousarray(part if part is not None else [0, N], np.int64)
     p = TreeParams(max_depth, max_bins, min_instances_per_node, 1 if classification else 0,
                    min_info_gain, int(dt_seed), off.ctypes.data, len(off) - 1, 0)
-    rc = lib().or_fit(_p(X), _p(y), N, F, _p(counts), L, _p(sub), _p(nsub), ctypes.byref(p),
-                      nthreads or os.cpu_count() or 1, _p(nodes), max_nodes, _p(stats), max_stats,
-                      _p(num_nodes), _p(num_stats), _p(exact))
+    rc = lib().or_fit_x(_p(X), xkind, _p(y), N, F, _p(counts), L, _p(sub), _p(nsub),
+                        ctypes.byref(p), nthreads or os.cpu_count() or 1, _p(nodes), max_nodes,
+                        _p(stats), max_stats, _p(num_nodes), _p(num_stats), _p(exact))
     if rc:
         raise ValueError(f"or_fit failed rc={rc}")
     return Forest(nodes, stats, num_nodes, num_stats, [np.asarray(s, np.int32) for s in subspaces],

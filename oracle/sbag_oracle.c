@@ -437,6 +437,52 @@ int or_find_splits(const double* X, int64_t N, int F, int feature, const uint8_t
   return nt;
 }
 
+/* MurmurHash3_x86_32 (= scala.util.hashing.MurmurHash3.bytesHash), exported so the tests
+   can pin it to SMHasher's published verification value. */
+uint32_t or_mm3_bytes_hash(const uint8_t* data, int len, uint32_t seed) {
+  return mm3_bytes_hash(data, len, seed);
+}
+
+/* Feature matrix accessor: X is fp64 [N][F] (xkind 0) or u8 value codes whose fp64 value is
+   the code itself (xkind 1; the synthetic workload of SURVEY.md §8d, 32 integer levels). */
+static inline double xval(const void* X, int xkind, int64_t i) {
+  return xkind ? (double)((const uint8_t*)X)[i] : ((const double*)X)[i];
+}
+
+/* Host restatement of the synthetic bench data (the product generates the same
+   rows on the device): x[r,f] = splitmix64(seed ^ (r*F+f)) mod 32; h2 = splitmix64(~seed ^ r);
+   regression y = (sum_{f<8} (f+1) x[r,f] + (h2 mod 64) - 32) / 64, class
+   y = (x0 + 3 x1 + 7 x2 + h2 mod 8) mod C.  Rows [row_begin, row_begin + n). */
+static uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+void or_synth(int64_t row_begin, int64_t n, int F, uint64_t seed, int C, int nthreads, uint8_t* X,
+              double* y) {
+  if (nthreads <= 0) nthreads = 1;
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+  for (int64_t i = 0; i < n; i++) {
+    const uint64_t r = (uint64_t)(row_begin + i);
+    int x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int f = 0; f < F; f++) {
+      const int v = (int)(splitmix64(seed ^ (r * (uint64_t)F + (uint64_t)f)) & 31u);
+      X[i * F + f] = (uint8_t)v;
+      if (f < 8) x[f] = v;
+    }
+    const uint64_t h2 = splitmix64(~seed ^ r);
+    if (C == 0) {
+      int64_t k = 0;
+      for (int f = 0; f < 8 && f < F; f++) k += (int64_t)(f + 1) * x[f];
+      k += (int64_t)(h2 & 63u) - 32;
+      y[i] = ldexp((double)k, -6);
+    } else {
+      y[i] = (double)((x[0] + 3 * x[1] + 7 * x[2] + (int)(h2 & 7u)) % C);
+    }
+  }
+}
+
 /* ======================================================================
  * Spark 2.4.3 DecisionTree (RandomForest.run, numTrees=1, "all"),
  * invoked by HasBaseLearner.fitBaseLearner (ml/ensemble/ensembleParams.scala:99-117).
@@ -603,10 +649,10 @@ static tn_ret to_node(const lnode_t* ln, int64_t hid, emit_t* e, int gini, int* 
   return ret;
 }
 
-static int fit_one(const double* X, const double* y, int64_t N, int F, const uint8_t* cnt,
+static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, const uint8_t* cnt,
                    const int32_t* sub, int Fr, const or_tree_params* p, or_node* out_nodes,
                    int max_nodes, double* out_stats, int stride, int32_t* out_num_nodes,
-                   int32_t* out_ns, int32_t* out_exact) {
+                   int32_t* out_ns, int32_t* out_exact, int inner) {
   const int gini = p->impurity == 1;
   const int D = p->max_depth;
   if (D < 0 || D > 20 || p->max_bins < 2 || Fr <= 0) return -1;
@@ -649,15 +695,17 @@ static int fit_one(const double* X, const double* y, int64_t N, int F, const uin
   } else {
     for (int64_t r = 0; r < N; r++) mult[r] = cnt[r];
   }
+  /* features are independent: split finding and binning run one feature per thread */
+#pragma omp parallel for schedule(dynamic, 1) num_threads(inner)
   for (int fl = 0; fl < Fr; fl++) {
     const int fg = sub[fl];
     int64_t nnz = 0;
     for (int64_t k = 0; k < nrows; k++)
-      if (X[rows[k] * F + fg] != 0.0) nnz += mult[rows[k]];
+      if (xval(X, xkind, rows[k] * F + fg) != 0.0) nnz += mult[rows[k]];
     double* vals = (double*)malloc(sizeof(double) * (size_t)(nnz + 1));
     int64_t q = 0;
     for (int64_t k = 0; k < nrows; k++) {
-      const double x = X[rows[k] * F + fg];
+      const double x = xval(X, xkind, rows[k] * F + fg);
       if (x != 0.0)
         for (int c = 0; c < mult[rows[k]]; c++) vals[q++] = x;
     }
@@ -665,7 +713,7 @@ static int fit_one(const double* X, const double* y, int64_t N, int F, const uin
     free(vals);
     const double* t = thr + (int64_t)fl * p->max_bins;
     for (int64_t k = 0; k < nrows; k++) {
-      const double x = X[rows[k] * F + fg];
+      const double x = xval(X, xkind, rows[k] * F + fg);
       int lo = 0, hi = nthr[fl]; /* #thresholds < x  == Arrays.binarySearch result */
       while (lo < hi) {
         int mid = (lo + hi) >> 1;
@@ -711,31 +759,44 @@ static int fit_one(const double* X, const double* y, int64_t N, int F, const uin
       }
       double* agg = (double*)calloc((size_t)(g * per_node), sizeof(double));
       double* par = (double*)calloc((size_t)(g * ns), sizeof(double));
-      for (int64_t k = 0; k < nrows; k++) {
-        const int64_t nd = node_of[k];
-        if (nd < first || nd > last) continue;
-        const int64_t s = slot[nd - first];
-        if (s < 0) continue;
-        const double lab = y[rows[k]];
-        double* a = agg + s * per_node;
-        double* pp = par + s * ns;
-        for (int c = 0; c < cnt[rows[k]]; c++) {
-          for (int fl = 0; fl < Fr; fl++) {
-            double* st = a + ((int64_t)fl * nb + bins[k * Fr + fl]) * ns;
-            if (!gini) {
-              st[0] += 1.0;
-              st[1] += 1.0 * lab;
-              st[2] += 1.0 * lab * lab;
-            } else {
-              st[(int)lab] += 1.0;
+      /* DTStatsAggregator.update in row order.  Each (feature, bin) cell is summed in row
+         order whatever the thread split: threads own disjoint feature ranges. */
+#pragma omp parallel num_threads(inner)
+      {
+        int nth = 1, tid = 0;
+#ifdef _OPENMP
+        nth = omp_get_num_threads();
+        tid = omp_get_thread_num();
+#endif
+        const int f0 = (int)((int64_t)Fr * tid / nth), f1 = (int)((int64_t)Fr * (tid + 1) / nth);
+        for (int64_t k = 0; k < nrows; k++) {
+          const int64_t nd = node_of[k];
+          if (nd < first || nd > last) continue;
+          const int64_t s = slot[nd - first];
+          if (s < 0) continue;
+          const double lab = y[rows[k]];
+          double* a = agg + s * per_node;
+          double* pp = par + s * ns;
+          for (int c = 0; c < cnt[rows[k]]; c++) {
+            for (int fl = f0; fl < f1; fl++) {
+              double* st = a + ((int64_t)fl * nb + bins[k * Fr + fl]) * ns;
+              if (!gini) {
+                st[0] += 1.0;
+                st[1] += 1.0 * lab;
+                st[2] += 1.0 * lab * lab;
+              } else {
+                st[(int)lab] += 1.0;
+              }
             }
-          }
-          if (!gini) {
-            pp[0] += 1.0;
-            pp[1] += 1.0 * lab;
-            pp[2] += 1.0 * lab * lab;
-          } else {
-            pp[(int)lab] += 1.0;
+            if (tid == 0) {
+              if (!gini) {
+                pp[0] += 1.0;
+                pp[1] += 1.0 * lab;
+                pp[2] += 1.0 * lab * lab;
+              } else {
+                pp[(int)lab] += 1.0;
+              }
+            }
           }
         }
       }
@@ -862,19 +923,24 @@ static int fit_one(const double* X, const double* y, int64_t N, int F, const uin
   return e.overflow ? -4 : 0;
 }
 
-int or_fit(const double* X, const double* y, int64_t N, int F, const uint8_t* counts, int L,
-           const int32_t* sub, const int32_t* nsub, const or_tree_params* p, int nthreads,
-           or_node* nodes, int max_nodes, double* stats, int stats_stride, int32_t* num_nodes,
-           int32_t* num_stats, int32_t* all_exact) {
+int or_fit_x(const void* X, int xkind, const double* y, int64_t N, int F, const uint8_t* counts,
+             int L, const int32_t* sub, const int32_t* nsub, const or_tree_params* p, int nthreads,
+             or_node* nodes, int max_nodes, double* stats, int stats_stride, int32_t* num_nodes,
+             int32_t* num_stats, int32_t* all_exact) {
   int err = 0;
   if (nthreads <= 0) nthreads = 1;
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+  const int outer = nthreads < L ? nthreads : (L > 0 ? L : 1);
+  const int inner = nthreads / outer > 0 ? nthreads / outer : 1; /* spare threads per learner */
+#ifdef _OPENMP
+  if (inner > 1) omp_set_max_active_levels(2);
+#endif
+#pragma omp parallel for schedule(dynamic, 1) num_threads(outer)
   for (int l = 0; l < L; l++) {
     int32_t ex = 1;
-    int rc = fit_one(X, y, N, F, counts + (int64_t)l * N, sub + (int64_t)l * F, nsub[l], p,
+    int rc = fit_one(X, xkind, y, N, F, counts + (int64_t)l * N, sub + (int64_t)l * F, nsub[l], p,
                      nodes + (int64_t)l * max_nodes, max_nodes,
                      stats + (int64_t)l * max_nodes * stats_stride, stats_stride, &num_nodes[l],
-                     &num_stats[l], &ex);
+                     &num_stats[l], &ex, inner);
     all_exact[l] = ex;
     if (rc) {
 #pragma omp critical
@@ -884,53 +950,66 @@ int or_fit(const double* X, const double* y, int64_t N, int F, const uint8_t* co
   return err;
 }
 
+int or_fit(const double* X, const double* y, int64_t N, int F, const uint8_t* counts, int L,
+           const int32_t* sub, const int32_t* nsub, const or_tree_params* p, int nthreads,
+           or_node* nodes, int max_nodes, double* stats, int stats_stride, int32_t* num_nodes,
+           int32_t* num_stats, int32_t* all_exact) {
+  return or_fit_x(X, 0, y, N, F, counts, L, sub, nsub, p, nthreads, nodes, max_nodes, stats,
+                  stats_stride, num_nodes, num_stats, all_exact);
+}
+
 /* BaggingRegressionModel.predict (ml/regression/BaggingRegressor.scala:248-256) and
    BaggingClassificationModel.predict (ml/classification/BaggingClassifier.scala:248-257):
    slicer (HasSubBag.scala:128-131) + Node.predictImpl + breeze sum / mode. */
 void or_predict(const double* X, int64_t N, int F, int L, const int32_t* sub, const int32_t* nsub,
                 const or_node* nodes, int max_nodes, int agg, double* out, double* per_tree) {
   (void)nsub;
-  double* votes = (double*)malloc(sizeof(double) * (size_t)L);
-  double* vv = (double*)malloc(sizeof(double) * (size_t)L);
-  int* vc = (int*)malloc(sizeof(int) * (size_t)L);
-  for (int64_t r = 0; r < N; r++) {
-    const double* x = X + r * F;
-    for (int l = 0; l < L; l++) {
-      const or_node* t = nodes + (int64_t)l * max_nodes;
-      int id = 0;
-      while (t[id].left >= 0) {
-        const double v = x[sub[(int64_t)l * F + t[id].feature]];
-        id = (v <= t[id].threshold) ? t[id].left : t[id].right;
-      }
-      votes[l] = t[id].prediction;
-      if (per_tree) per_tree[(int64_t)l * N + r] = votes[l];
-    }
-    if (agg == 0) {
-      double s = 0.0;
-      for (int l = 0; l < L; l++) s += votes[l];
-      out[r] = s / (double)L;
-    } else {
-      /* breeze.stats.mode: first value to reach the final max count */
-      int nd = 0, maxc = 0;
-      double mode = 0.0;
+  /* rows are independent: one row per iteration, per-thread vote buffers */
+#pragma omp parallel
+  {
+    double* votes = (double*)malloc(sizeof(double) * (size_t)L);
+    double* vv = (double*)malloc(sizeof(double) * (size_t)L);
+    int* vc = (int*)malloc(sizeof(int) * (size_t)L);
+#pragma omp for schedule(static)
+    for (int64_t r = 0; r < N; r++) {
+      const double* x = X + r * F;
       for (int l = 0; l < L; l++) {
-        int j = 0;
-        while (j < nd && vv[j] != votes[l]) j++;
-        if (j == nd) {
-          vv[nd] = votes[l];
-          vc[nd] = 0;
-          nd++;
+        const or_node* t = nodes + (int64_t)l * max_nodes;
+        int id = 0;
+        while (t[id].left >= 0) {
+          const double v = x[sub[(int64_t)l * F + t[id].feature]];
+          id = (v <= t[id].threshold) ? t[id].left : t[id].right;
         }
-        vc[j]++;
-        if (vc[j] > maxc) {
-          maxc = vc[j];
-          mode = votes[l];
-        }
+        votes[l] = t[id].prediction;
+        if (per_tree) per_tree[(int64_t)l * N + r] = votes[l];
       }
-      out[r] = mode;
+      if (agg == 0) {
+        double s = 0.0;
+        for (int l = 0; l < L; l++) s += votes[l];
+        out[r] = s / (double)L;
+      } else {
+        /* breeze.stats.mode: first value to reach the final max count */
+        int nd = 0, maxc = 0;
+        double mode = 0.0;
+        for (int l = 0; l < L; l++) {
+          int j = 0;
+          while (j < nd && vv[j] != votes[l]) j++;
+          if (j == nd) {
+            vv[nd] = votes[l];
+            vc[nd] = 0;
+            nd++;
+          }
+          vc[j]++;
+          if (vc[j] > maxc) {
+            maxc = vc[j];
+            mode = votes[l];
+          }
+        }
+        out[r] = mode;
+      }
     }
+    free(votes);
+    free(vv);
+    free(vc);
   }
-  free(votes);
-  free(vv);
-  free(vc);
 }

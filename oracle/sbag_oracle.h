@@ -65,6 +65,17 @@ int or_fit(const double* X, const double* y, int64_t N, int F, const uint8_t* co
            or_node* nodes, int max_nodes, double* stats, int stats_stride, int32_t* num_nodes,
            int32_t* num_stats, int32_t* all_exact);
 
+/* or_fit over fp64 X (xkind 0) or u8 value codes (xkind 1, value = code) */
+int or_fit_x(const void* X, int xkind, const double* y, int64_t N, int F, const uint8_t* counts,
+             int L, const int32_t* sub, const int32_t* nsub, const or_tree_params* p, int nthreads,
+             or_node* nodes, int max_nodes, double* stats, int stats_stride, int32_t* num_nodes,
+             int32_t* num_stats, int32_t* all_exact);
+
+/* synthetic bench rows [row_begin, row_begin+n) as u8 codes + labels */
+void or_synth(int64_t row_begin, int64_t n, int F, uint64_t seed, int C, int nthreads, uint8_t* X,
+              double* y);
+uint32_t or_mm3_bytes_hash(const uint8_t* data, int len, uint32_t seed);
+
 /* ensemble prediction: agg 0 = mean (BaggingRegressionModel.predict),
    1 = breeze mode (BaggingClassificationModel.predict).                  */
 void or_predict(const double* X, int64_t N, int F, int L, const int32_t* sub, const int32_t* nsub,

@@ -23,6 +23,20 @@ def test_default_seeds_are_java_string_hashes():
     assert oracle.DEFAULT_SEED_REGRESSOR == -1395689524
 
 
+def test_murmur3_x86_32_smhasher_verification():
+    """XORShiftRandom.hashSeed rests on scala.util.hashing.MurmurHash3.bytesHash, which is
+    MurmurHash3_x86_32.  SMHasher's VerificationTest: hash {}, {0}, {0,1}, ... {0..254}
+    with seed 256-i, hash the 1024-byte array of little-endian results with seed 0; the
+    published value for MurmurHash3_x86_32 is 0xB0F57EE3 (an anchor outside this repo)."""
+    key = bytes(range(256))
+    hashes = b"".join(oracle.mm3_bytes_hash(key[:i], 256 - i).to_bytes(4, "little")
+                      for i in range(256))
+    assert oracle.mm3_bytes_hash(hashes, 0) == 0xB0F57EE3
+    # the Python twin agrees on the same keys (it implements hashSeed independently)
+    for i in (0, 1, 3, 4, 7, 8, 255):
+        assert po.bytes_hash(key[:i], 256 - i) == oracle.mm3_bytes_hash(key[:i], 256 - i)
+
+
 @pytest.mark.parametrize("seed", [0, 1, -1, 12345, -1395689524, 2**62 + 11, -(2**63)])
 def test_rng_streams_c_vs_python(seed):
     assert oracle.hash_seed(seed) == po.hash_seed(seed)
@@ -292,3 +306,21 @@ def test_sampled_split_finding_in_fit():
             vm[X[r, f]] = vm.get(X[r, f], 0) + mult[r]
     thr = po.find_splits(vm, n, 16, num_samples=ns)
     assert root["threshold"] in thr
+
+
+def test_oracle_u8_codes_equal_fp64_rows():
+    """oracle.fit over the synthetic u8 codes (value = code, the bench workload's rows as
+    tests/test_gpu_bench_configs.py feeds them) equals the same fit over fp64 rows."""
+    X, y = oracle.synth(3000, 7, 99, 0, nthreads=2)
+    X2, y2 = oracle.synth(3000, 7, 99, 0, row_begin=0, nthreads=1)
+    assert (X == X2).all() and (y == y2).all()
+    counts = oracle.bag(True, 1.0, 0, 2, 5, [0, 1000, 3000], 3000)
+    subs = [oracle.subspace(1.0, 7, 5 + i) for i in range(2)]
+    a = oracle.fit(X, y, counts, subs, max_depth=6, max_bins=32, nthreads=4)
+    b = oracle.fit(X.astype(np.float64), y, counts, subs, max_depth=6, max_bins=32, nthreads=1)
+    for t in range(2):
+        (na, sa), (nb, sb_) = a.tree(t), b.tree(t)
+        assert na.tobytes() == nb.tobytes() and (sa == sb_).all()
+    # rows of a later range are the same rows (row_begin offsets the generator)
+    Xt, yt = oracle.synth(1000, 7, 99, 0, row_begin=2000, nthreads=2)
+    assert (Xt == X[2000:]).all() and (yt == y[2000:]).all()
