@@ -26,22 +26,28 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
 # ds_add_u64 throughput measured on MI355X by scripts/micro/lds_atomic.hip:
 # 7.16 cycles per wave-instruction per CU (4 x 512-thread workgroups per CU), 256 CUs, 2.4 GHz
 LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01g", "summary.json")
+# committed rocprofv3 PMC summaries of this command per workload (scripts/profile.sh +
+# scripts/pmc_summary.py); the newest one present is used
+PMC_SUMMARIES = {"c3": ["profiles/r02/c3/summary.json", "profiles/r01g/summary.json"],
+                 "c4": ["profiles/r02/c4/summary.json"],
+                 "c5": ["profiles/r02/c5/summary.json", "profiles/r01g_c5/summary.json"]}
 
 
-def pmc_traffic():
-    """HBM bytes per k_hist launch from the committed rocprofv3 PMC summary of this
-    same command (scripts/profile.sh + scripts/pmc_summary.py): 2 x FETCH_SIZE (gfx950
-    reports half of wide reads) + WRITE_SIZE, in bytes; None if not profiled."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            d = json.load(f)
+def pmc_traffic(workload):
+    """HBM bytes per histogram launch from the committed PMC summary of this same command:
+    2 x FETCH_SIZE (gfx950 reports half of 128-B reads) + WRITE_SIZE.  The counters need
+    their own rocprofv3 passes, so they are not collected inside this run: the value is
+    returned with the summary it came from (stale if the kernel changed since)."""
+    for rel in PMC_SUMMARIES.get(workload, []):
+        try:
+            with open(os.path.join(ROOT, rel)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
         for k, v in d.items():
             if k.startswith("sbag::k_hist") and "hbm_bytes_per_launch" in v:
-                return round(v["hbm_bytes_per_launch"])
-    except (OSError, ValueError):
-        pass
-    return None
+                return round(v["hbm_bytes_per_launch"]), rel, k
+    return None, None, None
 
 
 # BASELINE.json configs as bench workloads (per GPU).  c3 is the headline (default);
@@ -93,6 +99,8 @@ def parse():
     ap.add_argument("--bins", type=int, default=32)
     ap.add_argument("--partitions", type=int, default=128)
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--sampler-partitions", type=int, default=None,
+                    help="also time one fit's sampler at this P (default: nproc)")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-learners", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -114,7 +122,7 @@ def cpu_baseline(args):
     from spark_bagging_amd import synthetic
 
     n, L = args.cpu_rows, args.cpu_learners
-    cores = min(L, os.cpu_count() or 1, 16)
+    cores = nproc()  # all host cores this process may use (what `nproc` prints)
     cls = args.classes > 0
     seed = SEED_CLS if cls else SEED_REG
     X, y = synthetic.generate(n, args.features, args.seed, args.classes)
@@ -129,6 +137,13 @@ def cpu_baseline(args):
             "sample": f"{n} rows x {args.features} features, {L} learners, depth {args.depth}, "
                       f"{args.partitions} partitions; oracle/sbag_oracle.c fit only "
                       f"({dt:.1f} s, restatement, not Spark)"}
+
+
+def nproc():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def main():
@@ -185,26 +200,56 @@ def main():
     read_bytes = sum(t["hist_alg_bytes"] for t in timings)
     nl = max(hist_launches, 1)
     avg_s = hist_ms / 1e3 / nl
-    achieved = work_bytes / nl / avg_s / 1e9 if hist_ms > 0 else 0.0
+    # achieved: the bytes one launch processes -- its entries x (F_r + 4): the in-bag
+    # rows of the nodes it histograms (u8 bins of the replica's features + the 4-byte
+    # label word) -- over the launch's average duration (HIP events on the context
+    # stream, the stream the kernel runs on)
+    achieved = read_bytes / nl / avg_s / 1e9 if hist_ms > 0 else 0.0
+    # SURVEY 8d's work-defined figure also counts every sibling histogram obtained by
+    # subtraction as if read: reported separately, it can exceed the peak
+    effective = work_bytes / nl / avg_s / 1e9 if hist_ms > 0 else 0.0
     # LDS atomic co-limiter, counted by the host per launch (variance: ds_add_u64 of the
     # packed (count, sum) word after the screening of DESIGN.md §5; gini: ds_add_u32)
     lds_instr = sum(t["hist_lds_atomics"] for t in timings)
     lds_rate = lds_instr / (hist_ms / 1e3) if hist_ms > 0 else 0.0
+    traffic, traffic_src, traffic_kernel = pmc_traffic(args.workload)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic() if args.workload == "c3" else None,
+                "traffic": traffic,
+                "traffic_source": (f"{traffic_src} ({traffic_kernel}; rocprofv3 PMC passes of this "
+                                   "command, not re-measured inside this run)") if traffic else None,
                 "kernel": hist_kernel_name(F, cls, N),
                 "avg_launch_ms": round(hist_ms / nl, 4),
-                "alg_bytes_per_launch": round(work_bytes / nl),
-                "alg_bytes_def": "SURVEY 8d: sum over histograms built (read or by subtraction) of "
-                                 "n(r,d)*(F_r+s_y) + 3N, s_y = 4 (regression) / 1 (class)",
-                "kernel_read_bytes_per_launch": round(read_bytes / nl),
-                "kernel_read_GBs": round(read_bytes / nl / avg_s / 1e9, 1) if hist_ms > 0 else 0.0,
+                "alg_bytes_per_launch": round(read_bytes / nl),
+                "alg_bytes_def": "entries the launch histograms x (F_r + 4): u8 bin per feature of "
+                                 "the replica's subspace + 4-byte label word (DESIGN.md §4)",
+                "effective": {"achieved": round(effective, 1), "frac": round(effective / HBM_PEAK_GBS, 4),
+                              "bytes_per_launch": round(work_bytes / nl),
+                              "def": "SURVEY 8d: sum over histograms built (read or by subtraction) "
+                                     "of n(r,d)*(F_r+s_y) + 3N, s_y = 4 (regression) / 1 (class)"},
+                "binding_limiter": "lds_atomic",
                 "lds_atomic": {"achieved": round(lds_rate / 1e9, 2),
                                "peak": round(LDS_ATOMIC_PEAK / 1e9, 2),
-                               "unit": "G wave-instr/s (ds_add_u64 peak)",
+                               "unit": "G wave-instr/s (ds_add_u64 peak, scripts/micro/lds_atomic.hip)",
                                "frac": round(lds_rate / LDS_ATOMIC_PEAK, 4)}}
     breakdown = {k: round(v, 3) for k, v in timings[-1].items() if k.endswith("_ms")}
+    # the sampler's cost depends on rows per partition stream (Poisson.scala:53-56 reseeds
+    # per partition): one extra fit, outside the timed region, at P = nproc
+    sp = args.sampler_partitions or nproc()
+    if sp != args.partitions:
+        part_sp = [int(round(i * N / sp)) for i in range(sp + 1)]
+        f = nat.fit(ctx, ds, replacement=args.replacement, sample_ratio=args.ratio,
+                    seed=SEED_CLS if cls else SEED_REG, learner_begin=lb, learner_end=lb + L,
+                    partition_offsets=part_sp, max_depth=args.depth, max_bins=args.bins,
+                    impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+        tsp = f.timing()
+        f.free()
+        sampler_p = {"partitions": sp, "partitions_is": "nproc of this host" if not args.sampler_partitions
+                     else "--sampler-partitions", "sample_ms": round(tsp["sample_ms"], 3),
+                     "fit_ms": round(tsp["total_ms"], 3),
+                     "headline_partitions": args.partitions, "headline_sample_ms": breakdown["sample_ms"]}
+    else:
+        sampler_p = {"partitions": sp, "sample_ms": breakdown["sample_ms"]}
     out = {
         "metric": "estimator×rows trained/sec", "value": round(value, 1),
         "unit": "estimator*rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -217,7 +262,7 @@ def main():
                    "max_depth": args.depth, "max_bins": args.bins, "partitions": args.partitions,
                    "classes": args.classes, "replacement": args.replacement,
                    "sample_ratio": args.ratio, "parallelism": f"learner-shard x{world}"},
-        "roofline": roofline, "breakdown_ms": breakdown,
+        "roofline": roofline, "breakdown_ms": breakdown, "sampler_at_nproc_partitions": sampler_p,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

@@ -16,9 +16,11 @@
  *  - sbag_last_error() returns the message of the calling thread's last failure.
  *  - Host buffers passed in are read during the call only; the library owns
  *    device memory and the objects it returns until the matching *_free/_destroy.
- *  - A context is bound to one device; calls on one context must be serialized
- *    by the caller (the reference runs learner Futures on a pool,
- *    ml/regression/BaggingRegressor.scala:169-191; the shim serializes per context).
+ *  - A context is bound to one device.  Calls on one context are serialized by the
+ *    library (a per-context lock): the reference runs learner Futures on a pool
+ *    (ml/regression/BaggingRegressor.scala:169-191) and CrossValidator fits models
+ *    concurrently, so several JVM threads may share a context.  Separate contexts
+ *    run concurrently.  A dataset must be used with a context on its own device.
  */
 #ifndef SBAG_H
 #define SBAG_H
@@ -170,10 +172,34 @@ int sbag_predict(sbag_ctx* ctx, const sbag_forest* f, const double* X, int64_t n
                  double* per_tree_out /* [trees x num_rows] or NULL */);
 int sbag_predict_dataset(sbag_ctx* ctx, const sbag_forest* f, const sbag_dataset* ds, int32_t agg,
                          double* out /* [num_rows] */);
-/* ordered aggregation of per-learner predictions gathered from several
-   devices (RCCL all-gather in learner order): votes [num_learners x num_rows] */
+/* ordered aggregation of per-learner predictions on the host:
+   votes [num_learners x num_rows] fp64, learner order */
 int sbag_aggregate(sbag_ctx* ctx, const double* votes, int32_t num_learners, int64_t num_rows,
                    int32_t agg, double* out);
+
+/* ---- multi-GPU transform: device-resident outputs ----------
+ * One process per GPU, each holding a learner shard [g*L/G, (g+1)*L/G) and the
+ * replicated dataset.  The reference's aggregation is breeze's in-order sum / L
+ * (BaggingRegressor.scala:248-256) and breeze mode (BaggingClassifier.scala:248-257);
+ * across devices it becomes
+ *   regression:      SBAG_OUT_SUM per rank (in-order sum of the shard's trees), an
+ *                    RCCL all-to-all by row shard, then sbag_aggregate_device(MEAN) of
+ *                    the G partial sums in rank order / L;
+ *   classification:  SBAG_OUT_VOTES per rank ([trees x N] u8 / u16 class ids), an RCCL
+ *                    all-to-all by row shard (rank order = learner order), then
+ *                    sbag_aggregate_device(MODE) over all L votes of the shard's rows.
+ * Pointers named d_* are device memory on the context's device (e.g. a torch tensor's
+ * data_ptr()); both calls return after their work is complete on the device.       */
+#define SBAG_OUT_SUM 2   /* fp64 [num_rows]: in-order sum of the forest's tree predictions */
+#define SBAG_OUT_VOTES 3 /* [trees x num_rows] class ids, vote_bytes 1 (u8) or 2 (u16)    */
+int sbag_predict_dataset_device(sbag_ctx* ctx, const sbag_forest* f, const sbag_dataset* ds,
+                                int32_t out_kind, int32_t vote_bytes, void* d_out);
+/* d_in [K x num_rows]: in_bytes 8 -> fp64 values, MEAN: out = (in-order sum of the K
+   rows) / num_learners; in_bytes 1 / 2 -> u8 / u16 class ids < num_classes, MODE:
+   breeze mode over the K votes in order.  d_out fp64 [num_rows].                   */
+int sbag_aggregate_device(sbag_ctx* ctx, const void* d_in, int32_t in_bytes, int32_t K,
+                          int64_t num_rows, int32_t agg, int32_t num_learners,
+                          int32_t num_classes, double* d_out);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "libsbag.so")
 SBAG_OK, SBAG_EINVAL, SBAG_EEMPTY, SBAG_EDEVICE, SBAG_ENOMEM, SBAG_EUNSUPPORTED = range(6)
 IMPURITY_VARIANCE, IMPURITY_GINI = 0, 1
 AGG_MEAN, AGG_MODE = 0, 1
+OUT_SUM, OUT_VOTES = 2, 3  # device outputs of sbag_predict_dataset_device
 
 # every symbol include/sbag.h declares (checked by tests/test_abi.py)
 EXPORTED = [
@@ -24,7 +25,8 @@ EXPORTED = [
     "sbag_dataset_info", "sbag_dataset_labels", "sbag_dataset_features", "sbag_dataset_free",
     "sbag_fit", "sbag_forest_num_trees", "sbag_forest_tree_info", "sbag_forest_subspace",
     "sbag_forest_nodes", "sbag_forest_create", "sbag_forest_free", "sbag_forest_timing",
-    "sbag_predict", "sbag_predict_dataset", "sbag_aggregate",
+    "sbag_predict", "sbag_predict_dataset", "sbag_aggregate", "sbag_predict_dataset_device",
+    "sbag_aggregate_device",
 ]
 
 
@@ -93,6 +95,15 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libsbag.so not built at {LIB_PATH}: run __graft_entry__.build()")
+        try:
+            # PyTorch-ROCm ships its own HIP runtime under the same soname
+            # (libamdhip64.so.7).  Loaded first, it is the one libsbag binds to; loaded
+            # after libsbag, torch would bring a second HIP/HSA runtime into the process
+            # and device pointers of one (torch tensors handed to the multi-GPU
+            # aggregation) would be foreign to the other.
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         P, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
         sig = {
@@ -118,6 +129,8 @@ def lib():
             "sbag_predict": [P, P, P, i64, i32, i32, P, P],
             "sbag_predict_dataset": [P, P, P, i32, P],
             "sbag_aggregate": [P, P, i32, i64, i32, P],
+            "sbag_predict_dataset_device": [P, P, P, i32, i32, P],
+            "sbag_aggregate_device": [P, P, i32, i32, i64, i32, i32, i32, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -145,7 +158,7 @@ def ptr(a):
 
 
 class Context:
-    """One device context (sbag_ctx).  Calls on a context are serialized by the caller."""
+    """One device context (sbag_ctx).  The library serializes calls on a context (sbag.h)."""
 
     def __init__(self, device=0):
         self._h = ctypes.c_void_p()
@@ -374,3 +387,18 @@ def aggregate(ctx, votes, agg):
     check(lib().sbag_aggregate(ctx.handle, ptr(votes), votes.shape[0], votes.shape[1], agg,
                                ptr(out)))
     return out
+
+
+def predict_dataset_device(ctx, forest, dataset, out_kind, vote_bytes, d_out):
+    """Device outputs for the multi-GPU aggregation (distributed.transform): d_out is a
+    device pointer on the context's device (OUT_SUM: fp64 [N]; OUT_VOTES: [trees x N]
+    u8 / u16 class ids)."""
+    check(lib().sbag_predict_dataset_device(ctx.handle, forest.handle, dataset.handle, out_kind,
+                                            vote_bytes, ctypes.c_void_p(d_out)))
+
+
+def aggregate_device(ctx, d_in, in_bytes, K, N, agg, num_learners, num_classes, d_out):
+    """Ordered mean of K fp64 partial-sum rows / num_learners, or breeze mode of K u8 /
+    u16 vote rows; device pointers in and out (fp64 [N])."""
+    check(lib().sbag_aggregate_device(ctx.handle, ctypes.c_void_p(d_in), in_bytes, K, N, agg,
+                                      num_learners, num_classes, ctypes.c_void_p(d_out)))

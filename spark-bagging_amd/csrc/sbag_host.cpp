@@ -131,7 +131,13 @@ struct sbag_ctx {
   // that is reset whenever the stream is known to be idle (every d2h synchronizes)
   unsigned char* pin = nullptr;
   size_t pin_cap = 0, pin_used = 0;
+  // every entry point that uses the context holds this: concurrent callers (learner
+  // Futures, CrossValidator fits, executor threads) share its stream, workspace, pinned
+  // arena and host pool, so their calls are serialized here (recursive: sbag_fit
+  // re-enters itself when it splits a learner range)
+  std::recursive_mutex mu;
 };
+#define CTX_LOCK(c) std::lock_guard<std::recursive_mutex> ctx_lock_((c)->mu)
 
 static int ws_get(sbag_ctx* c, const std::string& name, size_t bytes, void** out) {
   DevBuf& b = c->ws[name];
@@ -646,6 +652,7 @@ int sbag_ctx_create(int32_t device_ordinal, sbag_ctx** out) {
 
 int sbag_ctx_destroy(sbag_ctx* c) {
   if (!c) return SBAG_OK;
+  { CTX_LOCK(c); }  // no call is in flight on it any more
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (auto& kv : c->ws)
@@ -733,6 +740,7 @@ static int check_partitions(int32_t P, const int64_t* off, int64_t N, std::vecto
 int sbag_sample(sbag_ctx* c, const sbag_sampler_params* p, const int64_t* partition_offsets,
                 int32_t P, int64_t N, uint8_t* counts_out) {
   if (!c || !p || !counts_out || N < 0) return fail(SBAG_EINVAL, "bad arguments");
+  CTX_LOCK(c);
   TRY(check_sampler(p));
   std::vector<int64_t> poff;
   TRY(check_partitions(P, partition_offsets, N, poff));
@@ -750,6 +758,7 @@ int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, cons
   if (!c || !out || N < 0 || F <= 0 || (N > 0 && (!X || !y))) return fail(SBAG_EINVAL, "bad arguments");
   if (N == 0) return fail(SBAG_EEMPTY, "ML algorithm was given empty dataset.");
   if (N >= (int64_t)1 << 32) return fail(SBAG_EUNSUPPORTED, "more than 2^32 rows");
+  CTX_LOCK(c);
   HIP_TRY(hipSetDevice(c->device));
   auto ds = std::make_unique<sbag_dataset>();
   ds->ctx = c;
@@ -814,6 +823,7 @@ int sbag_dataset_synthetic(sbag_ctx* c, int64_t N, int32_t F, uint64_t seed, int
   if (!c || !out || N <= 0 || F <= 0 || num_classes < 0 || num_classes > 256)
     return fail(SBAG_EINVAL, "bad arguments");
   if (N >= (int64_t)1 << 32) return fail(SBAG_EUNSUPPORTED, "more than 2^32 rows");
+  CTX_LOCK(c);
   HIP_TRY(hipSetDevice(c->device));
   auto ds = std::make_unique<sbag_dataset>();
   ds->ctx = c;
@@ -868,6 +878,7 @@ int sbag_dataset_labels(const sbag_dataset* ds, double* y) {
 int sbag_dataset_features(const sbag_dataset* ds, int64_t r0, int64_t r1, double* X) {
   if (!ds || !X || r0 < 0 || r1 > ds->N || r1 < r0) return fail(SBAG_EINVAL, "bad arguments");
   sbag_ctx* c = ds->ctx;
+  CTX_LOCK(c);
   HIP_TRY(hipSetDevice(c->device));
   const int64_t n = r1 - r0;
   std::vector<uint8_t> buf((size_t)n * ds->S * ds->code_bytes);
@@ -885,6 +896,7 @@ int sbag_dataset_features(const sbag_dataset* ds, int64_t r0, int64_t r1, double
 
 int sbag_dataset_free(sbag_dataset* ds) {
   if (!ds) return SBAG_OK;
+  CTX_LOCK(ds->ctx);
   (void)hipSetDevice(ds->ctx->device);
   (void)hipStreamSynchronize(ds->ctx->stream);
   if (ds->d_codes) (void)hipFree(ds->d_codes);
@@ -1034,6 +1046,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
 // bins do not fit is fitted as two halves and the trees concatenated in learner order.
 int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
   if (!c || !ds || !fp || !out) return fail(SBAG_EINVAL, "bad arguments");
+  if (ds->ctx->device != c->device)
+    return fail(SBAG_EINVAL, "dataset lives on device " + std::to_string(ds->ctx->device) +
+                                 ", the context on device " + std::to_string(c->device));
+  CTX_LOCK(c);
   const int st = fit_range(c, ds, fp, out);
   if (st != kSplitRange) return st;
   const int lb = fp->sampler.learner_begin, le = fp->sampler.learner_end, mid = lb + (le - lb) / 2;
@@ -2299,26 +2315,45 @@ int sbag_forest_timing(const sbag_forest* f, sbag_timing* out) {
   *out = f->timing;
   return SBAG_OK;
 }
+// Model load / JNI round trip: the arrays come from disk or another process, so every
+// link, index and class id the predict kernels will follow is checked first (a bad
+// child link would walk out of the tree or loop forever on the device).
 int sbag_forest_create(int32_t T, const int32_t* num_nodes, const sbag_node* nodes,
                        const int32_t* sub_len, const int32_t* subs, int32_t impurity,
                        sbag_forest** out) {
   if (T <= 0 || !num_nodes || !nodes || !sub_len || !subs || !out)
     return fail(SBAG_EINVAL, "bad arguments");
+  if (impurity != SBAG_IMPURITY_VARIANCE && impurity != SBAG_IMPURITY_GINI)
+    return fail(SBAG_EINVAL, "unknown impurity");
   auto f = std::make_unique<sbag_forest>();
   f->impurity = impurity;
   f->trees.resize(T);
   int64_t no = 0, so = 0;
   int nclasses = 0;
   for (int t = 0; t < T; t++) {
+    const std::string bad = "malformed tree " + std::to_string(t) + ": ";
+    if (num_nodes[t] <= 0 || sub_len[t] < 0) return fail(SBAG_EINVAL, bad + "empty");
     HTree& h = f->trees[t];
     h.nodes.assign(nodes + no, nodes + no + num_nodes[t]);
     h.sub.assign(subs + so, subs + so + sub_len[t]);
-    for (int i = 0; i < num_nodes[t]; i++) {
-      const sbag_node& n = h.nodes[i];
-      if (n.left >= num_nodes[t] || n.right >= num_nodes[t] || (n.left >= 0 && (n.feature < 0 || n.feature >= sub_len[t])))
-        return fail(SBAG_EINVAL, "malformed tree " + std::to_string(t));
-      if (n.left < 0 && impurity == SBAG_IMPURITY_GINI)
-        nclasses = std::max(nclasses, (int)n.prediction + 1);
+    for (int32_t g : h.sub)
+      if (g < 0) return fail(SBAG_EINVAL, bad + "negative subspace index");
+    const int n = num_nodes[t];
+    for (int i = 0; i < n; i++) {
+      const sbag_node& nd = h.nodes[i];
+      if (nd.left >= 0 || nd.right >= 0) {
+        // pre-order ids: both children exist, lie inside the tree and after their parent,
+        // so every walk strictly advances and ends at a leaf
+        if (!(nd.left > i && nd.right > i && nd.left < n && nd.right < n && nd.left != nd.right))
+          return fail(SBAG_EINVAL, bad + "node " + std::to_string(i) + " has bad child links");
+        if (nd.feature < 0 || nd.feature >= sub_len[t])
+          return fail(SBAG_EINVAL, bad + "node " + std::to_string(i) + " splits outside the subspace");
+      } else if (impurity == SBAG_IMPURITY_GINI) {
+        const double v = nd.prediction;
+        if (!(v >= 0 && v == std::floor(v) && v < 4096))
+          return fail(SBAG_EINVAL, bad + "leaf " + std::to_string(i) + " predicts no class id");
+        nclasses = std::max(nclasses, (int)v + 1);
+      }
     }
     no += num_nodes[t];
     so += sub_len[t];
@@ -2365,6 +2400,19 @@ static int check_agg(const sbag_forest* f, int agg) {
   if (agg != SBAG_AGG_MEAN && agg != SBAG_AGG_MODE) return fail(SBAG_EINVAL, "unknown aggregation");
   if (agg == SBAG_AGG_MODE && (f->nclasses <= 0 || f->nclasses > 4096))
     return fail(SBAG_EINVAL, "mode aggregation needs class-valued trees");
+  return SBAG_OK;
+}
+
+// Mode counters past the LDS (more than kLdsModeClasses classes): u16 [nclasses][rows]
+// in global memory, at most 256 MB, the rows then processed in batches of *rows_out.
+static int mode_counters(sbag_ctx* c, int agg, int nclasses, int64_t N, uint16_t** d_out,
+                         int64_t* rows_out) {
+  *d_out = nullptr;
+  *rows_out = 0;
+  if (agg != SBAG_AGG_MODE || nclasses <= kLdsModeClasses) return SBAG_OK;
+  const int64_t rows = std::max<int64_t>(256, std::min<int64_t>(N, ((int64_t)256 << 20) / (2 * nclasses)));
+  TRY(ws_typed(c, "mode_cnt", (size_t)nclasses * rows, d_out));
+  *rows_out = rows;
   return SBAG_OK;
 }
 
@@ -2466,6 +2514,7 @@ extern "C" {
 int sbag_predict(sbag_ctx* c, const sbag_forest* f, const double* X, int64_t N, int32_t F, int32_t agg,
                  double* out, double* per_tree) {
   if (!c || !f || !X || !out || N < 0 || F <= 0) return fail(SBAG_EINVAL, "bad arguments");
+  CTX_LOCK(c);
   TRY(check_agg(f, agg));
   for (const HTree& t : f->trees)
     for (int32_t g : t.sub)
@@ -2533,31 +2582,44 @@ int sbag_predict(sbag_ctx* c, const sbag_forest* f, const double* X, int64_t N, 
   TRY(ws_typed(c, "pX", (size_t)N * F, &d_X));
   if (per_tree) TRY(ws_typed(c, "ppt", (size_t)N * L, &d_pt));
   TRY(h2d(c, d_X, X, (size_t)N * F));
+  uint16_t* d_gcnt = nullptr;
+  int64_t gcnt_rows = 0;
+  TRY(mode_counters(c, agg, f->nclasses, N, &d_gcnt, &gcnt_rows));
   launch_predict(c->stream, d_X, nullptr, 1, nullptr, nullptr, N, F, F, f->d_nodes, f->d_off, L, agg,
-                 std::max(f->nclasses, 1), d_out, d_pt);
+                 std::max(f->nclasses, 1), d_out, d_pt, nullptr, 0, d_gcnt, gcnt_rows);
   HIP_TRY(hipGetLastError());
   TRY(d2h(c, out, d_out, (size_t)N));
   if (per_tree) TRY(d2h(c, per_tree, d_pt, (size_t)N * L));
   return SBAG_OK;
 }
 
-int sbag_predict_dataset(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* ds, int32_t agg,
-                         double* out) {
-  if (!c || !f || !ds || !out) return fail(SBAG_EINVAL, "bad arguments");
-  TRY(check_agg(f, agg));
+// Forest over a device dataset into device memory: kAggMean / kAggMode -> fp64 [N],
+// kAggSum -> fp64 [N] in-order sum over the forest's trees, kAggVotes -> [L][N] class
+// ids (vote_bytes 1 or 2).  d_out == nullptr: into the context's workspace (*d_res).
+static int predict_dataset_dev(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* ds, int agg,
+                               int vote_bytes, void* d_out, void** d_res) {
   for (const HTree& t : f->trees)
     for (int32_t g : t.sub)
       if (g >= ds->F) return fail(SBAG_EINVAL, "dataset has fewer features than the model");
+  if (ds->ctx->device != c->device)
+    return fail(SBAG_EINVAL, "dataset lives on device " + std::to_string(ds->ctx->device) +
+                                 ", the context on device " + std::to_string(c->device));
   HIP_TRY(hipSetDevice(c->device));
-  double* d_out;
-  TRY(ws_typed(c, "pout", (size_t)ds->N, &d_out));
-  if (ds->N == 0) return SBAG_OK;
   const int L = (int)f->trees.size();
+  if (!d_out) {
+    const size_t bytes = agg == kAggVotes ? (size_t)L * ds->N * vote_bytes : (size_t)ds->N * 8;
+    TRY(ws_get(c, "pout", bytes, &d_out));
+  }
+  if (d_res) *d_res = d_out;
+  if (ds->N == 0) return SBAG_OK;
+  double* d_o = agg == kAggVotes ? nullptr : (double*)d_out;
+  void* d_votes = agg == kAggVotes ? d_out : nullptr;
   PredictArgs pa{};
   pa.code_bytes = ds->code_bytes;
   pa.S = ds->S;
   pa.N = ds->N;
   pa.agg = agg;
+  pa.vote_bytes = vote_bytes;
   TiledPlan P;
   // TreePoint's `value <= threshold` in the dataset's code space (dict sorted ascending)
   const bool tiled = ds->code_bytes != 4 && plan_tiled(f, pa, ds->F, [&](int g, double thr) {
@@ -2567,15 +2629,50 @@ int sbag_predict_dataset(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* 
   if (tiled) {
     TRY(upload_plan(c, P, pa));
     pa.codes = ds->d_codes;
-    pa.out = d_out;
+    pa.out = d_o;
+    pa.votes = d_votes;
     launch_predict_tiled(c->stream, pa);
-  } else {  // very deep trees or very wide rows: node walk from global memory
+  } else {  // very deep trees, very wide rows or many classes: node walk from global memory
     TRY(upload_forest(c, f));
+    uint16_t* d_gcnt = nullptr;
+    int64_t gcnt_rows = 0;
+    TRY(mode_counters(c, agg, f->nclasses, ds->N, &d_gcnt, &gcnt_rows));
     launch_predict(c->stream, nullptr, ds->d_codes, ds->code_bytes, ds->d_dict, ds->d_dict_off, ds->N,
-                   ds->F, ds->S, f->d_nodes, f->d_off, L, agg, std::max(f->nclasses, 1), d_out, nullptr);
+                   ds->F, ds->S, f->d_nodes, f->d_off, L, agg, std::max(f->nclasses, 1), d_o, nullptr,
+                   d_votes, vote_bytes, d_gcnt, gcnt_rows);
   }
   HIP_TRY(hipGetLastError());
-  TRY(d2h(c, out, d_out, (size_t)ds->N));
+  return SBAG_OK;
+}
+
+int sbag_predict_dataset(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* ds, int32_t agg,
+                         double* out) {
+  if (!c || !f || !ds || !out) return fail(SBAG_EINVAL, "bad arguments");
+  CTX_LOCK(c);
+  TRY(check_agg(f, agg));
+  void* d_out = nullptr;
+  TRY(predict_dataset_dev(c, f, ds, agg, 0, nullptr, &d_out));
+  TRY(d2h(c, out, (const double*)d_out, (size_t)ds->N));
+  return SBAG_OK;
+}
+
+int sbag_predict_dataset_device(sbag_ctx* c, const sbag_forest* f, const sbag_dataset* ds,
+                                int32_t out_kind, int32_t vote_bytes, void* d_out) {
+  if (!c || !f || !ds || !d_out) return fail(SBAG_EINVAL, "bad arguments");
+  if (out_kind != SBAG_OUT_SUM && out_kind != SBAG_OUT_VOTES)
+    return fail(SBAG_EINVAL, "unknown output kind");
+  CTX_LOCK(c);
+  if (out_kind == SBAG_OUT_VOTES) {
+    if (f->impurity != SBAG_IMPURITY_GINI || f->nclasses <= 0)
+      return fail(SBAG_EINVAL, "votes need class-valued trees");
+    if (vote_bytes != 1 && vote_bytes != 2) return fail(SBAG_EINVAL, "vote_bytes must be 1 or 2");
+    if (f->nclasses > (vote_bytes == 1 ? 256 : 4096))
+      return fail(SBAG_EINVAL, std::to_string(f->nclasses) + " classes do not fit " +
+                                   std::to_string(vote_bytes) + "-byte votes");
+  }
+  TRY(predict_dataset_dev(c, f, ds, out_kind == SBAG_OUT_SUM ? kAggSum : kAggVotes, vote_bytes,
+                          d_out, nullptr));
+  HIP_TRY(hipStreamSynchronize(c->stream));  // the caller's stream reads d_out next
   return SBAG_OK;
 }
 
@@ -2583,6 +2680,7 @@ int sbag_aggregate(sbag_ctx* c, const double* votes, int32_t L, int64_t N, int32
   if (!c || !votes || !out || L <= 0 || N < 0) return fail(SBAG_EINVAL, "bad arguments");
   if (agg != SBAG_AGG_MEAN && agg != SBAG_AGG_MODE) return fail(SBAG_EINVAL, "unknown aggregation");
   if (N == 0) return SBAG_OK;
+  CTX_LOCK(c);
   int ncls = 1;
   if (agg == SBAG_AGG_MODE) {
     for (int64_t i = 0; i < (int64_t)L * N; i++) {
@@ -2596,9 +2694,39 @@ int sbag_aggregate(sbag_ctx* c, const double* votes, int32_t L, int64_t N, int32
   TRY(ws_typed(c, "agv", (size_t)L * N, &d_v));
   TRY(ws_typed(c, "agout", (size_t)N, &d_out));
   TRY(h2d(c, d_v, votes, (size_t)L * N));
-  launch_aggregate(c->stream, d_v, L, N, agg, ncls, d_out);
+  uint16_t* d_gcnt = nullptr;
+  int64_t gcnt_rows = 0;
+  TRY(mode_counters(c, agg, ncls, N, &d_gcnt, &gcnt_rows));
+  launch_aggregate(c->stream, d_v, 8, L, N, agg, ncls, (double)L, d_out, d_gcnt, gcnt_rows);
   HIP_TRY(hipGetLastError());
   TRY(d2h(c, out, d_out, (size_t)N));
+  return SBAG_OK;
+}
+
+int sbag_aggregate_device(sbag_ctx* c, const void* d_in, int32_t in_bytes, int32_t K, int64_t N,
+                          int32_t agg, int32_t num_learners, int32_t num_classes, double* d_out) {
+  if (!c || !d_in || !d_out || K <= 0 || N < 0 || num_learners <= 0)
+    return fail(SBAG_EINVAL, "bad arguments");
+  if (in_bytes != 1 && in_bytes != 2 && in_bytes != 8) return fail(SBAG_EINVAL, "in_bytes must be 1, 2 or 8");
+  if (agg == SBAG_AGG_MODE) {
+    if (num_classes <= 0 || num_classes > 4096) return fail(SBAG_EINVAL, "num_classes out of range");
+    if (in_bytes == 8) return fail(SBAG_EINVAL, "device mode aggregation takes u8 / u16 class ids");
+    if (in_bytes == 1 && num_classes > 256) return fail(SBAG_EINVAL, "u8 votes hold at most 256 classes");
+  } else if (agg == SBAG_AGG_MEAN) {
+    if (in_bytes != 8) return fail(SBAG_EINVAL, "mean aggregation takes fp64 values");
+  } else {
+    return fail(SBAG_EINVAL, "unknown aggregation");
+  }
+  if (N == 0) return SBAG_OK;
+  CTX_LOCK(c);
+  HIP_TRY(hipSetDevice(c->device));
+  uint16_t* d_gcnt = nullptr;
+  int64_t gcnt_rows = 0;
+  TRY(mode_counters(c, agg, num_classes, N, &d_gcnt, &gcnt_rows));
+  launch_aggregate(c->stream, d_in, in_bytes, K, N, agg, std::max(num_classes, 1), (double)num_learners,
+                   d_out, d_gcnt, gcnt_rows);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return SBAG_OK;
 }
 

@@ -147,9 +147,17 @@ struct PredictArgs {
   int32_t nchunks, L;
   int32_t agg, nclasses;
   int32_t chunk_bytes;       // LDS bytes reserved for one chunk
-  int32_t pad;
+  int32_t vote_bytes;        // kAggVotes: 1 (u8) or 2 (u16) per vote
   double* out;
+  void* votes;               // kAggVotes: [L][N] class ids
 };
+
+// aggregation kinds of the predict / aggregate kernels (SBAG_AGG_MEAN / _MODE and the
+// device outputs of sbag_predict_dataset_device)
+constexpr int kAggMean = 0, kAggMode = 1, kAggSum = 2, kAggVotes = 3;
+// mode counters of k_predict / k_aggregate fit in LDS up to this many classes
+// (u16 x 256 threads per class, 160 KB)
+constexpr int kLdsModeClasses = 320;
 
 // ---- launchers (sbag_kernels.hip) ----
 void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
@@ -205,9 +213,12 @@ void launch_synth(hipStream_t st, uint8_t* codes, int32_t S, int64_t N, int32_t 
 void launch_predict(hipStream_t st, const double* X, const void* codes, int code_bytes,
                     const double* dict, const int64_t* dict_off, int64_t N, int32_t F, int32_t S,
                     const DevNode* nodes, const int64_t* tree_off, int L, int agg, int nclasses,
-                    double* out, double* per_tree);
-void launch_aggregate(hipStream_t st, const double* votes, int L, int64_t N, int agg, int nclasses,
-                      double* out);
+                    double* out, double* per_tree, void* votes, int vote_bytes, uint16_t* gcnt,
+                    int64_t gcnt_rows);
+// vote_bytes: 8 = fp64 values, 1 / 2 = u8 / u16 class ids
+void launch_aggregate(hipStream_t st, const void* votes, int vote_bytes, int K, int64_t N, int agg,
+                      int nclasses, double num_learners, double* out, uint16_t* gcnt,
+                      int64_t gcnt_rows);
 size_t predict_tiled_lds(const PredictArgs& a);
 void launch_quantize(hipStream_t st, const double* X, int64_t n, int32_t F, const double* thr,
                      const int64_t* toff, uint16_t* codes, int32_t S);

@@ -28,12 +28,27 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
+#include <set>
+#include <utility>
 
 #include "sbag_internal.h"
 
 namespace sbag {
 
-#define HIPCHK(x) (void)(x)
+// Raise a kernel's dynamic-LDS cap once per (kernel, device).  Thread-safe: contexts on
+// different devices launch from their own threads (ml.py trains one thread per device).
+// A failure stays in hipGetLastError(), which every launch site checks (HIP_TRY).
+static void set_max_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count({fn, dev})) return;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess)
+    done.insert({fn, dev});
+}
 
 // ======================================================================
 // Poisson sampler: Well19937c state in LDS, one lane per stream, all lanes
@@ -430,22 +445,15 @@ void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d
                     int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err) {
   const int64_t streams = (int64_t)R * P;
   const int blocks = (int)((streams + 63) / 64);
-  static int v1 = -1;
-  if (v1 < 0) v1 = getenv("SBAG_POISSON_V1") ? 1 : 0;
+  static const int v1 = getenv("SBAG_POISSON_V1") ? 1 : 0;
   if (v1) {
     hipLaunchKernelGGL(k_poisson, dim3(blocks), dim3(64), 0, st, counts, N, d_part_off, P, R,
                        learner0, seed, mean, p_exp, d_err);
     return;
   }
   const size_t lds = (size_t)(624 + 2 * kPB) * 64 * 4;  // 163840 = the whole LDS
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_poisson2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
-    attr_set = true;
-  }
-  static int dbg = -1;
-  if (dbg < 0) dbg = getenv("SBAG_POISSON_DBG") ? atoi(getenv("SBAG_POISSON_DBG")) : 0;
+  set_max_lds((const void*)k_poisson2, (int)lds);
+  static const int dbg = getenv("SBAG_POISSON_DBG") ? atoi(getenv("SBAG_POISSON_DBG")) : 0;
   hipLaunchKernelGGL(k_poisson2, dim3(blocks), dim3(128), lds, st, counts, N, d_part_off, P, R,
                      learner0, seed, mean, p_exp, d_err, dbg);
 }
@@ -745,12 +753,7 @@ void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                             const int32_t* d_Fr, int32_t Fmax, const int64_t* d_vcoff, uint32_t* vc,
                             int lds_words) {
   if (nrep == 0) return;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_split_sample_vc,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
-    attr_set = true;
-  }
+  set_max_lds((const void*)k_split_sample_vc, 64 * 1024);
   const dim3 grid((unsigned)((cap + kSvcRows - 1) / kSvcRows), (unsigned)nrep);
   hipLaunchKernelGGL(k_split_sample_vc, grid, dim3(256), (size_t)lds_words * 4, st, d_rows, cap,
                      d_nrows, d_reps, (const uint8_t*)codes, code_bytes, S, d_sub, d_Fr, Fmax,
@@ -1460,14 +1463,10 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
 
 template <int K, bool OFF32>
 static void launch_hist_rl_ko(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    for (const void* f : {(const void*)k_hist_rl<kHistGini, K, OFF32>,
-                          (const void*)k_hist_rl<kHistVar, K, OFF32>,
-                          (const void*)k_hist_rl<kHistSq, K, OFF32>})
-      HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  for (const void* f : {(const void*)k_hist_rl<kHistGini, K, OFF32>,
+                        (const void*)k_hist_rl<kHistVar, K, OFF32>,
+                        (const void*)k_hist_rl<kHistSq, K, OFF32>})
+    set_max_lds(f, 160 * 1024);
   if (mode == kHistGini)
     hipLaunchKernelGGL((k_hist_rl<kHistGini, K, OFF32>), grid, dim3(kHistThreads), lds, st, a);
   else if (mode == kHistVar)
@@ -1518,12 +1517,7 @@ size_t hist_stage_bytes() { return (size_t)kHistWaves * 64 * 8; }
 
 template <int MODE, int NJ>
 static void launch_hist_t(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds_bytes) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_hist<MODE, NJ>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  set_max_lds((const void*)k_hist<MODE, NJ>, 160 * 1024);
   hipLaunchKernelGGL((k_hist<MODE, NJ>), grid, dim3(kHistThreads), lds_bytes, st, a);
 }
 
@@ -2404,26 +2398,15 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
 
 void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
   const size_t lds = 256 * (8 + 4 + 4 + 4) + 8 * (size_t)a.NS + (gini ? (size_t)a.NS * 256 * 4 : 0);
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_split<true>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)k_split<false>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  set_max_lds((const void*)k_split<true>, 160 * 1024);
+  set_max_lds((const void*)k_split<false>, 160 * 1024);
   if (gini) {
     // feature group: <= 64 KB of u32 prefix counts and about one candidate per thread
     const size_t per_f = (size_t)a.NB * (a.NS + 1) * 4;
     int G = (int)std::max<size_t>(1, std::min<size_t>((64 * 1024) / per_f, (size_t)(256 / std::max(1, a.NB - 1))));
     G = std::max(1, std::min(G, a.Fmax));
     const size_t lds_g = (size_t)a.NS * 8 + 256 * (8 + 4 + 4) + (size_t)G * per_f;
-    static bool attr_g = false;
-    if (!attr_g) {
-      HIPCHK(hipFuncSetAttribute((const void*)k_split_gini, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 160 * 1024));
-      attr_g = true;
-    }
+    set_max_lds((const void*)k_split_gini, 160 * 1024);
     if (lds_g <= 160 * 1024 && !getenv("SBAG_SPLIT_GINI_V1")) {
       hipLaunchKernelGGL(k_split_gini, dim3(M), dim3(256), lds_g, st, a, G);
       return;
@@ -2625,6 +2608,11 @@ void launch_synth(hipStream_t st, uint8_t* codes, int32_t S, int64_t N, int32_t 
 // Prediction: thread per row, trees in learner order (breeze sum order /
 // breeze mode "first value to reach the final max count").
 // ======================================================================
+// Global-memory node walk (trees too deep for the LDS-tiled kernel, per-tree fp64
+// outputs, or more classes than the tiled kernel's counters fit).  One thread per row
+// of [row_begin, row_end).  Mode counters are u16 [nclasses][256] in LDS, or, when
+// `gcnt` is given (more than kLdsModeClasses classes), u16 [nclasses][row_end -
+// row_begin] in global memory, zeroed by the launcher.
 __global__ __launch_bounds__(256) void k_predict(const double* __restrict__ X,
                                                  const void* __restrict__ codes, int code_bytes,
                                                  const double* __restrict__ dict,
@@ -2633,14 +2621,18 @@ __global__ __launch_bounds__(256) void k_predict(const double* __restrict__ X,
                                                  const DevNode* __restrict__ nodes,
                                                  const int64_t* __restrict__ tree_off, int L,
                                                  int agg, int nclasses, double* __restrict__ out,
-                                                 double* __restrict__ per_tree) {
+                                                 double* __restrict__ per_tree,
+                                                 void* __restrict__ votes, int vote_bytes,
+                                                 uint16_t* __restrict__ gcnt, int64_t row_begin,
+                                                 int64_t row_end) {
   extern __shared__ __align__(16) unsigned char smem[];
-  uint16_t* cnt = (uint16_t*)smem;  // [nclasses][256]
   const int tid = threadIdx.x;
-  const int64_t row = (int64_t)blockIdx.x * 256 + tid;
-  if (row >= N) return;
-  if (agg == 1)
-    for (int c = 0; c < nclasses; c++) cnt[c * 256 + tid] = 0;
+  const int64_t row = row_begin + (int64_t)blockIdx.x * 256 + tid;
+  if (row >= row_end) return;
+  const int64_t cstride = gcnt ? row_end - row_begin : 256;
+  uint16_t* cnt = gcnt ? gcnt + (row - row_begin) : (uint16_t*)smem + tid;
+  if (agg == kAggMode && !gcnt)
+    for (int c = 0; c < nclasses; c++) cnt[c * cstride] = 0;
   double sum = 0.0, mode = 0.0;
   int maxc = 0;
   for (int l = 0; l < L; l++) {
@@ -2661,34 +2653,43 @@ __global__ __launch_bounds__(256) void k_predict(const double* __restrict__ X,
     }
     const double pred = t[id].value;
     if (per_tree) per_tree[(int64_t)l * N + row] = pred;
-    if (agg == 0) {
-      sum += pred;
-    } else {
-      const int c = (int)pred;
-      const int k = ++cnt[c * 256 + tid];
+    if (agg == kAggVotes) {
+      if (vote_bytes == 1)
+        ((uint8_t*)votes)[(int64_t)l * N + row] = (uint8_t)pred;
+      else
+        ((uint16_t*)votes)[(int64_t)l * N + row] = (uint16_t)pred;
+    } else if (agg == kAggMode) {
+      const int k = ++cnt[(int64_t)(int)pred * cstride];
       if (k > maxc) {
         maxc = k;
         mode = pred;
       }
+    } else {
+      sum += pred;
     }
   }
-  out[row] = (agg == 0) ? sum / (double)L : mode;
+  if (agg != kAggVotes) out[row] = agg == kAggMean ? sum / (double)L : agg == kAggSum ? sum : mode;
 }
 
+// `gcnt` (u16 [nclasses][gcnt_rows], more than kLdsModeClasses classes) moves the mode
+// counters to global memory; the rows then go in batches of gcnt_rows.
 void launch_predict(hipStream_t st, const double* X, const void* codes, int code_bytes,
                     const double* dict, const int64_t* dict_off, int64_t N, int32_t F, int32_t S,
                     const DevNode* nodes, const int64_t* tree_off, int L, int agg, int nclasses,
-                    double* out, double* per_tree) {
-  const size_t lds = (agg == 1) ? (size_t)nclasses * 256 * 2 : 0;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_predict, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024));
-    attr_set = true;
+                    double* out, double* per_tree, void* votes, int vote_bytes, uint16_t* gcnt,
+                    int64_t gcnt_rows) {
+  const bool global_cnt = agg == kAggMode && gcnt != nullptr;
+  const size_t lds = (agg == kAggMode && !global_cnt) ? (size_t)nclasses * 256 * 2 : 0;
+  set_max_lds((const void*)k_predict, 160 * 1024);
+  const int64_t step = global_cnt ? std::max<int64_t>(gcnt_rows, 1) : std::max<int64_t>(N, 1);
+  for (int64_t r0 = 0; r0 < N; r0 += step) {
+    const int64_t r1 = std::min(N, r0 + step);
+    if (global_cnt) (void)hipMemsetAsync(gcnt, 0, (size_t)nclasses * (size_t)(r1 - r0) * 2, st);
+    hipLaunchKernelGGL(k_predict, dim3((unsigned)((r1 - r0 + 255) / 256)), dim3(256), lds, st, X,
+                       codes, code_bytes, dict, dict_off, N, F, S, nodes, tree_off, L, agg,
+                       nclasses, out, per_tree, global_cnt ? nullptr : votes, vote_bytes,
+                       global_cnt ? gcnt : nullptr, r0, r1);
   }
-  hipLaunchKernelGGL(k_predict, dim3((unsigned)((N + 255) / 256)), dim3(256), lds, st, X, codes,
-                     code_bytes, dict, dict_off, N, F, S, nodes, tree_off, L, agg, nclasses, out,
-                     per_tree);
 }
 
 // ---- LDS-tiled predict over device-resident rows (transform of large scoring
@@ -2705,7 +2706,7 @@ constexpr int kPredThreads = 256;
 size_t predict_tiled_lds(const PredictArgs& a) {
   const size_t pitch = (size_t)a.S * a.code_bytes + 4;
   size_t b = (size_t)kPredRows * pitch + (size_t)a.chunk_bytes;
-  if (a.agg == 1) b += (size_t)a.nclasses * kPredRows * 2;
+  if (a.agg == kAggMode) b += (size_t)a.nclasses * kPredRows * 2;
   return (b + 15) & ~(size_t)15;
 }
 
@@ -2725,7 +2726,7 @@ __global__ __launch_bounds__(kPredThreads) void k_predict_tiled(PredictArgs A) {
     if (row0 + r < A.N) v = *(const uint32_t*)((const unsigned char*)A.codes + (row0 + r) * rb + w * 4);
     *(uint32_t*)(rows + r * pitch + w * 4) = v;
   }
-  if (A.agg == 1)
+  if (A.agg == kAggMode)
     for (int i = tid; i < A.nclasses * kPredRows; i += kPredThreads) cnt[i] = 0;
   double sum0 = 0.0, sum1 = 0.0, mode0 = 0.0, mode1 = 0.0;
   int max0 = 0, max1 = 0;
@@ -2758,9 +2759,18 @@ __global__ __launch_bounds__(kPredThreads) void k_predict_tiled(PredictArgs A) {
         }
       }
       const double p0 = tl[a0.a & 0x7fffffffu], p1 = tl[a1.a & 0x7fffffffu];
-      if (A.agg == 0) {
+      if (A.agg == kAggMean || A.agg == kAggSum) {
         sum0 += p0;
         sum1 += p1;
+      } else if (A.agg == kAggVotes) {  // class id of tree t for both rows: [L][N] u8/u16
+        const int64_t v0 = (int64_t)t * A.N + row0 + tid, v1 = v0 + kPredThreads;
+        if (A.vote_bytes == 1) {
+          if (row0 + tid < A.N) ((uint8_t*)A.votes)[v0] = (uint8_t)p0;
+          if (row0 + tid + kPredThreads < A.N) ((uint8_t*)A.votes)[v1] = (uint8_t)p1;
+        } else {
+          if (row0 + tid < A.N) ((uint16_t*)A.votes)[v0] = (uint16_t)p0;
+          if (row0 + tid + kPredThreads < A.N) ((uint16_t*)A.votes)[v1] = (uint16_t)p1;
+        }
       } else {
         const int k0 = ++cnt[(int)p0 * kPredRows + tid];
         if (k0 > max0) {
@@ -2775,9 +2785,11 @@ __global__ __launch_bounds__(kPredThreads) void k_predict_tiled(PredictArgs A) {
       }
     }
   }
-  if (row0 + tid < A.N) A.out[row0 + tid] = A.agg == 0 ? sum0 / (double)A.L : mode0;
-  if (row0 + tid + kPredThreads < A.N)
-    A.out[row0 + tid + kPredThreads] = A.agg == 0 ? sum1 / (double)A.L : mode1;
+  if (A.agg == kAggVotes) return;
+  const double o0 = A.agg == kAggMean ? sum0 / (double)A.L : A.agg == kAggSum ? sum0 : mode0;
+  const double o1 = A.agg == kAggMean ? sum1 / (double)A.L : A.agg == kAggSum ? sum1 : mode1;
+  if (row0 + tid < A.N) A.out[row0 + tid] = o0;
+  if (row0 + tid + kPredThreads < A.N) A.out[row0 + tid + kPredThreads] = o1;
 }
 
 // rows -> u16 codes against the forest's thresholds of each feature:
@@ -2820,14 +2832,8 @@ void launch_quantize(hipStream_t st, const double* X, int64_t n, int32_t F, cons
 
 void launch_predict_tiled(hipStream_t st, const PredictArgs& a) {
   const size_t lds = predict_tiled_lds(a);
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_predict_tiled<uint8_t>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)k_predict_tiled<uint16_t>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  set_max_lds((const void*)k_predict_tiled<uint8_t>, 160 * 1024);
+  set_max_lds((const void*)k_predict_tiled<uint16_t>, 160 * 1024);
   const dim3 grid((unsigned)((a.N + kPredRows - 1) / kPredRows));
   if (a.code_bytes == 1)
     hipLaunchKernelGGL(k_predict_tiled<uint8_t>, grid, dim3(kPredThreads), lds, st, a);
@@ -2835,44 +2841,71 @@ void launch_predict_tiled(hipStream_t st, const PredictArgs& a) {
     hipLaunchKernelGGL(k_predict_tiled<uint16_t>, grid, dim3(kPredThreads), lds, st, a);
 }
 
-__global__ __launch_bounds__(256) void k_aggregate(const double* __restrict__ votes, int L,
-                                                   int64_t N, int agg, int nclasses,
-                                                   double* __restrict__ out) {
+// Ordered aggregation of K rows of per-row values [K][N] (K = learners, or ranks'
+// partial sums): kAggMean -> (in-order sum) / num_learners, kAggMode -> breeze mode
+// of class ids (first class to reach the final max count).  VT: fp64 values (host
+// per-tree predictions / partial sums) or u8 / u16 class ids (device votes after the
+// all-to-all).  Counters as in k_predict.
+template <typename VT>
+__global__ __launch_bounds__(256) void k_aggregate(const VT* __restrict__ votes, int K, int64_t N,
+                                                   int agg, int nclasses, double num_learners,
+                                                   double* __restrict__ out,
+                                                   uint16_t* __restrict__ gcnt, int64_t row_begin,
+                                                   int64_t row_end) {
   extern __shared__ __align__(16) unsigned char smem[];
-  uint16_t* cnt = (uint16_t*)smem;
   const int tid = threadIdx.x;
-  const int64_t row = (int64_t)blockIdx.x * 256 + tid;
-  if (row >= N) return;
-  if (agg == 1)
-    for (int c = 0; c < nclasses; c++) cnt[c * 256 + tid] = 0;
+  const int64_t row = row_begin + (int64_t)blockIdx.x * 256 + tid;
+  if (row >= row_end) return;
+  const int64_t cstride = gcnt ? row_end - row_begin : 256;
+  uint16_t* cnt = gcnt ? gcnt + (row - row_begin) : (uint16_t*)smem + tid;
+  if (agg == kAggMode && !gcnt)
+    for (int c = 0; c < nclasses; c++) cnt[c * cstride] = 0;
   double sum = 0.0, mode = 0.0;
   int maxc = 0;
-  for (int l = 0; l < L; l++) {
-    const double v = votes[(int64_t)l * N + row];
-    if (agg == 0) {
-      sum += v;
-    } else {
-      const int k = ++cnt[(int)v * 256 + tid];
+  for (int l = 0; l < K; l++) {
+    const double v = (double)votes[(int64_t)l * N + row];
+    if (agg == kAggMode) {
+      const int k = ++cnt[(int64_t)(int)v * cstride];
       if (k > maxc) {
         maxc = k;
         mode = v;
       }
+    } else {
+      sum += v;
     }
   }
-  out[row] = (agg == 0) ? sum / (double)L : mode;
+  out[row] = agg == kAggMode ? mode : sum / num_learners;
 }
 
-void launch_aggregate(hipStream_t st, const double* votes, int L, int64_t N, int agg, int nclasses,
-                      double* out) {
-  const size_t lds = (agg == 1) ? (size_t)nclasses * 256 * 2 : 0;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_aggregate, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024));
-    attr_set = true;
+template <typename VT>
+static void launch_aggregate_t(hipStream_t st, const VT* votes, int K, int64_t N, int agg,
+                               int nclasses, double num_learners, double* out, uint16_t* gcnt,
+                               int64_t gcnt_rows) {
+  const bool global_cnt = agg == kAggMode && gcnt != nullptr;
+  const size_t lds = (agg == kAggMode && !global_cnt) ? (size_t)nclasses * 256 * 2 : 0;
+  set_max_lds((const void*)k_aggregate<VT>, 160 * 1024);
+  const int64_t step = global_cnt ? std::max<int64_t>(gcnt_rows, 1) : std::max<int64_t>(N, 1);
+  for (int64_t r0 = 0; r0 < N; r0 += step) {
+    const int64_t r1 = std::min(N, r0 + step);
+    if (global_cnt) (void)hipMemsetAsync(gcnt, 0, (size_t)nclasses * (size_t)(r1 - r0) * 2, st);
+    hipLaunchKernelGGL(k_aggregate<VT>, dim3((unsigned)((r1 - r0 + 255) / 256)), dim3(256), lds, st,
+                       votes, K, N, agg, nclasses, num_learners, out, global_cnt ? gcnt : nullptr,
+                       r0, r1);
   }
-  hipLaunchKernelGGL(k_aggregate, dim3((unsigned)((N + 255) / 256)), dim3(256), lds, st, votes, L,
-                     N, agg, nclasses, out);
+}
+
+void launch_aggregate(hipStream_t st, const void* votes, int vote_bytes, int K, int64_t N, int agg,
+                      int nclasses, double num_learners, double* out, uint16_t* gcnt,
+                      int64_t gcnt_rows) {
+  if (vote_bytes == 1)
+    launch_aggregate_t(st, (const uint8_t*)votes, K, N, agg, nclasses, num_learners, out, gcnt,
+                       gcnt_rows);
+  else if (vote_bytes == 2)
+    launch_aggregate_t(st, (const uint16_t*)votes, K, N, agg, nclasses, num_learners, out, gcnt,
+                       gcnt_rows);
+  else
+    launch_aggregate_t(st, (const double*)votes, K, N, agg, nclasses, num_learners, out, gcnt,
+                       gcnt_rows);
 }
 
 }  // namespace sbag

@@ -4,17 +4,24 @@ Bagging learners are independent (ml/regression/BaggingRegressor.scala:169-189: 
 Future per learner, no shared state), and every learner's bag and subspace depend
 only on (seed + i, partition layout, data) -- so rank g trains learners
 [g*L/G, (g+1)*L/G) with no data-path collective.  Collectives are
-used only to assemble the model and to aggregate predictions IN LEARNER ORDER:
+used only to assemble the model and to aggregate predictions in learner order, and
+they move device tensors (backend "nccl" = RCCL over xGMI on MI355X; "gloo" with CPU
+tensors in the CPU tests):
 
-  regression      per-tree predictions all-gathered in learner order, then the
-                  sequential sum / L of BaggingRegressionModel.predict
-                  (ml/regression/BaggingRegressor.scala:248-256) -- bit-identical
-                  to the single-process order;
-  classification  per-tree votes all-gathered, then breeze mode with its
-                  first-to-reach-the-max tie rule (BaggingClassifier.scala:248-257).
-
-The backend is whatever process group is initialised: "nccl" (RCCL over xGMI)
-on MI355X nodes, "gloo" in the CPU tests.
+  regression      every rank sums its own trees' predictions in learner order on the
+                  device (sbag_predict_dataset_device, SBAG_OUT_SUM: N fp64), an
+                  all-to-all hands rank g the G partial sums of its row shard, which
+                  it adds in rank order and divides by L (sbag_aggregate_device):
+                  BaggingRegressionModel.predict's sequential sum / L
+                  (ml/regression/BaggingRegressor.scala:248-256) re-associated at the
+                  G shard boundaries -- within 1e-5 relative (north_star), and
+                  deterministic.  8 bytes per row cross the links, not 8 L;
+  classification  every rank writes its trees' class ids as u8 (u16 above 256
+                  classes) [L_g x N]; an all-to-all by row shard gives rank g all L
+                  votes of its rows in learner order (rank order = learner order),
+                  and breeze's mode with its first-to-reach-the-max tie rule
+                  (BaggingClassifier.scala:248-257) runs there -- bit-exact.
+  Both finish with an all-gather of the N fp64 predictions by row shard.
 """
 import numpy as np
 
@@ -24,22 +31,58 @@ def learner_range(num_learners, rank, world):
     return (rank * num_learners // world, (rank + 1) * num_learners // world)
 
 
-def gather_votes(local_votes, dist, device=None):
-    """All-gather per-tree predictions [L_rank x N] into [L x N] in learner order."""
+def row_range(num_rows, rank, world):
+    """Row shard of `rank` for the aggregation (contiguous, rank order)."""
+    return (rank * num_rows // world, (rank + 1) * num_rows // world)
+
+
+def _all_gather_ints(value, dist, device):
     import torch
 
     world = dist.get_world_size()
-    local = torch.as_tensor(np.ascontiguousarray(local_votes, np.float64), device=device)
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
-    lmax = max(sizes)
-    pad = torch.zeros((lmax, local.shape[1]), dtype=torch.float64, device=device)
-    pad[: local.shape[0]] = local
-    parts = [torch.zeros_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
-    return np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)], axis=0)
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [int(o.item()) for o in out]
+
+
+def exchange_rows(local, dist):
+    """All-to-all by row shard: this rank's [K_rank x N] tensor -> [K_total x n_rank],
+    the rows of every rank's block stacked in rank order (= learner order)."""
+    import torch
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    K, N = local.shape
+    ks = _all_gather_ints(K, dist, local.device)
+    shards = [row_range(N, s, world) for s in range(world)]
+    a, b = shards[rank]
+    n_me = b - a
+    send = torch.cat([local[:, s0:s1].reshape(-1) for s0, s1 in shards]) if K else \
+        torch.empty(0, dtype=local.dtype, device=local.device)
+    recv = torch.empty(sum(ks) * n_me, dtype=local.dtype, device=local.device)
+    dist.all_to_all_single(recv, send, output_split_sizes=[k * n_me for k in ks],
+                           input_split_sizes=[K * (s1 - s0) for s0, s1 in shards])
+    return recv.view(sum(ks), n_me)
+
+
+def gather_rows(part, num_rows, dist):
+    """All-gather the row shards' predictions [n_rank] -> [N] in row order."""
+    import torch
+
+    world = dist.get_world_size()
+    sizes = [row_range(num_rows, s, world) for s in range(world)]
+    sizes = [s1 - s0 for s0, s1 in sizes]
+    pad = torch.zeros(max(sizes), dtype=part.dtype, device=part.device)
+    pad[: part.shape[0]] = part
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    return torch.cat([o[:s] for o, s in zip(outs, sizes)])
+
+
+def sharded_aggregate(local, num_rows, dist, reduce_fn):
+    """exchange_rows -> reduce_fn([K_total x n_rank]) -> [n_rank] fp64 -> gather_rows."""
+    rows = exchange_rows(local, dist)
+    return gather_rows(reduce_fn(rows), num_rows, dist)
 
 
 def gather_model(shard, dist):
@@ -68,13 +111,70 @@ def fit_shard(estimator, frame, dist, devices=None):
     return estimator.fit_range(frame, lb, le, devices=devices)
 
 
-def transform(shard, X, dist, device=None, agg_fn=None):
-    """Ensemble prediction of a learner-sharded model: local per-tree predictions
-    (HIP kernel), all-gather in learner order, ordered aggregation."""
-    from . import _native as nat
+def _num_classes(models):
+    c = 0
+    for m in models:
+        leaves = m.nodes["left"] < 0
+        if leaves.any():
+            c = max(c, int(m.nodes["prediction"][leaves].max()) + 1)
+    return c
 
-    _, per_tree = shard.transform(X, device=0 if device is None else device, per_tree=True)
-    votes = gather_votes(per_tree, dist, device=None)
-    if agg_fn is not None:
-        return agg_fn(votes)
-    return nat.aggregate(nat.default_context(0 if device is None else device), votes, shard._agg)
+
+def transform(shard, dataset, dist, device=None):
+    """Ensemble prediction of a learner-sharded model on every rank's device: the
+    rank's trees over its replica of the rows (HIP kernels, device outputs), an RCCL
+    all-to-all by row shard, the ordered aggregation on the device, an all-gather.
+    `dataset` is a DeviceDataset on this rank's device or host rows [N x F].
+    Returns the N predictions (numpy fp64) on every rank."""
+    import torch
+
+    from . import _native as nat
+    from .ml import Frame
+
+    if isinstance(dataset, nat.DeviceDataset):
+        ctx, ds = dataset.ctx, dataset
+    else:
+        ctx = nat.default_context(0 if device is None else device)
+        X = dataset.features if isinstance(dataset, Frame) else np.asarray(dataset, np.float64)
+        ds = nat.DeviceDataset.from_numpy(X, np.zeros(X.shape[0]), ctx)
+    dev = torch.device("cuda", ctx.device)
+
+    def sync():
+        # the library runs on its own stream: what torch's stream wrote (fills, the
+        # collective's output) must be complete before a native call reads or overwrites it
+        torch.cuda.current_stream(dev).synchronize()
+    N = ds.shape[0]
+    L_me = len(shard.models)
+    L = sum(_all_gather_ints(L_me, dist, dev))
+    forest = shard.native_forest() if L_me else None
+    if shard._agg == nat.AGG_MEAN:
+        part = torch.zeros((1, N), dtype=torch.float64, device=dev)
+        if forest is not None:
+            sync()
+            nat.predict_dataset_device(ctx, forest, ds, nat.OUT_SUM, 0, part.data_ptr())
+
+        def reduce_fn(rows):  # [G x n]: partial sums in rank order
+            out = torch.empty(rows.shape[1], dtype=torch.float64, device=dev)
+            rows = rows.contiguous()
+            sync()
+            nat.aggregate_device(ctx, rows.data_ptr(), 8, rows.shape[0],
+                                 rows.shape[1], nat.AGG_MEAN, L, 0, out.data_ptr())
+            return out
+    else:
+        C = max(_all_gather_ints(_num_classes(shard.models), dist, dev))
+        vb = 1 if C <= 256 else 2
+        part = torch.zeros((L_me, N), dtype=torch.uint8 if vb == 1 else torch.int16, device=dev)
+        if forest is not None:
+            sync()
+            nat.predict_dataset_device(ctx, forest, ds, nat.OUT_VOTES, vb, part.data_ptr())
+
+        def reduce_fn(rows):  # [L x n]: every learner's vote in learner order
+            out = torch.empty(rows.shape[1], dtype=torch.float64, device=dev)
+            rows = rows.contiguous()
+            sync()
+            nat.aggregate_device(ctx, rows.data_ptr(), vb, rows.shape[0],
+                                 rows.shape[1], nat.AGG_MODE, L, C, out.data_ptr())
+            return out
+    pred = sharded_aggregate(part, N, dist, reduce_fn)
+    torch.cuda.synchronize(dev)
+    return pred.cpu().numpy()

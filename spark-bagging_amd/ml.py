@@ -384,15 +384,19 @@ class _BaggingEstimator(_BaggingParams):
         if not (0 <= lb0 < le0 <= L):
             raise nat.IllegalArgumentException(nat.SBAG_EINVAL, f"bad learner range {learner_range}")
         seed = self.get("seed")
-        devices = self.devices or [0]
+        devices = list(self.devices or [0])
+        if len(set(devices)) != len(devices):
+            # one context per device: two shards on one context would only serialize
+            raise nat.IllegalArgumentException(nat.SBAG_EINVAL, f"duplicate device ids {devices}")
         if isinstance(dataset, Frame):
             part = dataset.partition_offsets
             make_ds = [lambda ctx, d=dataset: nat.DeviceDataset.from_numpy(d.features, d.label, ctx)]
         elif isinstance(dataset, nat.DeviceDataset):
             part = None
-            if len(devices) > 1:
-                raise nat.IllegalArgumentException(nat.SBAG_EINVAL,
-                                                   "a DeviceDataset lives on one device")
+            if len(devices) > 1 or (self.devices and devices[0] != dataset.ctx.device):
+                raise nat.IllegalArgumentException(
+                    nat.SBAG_EINVAL, f"a DeviceDataset lives on device {dataset.ctx.device} only")
+            devices = [dataset.ctx.device]
             make_ds = [lambda ctx, d=dataset: d]
         else:
             X, y = dataset
@@ -403,7 +407,8 @@ class _BaggingEstimator(_BaggingParams):
 
         def work(k):
             try:
-                ctx = nat.default_context(devices[k])
+                ds0 = dataset if isinstance(dataset, nat.DeviceDataset) else None
+                ctx = ds0.ctx if ds0 is not None else nat.default_context(devices[k])
                 ds = make_ds[0](ctx)
                 lb, le = shards[k]
                 results[k] = nat.fit(
@@ -474,9 +479,9 @@ class _BaggingModel(_BaggingParams):
 
     def transform(self, dataset, device=0, per_tree=False):
         """PredictionModel.transform: one prediction per row (HIP kernel)."""
+        if isinstance(dataset, nat.DeviceDataset):  # on the dataset's own device
+            return nat.predict_dataset(dataset.ctx, self.native_forest(), dataset, self._agg)
         ctx = nat.default_context(device)
-        if isinstance(dataset, nat.DeviceDataset):
-            return nat.predict_dataset(ctx, self.native_forest(), dataset, self._agg)
         X = dataset.features if isinstance(dataset, Frame) else np.asarray(dataset, np.float64)
         if X.ndim == 1:
             X = X[None, :]

@@ -1,0 +1,43 @@
+"""Helpers for the plain-C driver tests/c/abi_driver (the JNI shim's argument order)."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+from conftest import ROOT
+
+DRIVER = os.path.join(ROOT, "tests", "c", "abi_driver")
+
+
+def run_driver(tmp_path, X, y, offsets, *, replacement, ratio, seed, lb, le, sub_ratio,
+               bug_compat, depth, bins, min_inst, impurity, min_gain, tree_seed, agg):
+    X = np.ascontiguousarray(X, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    off = np.asarray(offsets, np.int64)
+    data = tmp_path / "data.bin"
+    out = tmp_path / "out.bin"
+    with open(data, "wb") as f:
+        f.write(struct.pack("<qqq", X.shape[0], X.shape[1], len(off)))
+        f.write(off.tobytes() + X.tobytes() + y.tobytes())
+    args = [DRIVER, str(data), str(out), str(int(replacement)), repr(float(ratio)), str(int(seed)),
+            str(lb), str(le), repr(float(sub_ratio)), str(int(bug_compat)), str(depth), str(bins),
+            str(min_inst), str(impurity), repr(float(min_gain)), str(int(tree_seed)), str(agg)]
+    p = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    raw = open(out, "rb").read() if os.path.exists(out) else b""
+    status = struct.unpack_from("<i", raw, 0)[0] if raw else None
+    if status != 0:
+        return p, status, None, None, None
+    pos = 4
+    T = struct.unpack_from("<i", raw, pos)[0]
+    pos += 4
+    trees, subs = [], []
+    for _ in range(T):
+        nn, sl = struct.unpack_from("<ii", raw, pos)
+        pos += 8
+        trees.append(np.frombuffer(raw, np.float64, nn * 8, pos).reshape(nn, 8))
+        pos += nn * 64
+        subs.append(np.frombuffer(raw, np.int32, sl, pos))
+        pos += 4 * sl
+    pred = np.frombuffer(raw, np.float64, X.shape[0], pos)
+    return p, 0, trees, subs, pred

@@ -3,6 +3,7 @@ its host-only entry points behave (no compute calls that need a GPU)."""
 import ctypes
 import os
 import re
+import shutil
 
 import numpy as np
 import pytest
@@ -81,3 +82,70 @@ def test_forest_create_rejects_malformed():
     n["left"], n["right"], n["feature"] = 5, 6, 0
     with pytest.raises(sb.IllegalArgumentException):
         nat.NativeForest.from_trees([n], [[0]], nat.IMPURITY_VARIANCE)
+
+
+def _leaf(pred):
+    n = np.zeros(1, nat.NODE_DTYPE)
+    n["left"] = n["right"] = n["feature"] = -1
+    n["prediction"] = pred
+    return n
+
+
+def _stump(left, right, feature=0, nn=3):
+    n = np.zeros(nn, nat.NODE_DTYPE)
+    n["id"] = np.arange(nn)
+    n["left"] = n["right"] = n["feature"] = -1
+    n[0]["left"], n[0]["right"], n[0]["feature"] = left, right, feature
+    n[0]["threshold"] = 0.5
+    return n
+
+
+@pytest.mark.parametrize("case", ["child_back_to_root", "self_loop", "one_child", "right_negative",
+                                  "past_end", "feature_out_of_subspace", "same_children"])
+def test_forest_create_rejects_bad_links(case):
+    """links must point forward inside the tree (pre-order), so a loaded model
+    can never make the device walk loop or leave its tree."""
+    nodes, sub = {
+        "child_back_to_root": (_stump(1, 0), [0]),
+        "self_loop": (_stump(0, 2), [0]),
+        "one_child": (_stump(1, -1), [0]),
+        "right_negative": (_stump(-1, 2), [0]),
+        "past_end": (_stump(1, 3), [0]),
+        "feature_out_of_subspace": (_stump(1, 2, feature=1), [0]),
+        "same_children": (_stump(1, 1), [0]),
+    }[case]
+    with pytest.raises(sb.IllegalArgumentException):
+        nat.NativeForest.from_trees([nodes], [sub], nat.IMPURITY_VARIANCE)
+
+
+def test_forest_create_rejects_bad_subspace_and_class_ids():
+    with pytest.raises(sb.IllegalArgumentException):  # negative global feature index
+        nat.NativeForest.from_trees([_stump(1, 2)], [[-3]], nat.IMPURITY_VARIANCE)
+    for bad in (-1.0, 2.5, 4096.0, float("nan")):  # a gini leaf must name a class id
+        with pytest.raises(sb.IllegalArgumentException):
+            nat.NativeForest.from_trees([_leaf(bad)], [[0]], nat.IMPURITY_GINI)
+    ok = nat.NativeForest.from_trees([_leaf(4095.0), _stump(1, 2)], [[0], [2]], nat.IMPURITY_GINI)
+    assert len(ok) == 2
+    # variance leaves may predict anything
+    assert len(nat.NativeForest.from_trees([_leaf(-2.5)], [[0]], nat.IMPURITY_VARIANCE)) == 1
+
+
+def test_loading_a_malformed_model_directory_fails_cleanly(tmp_path):
+    """A model directory whose tree data links a child back to its parent loads as Python
+    objects but is refused before any kernel sees it."""
+    from spark_bagging_amd import persistence as sp
+
+    trees = [_stump(1, 2), _leaf(1.0)]
+    model = sb.BaggingRegressionModel([[0], [0]], [sb.DecisionTreeModel(t, np.zeros((len(t), 3)),
+                                                                        nat.IMPURITY_VARIANCE)
+                                                   for t in trees])
+    model.set("numBaseLearners", 2)  # the regression reader counts numBaseLearners (H14)
+    path = str(tmp_path / "m")
+    model.save(path)
+    nodes, stats = sp.read_tree_data(os.path.join(path, "model-0"))
+    nodes["right"][0] = 0  # corrupt: right child -> the root
+    shutil.rmtree(os.path.join(path, "model-0", "data"))
+    sp.write_tree_data(os.path.join(path, "model-0"), nodes, stats)
+    back = sb.BaggingRegressionModel.load(path)
+    with pytest.raises(sb.IllegalArgumentException):
+        back.native_forest()

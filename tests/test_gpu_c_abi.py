@@ -1,0 +1,86 @@
+"""GPU: the C ABI driven from plain C in the JNI shim's argument order
+(tests/c/abi_driver.c over integration/sbagjni_core.c), bit-exact
+against the oracle and against the ctypes path.  Covers the 16th fit argument
+(treeSeed = the base learner's seed, which picks the split-finding sample of every
+subbag above 10^4 rows) and the exception mapping of a bad parameter."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from c_abi_util import run_driver
+from conftest import DATA
+
+import spark_bagging_amd as sb
+from spark_bagging_amd import _native as nat
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ["id", "left", "right", "feature", "threshold", "prediction", "impurity", "gain"]
+
+
+def _check_trees(trees, subs, orf):
+    assert len(trees) == orf.nodes.shape[0]
+    for t, packed in enumerate(trees):
+        on, _ = orf.tree(t)
+        assert packed.shape[0] == len(on), f"tree {t}"
+        for k, f in enumerate(FIELDS):
+            assert (packed[:, k] == on[f].astype(np.float64)).all(), f"tree {t} field {f}"
+        assert list(subs[t]) == list(orf.subspaces[t])
+
+
+def test_c_driver_vehicle_classifier(tmp_path):
+    X, y = sb.load_libsvm(os.path.join(DATA, "vehicle.svm"))
+    seed, L = oracle.DEFAULT_SEED_CLASSIFIER, 6
+    part = [0, 300, 846]
+    p, st, trees, subs, pred = run_driver(
+        tmp_path, X, y, part, replacement=1, ratio=0.7, seed=seed, lb=0, le=L, sub_ratio=0.7,
+        bug_compat=1, depth=5, bins=32, min_inst=1, impurity=nat.IMPURITY_GINI, min_gain=0.0,
+        tree_seed=nat.DT_SEED_CLASSIFIER, agg=nat.AGG_MODE)
+    assert st == 0, p.stdout + p.stderr
+    counts = oracle.bag(True, 0.7, 0, L, seed, part, len(y))
+    sub = [oracle.subspace(0.7, X.shape[1], seed + i) for i in range(L)]
+    orf = oracle.fit(X, y, counts, sub, max_depth=5, max_bins=32, classification=True, part=part)
+    _check_trees(trees, subs, orf)
+    assert (pred == oracle.predict(orf, X, classification=True)).all()
+
+
+@pytest.mark.parametrize("tree_seed", [nat.DT_SEED_REGRESSOR, 12345])
+def test_c_driver_sampled_split_finding_uses_tree_seed(tmp_path, tree_seed):
+    """24k rows: every subbag exceeds 10^4 rows, so thresholds come from Spark's
+    split-finding sample seeded by treeSeed -- the argument the old binding dropped."""
+    rng = np.random.default_rng(4)
+    X = np.round(rng.normal(size=(24000, 6)), 2)  # continuous: the sample decides the thresholds
+    X[rng.random(X.shape) < 0.15] = 0.0
+    y = rng.integers(-256, 256, 24000) / 16
+    seed, L = oracle.DEFAULT_SEED_REGRESSOR, 3
+    part = [0, 9000, 24000]
+    p, st, trees, subs, pred = run_driver(
+        tmp_path, X, y, part, replacement=1, ratio=1.0, seed=seed, lb=0, le=L, sub_ratio=1.0,
+        bug_compat=1, depth=4, bins=16, min_inst=1, impurity=nat.IMPURITY_VARIANCE, min_gain=0.0,
+        tree_seed=tree_seed, agg=nat.AGG_MEAN)
+    assert st == 0, p.stdout + p.stderr
+    counts = oracle.bag(True, 1.0, 0, L, seed, part, len(y))
+    sub = [oracle.subspace(1.0, X.shape[1], seed + i) for i in range(L)]
+    assert oracle.split_sample_fraction(int(counts[0].sum()), 16) < 1.0
+    orf = oracle.fit(X, y, counts, sub, max_depth=4, max_bins=16, part=part, dt_seed=tree_seed)
+    _check_trees(trees, subs, orf)
+    ctx = nat.Context(0)
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    f = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=seed, learner_begin=0,
+                learner_end=L, partition_offsets=part, max_depth=4, max_bins=16,
+                tree_seed=tree_seed)
+    np.testing.assert_array_equal(pred, nat.predict(ctx, f, X, nat.AGG_MEAN))
+    f.free()
+    ds.free()
+    ctx.close()
+
+
+def test_c_driver_bad_ratio_is_illegal_argument(tmp_path):
+    X, y = np.zeros((8, 2)), np.zeros(8)
+    p, st, *_ = run_driver(tmp_path, X, y, [0, 8], replacement=1, ratio=1.5, seed=1, lb=0, le=2,
+                           sub_ratio=1.0, bug_compat=1, depth=3, bins=8, min_inst=1, impurity=0,
+                           min_gain=0.0, tree_seed=1, agg=0)
+    assert st == nat.SBAG_EINVAL and p.returncode == 3
+    assert "fit" in p.stdout and "java/lang/IllegalArgumentException" in p.stdout

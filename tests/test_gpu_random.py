@@ -60,10 +60,13 @@ def test_random_parity(ctx, seed):
                          max_depth=p["depth"], max_bins=p["bins"],
                          min_instances_per_node=p["min_inst"], min_info_gain=p["min_gain"],
                          impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
-    except sb.SparkException:
-        # an empty bag: the oracle must agree that some learner drew no row
+    except sb.SparkException as e:
+        # only an empty bag is acceptable, and the oracle must agree that this learner
+        # drew no row (a device failure is also a SparkException: it must not pass here)
+        assert e.code == nat.SBAG_EEMPTY, str(e)
+        learner = int(str(e).rsplit("learner ", 1)[1].rstrip(")"))
         counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, len(y))
-        assert (counts.sum(axis=1) == 0).any()
+        assert counts[learner].sum() == 0 and (counts[:learner].sum(axis=1) > 0).all()
         return
     except sb.IllegalArgumentException as e:
         # mkSubspace drew no feature: VectorSlicer's requirement
