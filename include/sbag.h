@@ -85,6 +85,21 @@ int sbag_subspace(double ratio, int32_t num_features, int64_t seed, int32_t* idx
    codes by the widest feature) + labels.                                      */
 int sbag_dataset_create(sbag_ctx* ctx, int64_t num_rows, int32_t num_features, const double* X,
                         const double* y, sbag_dataset** out);
+/* SparseVector rows (CSR): indptr [num_rows+1] (indptr[0] == 0), per row strictly
+   increasing indices in [0, num_features), values [indptr[num_rows]]; absent entries
+   are 0.0 -- Spark's SparseVector semantics, which HasSubBag.slicer
+   (ml/ensemble/HasSubBag.scala:128-131) and DecisionTree see.  No dense copy is made. */
+int sbag_dataset_create_csr(sbag_ctx* ctx, int64_t num_rows, int32_t num_features,
+                            const int64_t* indptr, const int32_t* indices, const double* values,
+                            const double* y, sbag_dataset** out);
+/* Columnar features (Arrow / Parquet column chunks, or values quantized upstream):
+   columns[f] points to num_rows values of type col_type.                         */
+#define SBAG_COL_F64 0
+#define SBAG_COL_F32 1
+#define SBAG_COL_U8 2
+int sbag_dataset_create_columns(sbag_ctx* ctx, int64_t num_rows, int32_t num_features,
+                                int32_t col_type, const void* const* columns, const double* y,
+                                sbag_dataset** out);
 /* Deterministic synthetic data generated directly in HBM (bench workload):
    x[r,f] = splitmix64(seed ^ (r*F+f)) mod 32; num_classes == 0 -> dyadic
    regression label, else a class label in [0, num_classes). */

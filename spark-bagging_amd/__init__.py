@@ -8,7 +8,7 @@ The directory name is not a Python identifier; import it with
 from . import _native  # noqa: F401
 from ._native import (Context, DeviceDataset, NativeForest, IllegalArgumentException,  # noqa: F401
                       SparkException, SbagError, default_context, device_count)
-from .libsvm import load_libsvm  # noqa: F401
+from .libsvm import SparseRows, load_libsvm  # noqa: F401
 from .ml import (BaggingClassificationModel, BaggingClassifier, BaggingRegressionModel,  # noqa: F401
                  BaggingRegressor, DecisionTreeClassifier, DecisionTreeModel,
                  DecisionTreeRegressor, Frame, even_partitions, java_string_hash)

@@ -17,11 +17,13 @@ SBAG_OK, SBAG_EINVAL, SBAG_EEMPTY, SBAG_EDEVICE, SBAG_ENOMEM, SBAG_EUNSUPPORTED 
 IMPURITY_VARIANCE, IMPURITY_GINI = 0, 1
 AGG_MEAN, AGG_MODE = 0, 1
 OUT_SUM, OUT_VOTES = 2, 3  # device outputs of sbag_predict_dataset_device
+COL_F64, COL_F32, COL_U8 = 0, 1, 2  # sbag_dataset_create_columns
 
 # every symbol include/sbag.h declares (checked by tests/test_abi.py)
 EXPORTED = [
     "sbag_device_count", "sbag_ctx_create", "sbag_ctx_destroy", "sbag_last_error", "sbag_version",
-    "sbag_sample", "sbag_subspace", "sbag_dataset_create", "sbag_dataset_synthetic",
+    "sbag_sample", "sbag_subspace", "sbag_dataset_create", "sbag_dataset_create_csr",
+    "sbag_dataset_create_columns", "sbag_dataset_synthetic",
     "sbag_dataset_info", "sbag_dataset_labels", "sbag_dataset_features", "sbag_dataset_free",
     "sbag_fit", "sbag_forest_num_trees", "sbag_forest_tree_info", "sbag_forest_subspace",
     "sbag_forest_nodes", "sbag_forest_create", "sbag_forest_free", "sbag_forest_timing",
@@ -114,6 +116,8 @@ def lib():
             "sbag_subspace": [dbl, i32, i64, P, P],
             "sbag_dataset_create": [P, i64, i32, P, P, P],
             "sbag_dataset_synthetic": [P, i64, i32, ctypes.c_uint64, i32, P],
+            "sbag_dataset_create_csr": [P, i64, i32, P, P, P, P, P],
+            "sbag_dataset_create_columns": [P, i64, i32, i32, P, P, P],
             "sbag_dataset_info": [P, P, P],
             "sbag_dataset_labels": [P, P],
             "sbag_dataset_features": [P, i64, i64, P],
@@ -214,6 +218,43 @@ class DeviceDataset:
         h = ctypes.c_void_p()
         check(lib().sbag_dataset_create(ctx.handle, X.shape[0], X.shape[1], ptr(X), ptr(y),
                                         ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_csr(cls, rows, y, ctx=None):
+        """SparseVector rows (libsvm.SparseRows or a scipy.sparse CSR matrix): absent
+        entries are 0.0; no dense copy is made (sbag_dataset_create_csr)."""
+        ctx = ctx or default_context()
+        n, f = rows.shape
+        indptr = np.ascontiguousarray(rows.indptr, np.int64)
+        indices = np.ascontiguousarray(rows.indices, np.int32)
+        values = np.ascontiguousarray(rows.data, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        if len(indptr) != n + 1 or len(y) != n:
+            raise IllegalArgumentException(SBAG_EINVAL, "indptr / labels do not match the row count")
+        h = ctypes.c_void_p()
+        check(lib().sbag_dataset_create_csr(ctx.handle, n, f, ptr(indptr), ptr(indices), ptr(values),
+                                            ptr(y), ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_columns(cls, columns, y, ctx=None):
+        """Columnar features: a list of F arrays of N values (fp64, fp32 or u8, one dtype),
+        e.g. Arrow / Parquet column chunks (sbag_dataset_create_columns)."""
+        ctx = ctx or default_context()
+        kinds = {np.dtype(np.float64): COL_F64, np.dtype(np.float32): COL_F32,
+                 np.dtype(np.uint8): COL_U8}
+        cols = [np.ascontiguousarray(c) for c in columns]
+        dts = {c.dtype for c in cols}
+        if len(dts) != 1 or next(iter(dts)) not in kinds:
+            raise IllegalArgumentException(SBAG_EINVAL, "columns must share one of fp64 / fp32 / u8")
+        y = np.ascontiguousarray(y, np.float64)
+        if any(len(c) != len(y) for c in cols):
+            raise IllegalArgumentException(SBAG_EINVAL, "columns and labels differ in length")
+        arr = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        h = ctypes.c_void_p()
+        check(lib().sbag_dataset_create_columns(ctx.handle, len(y), len(cols), kinds[cols[0].dtype],
+                                                arr, ptr(y), ctypes.byref(h)))
         return cls(ctx, h)
 
     @classmethod

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -68,8 +69,15 @@ struct HostPool {
   int n = 0, pending = 0;
   uint64_t gen = 0;
   bool stop = false;
+  // host threads for node bookkeeping, thresholds, tree emission and ingest: 16 (the
+  // CPU share of one GPU on an 8-GPU node) unless SBAG_HOST_THREADS says otherwise
   static int width() {
-    return std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    static const int w = [] {
+      const char* e = getenv("SBAG_HOST_THREADS");
+      const int hw = std::max(1, (int)std::thread::hardware_concurrency());
+      return e ? std::max(1, std::min(atoi(e), 1024)) : std::min(16, hw);
+    }();
+    return w;
   }
   void run(int nw, const std::function<void(int)>& f) {
     nw = std::max(1, std::min(nw, width()));
@@ -753,13 +761,64 @@ int sbag_sample(sbag_ctx* c, const sbag_sampler_params* p, const int64_t* partit
   return SBAG_OK;
 }
 
-int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, const double* y,
-                        sbag_dataset** out) {
-  if (!c || !out || N < 0 || F <= 0 || (N > 0 && (!X || !y))) return fail(SBAG_EINVAL, "bad arguments");
-  if (N == 0) return fail(SBAG_EEMPTY, "ML algorithm was given empty dataset.");
-  if (N >= (int64_t)1 << 32) return fail(SBAG_EUNSUPPORTED, "more than 2^32 rows");
-  CTX_LOCK(c);
-  HIP_TRY(hipSetDevice(c->device));
+// ---- dataset ingest.  Three layouts of the DataFrame's features column, one result:
+// per-feature sorted dictionaries of the distinct values (-0.0 == 0.0, as Spark's
+// `<=` splits and findSplitsBySorting's `!= 0.0` filter see them) and the [N][S] value
+// codes in HBM.
+//   dense    row-major fp64 [N x F] (DenseVector rows)
+//   csr      SparseVector rows: indptr [N+1], strictly increasing indices per row,
+//            values; absent entries are 0.0 (HasSubBag.scala:128-131 slices them the
+//            same way)
+//   columns  one pointer per feature to N values (fp64, fp32 or u8): Arrow / Parquet
+//            column chunks, or features quantized upstream
+// Codes are built and uploaded in row batches, so no dense fp64 copy of a sparse or
+// columnar input is ever made.
+struct DsSource {
+  int kind = 0;  // 0 dense, 1 csr, 2 columns
+  const double* X = nullptr;
+  const int64_t* indptr = nullptr;
+  const int32_t* indices = nullptr;
+  const double* values = nullptr;
+  const void* const* cols = nullptr;
+  int col_type = SBAG_COL_F64;
+  double col(int f, int64_t i) const {
+    if (col_type == SBAG_COL_F32) return (double)((const float*)cols[f])[i];
+    if (col_type == SBAG_COL_U8) return (double)((const uint8_t*)cols[f])[i];
+    return ((const double*)cols[f])[i];
+  }
+};
+
+static inline double canon(double v) { return v == 0.0 ? 0.0 : v; }  // -0.0 -> 0.0
+
+static int check_source(const DsSource& src, int64_t N, int32_t F) {
+  if (src.kind == 1) {
+    if (!src.indptr || src.indptr[0] != 0) return fail(SBAG_EINVAL, "indptr must start at 0");
+    const int64_t nnz = src.indptr[N];
+    if (nnz > 0 && (!src.indices || !src.values)) return fail(SBAG_EINVAL, "bad arguments");
+    for (int64_t i = 0; i < N; i++) {
+      if (src.indptr[i + 1] < src.indptr[i]) return fail(SBAG_EINVAL, "indptr must be non-decreasing");
+      for (int64_t k = src.indptr[i]; k < src.indptr[i + 1]; k++) {
+        const int32_t j = src.indices[k];
+        if (j < 0 || j >= F || (k > src.indptr[i] && j <= src.indices[k - 1]))
+          return fail(SBAG_EINVAL, "row " + std::to_string(i) +
+                                       ": indices must be strictly increasing in [0, numFeatures)");
+        if (std::isnan(src.values[k])) return fail(SBAG_EINVAL, "NaN feature value");
+      }
+    }
+  } else if (src.kind == 2) {
+    if (!src.cols) return fail(SBAG_EINVAL, "bad arguments");
+    if (src.col_type != SBAG_COL_F64 && src.col_type != SBAG_COL_F32 && src.col_type != SBAG_COL_U8)
+      return fail(SBAG_EINVAL, "unknown column type");
+    for (int f = 0; f < F; f++)
+      if (!src.cols[f]) return fail(SBAG_EINVAL, "column " + std::to_string(f) + " is NULL");
+  } else if (!src.X) {
+    return fail(SBAG_EINVAL, "bad arguments");
+  }
+  return SBAG_OK;
+}
+
+static int build_dataset(sbag_ctx* c, int64_t N, int32_t F, const DsSource& src, const double* y,
+                         sbag_dataset** out) {
   auto ds = std::make_unique<sbag_dataset>();
   ds->ctx = c;
   ds->N = N;
@@ -767,48 +826,90 @@ int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, cons
   ds->S = row_stride(F);
   ds->dict.resize(F);
   ds->zero_code.assign(F, -1);
-  size_t maxd = 0;
-  std::vector<double> col(N);
-  for (int f = 0; f < F; f++) {
-    for (int64_t i = 0; i < N; i++) {
-      double v = X[i * F + f];
-      if (std::isnan(v)) return fail(SBAG_EINVAL, "NaN feature value");
-      if (v == 0.0) v = 0.0;  // -0.0 and 0.0 are one value for split finding
-      col[i] = v;
+  // CSR: the explicit values of every feature (a CSC copy of the values only)
+  std::vector<int64_t> coff;
+  std::vector<double> cval;
+  if (src.kind == 1) {
+    const int64_t nnz = src.indptr[N];
+    coff.assign(F + 1, 0);
+    for (int64_t k = 0; k < nnz; k++) coff[src.indices[k] + 1]++;
+    for (int f = 0; f < F; f++) coff[f + 1] += coff[f];
+    cval.resize((size_t)std::max<int64_t>(nnz, 1));
+    std::vector<int64_t> fill(coff.begin(), coff.end() - 1);
+    for (int64_t k = 0; k < nnz; k++) cval[fill[src.indices[k]]++] = canon(src.values[k]);
+  }
+  std::atomic<int> nan_seen{0};
+  const int nw = HostPool::width();
+  c->pool.run(nw, [&](int w) {
+    std::vector<double> col;
+    for (int f = w; f < F; f += nw) {
+      if (src.kind == 1) {
+        col.assign(cval.begin() + coff[f], cval.begin() + coff[f + 1]);
+        if (coff[f + 1] - coff[f] < N) col.push_back(0.0);  // implicit zeros
+      } else {
+        col.resize(N);
+        for (int64_t i = 0; i < N; i++) {
+          const double v = src.kind == 0 ? src.X[i * F + f] : src.col(f, i);
+          if (std::isnan(v)) nan_seen = 1;
+          col[i] = canon(v);
+        }
+      }
+      std::sort(col.begin(), col.end());
+      col.erase(std::unique(col.begin(), col.end()), col.end());
+      ds->dict[f] = col;
     }
-    std::vector<double> d(col);
-    std::sort(d.begin(), d.end());
-    d.erase(std::unique(d.begin(), d.end()), d.end());
+  });
+  if (nan_seen) return fail(SBAG_EINVAL, "NaN feature value");
+  size_t maxd = 0;
+  for (int f = 0; f < F; f++) {
+    const auto& d = ds->dict[f];
     maxd = std::max(maxd, d.size());
-    for (size_t k = 0; k < d.size(); k++)
-      if (d[k] == 0.0) ds->zero_code[f] = (int)k;
-    ds->dict[f] = std::move(d);
+    const auto z = std::lower_bound(d.begin(), d.end(), 0.0);
+    if (z != d.end() && *z == 0.0) ds->zero_code[f] = (int)(z - d.begin());
   }
   ds->code_bytes = maxd <= 256 ? 1 : maxd <= 65536 ? 2 : 4;
-  const size_t bytes = (size_t)N * ds->S * ds->code_bytes;
+  const int cb = ds->code_bytes;
+  const size_t row_bytes = (size_t)ds->S * cb;
+  const size_t bytes = (size_t)N * row_bytes;
   HIP_TRY(hipMalloc(&ds->d_codes, bytes + 256));  // zero slack: k_hist_rl over-reads rows
   HIP_TRY(hipMemset((uint8_t*)ds->d_codes + bytes, 0, 256));
-  {
-    std::vector<uint8_t> buf(bytes, 0);
-    for (int f = 0; f < F; f++) {
-      const auto& d = ds->dict[f];
-      for (int64_t i = 0; i < N; i++) {
-        double v = X[i * F + f];
-        if (v == 0.0) v = 0.0;
-        const size_t k = (size_t)(std::lower_bound(d.begin(), d.end(), v) - d.begin());
-        if (ds->code_bytes == 1)
-          buf[(size_t)i * ds->S + f] = (uint8_t)k;
-        else if (ds->code_bytes == 2)
-          ((uint16_t*)buf.data())[(size_t)i * ds->S + f] = (uint16_t)k;
-        else
-          ((uint32_t*)buf.data())[(size_t)i * ds->S + f] = (uint32_t)k;
+  if (cb == 4) ds->h_codes.resize((size_t)N * ds->S);  // split finding gathers wide codes on the host
+  const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(N, ((int64_t)256 << 20) / (int64_t)row_bytes));
+  std::vector<uint8_t> buf((size_t)batch * row_bytes);
+  std::vector<int> zfill;  // CSR: features whose 0.0 is not code 0 (negative values exist)
+  for (int f = 0; f < F; f++)
+    if (ds->zero_code[f] > 0) zfill.push_back(f);
+  for (int64_t r0 = 0; r0 < N; r0 += batch) {
+    const int64_t n = std::min(batch, N - r0);
+    c->pool.run(nw, [&](int w) {
+      const int64_t a = r0 + n * w / nw, b = r0 + n * (w + 1) / nw;
+      for (int64_t i = a; i < b; i++) {
+        uint8_t* row = buf.data() + (size_t)(i - r0) * row_bytes;
+        auto put = [&](int f, size_t k) {
+          if (cb == 1)
+            row[f] = (uint8_t)k;
+          else if (cb == 2)
+            ((uint16_t*)row)[f] = (uint16_t)k;
+          else
+            ((uint32_t*)row)[f] = (uint32_t)k;
+        };
+        auto code = [&](int f, double v) {
+          const auto& d = ds->dict[f];
+          return (size_t)(std::lower_bound(d.begin(), d.end(), canon(v)) - d.begin());
+        };
+        std::memset(row, 0, row_bytes);
+        if (src.kind == 1) {
+          for (int f : zfill) put(f, (size_t)ds->zero_code[f]);
+          for (int64_t k = src.indptr[i]; k < src.indptr[i + 1]; k++)
+            put(src.indices[k], code(src.indices[k], src.values[k]));
+        } else {
+          for (int f = 0; f < F; f++) put(f, code(f, src.kind == 0 ? src.X[i * F + f] : src.col(f, i)));
+        }
       }
-    }
-    HIP_TRY(hipMemcpy(ds->d_codes, buf.data(), bytes, hipMemcpyHostToDevice));
-    if (ds->code_bytes == 4) {  // split finding gathers the sampled rows' codes on the host
-      ds->h_codes.resize((size_t)N * ds->S);
-      std::memcpy(ds->h_codes.data(), buf.data(), bytes);
-    }
+    });
+    HIP_TRY(hipMemcpy((uint8_t*)ds->d_codes + (size_t)r0 * row_bytes, buf.data(), (size_t)n * row_bytes,
+                      hipMemcpyHostToDevice));
+    if (cb == 4) std::memcpy((uint8_t*)ds->h_codes.data() + (size_t)r0 * row_bytes, buf.data(), (size_t)n * row_bytes);
   }
   ds->y.assign(y, y + N);
   analyze_labels(ds.get());
@@ -816,6 +917,45 @@ int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, cons
   TRY(upload_dict(ds.get()));
   *out = ds.release();
   return SBAG_OK;
+}
+
+static int dataset_from(sbag_ctx* c, int64_t N, int32_t F, const DsSource& src, const double* y,
+                        sbag_dataset** out) {
+  if (!c || !out || N < 0 || F <= 0 || (N > 0 && !y)) return fail(SBAG_EINVAL, "bad arguments");
+  if (N == 0) return fail(SBAG_EEMPTY, "ML algorithm was given empty dataset.");
+  if (N >= (int64_t)1 << 32) return fail(SBAG_EUNSUPPORTED, "more than 2^32 rows");
+  TRY(check_source(src, N, F));
+  CTX_LOCK(c);
+  HIP_TRY(hipSetDevice(c->device));
+  return build_dataset(c, N, F, src, y, out);
+}
+
+int sbag_dataset_create(sbag_ctx* c, int64_t N, int32_t F, const double* X, const double* y,
+                        sbag_dataset** out) {
+  DsSource src;
+  src.kind = 0;
+  src.X = X;
+  return dataset_from(c, N, F, src, y, out);
+}
+
+int sbag_dataset_create_csr(sbag_ctx* c, int64_t N, int32_t F, const int64_t* indptr,
+                            const int32_t* indices, const double* values, const double* y,
+                            sbag_dataset** out) {
+  DsSource src;
+  src.kind = 1;
+  src.indptr = indptr;
+  src.indices = indices;
+  src.values = values;
+  return dataset_from(c, N, F, src, y, out);
+}
+
+int sbag_dataset_create_columns(sbag_ctx* c, int64_t N, int32_t F, int32_t col_type,
+                                const void* const* columns, const double* y, sbag_dataset** out) {
+  DsSource src;
+  src.kind = 2;
+  src.cols = columns;
+  src.col_type = col_type;
+  return dataset_from(c, N, F, src, y, out);
 }
 
 int sbag_dataset_synthetic(sbag_ctx* c, int64_t N, int32_t F, uint64_t seed, int32_t num_classes,
@@ -909,6 +1049,7 @@ int sbag_dataset_free(sbag_dataset* ds) {
 
 // ---------------------------------------------------------------- fit
 struct HistGeom {
+  bool grouped = false;  // gini class tiles over entries grouped by tile (group_tiles)
   int T, FT, FPH, ntf, CT, ntiles;
   int rl;  // row-lane kernel (k_hist_rl)
   size_t lds;
@@ -921,17 +1062,21 @@ static int roundup(int x, int a) { return (x + a - 1) / a * a; }
 // Many classes (BASELINE config 5: 64) are split into class tiles first: a class
 // tile re-reads the 8-byte entries but loads the row bytes of its own entries only,
 // whereas a feature tile re-reads every row.
+// grouped: gini class tiles over entries grouped by tile (no staging area; a smaller LDS
+// target so that four workgroups share a CU and keep more row gathers in flight)
 static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, HistGeom& g,
-                          int rl_mode = 0) {
+                          int rl_mode = 0, bool grouped = false) {
   (void)S;
   g.T = 64;  // piece granularity (entries)
   const int align = gini_layout ? 32 : 16;
-  size_t soft = 80 * 1024;
-  if (const char* e = getenv("SBAG_HIST_LDS_KB")) soft = (size_t)atoi(e) * 1024;
+  size_t soft = grouped ? 38 * 1024 : 80 * 1024;
+  if (const char* e = getenv(grouped ? "SBAG_HIST_GROUPED_LDS_KB" : "SBAG_HIST_LDS_KB"))
+    soft = (size_t)atoi(e) * 1024;
   const size_t hard = 160 * 1024 - 256;
+  const size_t stage = grouped ? 0 : hist_stage_bytes();
   auto lds_for = [&](int ft, int ct) {
     size_t b = hist_lds_bytes(NB, gini_layout ? ct : 1, roundup(ft, align), gini_layout);
-    if (gini_layout && ct < NS) b += hist_stage_bytes();
+    if (gini_layout && ct < NS) b += stage;
     return b;
   };
   int ft = std::min(256, roundup(Fmax, align));
@@ -947,7 +1092,7 @@ static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, His
       ct = NS;
       break;
     }
-    const long c = soft > hist_stage_bytes() ? (long)((soft - hist_stage_bytes()) / P) : 0;
+    const long c = soft > stage ? (long)((soft - stage) / P) : 0;
     if (c >= 1) {
       const int nct = (NS + (int)c - 1) / (int)c;
       ct = (NS + nct - 1) / nct;  // balanced class tiles
@@ -1293,11 +1438,98 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     for (int r = 0; r < R; r++) hist_work += act[r] ? 3.0 * N : 0.0;
   };
   int64_t hist_launches = 0;
+  static const bool group_off = getenv("SBAG_NO_TILE_GROUPING") != nullptr;
+  std::vector<std::pair<int64_t, int64_t>> gsegs;
+  std::vector<ParentInfo> gpar;
+  // Gini class tiles: regroup the entries to be histogrammed so that each (segment,
+  // class tile) is contiguous (k_tile_count / k_tile_scatter into "entG"), and hand the
+  // histogram one sub-segment per (segment, tile) with ParentInfo.tile.
+  auto group_tiles = [&](const HistGeom& g, const std::vector<std::pair<int64_t, int64_t>>& segs,
+                         const std::vector<ParentInfo>& par, uint64_t** ent_out) -> int {
+    const int CT = g.CT, ntc = (NS + CT - 1) / CT;
+    std::vector<HistChunk> pcs;
+    std::vector<int> pseg;
+    constexpr int64_t kPiece = 1 << 16;
+    for (size_t q = 0; q < segs.size(); q++)
+      for (int64_t a = segs[q].first; a < segs[q].second; a += kPiece) {
+        pcs.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + kPiece, segs[q].second)});
+        pseg.push_back((int)q);
+      }
+    const int np = (int)pcs.size();
+    HistChunk* d_pcs;
+    uint32_t* d_cnt;
+    int64_t* d_base;
+    uint64_t* d_entg;
+    TRY(ws_typed(c, "tg_pieces", std::max(np, 1), &d_pcs));
+    TRY(ws_typed(c, "tg_counts", (size_t)std::max(np, 1) * ntc, &d_cnt));
+    TRY(ws_typed(c, "tg_base", (size_t)std::max(np, 1) * ntc, &d_base));
+    TRY(ws_typed(c, "entG", (size_t)R * cap, &d_entg));
+    TRY(h2d(c, d_pcs, pcs.data(), pcs.size()));
+    launch_tile_count(c->stream, d_pcs, np, ha.ent_in, CT, ntc, d_cnt);
+    HIP_TRY(hipGetLastError());
+    std::vector<uint32_t> cnt((size_t)np * ntc);
+    TRY(d2h(c, cnt.data(), d_cnt, cnt.size()));
+    // sub-segment of (q, t) at segs[q].first + sum of the tiles before t; pieces of q
+    // fill it in piece order
+    std::vector<int64_t> base((size_t)np * ntc);
+    gsegs.clear();
+    gpar.clear();
+    for (int p0 = 0; p0 < np;) {
+      int p1 = p0;
+      while (p1 < np && pseg[p1] == pseg[p0]) p1++;
+      const int q = pseg[p0];
+      int64_t o = segs[q].first;
+      for (int t = 0; t < ntc; t++) {
+        const int64_t start = o;
+        for (int p = p0; p < p1; p++) {
+          base[(size_t)p * ntc + t] = o;
+          o += cnt[(size_t)p * ntc + t];
+        }
+        if (o > start) {
+          gsegs.push_back({start, o});
+          ParentInfo pi = par[q];
+          pi.tile = t;
+          gpar.push_back(pi);
+        }
+      }
+      p0 = p1;
+    }
+    TRY(h2d(c, d_base, base.data(), base.size()));
+    launch_tile_scatter(c->stream, d_pcs, np, ha.ent_in, CT, ntc, d_base, d_entg);
+    HIP_TRY(hipGetLastError());
+    *ent_out = d_entg;
+    return SBAG_OK;
+  };
+  // class tiles of a gini histogram: group the entries by tile (k_hist only)
+  auto maybe_grouped = [&](HistGeom& g, int S_, int NB_) -> int {
+    if (!gini || g.CT >= NS || g.rl || group_off) return SBAG_OK;
+    HistGeom gg;
+    if (hist_geometry(S_, Fmax, NB_, NS, true, gg, 0, true) && gg.CT < NS) {
+      gg.grouped = true;
+      g = gg;
+    }
+    return SBAG_OK;
+  };
   auto launch = [&](const HistGeom& g, int mode, int cat,
-                    const std::vector<std::pair<int64_t, int64_t>>& segs,
-                    const std::vector<ParentInfo>& par) -> int {
-    const int wpc = std::max(1, std::min(2, (int)((160 * 1024) / g.lds)));  // 16 waves/CU
-    build_work(segs, flush_limit, 256 * wpc, g.T, work);
+                    const std::vector<std::pair<int64_t, int64_t>>& segs_in,
+                    const std::vector<ParentInfo>& par_in) -> int {
+    const bool grouped = g.grouped && mode == kHistGini && !ha.count_only;
+    // 16 waves per CU (two 512-thread workgroups), 32 for grouped class tiles
+    const int wpc = std::max(1, std::min(grouped ? 4 : 2, (int)((160 * 1024) / g.lds)));
+    const uint64_t* ent_saved = ha.ent_in;
+    int ntiles = g.ntiles;
+    int hg = -1;
+    if (grouped) {
+      hg = tm.begin(cat);
+      uint64_t* d_entg = nullptr;
+      TRY(group_tiles(g, segs_in, par_in, &d_entg));
+      ha.ent_in = d_entg;
+      ntiles = g.ntf;
+    }
+    ha.grouped = grouped ? 1 : 0;
+    const std::vector<std::pair<int64_t, int64_t>>& segs = grouped ? gsegs : segs_in;
+    const std::vector<ParentInfo>& par = grouped ? gpar : par_in;
+    build_work(segs, flush_limit, 256 * wpc * (grouped ? 2 : 1), g.T, work);
     TRY(upload_work(par));
     ha.chunks = d_pieces;
     ha.wg_piece = d_wg;
@@ -1307,10 +1539,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     ha.CT = g.CT;
     ha.ntf = g.ntf;
     ha.rl = g.rl;
-    int h = tm.begin(cat);
-    launch_hist(c->stream, ha, work.nwg, g.ntiles, mode, g.lds);
+    int h = hg >= 0 ? hg : tm.begin(cat);
+    launch_hist(c->stream, ha, work.nwg, ntiles, mode, g.lds);
     HIP_TRY(hipGetLastError());
     tm.end(h);
+    ha.ent_in = ent_saved;
+    ha.grouped = 0;
     if (cat == T_HIST) {
       hist_launches++;
       // LDS atomic wave-instructions per entry: per feature tile, k_hist one per 64-lane
@@ -1358,6 +1592,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   if (optimistic) {
     if (!hist_geometry(ds->S, Fmax, ncmax, NS, gini, g0, rl_mode_for(h_pos_codes, ds->S)))
       return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
+    TRY(maybe_grouped(g0, ds->S, ncmax));
     HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * Fmax * ncmax * NS * word_bytes, c->stream));
     ha.bins = (const uint8_t*)ds->d_codes;
     ha.bins_rstride = 0;
@@ -1771,6 +2006,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   HistGeom g;
   if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode_for(h_pos, S)))
     return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
+  TRY(maybe_grouped(g, S, NB));
   const int64_t slot_words = (int64_t)Fmax * NB * NS;
   std::vector<std::vector<HNode>> trees(R);
   std::vector<std::pair<int, int>> slots(R);  // (replica, node index)

@@ -28,7 +28,7 @@ struct ParentInfo {  // a node of level d whose rows are routed to level d+1
   int32_t write_r;
   int32_t hist_slot;  // histogram slot accumulated by this pass, -1 none
   int32_t hist_side;  // 0 = left child, 1 = right child
-  int32_t pad;
+  int32_t tile;       // grouped gini histograms: class tile of this sub-segment
 };
 
 enum { kHistGini = 0, kHistVar = 1, kHistSq = 2 };  // k_hist modes
@@ -54,6 +54,8 @@ struct HistArgs {
   int32_t CT;            // gini: classes per class tile (LDS holds CT class planes)
   int32_t ntf;           // feature tiles; blockIdx.y = class_tile * ntf + feature_tile
   int32_t rl;            // k_hist_rl (identity byte layout): 1 = 64-bit row addresses, 2 = 32-bit
+  int32_t grouped;       // gini: entries grouped by class tile, ParentInfo.tile per segment;
+                         // blockIdx.y walks feature tiles only
 };
 
 // k_partition: entries of each split node -> left block (from the segment start,
@@ -223,6 +225,11 @@ size_t predict_tiled_lds(const PredictArgs& a);
 void launch_quantize(hipStream_t st, const double* X, int64_t n, int32_t F, const double* thr,
                      const int64_t* toff, uint16_t* codes, int32_t S);
 void launch_predict_tiled(hipStream_t st, const PredictArgs& a);
+// class-tile grouping of gini histogram entries (one workgroup per piece)
+void launch_tile_count(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
+                       int CT, int ntc, uint32_t* counts);
+void launch_tile_scatter(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
+                         int CT, int ntc, const int64_t* base, uint64_t* ent_out);
 void launch_vc_global(hipStream_t st, const void* codes, int code_bytes, int32_t S, const uint64_t* ent,
                       int64_t cap, const unsigned long long* d_inbag, const int32_t* d_sub,
                       const int32_t* d_Fr, int32_t Fmax, int R, const int64_t* d_off, uint32_t* vc);

@@ -1005,7 +1005,11 @@ void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, con
 // ======================================================================
 constexpr int kHistThreads = 512;  // 8 waves; two workgroups per CU at <= 80 KB of LDS
 constexpr int kHistWaves = kHistThreads / 64;
-constexpr int kG = 8;              // entries per pipeline group
+// entries per pipeline group: row bytes of the next group are loaded while the current
+// one is added, so a wave keeps up to 2 groups of row gathers in flight (k_hist is bound
+// by their latency when the atomics are few: 16 for up to two 64-feature lane groups)
+template <int NJ>
+constexpr int hist_group() { return NJ <= 2 ? 16 : 8; }
 
 static __host__ __device__ inline uint32_t hist_plane_bytes(int NB, int FPH, bool gini) {
   return (uint32_t)(NB * FPH + 64) * (gini ? 4u : 8u);
@@ -1024,8 +1028,10 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
   if (MODE == kHistGini) {
     // class planes [0, nct) of the LDS hold classes [c0, c0 + nct)
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
+    // features fastest: consecutive lanes read consecutive LDS words (class planes and
+    // bin rows are multiples of 64 words apart, so any other order serializes on a bank)
     for (int q = tid; q < ftn * NB * nct; q += blockDim.x) {
-      const int cl = q % nct, b = (q / nct) % NB, f = q / (nct * NB);
+      const int f = q % ftn, b = (q / ftn) % NB, cl = q / (ftn * NB);
       const uint32_t v = *(const uint32_t*)(smem + (size_t)cl * plane + ((size_t)b * FPH + f) * 4);
       if (v) {
         uint32_t* dst = &gh[((int64_t)(ft0 + f) * NB + b) * NS + c0 + cl];
@@ -1040,7 +1046,7 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
     const int cs = A.cshift;
     const uint64_t MS = (1ull << cs) - 1;
     for (int q = tid; q < ftn * NB; q += blockDim.x) {
-      const int b = q % NB, f = q / NB;
+      const int f = q % ftn, b = q / ftn;  // features fastest, as above
       const uint64_t w = *(const uint64_t*)(smem + ((size_t)b * FPH + f) * 8);
       if (w) {
         const int64_t gb = ((int64_t)(ft0 + f) * NB + b) * 3;
@@ -1068,13 +1074,13 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
-// bytes of the NJ feature columns of entries [u0, u0 + kG) of the batch
-template <int NJ>
+// bytes of the NJ feature columns of entries [u0, u0 + KG) of the batch
+template <int NJ, int KG>
 __device__ __forceinline__ void hist_load_group(const uint8_t* __restrict__ binsr, uint32_t S,
                                                 uint32_t row, int u0, const uint32_t (&posr)[NJ],
-                                                uint32_t (&buf)[kG][NJ]) {
+                                                uint32_t (&buf)[KG][NJ]) {
 #pragma unroll
-  for (int t = 0; t < kG; t++) {
+  for (int t = 0; t < KG; t++) {
     const uint8_t* rp = binsr + (size_t)rdlane(row, u0 + t) * S;  // wave-uniform (SGPRs)
 #pragma unroll
     for (int jj = 0; jj < NJ; jj++) {
@@ -1087,13 +1093,13 @@ __device__ __forceinline__ void hist_load_group(const uint8_t* __restrict__ bins
 
 // one LDS atomic per entry and lane group: GINI adds count wl into class plane
 // (offset wh); the u64 modes add (wh:wl)
-template <int MODE, int NJ>
+template <int MODE, int NJ, int KG>
 __device__ __forceinline__ void hist_add_group(unsigned char* smem, int u0,
-                                               const uint32_t (&buf)[kG][NJ], uint32_t wl,
+                                               const uint32_t (&buf)[KG][NJ], uint32_t wl,
                                                uint32_t wh, const uint32_t (&amul)[NJ],
                                                const uint32_t (&abase)[NJ]) {
 #pragma unroll
-  for (int t = 0; t < kG; t++) {
+  for (int t = 0; t < KG; t++) {
     const int u = u0 + t;
     if (MODE == kHistGini) {
       const uint32_t cu = rdlane(wl, u), cou = rdlane(wh, u);
@@ -1121,10 +1127,11 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   const int NB = A.NB, FPH = A.FPH;
   const uint32_t S = (uint32_t)A.S;
   const int ft0 = (int)(blockIdx.y % (unsigned)A.ntf) * A.FT;
-  // gini class tiling: this workgroup accumulates classes [c0, c0 + nct) only
-  const int c0 = GINI ? (int)(blockIdx.y / (unsigned)A.ntf) * A.CT : 0;
-  const int nct = GINI ? min(A.CT, A.NS - c0) : 1;
-  const bool ctile = GINI && !A.count_only && A.CT < A.NS;
+  // gini class tiling: this workgroup accumulates classes [c0, c0 + nct) only -- the
+  // grid's tile, or (grouped) the tile of the current sub-segment
+  int c0 = GINI && !A.grouped ? (int)(blockIdx.y / (unsigned)A.ntf) * A.CT : 0;
+  int nct = GINI ? min(A.CT, A.NS - c0) : 1;
+  const bool ctile = GINI && !A.count_only && A.CT < A.NS && !A.grouped;
   constexpr uint32_t WB = GINI ? 4u : 8u;
   const uint32_t plane = hist_plane_bytes(NB, FPH, GINI);
   const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.CT : 1u);
@@ -1137,7 +1144,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
     *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 
   const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
-  int cur_slot = -1, cur_ftn = 0, cur_r = -1;
+  int cur_slot = -1, cur_ftn = 0, cur_r = -1, cur_tile = -1;
   bool cur_store = false;  // the current node run is this workgroup's alone and not yet flushed
   int64_t acc = 0;
   uint32_t posr[NJ], amul[NJ], abase[NJ];
@@ -1157,7 +1164,8 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
     const int slot = pi.hist_slot;
     if (ftn <= 0 || slot < 0) continue;
     const int64_t a = pc.a, b = pc.b;
-    if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
+    const int tile = A.grouped ? pi.tile : 0;
+    if (slot != cur_slot || tile != cur_tile || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
         hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
@@ -1167,10 +1175,15 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
         __syncthreads();
       }
       // a node split over several flushes by this workgroup adds from the second on
-      cur_store = (slot != cur_slot) && pc.excl != 0;
+      cur_store = (slot != cur_slot || tile != cur_tile) && pc.excl != 0;
       cur_slot = slot;
+      cur_tile = tile;
       cur_ftn = ftn;
       acc = 0;
+      if (GINI && A.grouped) {
+        c0 = tile * A.CT;
+        nct = min(A.CT, A.NS - c0);
+      }
     }
     acc += b - a;
     if (r != cur_r) {
@@ -1224,16 +1237,17 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
         wl = (uint32_t)w;
         wh = (uint32_t)(w >> 32);
       }
+      constexpr int kG = hist_group<NJ>();
       uint32_t bA[kG][NJ], bB[kG][NJ];
-      hist_load_group<NJ>(binsr, S, row, 0, posr, bA);
+      hist_load_group<NJ, kG>(binsr, S, row, 0, posr, bA);
 #pragma unroll
       for (int g = 0; g < 64 / kG; g += 2) {
-        if ((g + 1) * kG < n) hist_load_group<NJ>(binsr, S, row, (g + 1) * kG, posr, bB);
-        hist_add_group<MODE, NJ>(smem, g * kG, bA, wl, wh, amul, abase);
+        if ((g + 1) * kG < n) hist_load_group<NJ, kG>(binsr, S, row, (g + 1) * kG, posr, bB);
+        hist_add_group<MODE, NJ, kG>(smem, g * kG, bA, wl, wh, amul, abase);
         if ((g + 1) * kG >= n) break;
         if (g + 2 < 64 / kG && (g + 2) * kG < n)
-          hist_load_group<NJ>(binsr, S, row, (g + 2) * kG, posr, bA);
-        hist_add_group<MODE, NJ>(smem, (g + 1) * kG, bB, wl, wh, amul, abase);
+          hist_load_group<NJ, kG>(binsr, S, row, (g + 2) * kG, posr, bA);
+        hist_add_group<MODE, NJ, kG>(smem, (g + 1) * kG, bB, wl, wh, amul, abase);
         if ((g + 2) * kG >= n) break;
       }
     }
@@ -1378,9 +1392,9 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
   const int NB = A.NB, FPH = A.FPH;
   const uint32_t S = (uint32_t)A.S;
   const int ft0 = (int)(blockIdx.y % (unsigned)A.ntf) * A.FT;
-  const int c0 = GINI ? (int)(blockIdx.y / (unsigned)A.ntf) * A.CT : 0;
-  const int nct = GINI ? min(A.CT, A.NS - c0) : 1;
-  const bool ctile = GINI && A.CT < A.NS;
+  int c0 = GINI && !A.grouped ? (int)(blockIdx.y / (unsigned)A.ntf) * A.CT : 0;
+  int nct = GINI ? min(A.CT, A.NS - c0) : 1;
+  const bool ctile = GINI && A.CT < A.NS && !A.grouped;
   constexpr uint32_t WB = GINI ? 4u : 8u;
   const uint32_t plane = hist_plane_bytes(NB, FPH, GINI);
   const uint32_t hist_bytes = plane * (GINI ? (uint32_t)A.CT : 1u);
@@ -1394,7 +1408,7 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
     *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 
   const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
-  int cur_slot = -1, cur_ftn = 0, cur_ftn_lane = -1;
+  int cur_slot = -1, cur_ftn = 0, cur_ftn_lane = -1, cur_tile = -1;
   bool cur_store = false;
   int64_t acc = 0;
   // this lane's byte range of the tile: [off, off + K)
@@ -1409,7 +1423,8 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
     const int slot = pi.hist_slot;
     if (ftn <= 0 || slot < 0) continue;
     const int64_t a = pc.a, b = pc.b;
-    if (slot != cur_slot || acc + (b - a) > A.flush_limit) {
+    const int tile = A.grouped ? pi.tile : 0;
+    if (slot != cur_slot || tile != cur_tile || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
         hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
@@ -1418,10 +1433,15 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
           *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
         __syncthreads();
       }
-      cur_store = (slot != cur_slot) && pc.excl != 0;
+      cur_store = (slot != cur_slot || tile != cur_tile) && pc.excl != 0;
       cur_slot = slot;
+      cur_tile = tile;
       cur_ftn = ftn;
       acc = 0;
+      if (GINI && A.grouped) {
+        c0 = tile * A.CT;
+        nct = min(A.CT, A.NS - c0);
+      }
     }
     acc += b - a;
     if (ftn != cur_ftn_lane) {
@@ -1529,6 +1549,67 @@ static void launch_hist_m(hipStream_t st, const HistArgs& a, dim3 grid, size_t l
     case 3: launch_hist_t<MODE, 3>(st, a, grid, lds_bytes); break;
     default: launch_hist_t<MODE, 4>(st, a, grid, lds_bytes); break;
   }
+}
+
+// ---- class-tile grouping (gini with more classes than one workgroup's LDS holds).
+// Without it every class tile's workgroups stream all entries of a node and keep only
+// their own (ballot + stage), so an entry is read once per tile.  Per level, the
+// entries to be histogrammed are instead counted per (piece, tile) and scattered so
+// that each (node, tile) is one contiguous sub-segment; the histogram kernels then
+// read every entry once, in full batches.  Order inside a sub-segment is free: the
+// class counts are integers.
+constexpr int kTileThreads = 256;
+
+__global__ __launch_bounds__(kTileThreads) void k_tile_count(const HistChunk* __restrict__ pieces,
+                                                             const uint64_t* __restrict__ ent,
+                                                             int CT, int ntc,
+                                                             uint32_t* __restrict__ counts) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* cnt = (uint32_t*)smem;
+  const HistChunk pc = pieces[blockIdx.x];
+  for (int t = threadIdx.x; t < ntc; t += kTileThreads) cnt[t] = 0;
+  __syncthreads();
+  for (int64_t i = pc.a + threadIdx.x; i < pc.b; i += kTileThreads) {
+    const int k = (int32_t)(ent[i] >> 32) >> 8;
+    atomicAdd(&cnt[k / CT], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < ntc; t += kTileThreads)
+    counts[(int64_t)blockIdx.x * ntc + t] = cnt[t];
+}
+
+__global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const HistChunk* __restrict__ pieces,
+                                                               const uint64_t* __restrict__ ent,
+                                                               int CT, int ntc,
+                                                               const int64_t* __restrict__ base,
+                                                               uint64_t* __restrict__ ent_out) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int64_t* cur = (int64_t*)smem;  // [ntc] next output position of each tile
+  const HistChunk pc = pieces[blockIdx.x];
+  for (int t = threadIdx.x; t < ntc; t += kTileThreads) cur[t] = base[(int64_t)blockIdx.x * ntc + t];
+  __syncthreads();
+  for (int64_t i = pc.a + threadIdx.x; i < pc.b; i += kTileThreads) {
+    const uint64_t e = ent[i];
+    const int k = (int32_t)(e >> 32) >> 8;
+    const int64_t o = (int64_t)atomicAdd((unsigned long long*)&cur[k / CT], 1ull);
+    ent_out[o] = e;
+  }
+}
+
+void launch_tile_count(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
+                       int CT, int ntc, uint32_t* counts) {
+  if (npieces <= 0) return;
+  set_max_lds((const void*)k_tile_count, 160 * 1024);
+  hipLaunchKernelGGL(k_tile_count, dim3((unsigned)npieces), dim3(kTileThreads), (size_t)ntc * 4, st,
+                     pieces, ent, CT, ntc, counts);
+}
+
+void launch_tile_scatter(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
+                         int CT, int ntc, const int64_t* base, uint64_t* ent_out) {
+  if (npieces <= 0) return;
+  set_max_lds((const void*)k_tile_scatter, 160 * 1024);
+  hipLaunchKernelGGL(k_tile_scatter, dim3((unsigned)npieces), dim3(kTileThreads), (size_t)ntc * 8, st,
+                     pieces, ent, CT, ntc, base, ent_out);
 }
 
 void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mode,

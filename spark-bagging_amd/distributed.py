@@ -135,8 +135,8 @@ def transform(shard, dataset, dist, device=None):
         ctx, ds = dataset.ctx, dataset
     else:
         ctx = nat.default_context(0 if device is None else device)
-        X = dataset.features if isinstance(dataset, Frame) else np.asarray(dataset, np.float64)
-        ds = nat.DeviceDataset.from_numpy(X, np.zeros(X.shape[0]), ctx)
+        frame = dataset if isinstance(dataset, Frame) else Frame(dataset, np.zeros(dataset.shape[0]))
+        ds = frame.device_dataset(ctx)  # dense or SparseVector rows
     dev = torch.device("cuda", ctx.device)
 
     def sync():

@@ -25,6 +25,7 @@ import numpy as np
 
 from . import _native as nat
 from . import persistence as sp
+from .libsvm import is_sparse, load_libsvm
 
 
 def java_string_hash(s):
@@ -199,7 +200,9 @@ class Frame:
     """
 
     def __init__(self, features, label, partition_offsets=None, weight=None):
-        self.features = np.ascontiguousarray(features, np.float64)
+        # DenseVector rows (an [N x F] array) or SparseVector rows (libsvm.SparseRows /
+        # scipy CSR), kept sparse all the way to the device
+        self.features = features if is_sparse(features) else np.ascontiguousarray(features, np.float64)
         self.label = np.ascontiguousarray(label, np.float64)
         n = self.features.shape[0]
         if self.label.shape[0] != n:
@@ -208,11 +211,14 @@ class Frame:
         self.weight = weight
 
     @classmethod
-    def from_libsvm(cls, path, num_partitions=1):
-        from .libsvm import load_libsvm
-
-        X, y = load_libsvm(path)
+    def from_libsvm(cls, path, num_partitions=1, sparse=True):
+        X, y = load_libsvm(path, sparse=sparse)
         return cls(X, y, partition_offsets=even_partitions(len(y), num_partitions))
+
+    def device_dataset(self, ctx):
+        if is_sparse(self.features):
+            return nat.DeviceDataset.from_csr(self.features, self.label, ctx)
+        return nat.DeviceDataset.from_numpy(self.features, self.label, ctx)
 
     @property
     def num_rows(self):
@@ -390,7 +396,7 @@ class _BaggingEstimator(_BaggingParams):
             raise nat.IllegalArgumentException(nat.SBAG_EINVAL, f"duplicate device ids {devices}")
         if isinstance(dataset, Frame):
             part = dataset.partition_offsets
-            make_ds = [lambda ctx, d=dataset: nat.DeviceDataset.from_numpy(d.features, d.label, ctx)]
+            make_ds = [lambda ctx, d=dataset: d.device_dataset(ctx)]
         elif isinstance(dataset, nat.DeviceDataset):
             part = None
             if len(devices) > 1 or (self.devices and devices[0] != dataset.ctx.device):
@@ -482,7 +488,14 @@ class _BaggingModel(_BaggingParams):
         if isinstance(dataset, nat.DeviceDataset):  # on the dataset's own device
             return nat.predict_dataset(dataset.ctx, self.native_forest(), dataset, self._agg)
         ctx = nat.default_context(device)
-        X = dataset.features if isinstance(dataset, Frame) else np.asarray(dataset, np.float64)
+        X = dataset.features if isinstance(dataset, Frame) else dataset
+        if is_sparse(X):  # SparseVector rows: binned on the device from CSR, no dense copy
+            ds = nat.DeviceDataset.from_csr(X, np.zeros(X.shape[0]), ctx)
+            try:
+                return nat.predict_dataset(ctx, self.native_forest(), ds, self._agg)
+            finally:
+                ds.free()
+        X = np.asarray(X, np.float64)
         if X.ndim == 1:
             X = X[None, :]
         return nat.predict(ctx, self.native_forest(), X, self._agg, per_tree=per_tree)

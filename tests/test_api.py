@@ -1,5 +1,6 @@
 """CPU: the Spark-API mirror -- names, defaults, validation and error behaviour
 of the reference's BaggingRegressor / BaggingClassifier (no GPU calls)."""
+import os
 import warnings
 
 import numpy as np
@@ -110,3 +111,25 @@ def test_learner_shards_cover_in_order():
             sh = _learner_shards(L, k)
             assert sh[0][0] == 0 and sh[-1][1] == L
             assert all(sh[i][1] == sh[i + 1][0] for i in range(k - 1))
+
+
+def test_libsvm_sparse_rows_match_dense(tmp_path):
+    from conftest import DATA
+
+    X, y = sb.load_libsvm(os.path.join(DATA, "vehicle.svm"))
+    S, y2 = sb.load_libsvm(os.path.join(DATA, "vehicle.svm"), sparse=True)
+    assert S.shape == X.shape and (y == y2).all()
+    assert (S.toarray() == X).all()
+    sel = S[np.array([5, 0, 17])]
+    assert (sel.toarray() == X[[5, 0, 17]]).all()
+    bad = tmp_path / "bad.svm"
+    bad.write_text("1 3:1.0 2:2.0\n")
+    with pytest.raises(ValueError):
+        sb.load_libsvm(str(bad))
+
+
+def test_frame_keeps_sparse_rows():
+    S = sb.SparseRows([0, 1, 1, 3], [2, 0, 4], [1.5, -2.0, 0.0], (3, 5))
+    fr = sb.Frame(S, np.zeros(3))
+    assert fr.num_rows == 3 and fr.num_features == 5
+    assert fr.features is S
