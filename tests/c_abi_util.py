@@ -8,10 +8,12 @@ import numpy as np
 from conftest import ROOT
 
 DRIVER = os.path.join(ROOT, "tests", "c", "abi_driver")
+DRIVER_ASAN = os.path.join(ROOT, "tests", "c", "abi_driver_asan")
 
 
 def run_driver(tmp_path, X, y, offsets, *, replacement, ratio, seed, lb, le, sub_ratio,
-               bug_compat, depth, bins, min_inst, impurity, min_gain, tree_seed, agg):
+               bug_compat, depth, bins, min_inst, impurity, min_gain, tree_seed, agg,
+               driver=DRIVER, env=None):
     X = np.ascontiguousarray(X, np.float64)
     y = np.ascontiguousarray(y, np.float64)
     off = np.asarray(offsets, np.int64)
@@ -20,10 +22,11 @@ def run_driver(tmp_path, X, y, offsets, *, replacement, ratio, seed, lb, le, sub
     with open(data, "wb") as f:
         f.write(struct.pack("<qqq", X.shape[0], X.shape[1], len(off)))
         f.write(off.tobytes() + X.tobytes() + y.tobytes())
-    args = [DRIVER, str(data), str(out), str(int(replacement)), repr(float(ratio)), str(int(seed)),
+    args = [driver, str(data), str(out), str(int(replacement)), repr(float(ratio)), str(int(seed)),
             str(lb), str(le), repr(float(sub_ratio)), str(int(bug_compat)), str(depth), str(bins),
             str(min_inst), str(impurity), repr(float(min_gain)), str(int(tree_seed)), str(agg)]
-    p = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    p = subprocess.run(args, capture_output=True, text=True, timeout=300,
+                       env=None if env is None else dict(os.environ, **env))
     raw = open(out, "rb").read() if os.path.exists(out) else b""
     status = struct.unpack_from("<i", raw, 0)[0] if raw else None
     if status != 0:

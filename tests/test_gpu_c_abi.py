@@ -84,3 +84,30 @@ def test_c_driver_bad_ratio_is_illegal_argument(tmp_path):
                            min_gain=0.0, tree_seed=1, agg=0)
     assert st == nat.SBAG_EINVAL and p.returncode == 3
     assert "fit" in p.stdout and "java/lang/IllegalArgumentException" in p.stdout
+
+
+def test_c_driver_under_host_asan(tmp_path):
+    """The whole host side (C ABI, orchestration, ingest, predict planning) under
+    AddressSanitizer + UBSan (tests/c/abi_driver_asan; device code is not sanitized):
+    a classifier fit + transform and a sampled-split regression fit, no reports."""
+    from c_abi_util import DRIVER_ASAN
+
+    env = {"ASAN_OPTIONS": "detect_leaks=0:verify_asan_link_order=0:halt_on_error=1",
+           "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
+    X, y = sb.load_libsvm(os.path.join(DATA, "vehicle.svm"))
+    p, st, trees, subs, pred = run_driver(
+        tmp_path, X, y, [0, 300, 846], replacement=1, ratio=0.7, seed=5, lb=0, le=4,
+        sub_ratio=0.7, bug_compat=1, depth=5, bins=32, min_inst=1, impurity=nat.IMPURITY_GINI,
+        min_gain=0.0, tree_seed=nat.DT_SEED_CLASSIFIER, agg=nat.AGG_MODE, driver=DRIVER_ASAN,
+        env=env)
+    assert p.returncode == 0 and st == 0, p.stdout + p.stderr[-3000:]
+    assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr
+    rng = np.random.default_rng(9)
+    Xr = np.round(rng.normal(size=(20000, 5)), 2)
+    yr = rng.integers(-100, 100, 20000) / 4
+    p, st, *_ = run_driver(
+        tmp_path, Xr, yr, [0, 20000], replacement=1, ratio=1.0, seed=3, lb=2, le=4, sub_ratio=1.0,
+        bug_compat=1, depth=6, bins=16, min_inst=2, impurity=nat.IMPURITY_VARIANCE, min_gain=0.0,
+        tree_seed=nat.DT_SEED_REGRESSOR, agg=nat.AGG_MEAN, driver=DRIVER_ASAN, env=env)
+    assert p.returncode == 0 and st == 0, p.stdout + p.stderr[-3000:]
+    assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr
