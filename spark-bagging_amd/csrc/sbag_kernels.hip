@@ -441,12 +441,370 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
   }
 }
 
+// ---- k_poisson3: step-parallel Well19937c.  Well19937c's only step-to-step
+// dependency is z4 (AbstractWell's v0 = z4 of the previous step); every other word a
+// step reads was written >= 70 steps earlier.  Expanding AbstractWell.next,
+//   z4[n] = L(z4[n-1]) ^ c[n],  L(x) = x<<9 ^ x>>21 ^ (x & 0x7f)<<4,
+//   c[n]  = S(a) ^ z0 ^ z2<<21 ^ z2>>21,  a = m1 ^ m1>>27,  S(x) = x<<9 ^ x>>21,
+//   z3[n] = z4[n-1] ^ z4[n-1]<<25 ^ a ^ z2,
+// with c[n] a function of older ring words only.  So a batch of B = 16*SPL <= 64 steps
+// of one stream runs on 16 lanes (SPL consecutive steps each): all reads first, the
+// c terms in parallel, then an F2-linear Hillis-Steele scan of z4 across the lanes with
+// the powers L^(SPL*2^k) (3-6 shift/mask terms each, built at compile time).  A wave
+// holds 4 streams, 16 streams per 256-thread block (4 blocks per CU by LDS): 16 waves
+// per CU share the generator work that the two-wave k_poisson2 ran on one SIMD.  The
+// Poisson parse (PoissonDistribution.nextPoisson) stays serial per stream: all 16
+// lanes of a stream run it on doubles broadcast with DPP row_newbcast, lane e keeping
+// the e-th count the batch emits, then the lanes store the batch's counts together.
+// tests/test_sampler_algebra.py replays this schedule on the CPU against the
+// sequential generator.
+namespace wellsp {
+__host__ __device__ constexpr uint32_t L1(uint32_t x) {
+  return (x << 9) ^ (x >> 21) ^ ((x & 0x7Fu) << 4);
+}
+struct Masks {
+  uint32_t m[63];  // m[s + 31]: input bits i with output bit i + s
+};
+constexpr Masks lpow_masks(int k) {
+  Masks r{};
+  for (int i = 0; i < 32; i++) {
+    uint32_t x = 1u << i;
+    for (int s = 0; s < k; s++) x = L1(x);
+    for (int j = 0; j < 32; j++)
+      if ((x >> j) & 1u) r.m[j - i + 31] |= 1u << i;
+  }
+  return r;
+}
+template <int K>
+struct LP {
+  static constexpr Masks M = lpow_masks(K);
+};
+// L^K(x) as a XOR of shifted, masked copies of x (zero terms vanish at compile time)
+template <int K, int S = 0>
+__device__ __forceinline__ uint32_t lpow(uint32_t x) {
+  if constexpr (S == 63) {
+    return 0u;
+  } else {
+    constexpr uint32_t m = LP<K>::M.m[S];
+    constexpr int sh = S - 31;
+    if constexpr (m == 0u)
+      return lpow<K, S + 1>(x);
+    else if constexpr (sh >= 0)
+      return ((x & m) << sh) ^ lpow<K, S + 1>(x);
+    else
+      return ((x & m) >> (-sh)) ^ lpow<K, S + 1>(x);
+  }
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {  // lanes without a source read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+template <int LANE>
+__device__ __forceinline__ double row_bcast(double x) {  // DPP row_newbcast:LANE
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + LANE, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + LANE, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+}  // namespace wellsp
+
+constexpr int kSpLanes = 16;                             // lanes per stream
+constexpr int kSpStreams = 256 / kSpLanes;               // streams per 256-thread block
+// State pitch per stream: 625 = 1 mod 4 words, so the 4 streams of a wave, whose lanes
+// read 4 words apart (SPL = 4), fall on the 4 residue classes of the 64 banks
+// (a 624 pitch put all four on the same 16 banks: 75 % of LDS cycles were conflicts)
+constexpr int kSpPitch = 625;
+constexpr int kSpReadOff[5] = {70, 179, 449, 623, 622};  // m1, m2, m3, hb (j-1), lo (j-2)
+
+// The five ring words of steps n0 .. n0+SPL-1 of a batch starting at ring index i
+// (step n sits at index j = i - n).  FAST: no read window wraps round the ring in this
+// batch (a wave-uniform test), so each window is one base plus immediate offsets.
+// bit m: a batch of B steps starting at ring index 16m reads no window across the ring end
+constexpr uint64_t sp_fast_mask(int B) {
+  uint64_t m = 0;
+  for (int k = 0; k < 39; k++) {
+    bool fast = true;
+    for (int w = 0; w < 5; w++) {
+      const int x = 16 * k + kSpReadOff[w];
+      fast = fast && (x >= 624 ? x - 624 : x) >= B - 1;
+    }
+    if (fast) m |= 1ull << k;
+  }
+  return m;
+}
+
+template <int SPL, bool FAST>
+__device__ __forceinline__ void sp_read(const uint32_t* __restrict__ st, int i, int n0,
+                                        uint32_t (&w)[5][SPL]) {
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const int b = wrap624(i + kSpReadOff[k]);
+    if (FAST) {
+      const uint32_t* p = st + (b - n0 - (SPL - 1));
+#pragma unroll
+      for (int q = 0; q < SPL; q++) w[k][q] = p[SPL - 1 - q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < SPL; q++) {
+        int pos = b - n0 - q;
+        pos += pos < 0 ? 624 : 0;
+        w[k][q] = st[pos];
+      }
+    }
+  }
+}
+
+template <int SPL, bool CAP, bool PAR>
+__global__ __launch_bounds__(256) void k_poisson3(uint8_t* __restrict__ counts, int64_t N,
+                                                  const int64_t* __restrict__ part_off, int P,
+                                                  int R, int learner0, int64_t seed,
+                                                  double p_exp, int icap, int* err) {
+  static_assert(SPL == 2 || SPL == 4, "a lane holds whole doubles");
+  constexpr int B = kSpLanes * SPL;  // steps per batch (<= 69: reads precede the batch)
+  constexpr int DPL = SPL / 2;       // doubles per lane
+  __shared__ uint32_t sm[kSpStreams * kSpPitch];
+  const int t = threadIdx.x & (kSpLanes - 1);
+  const int slot = threadIdx.x / kSpLanes;
+  uint32_t* st = sm + slot * kSpPitch;
+  const int64_t sid = (int64_t)blockIdx.x * kSpStreams + slot;
+  const bool active = sid < (int64_t)R * P;
+  const int r = active ? (int)(sid / P) : 0;
+  const int p = active ? (int)(sid % P) : 0;
+  // PoissonDistribution.reseedRandomGenerator(seed + i + partitionIndex) ->
+  // AbstractWell.setSeed(int[]{hi, lo}): v[i] = 1812433253 * (v[i-2] ^ v[i-2] >>> 30) + i
+  // (sign-extended long arithmetic; the low word only needs the 32-bit arithmetic shift),
+  // two independent chains (even / odd i) on lanes 0 and 1.
+  if (t < 2) {
+    const uint64_t s64 = (uint64_t)seed + (uint64_t)(int64_t)(learner0 + r) + (uint64_t)(int64_t)p;
+    uint32_t x = t == 0 ? (uint32_t)(s64 >> 32) : (uint32_t)s64;
+    st[t] = x;
+    for (int i = 2 + t; i < 624; i += 2) {
+      x = 1812433253u * (x ^ (uint32_t)((int32_t)x >> 30)) + (uint32_t)i;
+      st[i] = x;
+    }
+  }
+  __syncthreads();
+  int64_t row = active ? part_off[p] : 0;
+  const int64_t row_end = active ? part_off[p + 1] : 0;
+  uint8_t* out = counts + (int64_t)r * N;
+  uint32_t carry = st[0];  // z4 "before" step 0 is v[0] (lane 0 of each stream uses it)
+  int i = 0, n = 0, bad = 0;
+  double racc = 1.0;      // serial parse: open row's product and count
+  double pr = 1.0;        // relaxation parse: carry in-state of lane 0
+  int pn = 0;
+  const int n0 = SPL * t;
+  while (__any(row < row_end)) {
+    uint32_t w[5][SPL];
+    // batch starts are multiples of 16 (B is): bit i/16 of kFast says no window wraps
+    constexpr uint64_t kFast = sp_fast_mask(B);
+    if ((kFast >> (i >> 4)) & 1u)
+      sp_read<SPL, true>(st, i, n0, w);
+    else
+      sp_read<SPL, false>(st, i, n0, w);
+    uint32_t a[SPL], z2[SPL], c[SPL];
+#pragma unroll
+    for (int q = 0; q < SPL; q++) {
+      a[q] = w[0][q] ^ (w[0][q] >> 27);
+      z2[q] = (w[1][q] >> 9) ^ w[2][q] ^ (w[2][q] >> 1);
+      const uint32_t z0 = (w[3][q] & 0x80000000u) | (w[4][q] & 0x7FFFFFFFu);
+      c[q] = (a[q] << 9) ^ (a[q] >> 21) ^ z0 ^ (z2[q] << 21) ^ (z2[q] >> 21);
+    }
+    // lane transfer: z4 after the lane's last step = L^SPL(z4 before) ^ C
+    uint32_t C = c[0];
+#pragma unroll
+    for (int q = 1; q < SPL; q++) C = wellsp::L1(C) ^ c[q];
+    C ^= t == 0 ? wellsp::lpow<SPL>(carry) : 0u;
+    C ^= wellsp::lpow<SPL>(wellsp::dpp<0x111>(C));      // row_shr:1
+    C ^= wellsp::lpow<2 * SPL>(wellsp::dpp<0x112>(C));  // row_shr:2
+    C ^= wellsp::lpow<4 * SPL>(wellsp::dpp<0x114>(C));  // row_shr:4
+    C ^= wellsp::lpow<8 * SPL>(wellsp::dpp<0x118>(C));  // row_shr:8
+    const uint32_t prevC = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)C, 0x121, 0xF, 0xF,
+                                                                  false);  // row_ror:1
+    uint32_t y = t == 0 ? carry : prevC;  // z4 before the lane's first step
+    carry = prevC;                        // lane 0: z4 of the batch's last step
+    uint32_t o[SPL];
+    uint32_t z3[SPL];
+#pragma unroll
+    for (int q = 0; q < SPL; q++) {
+      z3[q] = y ^ (y << 25) ^ a[q] ^ z2[q];
+      y = wellsp::L1(y) ^ c[q];
+      o[q] = well_temper26(y);
+    }
+    if (i >= B - 1) {  // the written block [i - B + 1, i] does not wrap
+      uint32_t* pw = st + (i - n0 - (SPL - 1));
+#pragma unroll
+      for (int q = 0; q < SPL; q++) pw[SPL - 1 - q] = z3[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < SPL; q++) {
+        int pos = i - n0 - q;
+        pos += pos < 0 ? 624 : 0;
+        st[pos] = z3[q];
+      }
+    }
+    i = wrap624(i - B);
+    // doubles: BitsStreamGenerator.nextDouble = (next(26) << 26 | next(26)) * 2^-52,
+    // built exactly as the bits of 1 + m * 2^-52 minus 1
+    double x[DPL];
+#pragma unroll
+    for (int k = 0; k < DPL; k++) {
+      const uint32_t hi = o[2 * k], lo = o[2 * k + 1];
+      x[k] = __hiloint2double((int)(0x3FF00000u | (hi >> 6)), (int)((hi << 26) | lo)) - 1.0;
+    }
+    // PoissonDistribution.nextPoisson (mean < 40): r *= nextDouble() while r >= exp(-mean),
+    // at most n < 1000 * mean draws counted.
+    if constexpr (PAR) {
+      // Lane-parallel parse by relaxation.  A lane's doubles map an in-state (r, n) (the
+      // running product and count of the row open before its first double) to an
+      // out-state; a lane whose doubles end a row emits counts and its out-state no
+      // longer depends on its in-state past that end.  Every lane re-evaluates its
+      // doubles from the previous lane's out-state (lane 0: the carry from the previous
+      // batch) until no in-state changes: the fixed point of this chain is unique and is
+      // the sequential parse, and since every double < exp(-mean) ends whatever row it
+      // is in, chains of lanes without an end are short (a few rounds).
+      double in_r = t == 0 ? pr : 1.0;
+      int in_n = t == 0 ? pn : 0;
+      int nk[DPL];
+      bool ek[DPL];
+      double out_r;
+      int out_n;
+      for (;;) {
+        double r_in = in_r;
+        int n_in = in_n;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+          const double rr = r_in * x[k];
+          const bool ge = rr >= p_exp;
+          const int nn = n_in + (ge ? 1 : 0);
+          const bool e = !ge || (CAP && nn >= icap);
+          nk[k] = nn;
+          ek[k] = e;
+          r_in = e ? 1.0 : rr;
+          n_in = e ? 0 : nn;
+        }
+        out_r = r_in;
+        out_n = n_in;
+        const int ph = (int)wellsp::dpp<0x111>((uint32_t)__double2hiint(out_r));  // row_shr:1
+        const int pl = (int)wellsp::dpp<0x111>((uint32_t)__double2loint(out_r));
+        const int pnn = (int)wellsp::dpp<0x111>((uint32_t)out_n);
+        // branch-free: bitwise, not short-circuit, so no exec-mask juggling per round
+        const int changed = (t != 0) & ((ph != __double2hiint(in_r)) |
+                                        (pl != __double2loint(in_r)) | (pnn != in_n));
+        if (!__any(changed)) break;
+        in_r = t != 0 ? __hiloint2double(ph, pl) : in_r;
+        in_n = t != 0 ? pnn : in_n;
+      }
+      // carry: lane 15's out-state to lane 0 (row_ror:1)
+      {
+        const int ch = __builtin_amdgcn_update_dpp(0, __double2hiint(out_r), 0x121, 0xF, 0xF, false);
+        const int cl = __builtin_amdgcn_update_dpp(0, __double2loint(out_r), 0x121, 0xF, 0xF, false);
+        pn = __builtin_amdgcn_update_dpp(0, out_n, 0x121, 0xF, 0xF, false);
+        pr = __hiloint2double(ch, cl);
+      }
+      // row of each emitted count: ends at earlier positions of this stream's batch
+      int below = 0, mine = 0;
+#pragma unroll
+      for (int k = 0; k < DPL; k++) {
+        const uint64_t m = __ballot(ek[k]);
+        below += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        mine += ek[k] ? 1 : 0;
+      }
+      const int rowbase = (int)__builtin_amdgcn_update_dpp(0, below, 0x150, 0xF, 0xF, false);
+      const int rowend =
+          (int)__builtin_amdgcn_update_dpp(0, below + mine, 0x15F, 0xF, 0xF, false);
+      int rank = below - rowbase;
+#pragma unroll
+      for (int k = 0; k < DPL; k++) {
+        if (ek[k]) {
+          if (row + rank < row_end) {
+            out[row + rank] = (uint8_t)min(nk[k], 255);
+            bad |= nk[k] > 255 ? 1 : 0;
+          }
+          rank++;
+        }
+      }
+      row += rowend - rowbase;
+      continue;
+    }
+    // serial parse: 16 doubles at a time, all lanes of the stream run it, lane e keeps
+    // the e-th count
+#pragma unroll
+    for (int h = 0; h < DPL; h++) {
+      int ne = 0;
+      int cap = 0;
+#pragma unroll
+      for (int d = 0; d < kSpLanes; d++) {
+        // double 16h + d of the batch, in stream order: lane l holds doubles DPL*l ..
+        // DPL*l + DPL - 1, so half h reads lanes 8h .. 8h+7 when DPL = 2
+        const int dl = (DPL == 1) ? d : (8 * h + (d >> 1));
+        const int dk = (DPL == 1) ? 0 : (d & 1);
+        double xd = 0.0;
+        // compile-time lane index for the DPP broadcast
+        switch (dl) {
+#define SBAG_BC(L) case L: xd = wellsp::row_bcast<L>(x[dk]); break;
+          SBAG_BC(0) SBAG_BC(1) SBAG_BC(2) SBAG_BC(3) SBAG_BC(4) SBAG_BC(5) SBAG_BC(6) SBAG_BC(7)
+          SBAG_BC(8) SBAG_BC(9) SBAG_BC(10) SBAG_BC(11) SBAG_BC(12) SBAG_BC(13) SBAG_BC(14)
+          SBAG_BC(15)
+#undef SBAG_BC
+        }
+        racc *= xd;
+        const bool ge = racc >= p_exp;
+        n += ge ? 1 : 0;
+        const bool done = !ge || (CAP && n >= icap);
+        cap = (done && ne == t) ? n : cap;
+        ne += done ? 1 : 0;
+        n = done ? 0 : n;
+        racc = done ? 1.0 : racc;
+      }
+      if (t < ne && row + t < row_end) {
+        out[row + t] = (uint8_t)min(cap, 255);
+        bad |= cap > 255 ? 1 : 0;
+      }
+      row += ne;
+    }
+  }
+  if (bad) atomicOr(err, 1);
+}
+
 void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
                     int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err) {
   const int64_t streams = (int64_t)R * P;
   const int blocks = (int)((streams + 63) / 64);
-  static const int v1 = getenv("SBAG_POISSON_V1") ? 1 : 0;
-  if (v1) {
+  // A/B knobs, read per launch so tests can switch them: SBAG_POISSON_V (3 = k_poisson3,
+  // 2 = the two-wave k_poisson2, 1 = one wave), SBAG_POISSON_SPL (steps per lane, 2 or 4),
+  // SBAG_POISSON_PAR (1 = lane-parallel relaxation parse, 0 = serial parse)
+  const char* ev = getenv("SBAG_POISSON_V");
+  const char* es = getenv("SBAG_POISSON_SPL");
+  const int ver = ev ? atoi(ev) : 3;
+  const int spl = es ? atoi(es) : 4;
+  if (ver == 3) {
+    // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean);
+    // the cap is only checked when it can end a row below the 255 limit
+    const int icap = (int)std::min(ceil(1000.0 * mean), 1e9);
+    const bool cap = icap <= 255;
+    const int sb = (int)((streams + kSpStreams - 1) / kSpStreams);
+    const char* ep = getenv("SBAG_POISSON_PAR");
+    const bool par = ep ? atoi(ep) != 0 : true;
+#define SBAG_P3(S, C, A)                                                                   \
+  hipLaunchKernelGGL((k_poisson3<S, C, A>), dim3(sb), dim3(256), 0, st, counts, N, d_part_off, \
+                     P, R, learner0, seed, p_exp, icap, d_err)
+    if (spl == 2) {
+      if (par) {
+        if (cap) SBAG_P3(2, true, true); else SBAG_P3(2, false, true);
+      } else {
+        if (cap) SBAG_P3(2, true, false); else SBAG_P3(2, false, false);
+      }
+    } else {
+      if (par) {
+        if (cap) SBAG_P3(4, true, true); else SBAG_P3(4, false, true);
+      } else {
+        if (cap) SBAG_P3(4, true, false); else SBAG_P3(4, false, false);
+      }
+    }
+#undef SBAG_P3
+    return;
+  }
+  if (ver == 1) {
     hipLaunchKernelGGL(k_poisson, dim3(blocks), dim3(64), 0, st, counts, N, d_part_off, P, R,
                        learner0, seed, mean, p_exp, d_err);
     return;

@@ -50,6 +50,25 @@ def test_poisson_bag_bit_exact(ctx, seed, ratio):
     assert (got == want).all()
 
 
+@pytest.mark.parametrize("variant", [("3", "4", "1"), ("3", "2", "1"), ("3", "4", "0"),
+                                     ("3", "2", "0"), ("2", "4", "1")])
+@pytest.mark.parametrize("ratio", [1.0, 0.2, 0.001])
+def test_poisson_sampler_variants_many_streams(ctx, monkeypatch, variant, ratio):
+    # k_poisson3 with 4 and 2 steps per lane, relaxation or serial parse (capped for
+    # ratio <= 0.255, where nextPoisson's n < 1000 * mean can end a row) and the
+    # two-wave k_poisson2, on 38
+    # learners x 7 ragged partitions (266 streams: 17 blocks, idle slots in the last)
+    # with streams long enough to run round the 624-word ring many times
+    monkeypatch.setenv("SBAG_POISSON_V", variant[0])
+    monkeypatch.setenv("SBAG_POISSON_SPL", variant[1])
+    monkeypatch.setenv("SBAG_POISSON_PAR", variant[2])
+    N = 120_000
+    off = [0, 1, 17_000, 17_000, 50_001, 77_777, 100_000, N]
+    got = nat.sample(ctx, True, ratio, SEED_REG, 5, 43, N, off)
+    want = oracle.bag(True, ratio, 5, 43, SEED_REG, off, N)
+    assert (got == want).all()
+
+
 @pytest.mark.parametrize("seed", [SEED_REG, SEED_CLS, 2**31 - 3, -2**31 + 1, 2**40 + 3])
 @pytest.mark.parametrize("ratio", [0.5, 0.3, 0.999])
 def test_bernoulli_bag_bit_exact(ctx, seed, ratio):
