@@ -759,6 +759,27 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
       }
       double* agg = (double*)calloc((size_t)(g * per_node), sizeof(double));
       double* par = (double*)calloc((size_t)(g * ns), sizeof(double));
+      /* the group's rows grouped by node, stably (row order kept within a node): a node's
+         cells then stay in cache while its rows are added; every (node, feature, bin) cell
+         still sees its rows in row order */
+      int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nrows + 1));
+      int64_t n_order = 0;
+      {
+        int64_t* start = (int64_t*)calloc((size_t)(g + 1), sizeof(int64_t));
+        for (int64_t k = 0; k < nrows; k++) {
+          const int64_t nd = node_of[k];
+          if (nd < first || nd > last || slot[nd - first] < 0) continue;
+          start[slot[nd - first] + 1]++;
+        }
+        for (int64_t s = 0; s < g; s++) start[s + 1] += start[s];
+        n_order = start[g];
+        for (int64_t k = 0; k < nrows; k++) {
+          const int64_t nd = node_of[k];
+          if (nd < first || nd > last || slot[nd - first] < 0) continue;
+          order[start[slot[nd - first]]++] = k;
+        }
+        free(start);
+      }
       /* DTStatsAggregator.update in row order.  Each (feature, bin) cell is summed in row
          order whatever the thread split: threads own disjoint feature ranges. */
 #pragma omp parallel num_threads(inner)
@@ -769,11 +790,9 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
         tid = omp_get_thread_num();
 #endif
         const int f0 = (int)((int64_t)Fr * tid / nth), f1 = (int)((int64_t)Fr * (tid + 1) / nth);
-        for (int64_t k = 0; k < nrows; k++) {
-          const int64_t nd = node_of[k];
-          if (nd < first || nd > last) continue;
-          const int64_t s = slot[nd - first];
-          if (s < 0) continue;
+        for (int64_t o = 0; o < n_order; o++) {
+          const int64_t k = order[o];
+          const int64_t s = slot[node_of[k] - first];
           const double lab = y[rows[k]];
           double* a = agg + s * per_node;
           double* pp = par + s * ns;
@@ -888,6 +907,7 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
       }
       free(agg);
       free(par);
+      free(order);
       free(members);
     }
     free(slot);

@@ -129,10 +129,12 @@ def test_c3_as_benched(ctx):
 def test_c4_shard_wide_rows_64bit_offsets(ctx):
     """C4 (BASELINE configs[3]) shard shape: 2^24 + 4097 rows x 256 features (k_hist with
     four 64-feature lane groups, row offsets past 32 bits), P=128, depth 8, learners
-    [448, 450) -- rank 7's first two of 512 learners over 8 GPUs."""
+    [448, 450) -- rank 7's first two of 512 learners over 8 GPUs.  Learner 449 is
+    checked against the oracle (a CPU fit of this size takes about a minute), 448
+    through the tree invariants."""
     n = (1 << 24) + 4097
     ds, X, forest, orf, _ = _run_config(ctx, n=n, f=256, classes=0, replacement=True, ratio=1.0,
-                                        seed=SEED_REG, lb=448, le=450, depth=8, check=[448, 449])
+                                        seed=SEED_REG, lb=448, le=450, depth=8, check=[449])
     forest.free()
     ds.free()
 
