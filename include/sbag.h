@@ -140,6 +140,27 @@ typedef struct {
 
 int sbag_fit(sbag_ctx* ctx, sbag_dataset* ds, const sbag_fit_params* p, sbag_forest** out);
 
+/* ---- GBM base learner: one boosting iteration's tree -----------------------
+ * GBMRegressor.trainBoosters (ml/regression/GBMRegressor.scala:302-319): the subbag of
+ * learner m (HasSubBag.extractSubBag of withBag's column m, HasSubBag.scala:108-126,
+ * the bag drawn by sbag_sample), sliced to the booster's subspace (mkSubspace with the
+ * boosting seed chain), fitted by DecisionTreeRegressor (fitBaseLearner,
+ * ensembleParams.scala:99-117) on fp64 labels -- the pseudo-residuals -grad(y, F(x)).
+ * Split statistics are fp64 sums in Spark's row order (DTStatsAggregator.update), so
+ * trees and leaf values are those of the reference's DecisionTree on the same subbag.
+ * Returns a forest of one tree (subspace = `subspace`).                           */
+typedef struct {
+  const uint8_t* counts;            /* host [num_rows]: the learner's bag column         */
+  const int32_t* subspace;          /* the booster's feature indices, increasing          */
+  int32_t subspace_len;
+  int32_t num_partitions;           /* partitions of the split-finding sample (0/1: one) */
+  const int64_t* partition_offsets; /* [num_partitions+1] or NULL                         */
+  sbag_tree_params tree;            /* DecisionTreeRegressor params (impurity VARIANCE)   */
+} sbag_booster_params;
+
+int sbag_fit_booster(sbag_ctx* ctx, const sbag_dataset* ds, const double* labels /* host [N] */,
+                     const sbag_booster_params* p, sbag_forest** out);
+
 /* ---- forest (BaggingRegressionModel / BaggingClassificationModel fields
  *      `subspaces`, `models`, `numBaseModels`, BaggingRegressor.scala:235-246) */
 typedef struct { /* DecisionTreeModelReadWrite.NodeData, pre-order ids */

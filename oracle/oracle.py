@@ -239,3 +239,111 @@ def predict(forest, X, classification=False, per_tree=False):
     lib().or_predict(_p(X), N, F, L, _p(sub), _p(nsub), _p(forest.nodes), forest.nodes.shape[1],
                      1 if classification else 0, _p(out), _p(pt) if per_tree else None)
     return (out, pt) if per_tree else out
+
+
+# ---------------------------------------------------------------- GBMRegressor
+_DOUBLE_MAX = np.finfo(np.float64).max
+DEFAULT_SEED_GBM_REGRESSOR = 1243996765  # "org.apache.spark.ml.regression.GBMRegressor".hashCode
+
+
+def _gbm_grad(loss, alpha):
+    """GBMRegressorParams.gradFunction (ml/regression/GBMRegressor.scala:107-118)."""
+    def signum(d):  # Math.signum: NaN and +-0.0 map to themselves
+        return np.where(d == 0, d, np.sign(d))
+    return {
+        "squared": lambda y, p: -(y - p),
+        "absolute": lambda y, p: -signum(y - p),
+        "huber": lambda y, p: -(y - p) / np.sqrt(1 + ((y - p) / alpha) * ((y - p) / alpha)),
+        "quantile": lambda y, p: np.where(p > y, -(alpha - 1.0), -alpha),
+    }[loss]
+
+
+def _gbm_loss(loss, alpha):
+    """GBMRegressorParams.lossFunction (ml/regression/GBMRegressor.scala:93-105)."""
+    return {
+        "squared": lambda y, p: (y - p) * (y - p) / 2.0,
+        "absolute": lambda y, p: np.abs(y - p),
+        "huber": lambda y, p: (alpha * alpha) * (np.sqrt(1.0 + ((y - p) / alpha) * ((y - p) / alpha)) - 1.0),
+        "quantile": lambda y, p: np.where(p > y, (alpha - 1.0) * (y - p), alpha * (y - p)),
+    }[loss]
+
+
+def gbm_regressor_fit(X, y, *, num_base_learners=10, learning_rate=1.0, loss="squared",
+                      alpha=0.9, replacement=False, sample_ratio=1.0, subspace_ratio=1.0,
+                      seed=DEFAULT_SEED_GBM_REGRESSOR, tol=1e-3, num_round=5, max_depth=5,
+                      max_bins=32, min_instances_per_node=1, min_info_gain=0.0, dt_seed=None,
+                      validation=None, nthreads=None):
+    """GBMRegressor.train with optimizedWeights = false (ml/regression/GBMRegressor.scala:
+    196-456): withBag over the training rows (seed), then per iteration m mkSubspace(
+    subspaceRatio, F, seed_m) with seed_{m+1} = seed_m + iter_m, residuals -grad(label,
+    dot(predictions, weights) + const), DecisionTreeRegressor on extractSubBag(bag m)
+    (this oracle's fit, fp64 sums in row order), weight = learningRate, and
+    terminate / terminateVal (ml/boosting/GBMParams.scala:308-326,
+    ml/boosting/BoostingParams.scala:150-177).  One partition.
+    Returns (weights, subspaces, trees [(nodes, stats)], const)."""
+    X = np.ascontiguousarray(X, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    vmask = np.zeros(len(y), bool) if validation is None else np.asarray(validation, bool)
+    with_validation = validation is not None
+    Xt, yt, Xv, yv = X[~vmask], y[~vmask], X[vmask], y[vmask]
+    Nt, F = Xt.shape
+    grad, lossf = _gbm_grad(loss, alpha), _gbm_loss(loss, alpha)
+    counts = bag(replacement, sample_ratio, 0, num_base_learners, seed, [0, Nt], Nt)
+    const = 0.0
+    weights, subs, trees = [], [], []
+    S, SV = np.zeros(Nt), np.zeros(len(yv))
+    it, error, num_try, s = num_base_learners, _DOUBLE_MAX, 0, seed
+    while it != 0:
+        m = num_base_learners - it
+        sub = subspace(subspace_ratio, F, s)
+        r = -grad(yt, S + const)
+        f = fit(Xt, r, counts[m:m + 1], [sub], max_depth=max_depth, max_bins=max_bins,
+                min_instances_per_node=min_instances_per_node, min_info_gain=min_info_gain,
+                nthreads=nthreads, dt_seed=dt_seed)
+        w = learning_rate * 1.0
+        _, p = predict(f, Xt, per_tree=True)
+        S = S + p[0] * w
+        if len(yv):
+            _, pv = predict(f, Xv, per_tree=True)
+            SV = SV + pv[0] * w
+            verror = float(np.cumsum(lossf(yv, SV + const))[-1])  # SQL sum, left to right
+        else:
+            verror = _DOUBLE_MAX
+        weights.append(w)
+        subs.append(sub)
+        trees.append(f.tree(0))
+        old = it
+        if w < tol * learning_rate:
+            it, error, num_try = 0, 0.0, 1
+        elif with_validation:
+            if verror < error * (1 - tol):
+                it, error, num_try = it - 1, verror, 0
+            elif num_try == num_round - 1:
+                it, error, num_try = 0, 0.0, num_try + 1
+            else:
+                it, num_try = it - 1, num_try + 1
+        else:
+            it, error, num_try = it - 1, 0.0, 0
+        s = s + old
+    keep = len(trees) - num_try
+    return weights[:keep], subs[:keep], trees[:keep], const
+
+
+def gbm_predict(weights, subspaces, trees, const, X):
+    """GBMRegressionModel.predict: BLAS.dot(tree predictions, weights) + const, the dot a
+    left-to-right sum of rounded products (F2J ddot)."""
+    X = np.ascontiguousarray(X, np.float64)
+    L = len(trees)
+    if L == 0:
+        return np.full(X.shape[0], 0.0 + const)
+    width = max(len(t[0]) for t in trees)
+    nodes = np.zeros((L, width), NODE_DTYPE)
+    for l, (n, _) in enumerate(trees):
+        nodes[l, : len(n)] = n
+    f = Forest(nodes, np.zeros((L, width, 3)), np.array([len(t[0]) for t in trees], np.int32),
+               np.full(L, 3, np.int32), [np.asarray(s, np.int32) for s in subspaces], np.ones(L, bool))
+    _, pt = predict(f, X, per_tree=True)
+    acc = np.zeros(X.shape[0])
+    for p, w in zip(pt, weights):
+        acc = acc + p * w
+    return acc + const

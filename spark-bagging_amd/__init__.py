@@ -12,3 +12,4 @@ from .libsvm import SparseRows, load_libsvm  # noqa: F401
 from .ml import (BaggingClassificationModel, BaggingClassifier, BaggingRegressionModel,  # noqa: F401
                  BaggingRegressor, DecisionTreeClassifier, DecisionTreeModel,
                  DecisionTreeRegressor, Frame, even_partitions, java_string_hash)
+from .gbm import GBMRegressionModel, GBMRegressor  # noqa: F401

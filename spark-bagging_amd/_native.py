@@ -25,7 +25,7 @@ EXPORTED = [
     "sbag_sample", "sbag_subspace", "sbag_dataset_create", "sbag_dataset_create_csr",
     "sbag_dataset_create_columns", "sbag_dataset_synthetic",
     "sbag_dataset_info", "sbag_dataset_labels", "sbag_dataset_features", "sbag_dataset_free",
-    "sbag_fit", "sbag_forest_num_trees", "sbag_forest_tree_info", "sbag_forest_subspace",
+    "sbag_fit", "sbag_fit_booster", "sbag_forest_num_trees", "sbag_forest_tree_info", "sbag_forest_subspace",
     "sbag_forest_nodes", "sbag_forest_create", "sbag_forest_free", "sbag_forest_timing",
     "sbag_predict", "sbag_predict_dataset", "sbag_aggregate", "sbag_predict_dataset_device",
     "sbag_aggregate_device",
@@ -67,6 +67,12 @@ DT_SEED_CLASSIFIER = 159147643    # "org.apache.spark.ml.classification.Decision
 class FitParams(ctypes.Structure):
     _fields_ = [("sampler", SamplerParams), ("subspace_ratio", ctypes.c_double),
                 ("subspace_bug_compat", ctypes.c_int32), ("num_partitions", ctypes.c_int32),
+                ("partition_offsets", ctypes.c_void_p), ("tree", TreeParams)]
+
+
+class BoosterParams(ctypes.Structure):
+    _fields_ = [("counts", ctypes.c_void_p), ("subspace", ctypes.c_void_p),
+                ("subspace_len", ctypes.c_int32), ("num_partitions", ctypes.c_int32),
                 ("partition_offsets", ctypes.c_void_p), ("tree", TreeParams)]
 
 
@@ -123,6 +129,7 @@ def lib():
             "sbag_dataset_features": [P, i64, i64, P],
             "sbag_dataset_free": [P],
             "sbag_fit": [P, P, ctypes.POINTER(FitParams), P],
+            "sbag_fit_booster": [P, P, P, ctypes.POINTER(BoosterParams), P],
             "sbag_forest_num_trees": [P, P],
             "sbag_forest_tree_info": [P, i32, P, P, P, P],
             "sbag_forest_subspace": [P, i32, P],
@@ -405,6 +412,33 @@ def fit(ctx, dataset, *, replacement, sample_ratio, seed, learner_begin, learner
     h = ctypes.c_void_p()
     check(lib().sbag_fit(ctx.handle, dataset.handle, ctypes.byref(fp), ctypes.byref(h)))
     return NativeForest(h, impurity)
+
+
+def fit_booster(ctx, dataset, labels, counts, subspace, *, partition_offsets=None, max_depth=5,
+                max_bins=32, min_instances_per_node=1, min_info_gain=0.0, tree_seed=None):
+    """One GBM base-learner fit (sbag_fit_booster): DecisionTreeRegressor on the subbag
+    `counts` (u8 per row) sliced to `subspace`, with fp64 labels (pseudo-residuals)."""
+    if tree_seed is None:
+        tree_seed = DT_SEED_REGRESSOR
+    labels = np.ascontiguousarray(labels, np.float64)
+    counts = np.ascontiguousarray(counts, np.uint8)
+    sub = np.ascontiguousarray(subspace, np.int32)
+    n = dataset.shape[0]
+    if len(labels) != n or len(counts) != n:
+        raise IllegalArgumentException(SBAG_EINVAL, "labels / counts do not match the row count")
+    off = None
+    P = 1
+    if partition_offsets is not None:
+        off = np.ascontiguousarray(partition_offsets, np.int64)
+        P = len(off) - 1
+    bp = BoosterParams(counts.ctypes.data, sub.ctypes.data, len(sub), P,
+                       off.ctypes.data if off is not None else None,
+                       TreeParams(max_depth, max_bins, min_instances_per_node, IMPURITY_VARIANCE,
+                                  float(min_info_gain), int(tree_seed)))
+    h = ctypes.c_void_p()
+    check(lib().sbag_fit_booster(ctx.handle, dataset.handle, ptr(labels), ctypes.byref(bp),
+                                 ctypes.byref(h)))
+    return NativeForest(h, IMPURITY_VARIANCE)
 
 
 def predict(ctx, forest, X, agg, per_tree=False):

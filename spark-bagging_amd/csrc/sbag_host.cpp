@@ -2967,3 +2967,434 @@ int sbag_aggregate_device(sbag_ctx* c, const void* d_in, int32_t in_bytes, int32
 }
 
 }  // extern "C"
+
+// ====================================================================== booster engine
+// GBMRegressor's base-learner fit (ml/regression/GBMRegressor.scala:302-319): the subbag
+// of learner m (extractSubBag of withBag's column m, HasSubBag.scala:108-126) sliced to
+// the booster's subspace, labels = the pseudo-residuals -grad(y, F(x)) in fp64, through
+// DecisionTreeRegressor.fit (HasBaseLearner.fitBaseLearner, ensembleParams.scala:99-117).
+// The labels are arbitrary doubles, so the bagging engine's exact integer histograms do
+// not apply: Spark's fp64 sums depend on their order.  Every (node, feature, bin) cell is
+// summed on the device by one lane in row order (k_bt_hist over stably partitioned row
+// lists, k_bt_partition); split selection (binsToBestSplit / calculateImpurityStats) runs
+// on the host in Spark's operation order.  Thresholds are Spark's findSplits of the
+// subbag, with the split-finding sample (k_split_sample) above max(maxBins^2, 1e4) rows.
+namespace {
+struct BtNode {  // LearningNode with fp64 ImpurityStats
+  int left = -1, right = -1;
+  bool is_leaf = false, has_split = false, valid = true;
+  int fl = -1, s = -1;
+  double thr = 0.0;
+  double calc[3] = {0, 0, 0};  // stats.impurityCalculator (count, sum, sumSq)
+  double impurity = 0.0, gain = NAN;
+};
+
+double bt_count(const double* s) { return s[0]; }
+// Variance.calculate (count, sum, sumSq)
+double bt_impurity(const double* s) {
+  const double count = s[0], sum = s[1], sumsq = s[2];
+  if (count == 0) return 0.0;
+  const double squared_loss = sumsq - (sum * sum) / count;
+  return squared_loss / count;
+}
+// VarianceCalculator.predict: sum / count (count as a Long)
+double bt_predict(const double* s) {
+  const int64_t cnt = (int64_t)s[0];
+  if (cnt == 0) return 0.0;
+  return s[1] / (double)cnt;
+}
+
+// LearningNode.toNode(prune = true), NodeData pre-order
+struct BtRet {
+  bool leaf;
+  double pred;
+};
+BtRet bt_emit(const std::vector<BtNode>& nodes, int idx, HTree& t) {
+  const BtNode& n = nodes[idx];
+  const int my = (int)t.nodes.size();
+  t.nodes.push_back(sbag_node{});
+  t.stats.resize((size_t)(my + 1) * 3);
+  auto fill = [&](int at) {
+    for (int i = 0; i < 3; i++) t.stats[(size_t)at * 3 + i] = n.calc[i];
+  };
+  if (n.has_split) {
+    const size_t mark = t.nodes.size();
+    const int lid = (int)t.nodes.size();
+    BtRet l = bt_emit(nodes, n.left, t);
+    const int rid = (int)t.nodes.size();
+    BtRet r = bt_emit(nodes, n.right, t);
+    if (l.leaf && r.leaf && l.pred == r.pred) {
+      t.nodes.resize(mark);
+      t.stats.resize(mark * 3);
+      sbag_node& p = t.nodes[my];
+      p = sbag_node{};
+      p.id = my;
+      p.left = p.right = -1;
+      p.feature = -1;
+      p.split_bin = -1;
+      p.prediction = l.pred;
+      p.impurity = n.impurity;
+      p.gain = -1.0;
+      fill(my);
+      return {true, l.pred};
+    }
+    sbag_node& o = t.nodes[my];
+    o.id = my;
+    o.left = lid;
+    o.right = rid;
+    o.feature = n.fl;
+    o.split_bin = n.s;
+    o.threshold = n.thr;
+    o.prediction = bt_predict(n.calc);
+    o.impurity = n.impurity;
+    o.gain = n.gain;
+    fill(my);
+    return {false, o.prediction};
+  }
+  sbag_node& o = t.nodes[my];
+  o.id = my;
+  o.left = o.right = -1;
+  o.feature = -1;
+  o.split_bin = -1;
+  o.prediction = bt_predict(n.calc);
+  o.impurity = n.valid ? n.impurity : -1.0;
+  o.gain = -1.0;
+  fill(my);
+  return {true, o.prediction};
+}
+
+// RandomForest.binsToBestSplit for one node over its fp64 histogram [Fr+1][NB][3]
+// (in place: mergeForFeature turns each feature's bins into prefixes).  `level > 0`:
+// the chain starts from the node's stats (set when its parent split); at the root from
+// the first candidate's left + right (calculateImpurityStats with stats == null).
+void bt_best_split(BtNode& node, int level, double* h, int Fr, int NB,
+                   const std::vector<int>& nsplits, const sbag_tree_params& tp, double left_out[3],
+                   double right_out[3], int* best_f_out, int* best_s_out) {
+  bool chain_set = level > 0;
+  double chain_calc[3] = {node.calc[0], node.calc[1], node.calc[2]};
+  double chain_imp = node.impurity;
+  int best_f = -1, best_s = -1;
+  bool best_valid = false;
+  double best_gain = 0.0;
+  for (int fl = 0; fl < Fr; fl++) {
+    const int nsp = nsplits[fl];
+    if (nsp == 0) continue;  // validFeatureSplits: features with splits only
+    double* fa = h + (size_t)fl * NB * 3;
+    for (int s = 0; s < nsp; s++)  // mergeForFeature(offset, s + 1, s)
+      for (int i = 0; i < 3; i++) fa[(s + 1) * 3 + i] += fa[s * 3 + i];
+    int fbest_s = -1;
+    bool fbest_valid = false;
+    double fbest_gain = 0.0;
+    for (int s = 0; s < nsp; s++) {
+      double left[3], right[3];
+      for (int i = 0; i < 3; i++) {
+        left[i] = fa[s * 3 + i];
+        right[i] = fa[nsp * 3 + i];
+      }
+      for (int i = 0; i < 3; i++) right[i] -= left[i];  // rightChildStats.subtract(left)
+      // calculateImpurityStats
+      if (!chain_set) {
+        for (int i = 0; i < 3; i++) chain_calc[i] = left[i] + right[i];
+        chain_imp = bt_impurity(chain_calc);
+        chain_set = true;
+      }
+      const int64_t lc = (int64_t)bt_count(left), rc = (int64_t)bt_count(right);
+      const int64_t total = lc + rc;
+      double gain;
+      bool valid;
+      if (lc < tp.min_instances_per_node || rc < tp.min_instances_per_node) {
+        gain = kDoubleMinValue;
+        valid = false;
+      } else {
+        const double li = bt_impurity(left), ri = bt_impurity(right);
+        const double lw = (double)lc / (double)total, rw = (double)rc / (double)total;
+        gain = chain_imp - lw * li - rw * ri;
+        valid = true;
+        if (gain < tp.min_info_gain) {
+          gain = kDoubleMinValue;
+          valid = false;
+        }
+      }
+      if (fbest_s < 0 || gain > fbest_gain) {  // maxBy: the first maximum
+        fbest_gain = gain;
+        fbest_s = s;
+        fbest_valid = valid;
+      }
+    }
+    if (best_f < 0 || fbest_gain > best_gain) {
+      best_gain = fbest_gain;
+      best_f = fl;
+      best_s = fbest_s;
+      best_valid = fbest_valid;
+    }
+  }
+  *best_f_out = best_f;
+  *best_s_out = best_s;
+  if (best_f < 0) {  // no feature has a split: invalid stats on the parent aggregate
+    const double* par = h + (size_t)Fr * NB * 3;
+    for (int i = 0; i < 3; i++) node.calc[i] = par[i];
+    node.gain = kDoubleMinValue;
+    node.impurity = bt_impurity(node.calc);
+    node.valid = false;
+    return;
+  }
+  for (int i = 0; i < 3; i++) node.calc[i] = chain_calc[i];
+  node.gain = best_gain;
+  node.impurity = chain_imp;
+  node.valid = best_valid;
+  const double* fa = h + (size_t)best_f * NB * 3;
+  const int nsp = nsplits[best_f];
+  for (int i = 0; i < 3; i++) {
+    left_out[i] = fa[best_s * 3 + i];
+    right_out[i] = fa[nsp * 3 + i] - fa[best_s * 3 + i];
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
+                     const sbag_booster_params* bp, sbag_forest** out) {
+  if (!c || !ds || !labels || !bp || !out || !bp->counts || !bp->subspace)
+    return fail(SBAG_EINVAL, "bad arguments");
+  if (ds->ctx->device != c->device)
+    return fail(SBAG_EINVAL, "dataset lives on device " + std::to_string(ds->ctx->device) +
+                                 ", the context on device " + std::to_string(c->device));
+  CTX_LOCK(c);
+  const sbag_tree_params& tp = bp->tree;
+  if (tp.impurity != SBAG_IMPURITY_VARIANCE)
+    return fail(SBAG_EINVAL, "the booster engine fits DecisionTreeRegressor (impurity variance)");
+  if (tp.max_depth < 0 || tp.max_depth > 30)
+    return fail(SBAG_EINVAL, "maxDepth given invalid value (must be in [0, 30])");
+  if (tp.max_depth > 24) return fail(SBAG_EUNSUPPORTED, "maxDepth > 24");
+  if (tp.max_bins < 2 || tp.max_bins > 256)
+    return fail(SBAG_EINVAL, "maxBins given invalid value (must be in [2, 256])");
+  if (tp.min_instances_per_node < 1)
+    return fail(SBAG_EINVAL, "minInstancesPerNode given invalid value (must be >= 1)");
+  if (!(tp.min_info_gain >= 0.0)) return fail(SBAG_EINVAL, "minInfoGain given invalid value");
+  if (ds->code_bytes == 4)
+    return fail(SBAG_EUNSUPPORTED, "booster fit on features with more than 65536 distinct values");
+  const int64_t N = ds->N;
+  const int F = ds->F;
+  if (N >= ((int64_t)1 << 32)) return fail(SBAG_EUNSUPPORTED, "booster fit on 2^32 rows or more");
+  const int Fr = bp->subspace_len;
+  if (Fr <= 0)
+    return fail(SBAG_EINVAL, "requirement failed: VectorSlicer requires that at least one "
+                             "feature be selected.");
+  std::vector<int32_t> sub(bp->subspace, bp->subspace + Fr);
+  for (int k = 0; k < Fr; k++)
+    if (sub[k] < 0 || sub[k] >= F || (k > 0 && sub[k] <= sub[k - 1]))
+      return fail(SBAG_EINVAL, "subspace indices must be increasing and within [0, num_features)");
+  for (int64_t r = 0; r < N; r++)
+    if (!std::isfinite(labels[r]))
+      return fail(SBAG_EUNSUPPORTED, "booster labels must be finite");
+  std::vector<int64_t> poff;
+  TRY(check_partitions(bp->num_partitions, bp->partition_offsets, N, poff));
+  HIP_TRY(hipSetDevice(c->device));
+  const int D = tp.max_depth;
+  // in-bag rows in row order; numExamples of the subbag = sum of the counts
+  std::vector<uint32_t> rows;
+  int64_t n_items = 0;
+  for (int64_t r = 0; r < N; r++)
+    if (bp->counts[r]) {
+      rows.push_back((uint32_t)r);
+      n_items += bp->counts[r];
+    }
+  if (n_items == 0)
+    return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
+                             "empty one.");
+  const int64_t nrows = (int64_t)rows.size();
+  uint32_t *d_rowsA, *d_rowsB;
+  uint8_t* d_cnt;
+  double* d_y;
+  int32_t* d_sub;
+  TRY(ws_typed(c, "bt_rowsA", (size_t)nrows, &d_rowsA));
+  TRY(ws_typed(c, "bt_rowsB", (size_t)nrows, &d_rowsB));
+  TRY(ws_typed(c, "bt_cnt", (size_t)N, &d_cnt));
+  TRY(ws_typed(c, "bt_y", (size_t)N, &d_y));
+  TRY(ws_typed(c, "bt_sub", (size_t)Fr, &d_sub));
+  TRY(h2d(c, d_rowsA, rows.data(), rows.size()));
+  TRY(h2d(c, d_cnt, bp->counts, (size_t)N));
+  TRY(h2d(c, d_y, labels, (size_t)N));
+  TRY(h2d(c, d_sub, sub.data(), sub.size()));
+
+  // ---- findSplits: value counts of the subbag or of its split-finding sample
+  std::vector<int64_t> vcoff(Fr + 1, 0);
+  for (int fl = 0; fl < Fr; fl++) vcoff[fl + 1] = vcoff[fl] + (int64_t)ds->dict[sub[fl]].size();
+  const int64_t vc_total = vcoff[Fr];
+  int64_t* d_vcoff;
+  uint32_t* d_vc;
+  TRY(ws_typed(c, "bt_vcoff", vcoff.size(), &d_vcoff));
+  TRY(ws_typed(c, "bt_vc", (size_t)std::max<int64_t>(vc_total, 1), &d_vc));
+  TRY(h2d(c, d_vcoff, vcoff.data(), vcoff.size()));
+  HIP_TRY(hipMemsetAsync(d_vc, 0, (size_t)std::max<int64_t>(vc_total, 1) * 4, c->stream));
+  const int64_t mpb = std::min<int64_t>(tp.max_bins, n_items);
+  const int64_t required = std::max<int64_t>(mpb * mpb, 10000);
+  int64_t nsamp = n_items;
+  if (required < n_items) {
+    // RDD.sample(false, required / n, XORShiftRandom(seed).nextInt()) over the subbag
+    const double frac = (double)required / (double)n_items;
+    const int P = (int)poff.size() - 1;
+    uint64_t js = ((uint64_t)(int64_t)HostXS(tp.seed).next(32) ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1);
+    auto jnext = [&]() {
+      js = (js * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+      return (int64_t)(int32_t)(uint32_t)(js >> 16);
+    };
+    std::vector<uint64_t> pst(P);
+    for (int q = 0; q < P; q++) {
+      const int64_t hi = jnext(), lo = jnext();
+      pst[q] = h_hash_seed((int64_t)((uint64_t)hi << 32) + lo);
+    }
+    const int32_t rep0 = 0, frs = Fr;
+    const double fl2[2] = {frac, std::log1p(-frac)};
+    int32_t *d_reps, *d_Fr;
+    double* d_frac;
+    uint64_t* d_pst;
+    int64_t* d_spoff;
+    TRY(ws_typed(c, "ss_reps", 1, &d_reps));
+    TRY(ws_typed(c, "bt_Fr", 1, &d_Fr));
+    TRY(ws_typed(c, "ss_frac", 2, &d_frac));
+    TRY(ws_typed(c, "ss_pst", pst.size(), &d_pst));
+    TRY(ws_typed(c, "ss_poff", poff.size(), &d_spoff));
+    TRY(h2d(c, d_reps, &rep0, 1));
+    TRY(h2d(c, d_Fr, &frs, 1));
+    TRY(h2d(c, d_frac, fl2, 2));
+    TRY(h2d(c, d_pst, pst.data(), pst.size()));
+    TRY(h2d(c, d_spoff, poff.data(), poff.size()));
+    const int64_t cap = required + 8 * (int64_t)std::ceil(std::sqrt((double)required)) + 1024;
+    uint32_t *d_srows, *d_snr;
+    uint16_t* d_gsums;
+    TRY(ws_typed(c, "ss_rows", (size_t)cap, &d_srows));
+    TRY(ws_typed(c, "ss_nrows", 1, &d_snr));
+    TRY(ws_typed(c, "ss_gsums", (size_t)split_sample_groups(N), &d_gsums));
+    HIP_TRY(hipMemsetAsync(d_snr, 0, 4, c->stream));
+    launch_split_sample(c->stream, d_cnt, N, 1, d_spoff, P, d_reps, 1, d_pst, d_frac, d_gsums,
+                        d_srows, cap, d_snr);
+    HIP_TRY(hipGetLastError());
+    launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, 1, ds->d_codes, ds->code_bytes,
+                           ds->S, d_sub, d_Fr, Fr, d_vcoff, d_vc,
+                           vc_total <= 16384 ? (int)vc_total : 0);
+    HIP_TRY(hipGetLastError());
+    uint32_t snr = 0;
+    TRY(d2h(c, &snr, d_snr, 1));
+    if ((int64_t)snr > cap) return fail(SBAG_EDEVICE, "split-finding sample exceeds its capacity");
+    nsamp = (int64_t)(int32_t)(frac * (double)n_items);  // (fraction * numExamples).toInt
+  } else {
+    launch_bt_valuecount(c->stream, d_rowsA, nrows, d_cnt, ds->d_codes, ds->code_bytes, ds->S,
+                         d_sub, Fr, d_vcoff, d_vc);
+    HIP_TRY(hipGetLastError());
+  }
+  std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1));
+  TRY(d2h(c, vc.data(), d_vc, vc.size()));
+  std::vector<std::vector<double>> thr(Fr);
+  std::vector<int> nsplits(Fr);
+  std::vector<uint8_t> lut((size_t)std::max<int64_t>(vc_total, 1), 0);
+  int NB = 1;
+  for (int fl = 0; fl < Fr; fl++) {
+    const int g = sub[fl];
+    nsplits[fl] = find_splits(ds->dict[g], vc.data() + vcoff[fl], ds->zero_code[g], n_items, nsamp,
+                              tp.max_bins, thr[fl]);
+    NB = std::max(NB, nsplits[fl] + 1);
+    // TreePoint.findBin: #thresholds < value
+    for (size_t k = 0; k < ds->dict[g].size(); k++)
+      lut[vcoff[fl] + (int64_t)k] = (uint8_t)(std::lower_bound(thr[fl].begin(), thr[fl].end(),
+                                                               ds->dict[g][k]) -
+                                              thr[fl].begin());
+  }
+  uint8_t* d_lut;
+  TRY(ws_typed(c, "bt_lut", lut.size(), &d_lut));
+  TRY(h2d(c, d_lut, lut.data(), lut.size()));
+
+  // ---- level-wise growth (RandomForest.run, numTrees = 1, featureSubsetStrategy "all")
+  std::vector<BtNode> nodes(1);
+  struct Seg {
+    int node;
+    int64_t a, b;
+  };
+  std::vector<Seg> level_nodes{{0, 0, nrows}};
+  for (int level = 0; level <= D && !level_nodes.empty(); level++) {
+    const int A = (int)level_nodes.size();
+    std::vector<int64_t> seg(2 * (size_t)A);
+    for (int q = 0; q < A; q++) {
+      seg[2 * q] = level_nodes[q].a;
+      seg[2 * q + 1] = level_nodes[q].b;
+    }
+    int64_t* d_seg;
+    double* d_hist;
+    const size_t hw = (size_t)A * (Fr + 1) * NB * 3;
+    TRY(ws_typed(c, "bt_seg", seg.size(), &d_seg));
+    TRY(ws_typed(c, "bt_hist", hw, &d_hist));
+    TRY(h2d(c, d_seg, seg.data(), seg.size()));
+    launch_bt_hist(c->stream, d_rowsA, d_seg, A, d_cnt, d_y, ds->d_codes, ds->code_bytes, ds->S,
+                   d_sub, Fr, d_lut, d_vcoff, NB, d_hist);
+    HIP_TRY(hipGetLastError());
+    std::vector<double> hist(hw);
+    TRY(d2h(c, hist.data(), d_hist, hw));
+    std::vector<BtSplitHost> splits;
+    std::vector<int> split_q;
+    for (int q = 0; q < A; q++) {
+      const int id = level_nodes[q].node;
+      double left[3], right[3];
+      int bf, bs;
+      bt_best_split(nodes[id], level, hist.data() + (size_t)q * (Fr + 1) * NB * 3, Fr, NB,
+                    nsplits, tp, left, right, &bf, &bs);
+      BtNode& node = nodes[id];
+      node.is_leaf = (node.gain <= 0) || (level == D);
+      if (node.is_leaf) continue;
+      node.has_split = true;
+      node.fl = bf;
+      node.s = bs;
+      node.thr = thr[bf][bs];
+      const bool child_leaf = (level + 1) == D;
+      BtNode L, R;
+      for (int i = 0; i < 3; i++) {
+        L.calc[i] = left[i];
+        R.calc[i] = right[i];
+      }
+      // LearningNode(child, isLeaf, ImpurityStats.getEmptyImpurityStats(calculator))
+      L.impurity = bt_impurity(L.calc);
+      R.impurity = bt_impurity(R.calc);
+      L.is_leaf = child_leaf || L.impurity == 0.0;
+      R.is_leaf = child_leaf || R.impurity == 0.0;
+      node.left = (int)nodes.size();
+      node.right = node.left + 1;
+      nodes.push_back(L);
+      nodes.push_back(R);
+      splits.push_back(BtSplitHost{level_nodes[q].a, level_nodes[q].b, vcoff[bf], sub[bf], bs});
+      split_q.push_back(q);
+    }
+    std::vector<Seg> next;
+    if (!splits.empty()) {
+      void* d_splits;
+      int64_t* d_nl;
+      TRY(ws_get(c, "bt_splits", splits.size() * sizeof(BtSplitHost), &d_splits));
+      TRY(ws_typed(c, "bt_nl", splits.size(), &d_nl));
+      TRY(h2d(c, (unsigned char*)d_splits, (const unsigned char*)splits.data(),
+              splits.size() * sizeof(BtSplitHost)));
+      launch_bt_partition(c->stream, d_rowsA, d_rowsB, d_splits, (int)splits.size(), ds->d_codes,
+                          ds->code_bytes, ds->S, d_lut, d_nl);
+      HIP_TRY(hipGetLastError());
+      std::vector<int64_t> nl(splits.size());
+      TRY(d2h(c, nl.data(), d_nl, nl.size()));
+      for (size_t k = 0; k < splits.size(); k++) {
+        const BtNode& pn = nodes[level_nodes[split_q[k]].node];
+        const int64_t a = splits[k].a, b = splits[k].b, m = a + nl[k];
+        if (!nodes[pn.left].is_leaf) next.push_back({pn.left, a, m});
+        if (!nodes[pn.right].is_leaf) next.push_back({pn.right, m, b});
+      }
+      std::swap(d_rowsA, d_rowsB);
+    }
+    level_nodes.swap(next);
+  }
+  auto forest = std::make_unique<sbag_forest>();
+  forest->impurity = SBAG_IMPURITY_VARIANCE;
+  HTree t;
+  t.sub = sub;
+  t.ns = 3;
+  bt_emit(nodes, 0, t);
+  forest->trees.push_back(std::move(t));
+  *out = forest.release();
+  return SBAG_OK;
+}
+
+}  // extern "C"

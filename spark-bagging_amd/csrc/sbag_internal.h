@@ -235,4 +235,22 @@ void launch_vc_global(hipStream_t st, const void* codes, int code_bytes, int32_t
                       const int32_t* d_Fr, int32_t Fmax, int R, const int64_t* d_off, uint32_t* vc);
 size_t hist_lds_limit();
 
+// ---- booster engine (GBM base-learner fits on fp64 labels, sbag_fit_booster)
+struct BtSplitHost {  // layout of the kernels' BtSplit
+  int64_t a, b;       // the node's rows [a, b) in the level's row list
+  int64_t lutoff;     // the split feature's code -> bin table
+  int32_t g, s;       // code column of the split feature, split bin
+};
+void launch_bt_valuecount(hipStream_t st, const uint32_t* rows, int64_t nrows, const uint8_t* cnt,
+                          const void* codes, int code_bytes, int32_t S, const int32_t* sub,
+                          int32_t Fr, const int64_t* vcoff, uint32_t* vc);
+int bt_lanes(int NB);
+void launch_bt_hist(hipStream_t st, const uint32_t* rows, const int64_t* seg, int nnodes,
+                    const uint8_t* cnt, const double* y, const void* codes, int code_bytes,
+                    int32_t S, const int32_t* sub, int32_t Fr, const uint8_t* lut,
+                    const int64_t* lutoff, int NB, double* hist);
+void launch_bt_partition(hipStream_t st, const uint32_t* in, uint32_t* out, const void* splits,
+                         int nsplit, const void* codes, int code_bytes, int32_t S,
+                         const uint8_t* lut, int64_t* nleft);
+
 }  // namespace sbag

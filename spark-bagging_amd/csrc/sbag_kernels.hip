@@ -3347,4 +3347,167 @@ void launch_aggregate(hipStream_t st, const void* votes, int vote_bytes, int K, 
                        gcnt_rows);
 }
 
+// ======================================================================
+// Booster engine (GBMRegressor's base-learner fits, ml/regression/GBMRegressor.scala:
+// 302-319): one DecisionTreeRegressor per boosting iteration on fp64 pseudo-residual
+// labels.  Spark sums a node's (feature, bin) statistics in fp64, one row at a time in
+// row order (DTStatsAggregator.update, each exploded copy of a row separately), so the
+// sums depend on that order: these kernels keep every node's rows in row order (a
+// stable partition) and give every (node, feature) cell chain to one lane.
+// ======================================================================
+__device__ __forceinline__ uint32_t bt_code(const void* codes, int code_bytes, int64_t at) {
+  return code_bytes == 1 ? (uint32_t)((const uint8_t*)codes)[at]
+                         : (code_bytes == 2 ? (uint32_t)((const uint16_t*)codes)[at]
+                                            : ((const uint32_t*)codes)[at]);
+}
+
+// value counts of the subbag: vc[vcoff[fl] + code] += count for every in-bag row
+__global__ void k_bt_valuecount(const uint32_t* __restrict__ rows, int64_t nrows,
+                                const uint8_t* __restrict__ cnt, const void* __restrict__ codes,
+                                int code_bytes, int32_t S, const int32_t* __restrict__ sub,
+                                int32_t Fr, const int64_t* __restrict__ vcoff,
+                                uint32_t* __restrict__ vc) {
+  const int64_t total = nrows * Fr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i / Fr;
+    const int fl = (int)(i - k * Fr);
+    const uint32_t r = rows[k];
+    const uint32_t code = bt_code(codes, code_bytes, (int64_t)r * S + sub[fl]);
+    atomicAdd(&vc[vcoff[fl] + code], (uint32_t)cnt[r]);
+  }
+}
+
+// Histogram of one level: workgroup (node q, feature chunk), lane = feature fl.  The
+// lane walks the node's rows in row order and adds count, label, label^2 to its bin in
+// LDS (count times: the reference's explode), exactly DTStatsAggregator.update's fp64
+// sequence for that (feature, bin).  fl == Fr is the node's total (its parent stats,
+// one bin).  hist: [q][Fr + 1][NB][3] fp64.
+__global__ __launch_bounds__(64) void k_bt_hist(const uint32_t* __restrict__ rows,
+                                                const int64_t* __restrict__ seg, /*[q][2]*/
+                                                const uint8_t* __restrict__ cnt,
+                                                const double* __restrict__ y,
+                                                const void* __restrict__ codes, int code_bytes,
+                                                int32_t S, const int32_t* __restrict__ sub,
+                                                int32_t Fr, const uint8_t* __restrict__ lut,
+                                                const int64_t* __restrict__ lutoff, int NB, int FL,
+                                                double* __restrict__ hist) {
+  extern __shared__ double acc[];  // [NB * 3][FL]
+  const int lane = threadIdx.x;
+  const int q = blockIdx.x;
+  const int fl = blockIdx.y * FL + lane;
+  const bool on = lane < FL && fl <= Fr;
+  for (int k = lane; k < NB * 3 * FL; k += 64) acc[k] = 0.0;
+  __syncthreads();
+  if (on) {
+    const int64_t a = seg[2 * q], b = seg[2 * q + 1];
+    const bool total = fl == Fr;
+    const int g = total ? 0 : sub[fl];
+    const uint8_t* lt = total ? nullptr : lut + lutoff[fl];
+    for (int64_t i = a; i < b; i++) {
+      const uint32_t r = rows[i];
+      const int c = cnt[r];
+      const double v = y[r];
+      const double w = 1.0 * v;  // instanceWeight * label
+      const double w2 = w * v;   // instanceWeight * label * label
+      const int bin = total ? 0 : lt[bt_code(codes, code_bytes, (int64_t)r * S + g)];
+      double* cell = acc + (size_t)bin * 3 * FL + lane;
+      double s0 = cell[0], s1 = cell[FL], s2 = cell[2 * FL];
+      for (int k = 0; k < c; k++) {
+        s0 += 1.0;
+        s1 += w;
+        s2 += w2;
+      }
+      cell[0] = s0;
+      cell[FL] = s1;
+      cell[2 * FL] = s2;
+    }
+    double* out = hist + ((int64_t)q * (Fr + 1) + fl) * NB * 3;
+    const int nb = total ? 1 : NB;
+    for (int k = 0; k < nb; k++) {
+      out[3 * k] = acc[(size_t)k * 3 * FL + lane];
+      out[3 * k + 1] = acc[(size_t)k * 3 * FL + FL + lane];
+      out[3 * k + 2] = acc[(size_t)k * 3 * FL + 2 * FL + lane];
+    }
+  }
+}
+
+// Stable partition of split nodes' rows: one wave per node; left rows (bin <= s, Spark's
+// ContinuousSplit.shouldGoLeft on the binned feature) keep their row order at the front
+// of the node's range, right rows after them.  nleft[q] receives the left row count.
+struct BtSplit {
+  int64_t a, b;
+  int64_t lutoff;
+  int32_t g, s;
+};
+__global__ __launch_bounds__(64) void k_bt_partition(const uint32_t* __restrict__ in,
+                                                     uint32_t* __restrict__ out,
+                                                     const BtSplit* __restrict__ sp,
+                                                     const void* __restrict__ codes, int code_bytes,
+                                                     int32_t S, const uint8_t* __restrict__ lut,
+                                                     int64_t* __restrict__ nleft) {
+  const BtSplit p = sp[blockIdx.x];
+  const int lane = threadIdx.x;
+  const uint8_t* lt = lut + p.lutoff;
+  int64_t nl = 0;
+  for (int64_t i0 = p.a; i0 < p.b; i0 += 64) {
+    const int64_t i = i0 + lane;
+    bool left = false;
+    if (i < p.b) left = lt[bt_code(codes, code_bytes, (int64_t)in[i] * S + p.g)] <= p.s;
+    nl += __popcll(__ballot(left));
+  }
+  int64_t lpos = p.a, rpos = p.a + nl;
+  for (int64_t i0 = p.a; i0 < p.b; i0 += 64) {
+    const int64_t i = i0 + lane;
+    const bool valid = i < p.b;
+    uint32_t r = 0;
+    bool left = false;
+    if (valid) {
+      r = in[i];
+      left = lt[bt_code(codes, code_bytes, (int64_t)r * S + p.g)] <= p.s;
+    }
+    const uint64_t ml = __ballot(valid && left), mr = __ballot(valid && !left);
+    const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
+    const uint32_t rank_r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mr >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mr, 0u));
+    if (valid) out[left ? lpos + rank_l : rpos + rank_r] = r;
+    lpos += __popcll(ml);
+    rpos += __popcll(mr);
+  }
+  if (lane == 0) nleft[blockIdx.x] = nl;
+}
+
+void launch_bt_valuecount(hipStream_t st, const uint32_t* rows, int64_t nrows, const uint8_t* cnt,
+                          const void* codes, int code_bytes, int32_t S, const int32_t* sub,
+                          int32_t Fr, const int64_t* vcoff, uint32_t* vc) {
+  const int64_t total = nrows * Fr;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (blocks > 0)
+    hipLaunchKernelGGL(k_bt_valuecount, dim3(blocks), dim3(256), 0, st, rows, nrows, cnt, codes,
+                       code_bytes, S, sub, Fr, vcoff, vc);
+}
+
+int bt_lanes(int NB) {  // features per workgroup: NB * 3 * FL doubles in 64 KB of LDS
+  return std::max(1, std::min(64, (int)(65536 / ((size_t)NB * 3 * 8))));
+}
+
+void launch_bt_hist(hipStream_t st, const uint32_t* rows, const int64_t* seg, int nnodes,
+                    const uint8_t* cnt, const double* y, const void* codes, int code_bytes,
+                    int32_t S, const int32_t* sub, int32_t Fr, const uint8_t* lut,
+                    const int64_t* lutoff, int NB, double* hist) {
+  const int FL = bt_lanes(NB);
+  const size_t lds = (size_t)NB * 3 * FL * 8;
+  set_max_lds((const void*)k_bt_hist, 64 * 1024);
+  hipLaunchKernelGGL(k_bt_hist, dim3(nnodes, (Fr + 1 + FL - 1) / FL), dim3(64), lds, st, rows, seg,
+                     cnt, y, codes, code_bytes, S, sub, Fr, lut, lutoff, NB, FL, hist);
+}
+
+void launch_bt_partition(hipStream_t st, const uint32_t* in, uint32_t* out, const void* splits,
+                         int nsplit, const void* codes, int code_bytes, int32_t S,
+                         const uint8_t* lut, int64_t* nleft) {
+  hipLaunchKernelGGL(k_bt_partition, dim3(nsplit), dim3(64), 0, st, in, out,
+                     (const BtSplit*)splits, codes, code_bytes, S, lut, nleft);
+}
+
 }  // namespace sbag

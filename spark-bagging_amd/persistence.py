@@ -219,3 +219,14 @@ def write_subspace(path, subspace):
 
 def read_subspace(path):
     return [int(x) for x in json.loads(_read_lines(path)[0])["subspace"]]
+
+
+# ------------------------------------------------------------------ one-row JSON data dirs
+def write_json_row(path, row):
+    """sparkSession.createDataFrame(Seq(data)).repartition(1).write.json(path): one JSON
+    line (GBMRegressionModelWriter's Data(weight, subspace, const), GBMRegressor.scala:551-556)."""
+    _write_part(path, [json.dumps(row, separators=(",", ":"))], suffix=".json")
+
+
+def read_json_row(path):
+    return json.loads(_read_lines(path)[0])

@@ -59,6 +59,7 @@ def test_null_arguments_are_rejected():
     lib = nat.lib()
     assert lib.sbag_subspace(1.0, 4, 0, None, None) == nat.SBAG_EINVAL
     assert lib.sbag_fit(None, None, None, None) == nat.SBAG_EINVAL
+    assert lib.sbag_fit_booster(None, None, None, None, None) == nat.SBAG_EINVAL
     assert lib.sbag_forest_num_trees(None, None) == nat.SBAG_EINVAL
 
 
