@@ -347,3 +347,96 @@ def gbm_predict(weights, subspaces, trees, const, X):
     for p, w in zip(pt, weights):
         acc = acc + p * w
     return acc + const
+
+
+DEFAULT_SEED_GBM_CLASSIFIER = -1593632877  # "org.apache.spark.ml.classification.GBMClassifier".hashCode
+
+
+def _softmax_rows(res):
+    """exp(res) / breeze sum(exp(res)) (GBMClassificationModel.predictRaw,
+    ml/classification/GBMClassifier.scala:540-548); the class sum left to right."""
+    e = np.exp(res)
+    tot = np.zeros(res.shape[0])
+    for k in range(res.shape[1]):
+        tot = tot + e[:, k]
+    return e / tot[:, None]
+
+
+def gbm_classifier_fit(X, y, *, num_base_learners=10, learning_rate=1.0, replacement=False,
+                       sample_ratio=1.0, subspace_ratio=1.0, seed=DEFAULT_SEED_GBM_CLASSIFIER,
+                       tol=1e-3, num_round=5, max_depth=5, max_bins=32, min_instances_per_node=1,
+                       min_info_gain=0.0, dt_seed=None, validation=None, nthreads=None):
+    """GBMClassifier.train, loss "divergence", optimizedWeights = false
+    (ml/classification/GBMClassifier.scala:190-482): per iteration and class k, residuals
+    -grad(1{label == k}, softmax(res)_k) = 1{label == k} - p_k, one DecisionTreeRegressor
+    on extractSubBag(bag m), weight learningRate; res_k += tree * weight.  The recursion
+    (:441-462) keeps `seed` fixed and passes numTry as numRound; terminate on all K weights
+    (ml/boosting/GBMParams.scala:288-306).  Returns (numClasses, weights[m][k],
+    subspaces[m], trees[m][k])."""
+    X = np.ascontiguousarray(X, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    K = int(y.max()) + 1
+    vmask = np.zeros(len(y), bool) if validation is None else np.asarray(validation, bool)
+    with_validation = validation is not None
+    Xt, yt, Xv, yv = X[~vmask], y[~vmask], X[vmask], y[vmask]
+    Nt, F = Xt.shape
+    counts = bag(replacement, sample_ratio, 0, num_base_learners, seed, [0, Nt], Nt)
+    weights, subs, trees = [], [], []
+    res, resv = np.zeros((Nt, K)), np.zeros((len(yv), K))
+    it, error, num_try, nround = num_base_learners, _DOUBLE_MAX, 0, num_round
+    while it != 0:
+        m = num_base_learners - it
+        sub = subspace(subspace_ratio, F, seed)
+        prob = _softmax_rows(res)
+        ws, ts, p_tr, p_v = [], [], [], []
+        for k in range(K):
+            lab = np.where(yt == k, 1.0, 0.0)
+            r = -(-(lab - prob[:, k]))
+            f = fit(Xt, r, counts[m:m + 1], [sub], max_depth=max_depth, max_bins=max_bins,
+                    min_instances_per_node=min_instances_per_node, min_info_gain=min_info_gain,
+                    nthreads=nthreads, dt_seed=dt_seed)
+            p_tr.append(predict(f, Xt, per_tree=True)[1][0])
+            p_v.append(predict(f, Xv, per_tree=True)[1][0] if len(yv) else np.zeros(0))
+            ws.append(learning_rate * 1.0)
+            ts.append(f.tree(0))
+        for k in range(K):
+            res[:, k] = res[:, k] + p_tr[k] * ws[k]
+            resv[:, k] = resv[:, k] + p_v[k] * ws[k]
+        weights.append(ws)
+        subs.append(sub)
+        trees.append(ts)
+        if len(yv):
+            pv = _softmax_rows(resv)
+            verror = 0.0
+            for k in range(K):
+                lab = np.where(yv == k, 1.0, 0.0)
+                verror = verror + float(np.cumsum(-lab * np.log(pv[:, k]))[-1])
+        else:
+            verror = _DOUBLE_MAX
+        if all(w < tol * learning_rate for w in ws):
+            nxt = (0, 0.0, 1)
+        elif with_validation:
+            if verror < error * (1 - tol):
+                nxt = (it - 1, verror, 0)
+            elif num_try == nround - 1:
+                nxt = (0, 0.0, num_try + 1)
+            else:
+                nxt = (it - 1, error, num_try + 1)
+        else:
+            nxt = (it - 1, 0.0, 0)
+        nround = num_try
+        it, error, num_try = nxt
+    keep = len(trees) - num_try
+    return K, weights[:keep], subs[:keep], trees[:keep]
+
+
+def gbm_classifier_predict(K, weights, subspaces, trees, X):
+    """(softmax probabilities [N, K], predictions = first argmax)."""
+    X = np.ascontiguousarray(X, np.float64)
+    res = np.zeros((X.shape[0], K))
+    for ws, s, ts in zip(weights, subspaces, trees):
+        for k in range(K):
+            p = gbm_predict([1.0], [s], [ts[k]], 0.0, X)  # 0 + p * 1.0 + 0.0 == p
+            res[:, k] = res[:, k] + p * ws[k]
+    prob = _softmax_rows(res)
+    return prob, np.argmax(prob, axis=1).astype(np.float64)

@@ -12,4 +12,5 @@ from .libsvm import SparseRows, load_libsvm  # noqa: F401
 from .ml import (BaggingClassificationModel, BaggingClassifier, BaggingRegressionModel,  # noqa: F401
                  BaggingRegressor, DecisionTreeClassifier, DecisionTreeModel,
                  DecisionTreeRegressor, Frame, even_partitions, java_string_hash)
-from .gbm import GBMRegressionModel, GBMRegressor  # noqa: F401
+from .gbm import (GBMClassificationModel, GBMClassifier, GBMRegressionModel,  # noqa: F401
+                  GBMRegressor)

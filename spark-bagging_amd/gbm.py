@@ -403,3 +403,258 @@ class GBMRegressor(_GBMParams):
             model._values[k] = self.get(k)
         model._values["baseLearner"] = bl
         return model
+
+
+# ====================================================================== GBMClassifier
+def divergence_loss(y, p):
+    """GBMClassifierParams.lossFunction("divergence") (GBMClassifier.scala:77-81)."""
+    return -y * np.log(p)
+
+
+def divergence_grad(y, p):
+    """GBMClassifierParams.gradFunction("divergence") (GBMClassifier.scala:83-87)."""
+    return -(y - p)
+
+
+def softmax_rows(res):
+    """GBMClassificationModel.predictRaw's exp(res) / sum(exp(res)) per row
+    (GBMClassifier.scala:540-548): breeze's sum is a left-to-right loop over the classes."""
+    e = np.exp(res)
+    tot = np.zeros(res.shape[0])
+    for k in range(res.shape[1]):
+        tot = tot + e[:, k]
+    return e / tot[:, None]
+
+
+class GBMClassificationModel(_GBMParams):
+    """GBMClassificationModel (GBMClassifier.scala:519-637): weights[m][k], subspaces[m],
+    models[m][k]; predictRaw = softmax of the per-class weighted tree sums, prediction its
+    first argmax."""
+
+    _spark_class = "org.apache.spark.ml.classification.GBMClassificationModel"
+    _defaults = dict(_GBMParams._defaults, loss="divergence", rawPredictionCol="rawPrediction",
+                     parallelism=1,
+                     seed=java_string_hash("org.apache.spark.ml.classification.GBMClassifier"))
+    _validators = dict(_GBMParams._validators, loss=lambda x: str(x).lower() == "divergence")
+
+    def __init__(self, num_classes, weights, subspaces, models, uid=None):
+        super().__init__(uid)
+        self.numClasses = int(num_classes)
+        self.weights = [[float(w) for w in ws] for ws in weights]
+        self.subspaces = [np.asarray(s, np.int32) for s in subspaces]
+        self.models = [list(ms) for ms in models]
+        self._forest = None
+
+    @property
+    def numBaseModels(self):
+        return len(self.models)
+
+    def native_forest(self):
+        """All K * M trees, iteration-major (tree m * K + k)."""
+        if self._forest is None:
+            trees = [t.nodes for ms in self.models for t in ms]
+            subs = [s for s, ms in zip(self.subspaces, self.models) for _ in ms]
+            self._forest = nat.NativeForest.from_trees(trees, subs, nat.IMPURITY_VARIANCE)
+        return self._forest
+
+    def raw_sums(self, X, ctx):
+        """res[:, k] = sum over m (in order) of models[m][k].predict * weights[m][k]."""
+        res = np.zeros((X.shape[0], self.numClasses))
+        if not self.models:
+            return res
+        _, pt = nat.predict(ctx, self.native_forest(), X, nat.AGG_MEAN, per_tree=True)
+        K = self.numClasses
+        for m in range(len(self.models)):
+            for k in range(K):
+                res[:, k] = res[:, k] + pt[m * K + k] * self.weights[m][k]
+        return res
+
+    def predict_raw(self, dataset, device=0):
+        X, ctx = _rows_and_ctx(dataset, device)
+        return softmax_rows(self.raw_sums(X, ctx))
+
+    def transform(self, dataset, device=0):
+        """prediction = rawPrediction.argmax (ClassificationModel.raw2prediction)."""
+        return np.argmax(self.predict_raw(dataset, device), axis=1).astype(np.float64)
+
+    def predict(self, features):
+        return float(self.transform(np.asarray(features, np.float64)[None, :])[0])
+
+    def save(self, path):
+        """GBMClassificationModelWriter (GBMClassifier.scala:568-596): model-$k-$idx and
+        data-$k-$idx ({weight, subspace}), metadata with numClasses and numBaseModels."""
+        if os.path.exists(path):
+            raise nat.IllegalArgumentException(
+                nat.SBAG_EINVAL, f"Path {path} already exists. To overwrite it, please use "
+                                 "write.overwrite().save(path) for Scala and use "
+                                 "write().overwrite().save(path) for Java and Python.")
+        params = {k: v for k, v in self.extractParamMap().items()
+                  if k != "baseLearner" and v is not None}
+        defaults = {k: v for k, v in self._defaults.items() if v is not None and k != "baseLearner"}
+        sp.save_metadata(path, self._spark_class, self.uid, params, defaults,
+                         {"numClasses": self.numClasses, "numBaseModels": self.numBaseModels})
+        bl = self.get("baseLearner") or DecisionTreeRegressor()
+        bl.save(os.path.join(path, "learner"))
+        tree_params = dict(bl._other_params, **bl._values)
+        for idx, (ms, ws, s) in enumerate(zip(self.models, self.weights, self.subspaces)):
+            for k, (m, w) in enumerate(zip(ms, ws)):
+                mp = os.path.join(path, f"model-{k}-{idx}")
+                sp.save_metadata(mp, bl._spark_model_class, bl.uid, tree_params,
+                                 bl._spark_defaults, {"numFeatures": int(len(s))})
+                sp.write_tree_data(mp, m.nodes, m.stats)
+                sp.write_json_row(os.path.join(path, f"data-{k}-{idx}"),
+                                  {"weight": w, "subspace": [int(x) for x in s]})
+
+    @classmethod
+    def load(cls, path):
+        meta = sp.load_metadata(path, cls._spark_class)
+        bl = _DecisionTreeEstimator.load(os.path.join(path, "learner"))
+        K, M = int(meta["numClasses"]), int(meta["numBaseModels"])
+        models, weights, subs = [], [], []
+        for idx in range(M):
+            ms, ws = [], []
+            for k in range(K):
+                nodes, stats = sp.read_tree_data(os.path.join(path, f"model-{k}-{idx}"))
+                ms.append(DecisionTreeModel(nodes, stats, nat.IMPURITY_VARIANCE))
+                row = sp.read_json_row(os.path.join(path, f"data-{k}-{idx}"))
+                ws.append(float(row["weight"]))
+                if k == 0:
+                    subs.append(np.asarray(row["subspace"], np.int32))
+            models.append(ms)
+            weights.append(ws)
+        m = cls(K, weights, subs, models, uid=meta["uid"])
+        for k, v in meta["paramMap"].items():
+            if k in m._defaults:
+                m._values[k] = v
+        m._values["baseLearner"] = bl
+        return m
+
+
+def _rows_and_ctx(dataset, device):
+    if isinstance(dataset, nat.DeviceDataset):
+        return dataset.features(), dataset.ctx
+    X = dataset.features if isinstance(dataset, Frame) else dataset
+    if is_sparse(X):
+        X = X.toarray()
+    X = np.asarray(X, np.float64)
+    if X.ndim == 1:
+        X = X[None, :]
+    return X, nat.default_context(device)
+
+
+class GBMClassifier(GBMRegressor):
+    """GBMClassifier (GBMClassifier.scala:122-486): one DecisionTreeRegressor per class and
+    iteration on the residuals of the one-vs-rest labels against the softmax of the current
+    model.  Reproduced as the reference runs, including two quirks of its recursion
+    (GBMClassifier.scala:441-462): it passes `numTry` where `numRound` goes, and the same
+    `seed` every iteration (so every iteration draws the same subspace)."""
+
+    _spark_class = "org.apache.spark.ml.classification.GBMClassifier"
+    _defaults = GBMClassificationModel._defaults
+    _validators = GBMClassificationModel._validators
+
+    def setLoss(self, v):
+        return self.set("loss", v)
+
+    def setParallelism(self, v):
+        return self.set("parallelism", int(v))
+
+    def _train(self, dataset, validation):
+        bl = self.get("baseLearner") or DecisionTreeRegressor()
+        if self.get("weightCol"):
+            import warnings
+            warnings.warn(f"weightCol is ignored, as it is not supported by {type(bl).__name__} now.")
+        if self.getOptimizedWeights():
+            raise nat.SparkException(
+                nat.SBAG_EUNSUPPORTED, "optimizedWeights = true (breeze LBFGS-B line search of "
+                                       "GBMParams.findOptimizedWeight) is not reproduced")
+        frame = dataset if isinstance(dataset, Frame) else Frame(*dataset)
+        X = frame.features.toarray() if is_sparse(frame.features) else np.asarray(frame.features)
+        X = np.asarray(X, np.float64)
+        y = frame.label
+        N, F = X.shape
+        K = int(y.max()) + 1 if N else 0  # computeNumClasses: max label + 1
+        bad = ~((y == np.floor(y)) & (y >= 0) & (y < K))
+        if bad.any():
+            raise nat.IllegalArgumentException(
+                nat.SBAG_EINVAL, f"Classifier was given dataset with invalid label {y[bad][0]}.  "
+                                 f"Labels must be integers in range [0, {K}).")
+        with_validation = bool(self.get("validationIndicatorCol"))
+        vmask = np.zeros(N, bool)
+        if with_validation:
+            if validation is None:
+                raise nat.IllegalArgumentException(
+                    nat.SBAG_EINVAL, "validationIndicatorCol is set but no indicator was given")
+            vmask = np.asarray(validation, bool)
+        part = frame.partition_offsets or [0, N]
+        tpart = [0] + [int((~vmask[part[p]:part[p + 1]]).sum()) for p in range(len(part) - 1)]
+        tpart = list(np.cumsum(tpart))
+        tr = ~vmask
+        Xt, yt, Xv, yv = X[tr], y[tr], X[vmask], y[vmask]
+        Nt = len(yt)
+        L = self.getNumBaseLearners()
+        lr = self.getLearningRate()
+        ctx = nat.default_context(0)
+        ds = nat.DeviceDataset.from_numpy(Xt, yt, ctx)
+        try:
+            counts = nat.sample(ctx, self.getReplacement(), self.getSampleRatio(), self.getSeed(),
+                                0, L, Nt, tpart if len(tpart) > 2 else None)
+            weights, subspaces, models = [], [], []
+            res = np.zeros((Nt, K))
+            resv = np.zeros((len(yv), K))
+            it, error, num_try = L, DOUBLE_MAX, 0
+            num_round, seed = self.getNumRound(), self.getSeed()
+            while it != 0:
+                m = L - it
+                sub = nat.subspace(self.getSubspaceRatio(), F, seed)
+                if len(sub) == 0:
+                    raise nat.IllegalArgumentException(
+                        nat.SBAG_EINVAL, "requirement failed: VectorSlicer requires that at least "
+                                         "one feature be selected.")
+                prob = softmax_rows(res)
+                ws, ms, preds, predv = [], [], [], []
+                for k in range(K):  # the reference's per-class Futures, joined in class order
+                    relabeled = np.where(yt == k, 1.0, 0.0)
+                    residual = -divergence_grad(relabeled, prob[:, k])
+                    f = nat.fit_booster(ctx, ds, residual, counts[m], sub,
+                                        partition_offsets=tpart if len(tpart) > 2 else None,
+                                        max_depth=bl.getMaxDepth(), max_bins=bl.getMaxBins(),
+                                        min_instances_per_node=bl.getMinInstancesPerNode(),
+                                        min_info_gain=bl.getMinInfoGain(), tree_seed=bl.getSeed())
+                    try:
+                        nodes, stats = f.tree(0)
+                        preds.append(nat.predict_dataset(ctx, f, ds, nat.AGG_MEAN))
+                        predv.append(nat.predict(ctx, f, Xv, nat.AGG_MEAN) if len(yv) else np.zeros(0))
+                    finally:
+                        f.free()
+                    ws.append(lr * 1.0)
+                    ms.append(DecisionTreeModel(nodes, stats, nat.IMPURITY_VARIANCE))
+                weights.append(ws)
+                subspaces.append(sub)
+                models.append(ms)
+                for k in range(K):
+                    res[:, k] = res[:, k] + preds[k] * ws[k]
+                    resv[:, k] = resv[:, k] + predv[k] * ws[k]
+                if len(yv):  # evaluateOnValidation: per class SQL sum, then Array.sum
+                    pv = softmax_rows(resv)
+                    verror = 0.0
+                    for k in range(K):
+                        verror = verror + seq_sum(divergence_loss(np.where(yv == k, 1.0, 0.0), pv[:, k]))
+                else:
+                    verror = DOUBLE_MAX
+                # GBMParams.terminate(weights: Array[Double], ...)
+                if all(w < self.getTol() * lr for w in ws):
+                    nxt = (0, 0.0, 1)
+                else:
+                    nxt = terminate_val(with_validation, error, verror, self.getTol(), num_round,
+                                        num_try, it)
+                num_round = num_try  # the recursion passes numTry as numRound
+                it, error, num_try = nxt
+            keep = len(models) - num_try
+        finally:
+            ds.free()
+        model = GBMClassificationModel(K, weights[:keep], subspaces[:keep], models[:keep])
+        for k in self._defaults:
+            model._values[k] = self.get(k)
+        model._values["baseLearner"] = bl
+        return model

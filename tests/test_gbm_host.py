@@ -88,3 +88,21 @@ def test_oracle_gbm_small_cpu():
     w, subs, trees, const = oracle.gbm_regressor_fit(X, y, num_base_learners=2, max_depth=5)
     assert w == [1.0, 1.0] and const == 0.0
     np.testing.assert_array_equal(oracle.gbm_predict(w, subs, trees, const, X), y)
+
+
+def test_classifier_defaults_and_validation():
+    est = sb.GBMClassifier()
+    assert est.getLoss() == "divergence"
+    assert est.getSeed() == oracle.DEFAULT_SEED_GBM_CLASSIFIER
+    with pytest.raises(sb.IllegalArgumentException):
+        est.setLoss("squared")  # GBMClassifierParams.supportedLossTypes = divergence only
+    X = np.zeros((4, 2))
+    with pytest.raises(sb.IllegalArgumentException):  # validateLabel: integers in [0, K)
+        est.fit((X, np.array([0.0, 1.0, 1.5, 2.0])))
+
+
+def test_softmax_class_sum_left_to_right():
+    res = np.array([[700.0, 0.0, -700.0], [1.0, 2.0, 3.0]])
+    e = np.exp(res)
+    np.testing.assert_array_equal(gbm.softmax_rows(res), e / (((0.0 + e[:, 0]) + e[:, 1]) + e[:, 2])[:, None])
+    np.testing.assert_array_equal(gbm.softmax_rows(res), oracle._softmax_rows(res))

@@ -158,3 +158,62 @@ def test_gbm_errors(ctx, cpusmall):
             nat.fit_booster(ctx, ds, y, np.zeros(len(y), np.uint8), np.arange(3, dtype=np.int32))
         finally:
             ds.free()
+
+
+@pytest.fixture(scope="module")
+def vehicle():
+    X, y = sb.load_libsvm(os.path.join(DATA, "vehicle.svm"))
+    return np.asarray(X, np.float64), y
+
+
+@pytest.mark.parametrize("lr,repl,ratio,sratio", [(0.5, True, 1.0, 0.7), (1.0, False, 0.8, 1.0)])
+def test_gbm_classifier_vehicle_bit_exact(ctx, vehicle, tmp_path, lr, repl, ratio, sratio):
+    """GBMClassifier (GBMClassifier.scala:190-482) on vehicle (classes 1-4, class 0 empty):
+    per iteration one booster per class on 1{label == k} - softmax_k; every booster, weight
+    and subspace bit-exact, probabilities and votes equal to the oracle's; save / load."""
+    X, y = vehicle
+    L = 6
+    est = sb.GBMClassifier().setBaseLearner(sb.DecisionTreeRegressor().setMaxDepth(4))
+    model = est.fit(sb.Frame(X, y), params={"numBaseLearners": L, "learningRate": lr,
+                                            "replacement": repl, "sampleRatio": ratio,
+                                            "subspaceRatio": sratio})
+    K, w, subs, trees = oracle.gbm_classifier_fit(X, y, num_base_learners=L, learning_rate=lr,
+                                                  replacement=repl, sample_ratio=ratio,
+                                                  subspace_ratio=sratio, max_depth=4)
+    assert model.numClasses == K == 5
+    assert model.weights == w and len(model.models) == len(trees)
+    for m in range(len(trees)):
+        assert list(model.subspaces[m]) == list(subs[m])
+        for k in range(K):
+            nodes, stats = trees[m][k]
+            mn = model.models[m][k]
+            for f in ("left", "right", "feature", "threshold", "prediction", "impurity", "gain"):
+                assert (mn.nodes[f] == nodes[f]).all(), f"booster {m} class {k} field {f}"
+            assert (mn.stats == stats).all(), f"booster {m} class {k} stats"
+    prob, votes = oracle.gbm_classifier_predict(K, w, subs, trees, X)
+    np.testing.assert_array_equal(model.predict_raw(X), prob)
+    np.testing.assert_array_equal(model.transform(X), votes)
+    path = str(tmp_path / "gbmc")
+    model.save(path)
+    back = sb.GBMClassificationModel.load(path)
+    np.testing.assert_array_equal(back.transform(X), votes)
+
+
+def test_gbm_classifier_validation_quirks(ctx, vehicle):
+    """With a validation set the reference's recursion replaces numRound by numTry and keeps
+    the seed (GBMClassifier.scala:441-462); the mirror stops where the oracle does."""
+    X, y = vehicle
+    v = np.zeros(len(y), bool)
+    v[1::3] = True
+    est = (sb.GBMClassifier().setBaseLearner(sb.DecisionTreeRegressor().setMaxDepth(3))
+           .setNumBaseLearners(12).setLearningRate(0.8).setTol(0.02)
+           .setValidationIndicatorCol("validation"))
+    model = est.fit(sb.Frame(X, y), params={"replacement": True, "subspaceRatio": 0.6},
+                    validation=v)
+    K, w, subs, trees = oracle.gbm_classifier_fit(X, y, num_base_learners=12, learning_rate=0.8,
+                                                  tol=0.02, replacement=True, subspace_ratio=0.6,
+                                                  max_depth=3, validation=v)
+    assert model.weights == w
+    assert len({tuple(s) for s in model.subspaces}) == 1  # the same seed every iteration
+    np.testing.assert_array_equal(model.transform(X),
+                                  oracle.gbm_classifier_predict(K, w, subs, trees, X)[1])
