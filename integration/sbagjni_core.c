@@ -97,3 +97,48 @@ int sbagb_predict(int64_t ctx, int64_t forest, const double* X, int64_t n, int32
                   double* out) {
   return sbag_predict(CTX(ctx), FOREST(forest), X, n, f, agg, out, NULL);
 }
+
+int sbagb_dataset_create_csr(int64_t ctx, int64_t n, int32_t f, const int64_t* indptr,
+                             const int32_t* indices, const double* values, const double* y,
+                             int64_t* ds_out) {
+  sbag_dataset* ds = NULL;
+  const int st = sbag_dataset_create_csr(CTX(ctx), n, f, indptr, indices, values, y, &ds);
+  *ds_out = (int64_t)(intptr_t)ds;
+  return st;
+}
+
+int sbagb_sample(int64_t ctx, int replacement, double sample_ratio, int64_t seed,
+                 int32_t learner_begin, int32_t learner_end, const int64_t* partition_offsets,
+                 int32_t num_offsets, int64_t n, uint8_t* counts_out) {
+  sbag_sampler_params p;
+  p.replacement = replacement ? 1 : 0;
+  p.pad_ = 0;
+  p.sample_ratio = sample_ratio;
+  p.seed = seed;
+  p.learner_begin = learner_begin;
+  p.learner_end = learner_end;
+  return sbag_sample(CTX(ctx), &p, partition_offsets, num_offsets - 1, n, counts_out);
+}
+
+int sbagb_fit_booster(int64_t ctx, int64_t ds, const double* labels, const uint8_t* counts,
+                      const int32_t* subspace, int32_t subspace_len,
+                      const int64_t* partition_offsets, int32_t num_offsets, int32_t max_depth,
+                      int32_t max_bins, int32_t min_instances_per_node, double min_info_gain,
+                      int64_t tree_seed, int64_t* forest_out) {
+  sbag_booster_params p;
+  p.counts = counts;
+  p.subspace = subspace;
+  p.subspace_len = subspace_len;
+  p.num_partitions = num_offsets - 1;
+  p.partition_offsets = partition_offsets;
+  p.tree.max_depth = max_depth;
+  p.tree.max_bins = max_bins;
+  p.tree.min_instances_per_node = min_instances_per_node;
+  p.tree.impurity = SBAG_IMPURITY_VARIANCE;
+  p.tree.min_info_gain = min_info_gain;
+  p.tree.seed = tree_seed;
+  sbag_forest* f = NULL;
+  const int st = sbag_fit_booster(CTX(ctx), DS(ds), labels, &p, &f);
+  *forest_out = (int64_t)(intptr_t)f;
+  return st;
+}

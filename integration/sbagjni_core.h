@@ -55,6 +55,28 @@ int sbagb_forest_free(int64_t forest);
 int sbagb_predict(int64_t ctx, int64_t forest, const double* X, int64_t n, int32_t f, int32_t agg,
                   double* out);
 
+/* SbagNative.datasetCreateCsr(ctx, n, f, indptr: Array[Long], indices: Array[Int],
+ *                             values: Array[Double], y: Array[Double]): Long
+ * SparseVector rows, Spark semantics (absent entries are 0.0) -- sbag_dataset_create_csr */
+int sbagb_dataset_create_csr(int64_t ctx, int64_t n, int32_t f, const int64_t* indptr,
+                             const int32_t* indices, const double* values, const double* y,
+                             int64_t* ds_out);
+/* SbagNative.sample(ctx, replacement, sampleRatio, seed, learnerBegin, learnerEnd,
+ *                   partitionOffsets, n): Array[Byte] -- withBag's counts
+ * (bfunctions.bag, sql/bfunctions.scala:46-68), [learners x n] */
+int sbagb_sample(int64_t ctx, int replacement, double sample_ratio, int64_t seed,
+                 int32_t learner_begin, int32_t learner_end, const int64_t* partition_offsets,
+                 int32_t num_offsets, int64_t n, uint8_t* counts_out);
+/* SbagNative.fitBooster(ctx, ds, labels, counts, subspace, partitionOffsets, maxDepth,
+ *                       maxBins, minInstancesPerNode, minInfoGain, treeSeed): Long
+ * one GBM booster (GBMRegressor.scala:311-319): DecisionTreeRegressor on the subbag
+ * `counts` sliced to `subspace`, fp64 labels -- sbag_fit_booster */
+int sbagb_fit_booster(int64_t ctx, int64_t ds, const double* labels, const uint8_t* counts,
+                      const int32_t* subspace, int32_t subspace_len,
+                      const int64_t* partition_offsets, int32_t num_offsets, int32_t max_depth,
+                      int32_t max_bins, int32_t min_instances_per_node, double min_info_gain,
+                      int64_t tree_seed, int64_t* forest_out);
+
 #ifdef __cplusplus
 }
 #endif

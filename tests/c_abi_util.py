@@ -44,3 +44,35 @@ def run_driver(tmp_path, X, y, offsets, *, replacement, ratio, seed, lb, le, sub
         pos += 4 * sl
     pred = np.frombuffer(raw, np.float64, X.shape[0], pos)
     return p, 0, trees, subs, pred
+
+
+GBM_DRIVER = os.path.join(ROOT, "tests", "c", "gbm_driver")
+
+
+def run_gbm_driver(tmp_path, X, y, subspaces, *, L, lr, replacement, ratio, seed, depth, bins,
+                   tree_seed):
+    """tests/c/gbm_driver: GBMRegressor's loop in C over the shim core (squared loss)."""
+    X = np.ascontiguousarray(X, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    data, subs, out = tmp_path / "gdata.bin", tmp_path / "gsubs.bin", tmp_path / "gout.bin"
+    with open(data, "wb") as f:
+        f.write(struct.pack("<qq", X.shape[0], X.shape[1]) + X.tobytes() + y.tobytes())
+    with open(subs, "wb") as f:
+        for s in subspaces:
+            s = np.asarray(s, np.int32)
+            f.write(struct.pack("<i", len(s)) + s.tobytes())
+    args = [GBM_DRIVER, str(data), str(subs), str(out), str(L), repr(float(lr)),
+            str(int(replacement)), repr(float(ratio)), str(int(seed)), str(depth), str(bins),
+            str(int(tree_seed))]
+    p = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    raw = open(out, "rb").read() if os.path.exists(out) else b""
+    status = struct.unpack_from("<i", raw, 0)[0] if raw else None
+    if status != 0:
+        return p, status, None, None
+    pos, trees = 4, []
+    for _ in range(L):
+        nn = struct.unpack_from("<i", raw, pos)[0]
+        pos += 4
+        trees.append(np.frombuffer(raw, np.float64, nn * 8, pos).reshape(nn, 8))
+        pos += nn * 64
+    return p, 0, trees, np.frombuffer(raw, np.float64, X.shape[0], pos)

@@ -7,12 +7,13 @@ import subprocess
 import numpy as np
 import pytest
 
-from c_abi_util import DRIVER, run_driver
+from c_abi_util import DRIVER, GBM_DRIVER, run_driver
 
 
-def test_driver_is_built_and_links_libsbag():
-    assert os.path.exists(DRIVER), "run __graft_entry__.build()"
-    out = subprocess.run(["ldd", DRIVER], capture_output=True, text=True).stdout
+@pytest.mark.parametrize("driver", [DRIVER, GBM_DRIVER])
+def test_driver_is_built_and_links_libsbag(driver):
+    assert os.path.exists(driver), "run __graft_entry__.build()"
+    out = subprocess.run(["ldd", driver], capture_output=True, text=True).stdout
     assert "libsbag.so" in out and "not found" not in out
 
 

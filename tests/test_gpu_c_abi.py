@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle
-from c_abi_util import run_driver
+from c_abi_util import run_driver, run_gbm_driver
 from conftest import DATA
 
 import spark_bagging_amd as sb
@@ -111,3 +111,24 @@ def test_c_driver_under_host_asan(tmp_path):
         tree_seed=nat.DT_SEED_REGRESSOR, agg=nat.AGG_MEAN, driver=DRIVER_ASAN, env=env)
     assert p.returncode == 0 and st == 0, p.stdout + p.stderr[-3000:]
     assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr
+
+
+def test_c_gbm_driver_matches_oracle_gbm(tmp_path):
+    """GBMRegressor's boosting loop from plain C through the shim core (SbagNative.sample /
+    fitBooster / forestNodes / predict) against the oracle's
+    restatement of GBMRegressor.train: every booster and F(x) bit-exact."""
+    X, y = sb.load_libsvm(os.path.join(DATA, "cpusmall.svm"))
+    X = np.asarray(X, np.float64)
+    L, lr, seed = 5, 0.1, oracle.DEFAULT_SEED_GBM_REGRESSOR
+    w, subs, trees, const = oracle.gbm_regressor_fit(X, y, num_base_learners=L, learning_rate=lr,
+                                                     replacement=True, subspace_ratio=0.7,
+                                                     seed=seed, max_depth=4)
+    p, st, ctrees, pred = run_gbm_driver(tmp_path, X, y, subs, L=L, lr=lr, replacement=1,
+                                         ratio=1.0, seed=seed, depth=4, bins=32,
+                                         tree_seed=nat.DT_SEED_REGRESSOR)
+    assert st == 0, p.stdout + p.stderr
+    for m, (nodes, _) in enumerate(trees):
+        assert ctrees[m].shape[0] == len(nodes), f"booster {m}"
+        for k, f in enumerate(FIELDS):
+            assert (ctrees[m][:, k] == nodes[f].astype(np.float64)).all(), f"booster {m} {f}"
+    np.testing.assert_array_equal(pred, oracle.gbm_predict(w, subs, trees, const, X))
