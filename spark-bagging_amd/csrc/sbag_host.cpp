@@ -147,7 +147,7 @@ struct sbag_ctx {
   // a second stream and workspace on the same device: sbag_fit runs the two halves of a
   // learner range on the two contexts from two host threads, so one half's host work
   // (split bookkeeping between levels) overlaps the other half's kernels
-  sbag_ctx* twin = nullptr;
+  std::vector<sbag_ctx*> twins;
 };
 #define CTX_LOCK(c) std::lock_guard<std::recursive_mutex> ctx_lock_((c)->mu)
 
@@ -665,7 +665,7 @@ int sbag_ctx_create(int32_t device_ordinal, sbag_ctx** out) {
 int sbag_ctx_destroy(sbag_ctx* c) {
   if (!c) return SBAG_OK;
   { CTX_LOCK(c); }  // no call is in flight on it any more
-  if (c->twin) (void)sbag_ctx_destroy(c->twin);
+  for (sbag_ctx* t : c->twins) (void)sbag_ctx_destroy(t);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (auto& kv : c->ws)
@@ -1253,35 +1253,47 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   // other half's kernels run (C3: 150 -> 135 ms per fit).  Each context keeps its own
   // copy of the dataset-derived buffers (column copy, side-bit planes), so by default
   // only fits of up to 2^25 rows with at least 16 learners overlap; SBAG_OVERLAP=0/1
-  // forces it off / on.
+  // forces it off / on; SBAG_OVERLAP=k runs k parts (3 and 4 were slower on C3: 151, 152 ms).
   const char* ov = getenv("SBAG_OVERLAP");
-  const bool overlap = ov ? atoi(ov) > 0 : (le - lb >= 16 && ds->N >= (1 << 20) && ds->N <= (1 << 25));
-  if (!overlap || le - lb < 2) return fit_learners(c, ds, fp, out);
-  if (!c->twin) TRY(sbag_ctx_create(c->device, &c->twin));
-  const int mid = lb + (le - lb) / 2;
-  sbag_fit_params h1 = *fp, h2 = *fp;
-  h1.sampler.learner_end = mid;
-  h2.sampler.learner_begin = mid;
-  sbag_forest *a = nullptr, *b = nullptr;
-  int st2 = SBAG_OK;
-  std::string err2;
+  int parts = ov ? atoi(ov) : ((le - lb >= 16 && ds->N >= (1 << 20) && ds->N <= (1 << 25)) ? 2 : 0);
+  if (parts == 1) parts = 2;  // SBAG_OVERLAP=1: on, two parts
+  parts = std::min(parts, le - lb);
+  if (parts < 2) return fit_learners(c, ds, fp, out);
+  while ((int)c->twins.size() < parts - 1) {
+    sbag_ctx* t = nullptr;
+    TRY(sbag_ctx_create(c->device, &t));
+    c->twins.push_back(t);
+  }
+  std::vector<sbag_fit_params> hp(parts, *fp);
+  for (int k = 0; k < parts; k++) {
+    hp[k].sampler.learner_begin = lb + (int)((int64_t)(le - lb) * k / parts);
+    hp[k].sampler.learner_end = lb + (int)((int64_t)(le - lb) * (k + 1) / parts);
+  }
+  std::vector<sbag_forest*> fs(parts, nullptr);
+  std::vector<int> sts(parts, SBAG_OK);
+  std::vector<std::string> errs(parts);
   const auto t0 = std::chrono::steady_clock::now();
-  std::thread th([&] {
-    CTX_LOCK(c->twin);
-    (void)hipSetDevice(c->device);
-    st2 = fit_learners(c->twin, ds, &h2, &b);
-    if (st2 != SBAG_OK) err2 = g_err;  // g_err is thread-local
-  });
-  const int st1 = fit_learners(c, ds, &h1, &a);
-  th.join();
-  std::unique_ptr<sbag_forest> fa(a), fb(b);
-  if (st1 != SBAG_OK) return st1;
-  if (st2 != SBAG_OK) return fail(st2, err2);
-  merge_forests(fa.get(), fb.get());
-  // the halves ran concurrently: the fit took the wall time, not the sum
-  fa->timing.total_ms =
+  std::vector<std::thread> th;
+  for (int k = 1; k < parts; k++)
+    th.emplace_back([&, k] {
+      sbag_ctx* t = c->twins[k - 1];
+      CTX_LOCK(t);
+      (void)hipSetDevice(c->device);
+      sts[k] = fit_learners(t, ds, &hp[k], &fs[k]);
+      if (sts[k] != SBAG_OK) errs[k] = g_err;  // g_err is thread-local
+    });
+  sts[0] = fit_learners(c, ds, &hp[0], &fs[0]);
+  for (auto& t : th) t.join();
+  std::vector<std::unique_ptr<sbag_forest>> own;
+  for (auto* f : fs) own.emplace_back(f);
+  if (sts[0] != SBAG_OK) return sts[0];
+  for (int k = 1; k < parts; k++)
+    if (sts[k] != SBAG_OK) return fail(sts[k], errs[k]);
+  for (int k = 1; k < parts; k++) merge_forests(own[0].get(), own[k].get());
+  // the parts ran concurrently: the fit took the wall time, not the sum
+  own[0]->timing.total_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  *out = fa.release();
+  *out = own[0].release();
   return SBAG_OK;
 }
 
