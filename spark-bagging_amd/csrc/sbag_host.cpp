@@ -71,11 +71,16 @@ struct HostPool {
   bool stop = false;
   // host threads for node bookkeeping, thresholds, tree emission and ingest: 16 (the
   // CPU share of one GPU on an 8-GPU node) unless SBAG_HOST_THREADS says otherwise
+  // host threads per context: 16, or the process's share of the cores when torchrun
+  // starts one process per GPU (LOCAL_WORLD_SIZE) and sbag_fit runs two contexts each
   static int width() {
     static const int w = [] {
       const char* e = getenv("SBAG_HOST_THREADS");
+      if (e) return std::max(1, std::min(atoi(e), 1024));
       const int hw = std::max(1, (int)std::thread::hardware_concurrency());
-      return e ? std::max(1, std::min(atoi(e), 1024)) : std::min(16, hw);
+      const char* lw = getenv("LOCAL_WORLD_SIZE");
+      const int procs = lw ? std::max(1, atoi(lw)) : 1;
+      return std::max(2, std::min(16, hw / (2 * procs)));
     }();
     return w;
   }
