@@ -1255,12 +1255,13 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   const int lb = fp->sampler.learner_begin, le = fp->sampler.learner_end;
   // The two halves of the learner range on two streams from two threads: while one half's
   // host thread turns a level's split results into the next level's work lists, the
-  // other half's kernels run (C3: 150 -> 135 ms per fit).  Each context keeps its own
-  // copy of the dataset-derived buffers (column copy, side-bit planes), so by default
-  // only fits of up to 2^25 rows with at least 16 learners overlap; SBAG_OVERLAP=0/1
+  // other half's kernels run (C3: 150 -> 136 ms per fit, C5 shard 265 -> 238).  Each
+  // context keeps its own copy of the dataset-derived buffers (column copy, side-bit
+  // planes: C4's 100M x 256 would need 2 x 125 GB), so by default only fits of up to 2^26
+  // rows with at least 16 learners overlap; SBAG_OVERLAP=0/1
   // forces it off / on; SBAG_OVERLAP=k runs k parts (3 and 4 were slower on C3: 151, 152 ms).
   const char* ov = getenv("SBAG_OVERLAP");
-  int parts = ov ? atoi(ov) : ((le - lb >= 16 && ds->N >= (1 << 20) && ds->N <= (1 << 25)) ? 2 : 0);
+  int parts = ov ? atoi(ov) : ((le - lb >= 16 && ds->N >= (1 << 20) && ds->N <= (1 << 26)) ? 2 : 0);
   if (parts == 1) parts = 2;  // SBAG_OVERLAP=1: on, two parts
   parts = std::min(parts, le - lb);
   if (parts < 2) return fit_learners(c, ds, fp, out);
