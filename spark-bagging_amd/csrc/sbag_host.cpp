@@ -321,6 +321,14 @@ struct sbag_dataset {
   bool integral = false;                  // all labels integers >= 0 (classifiable)
   double* d_dict = nullptr;
   int64_t* d_dict_off = nullptr;
+  // Layouts derived from the codes alone, for fits whose bins are the codes: the
+  // column-major copy [cols_ncol][npad] and the side-bit planes [cols_ncol][planes_nsp][nw32]
+  // of k_partition.  Part of ingest: built by the first such fit, kept with the dataset.
+  std::mutex layout_mu;
+  uint8_t* d_cols = nullptr;
+  int32_t cols_ncol = 0;
+  uint32_t* d_planes = nullptr;
+  int32_t planes_nsp = 0;
 };
 
 static int32_t row_stride(int32_t F) {
@@ -1053,6 +1061,8 @@ int sbag_dataset_free(sbag_dataset* ds) {
   if (ds->d_labk) (void)hipFree(ds->d_labk);
   if (ds->d_dict) (void)hipFree(ds->d_dict);
   if (ds->d_dict_off) (void)hipFree(ds->d_dict_off);
+  if (ds->d_cols) (void)hipFree(ds->d_cols);
+  if (ds->d_planes) (void)hipFree(ds->d_planes);
   delete ds;
   return SBAG_OK;
 }
@@ -2045,22 +2055,50 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     const int Rc = bins_rstride ? R : 1;
     npad = (N + 63) / 64 * 64;
     cols_rstride = bins_rstride ? (int64_t)ncol * npad : 0;
-    uint8_t* d_c;
-    TRY(ws_typed(c, "cols", (size_t)Rc * ncol * npad, &d_c));
-    launch_transpose(c->stream, d_bins, N, S, ncol, d_c, npad, Rc, bins_rstride, cols_rstride);
-    HIP_TRY(hipGetLastError());
-    d_cols = d_c;
-    // side-bit planes (bin > s) of the shared bins for the partition's gather, when
-    // they fit in 8 GB (NB - 1 planes of N/8 bytes per column)
     plane_nw32 = (N + 31) / 32;
     plane_nsp = NB - 1;
-    if (bins_rstride == 0 && plane_nsp >= 1 &&
-        (double)ncol * plane_nsp * plane_nw32 * 4 <= 8.0 * (1ull << 30) && !getenv("SBAG_NO_PLANES")) {
-      uint32_t* d_pl;
-      TRY(ws_typed(c, "planes", (size_t)ncol * plane_nsp * plane_nw32, &d_pl));
-      launch_planes(c->stream, d_c, npad, ncol, plane_nsp, plane_nw32, d_pl);
+    // side-bit planes (bin > s) of the shared bins for the partition's gather, when
+    // they fit in 8 GB (NB - 1 planes of N/8 bytes per column)
+    auto planes_fit = [&](int nc, int nsp) {
+      return nsp >= 1 && (double)nc * nsp * plane_nw32 * 4 <= 8.0 * (1ull << 30) &&
+             !getenv("SBAG_NO_PLANES");
+    };
+    if (identity && !getenv("SBAG_NO_LAYOUT_CACHE")) {
+      // the codes are the bins: every column of every feature, once per dataset
+      std::lock_guard<std::mutex> lk(ds->layout_mu);
+      if (!ds->d_cols) {
+        const int nc = ds->F;
+        HIP_TRY(hipMalloc(&ds->d_cols, (size_t)nc * npad));
+        launch_transpose(c->stream, d_bins, N, S, nc, ds->d_cols, npad, 1, 0, 0);
+        HIP_TRY(hipGetLastError());
+        ds->cols_ncol = nc;
+        if (planes_fit(nc, plane_nsp)) {
+          HIP_TRY(hipMalloc(&ds->d_planes, (size_t)nc * plane_nsp * plane_nw32 * 4));
+          launch_planes(c->stream, ds->d_cols, npad, nc, plane_nsp, plane_nw32, ds->d_planes);
+          HIP_TRY(hipGetLastError());
+          ds->planes_nsp = plane_nsp;
+        }
+        // other contexts (the learner-part twins) read them without this stream's order
+        HIP_TRY(hipStreamSynchronize(c->stream));
+      }
+      d_cols = ds->d_cols;
+      if (ds->d_planes && ds->planes_nsp >= plane_nsp) {
+        d_planes = ds->d_planes;
+        plane_nsp = ds->planes_nsp;
+      }
+    } else {
+      uint8_t* d_c;
+      TRY(ws_typed(c, "cols", (size_t)Rc * ncol * npad, &d_c));
+      launch_transpose(c->stream, d_bins, N, S, ncol, d_c, npad, Rc, bins_rstride, cols_rstride);
       HIP_TRY(hipGetLastError());
-      d_planes = d_pl;
+      d_cols = d_c;
+      if (bins_rstride == 0 && planes_fit(ncol, plane_nsp)) {
+        uint32_t* d_pl;
+        TRY(ws_typed(c, "planes", (size_t)ncol * plane_nsp * plane_nw32, &d_pl));
+        launch_planes(c->stream, d_c, npad, ncol, plane_nsp, plane_nw32, d_pl);
+        HIP_TRY(hipGetLastError());
+        d_planes = d_pl;
+      }
     }
     tm.end(h);
   }
