@@ -15,6 +15,8 @@
 #include <cmath>
 #include <condition_variable>
 #include <functional>
+#include <array>
+#include <map>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
@@ -617,11 +619,14 @@ static int find_splits(const std::vector<double>& vals, const uint32_t* cnt, int
 struct EventTimer {
   hipStream_t st;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;  // category
+  std::vector<int> lv;  // tree level of each event (-1 before the level loop)
+  int level = -1;
   int begin(int cat) {
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
     (void)hipEventRecord(a, st);
     ev.push_back({cat, {a, b}});
+    lv.push_back(level);
     return (int)ev.size() - 1;
   }
   void end(int h) {
@@ -1517,6 +1522,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     for (int r = 0; r < R; r++) hist_work += act[r] ? 3.0 * N : 0.0;
   };
   int64_t hist_launches = 0;
+  static const bool trace = getenv("SBAG_LEVEL_TRACE") != nullptr;
+  int trace_level = -1;
   static const bool group_off = getenv("SBAG_NO_TILE_GROUPING") != nullptr;
   std::vector<std::pair<int64_t, int64_t>> gsegs;
   std::vector<ParentInfo> gpar;
@@ -1622,6 +1629,17 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     launch_hist(c->stream, ha, work.nwg, ntiles, mode, g.lds);
     HIP_TRY(hipGetLastError());
     tm.end(h);
+    if (trace) {
+      // SBAG_LEVEL_TRACE: one line per histogram launch (synchronizes; diagnostics only)
+      float ms = 0;
+      (void)hipEventSynchronize(tm.ev[h].second.second);
+      (void)hipEventElapsedTime(&ms, tm.ev[h].second.first, tm.ev[h].second.second);
+      int64_t ne = 0;
+      for (auto& sg : segs) ne += sg.second - sg.first;
+      fprintf(stderr, "[sbag] level %d cat %d mode %d grouped %d segs %zu entries %lld pieces %zu nwg %d ms %.3f\n",
+              trace_level, cat, mode, grouped ? 1 : 0, segs.size(), (long long)ne, work.pieces.size(),
+              work.nwg, ms);
+    }
     ha.ent_in = ent_saved;
     ha.grouped = 0;
     if (cat == T_HIST) {
@@ -2155,6 +2173,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     const int M = (int)slots.size();
     if (M == 0) break;
     levels++;
+    trace_level = level;
+    tm.level = level;
     hmark(7);
     // --- split search on the device
     std::vector<int32_t> h_slot_r(M);
@@ -2591,6 +2611,23 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   forest->nclasses = gini ? std::max(nclasses, (int)ds->kmax + 1) : 0;
   double cats[T_NCAT] = {0};
   tm.collect(cats, nullptr, -1);
+  if (trace) {
+    // per level and category: ms (categories as in enum T_*)
+    std::map<int, std::array<double, T_NCAT>> per;
+    for (size_t i = 0; i < tm.ev.size(); i++) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, tm.ev[i].second.first, tm.ev[i].second.second);
+      auto it = per.find(tm.lv[i]);
+      if (it == per.end()) it = per.emplace(tm.lv[i], std::array<double, T_NCAT>{}).first;
+      it->second[tm.ev[i].first] += ms;
+    }
+    for (auto& kv : per) {
+      fprintf(stderr, "[sbag] level %d ms: sample %.2f vc %.2f bin %.2f compact %.2f hist %.2f split %.2f "
+              "sub %.2f part %.2f fix %.2f\n", kv.first, kv.second[T_SAMPLE], kv.second[T_VC],
+              kv.second[T_BIN], kv.second[T_COMPACT], kv.second[T_HIST], kv.second[T_SPLIT],
+              kv.second[T_SUB], kv.second[T_PART], kv.second[T_FIX]);
+    }
+  }
   float total_ms = 0;
   (void)hipEventElapsedTime(&total_ms, ev_start, ev_stop);
   (void)hipEventDestroy(ev_start);

@@ -1384,19 +1384,34 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
   const int NB = A.NB, NS = A.NS, FPH = A.FPH;
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
   if (MODE == kHistGini) {
-    // class planes [0, nct) of the LDS hold classes [c0, c0 + nct)
+    // class planes [0, nct) of the LDS hold classes [c0, c0 + nct).  Lane q takes one
+    // (feature, bin): features fastest, so the LDS reads of a class plane hit distinct
+    // banks (planes and bin rows are multiples of 64 words apart), and the lane writes
+    // its nct classes -- contiguous in the global [f][b][NS] row -- as 16-byte stores
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
-    // features fastest: consecutive lanes read consecutive LDS words (class planes and
-    // bin rows are multiples of 64 words apart, so any other order serializes on a bank)
-    for (int q = tid; q < ftn * NB * nct; q += blockDim.x) {
-      const int f = q % ftn, b = (q / ftn) % NB, cl = q / (ftn * NB);
-      const uint32_t v = *(const uint32_t*)(smem + (size_t)cl * plane + ((size_t)b * FPH + f) * 4);
-      if (v) {
-        uint32_t* dst = &gh[((int64_t)(ft0 + f) * NB + b) * NS + c0 + cl];
-        if (store)
-          *dst = v;
-        else
-          atomicAdd(dst, v);
+    const bool vec = store && ((NS | c0) & 3) == 0;
+    for (int q = tid; q < ftn * NB; q += blockDim.x) {
+      const int f = q % ftn, b = q / ftn;
+      uint32_t* dst = &gh[((int64_t)(ft0 + f) * NB + b) * NS + c0];
+      const unsigned char* src = smem + ((size_t)b * FPH + f) * 4;
+      int cl = 0;
+      if (vec)
+        for (; cl + 4 <= nct; cl += 4) {
+          uint4 v;
+          v.x = *(const uint32_t*)(src + (size_t)cl * plane);
+          v.y = *(const uint32_t*)(src + (size_t)(cl + 1) * plane);
+          v.z = *(const uint32_t*)(src + (size_t)(cl + 2) * plane);
+          v.w = *(const uint32_t*)(src + (size_t)(cl + 3) * plane);
+          *(uint4*)(dst + cl) = v;
+        }
+      for (; cl < nct; cl++) {
+        const uint32_t v = *(const uint32_t*)(src + (size_t)cl * plane);
+        if (v) {
+          if (store)
+            dst[cl] = v;
+          else
+            atomicAdd(dst + cl, v);
+        }
       }
     }
   } else {
