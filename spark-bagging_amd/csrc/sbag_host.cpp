@@ -2078,7 +2078,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     // side-bit planes (bin > s) of the shared bins for the partition's gather, when
     // they fit in 8 GB (NB - 1 planes of N/8 bytes per column)
     auto planes_fit = [&](int nc, int nsp) {
-      return nsp >= 1 && (double)nc * nsp * plane_nw32 * 4 <= 8.0 * (1ull << 30) &&
+      static const double cap_gb = getenv("SBAG_PLANES_MAX_GB") ? atof(getenv("SBAG_PLANES_MAX_GB")) : 8.0;
+      return nsp >= 1 && (double)nc * nsp * plane_nw32 * 4 <= cap_gb * (1ull << 30) &&
              !getenv("SBAG_NO_PLANES");
     };
     if (identity && !getenv("SBAG_NO_LAYOUT_CACHE")) {

@@ -2855,11 +2855,16 @@ void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
   set_max_lds((const void*)k_split<true>, 160 * 1024);
   set_max_lds((const void*)k_split<false>, 160 * 1024);
   if (gini) {
-    // feature group: <= 64 KB of u32 prefix counts and about one candidate per thread
+    // feature group: about one candidate per thread, and <= 40 KB of LDS in all so that
+    // four blocks share a CU (the kernel waits on its staging loads; C5, 64 classes:
+    // G = 4 -> 17.6 ms of splits per fit, G = 7 at two blocks per CU -> 21.5 ms)
     const size_t per_f = (size_t)a.NB * (a.NS + 1) * 4;
-    int G = (int)std::max<size_t>(1, std::min<size_t>((64 * 1024) / per_f, (size_t)(256 / std::max(1, a.NB - 1))));
+    const size_t fixed = (size_t)a.NS * 8 + 256 * (8 + 4 + 4);
+    const size_t budget = 40 * 1024 > fixed ? 40 * 1024 - fixed : 0;
+    int G = (int)std::max<size_t>(1, std::min<size_t>(budget / per_f, (size_t)(256 / std::max(1, a.NB - 1))));
+    if (const char* e = getenv("SBAG_SPLIT_G")) G = atoi(e);
     G = std::max(1, std::min(G, a.Fmax));
-    const size_t lds_g = (size_t)a.NS * 8 + 256 * (8 + 4 + 4) + (size_t)G * per_f;
+    const size_t lds_g = fixed + (size_t)G * per_f;
     set_max_lds((const void*)k_split_gini, 160 * 1024);
     if (lds_g <= 160 * 1024 && !getenv("SBAG_SPLIT_GINI_V1")) {
       hipLaunchKernelGGL(k_split_gini, dim3(M), dim3(256), lds_g, st, a, G);

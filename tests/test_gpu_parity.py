@@ -371,3 +371,31 @@ def test_wide_features_more_than_65536_values(ctx, cls, replacement, ratio):
     np.testing.assert_array_equal(nat.predict(ctx, forest, X, agg), want)
     np.testing.assert_array_equal(nat.predict_dataset(ctx, forest, ds, agg), want)
     np.testing.assert_array_equal(ds.features(0, 1000), np.where(X[:1000] == 0.0, 0.0, X[:1000]))
+
+
+def test_layout_cache_shared_by_fits(ctx, monkeypatch):
+    """The column copy and side-bit planes of a codes-as-bins dataset are built by its
+    first fit and reused (sbag_dataset.d_cols / d_planes): fits with other impurities,
+    subspaces and depths on the same dataset, a fit without the cache, and learner
+    halves on two contexts racing to build it are all bit-exact against the oracle.
+    Depth 10 on 3-4 learners reaches >= 1024 parents, where the partition reads planes."""
+    N, F = 60000, 40
+
+    def check(ds, X, y, L, cls, ratio, depth):
+        forest = nat.fit(ctx, ds, replacement=True, sample_ratio=ratio, seed=SEED_CLS,
+                         learner_begin=0, learner_end=L, max_depth=depth, max_bins=32,
+                         impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+        counts = oracle.bag(True, ratio, 0, L, SEED_CLS, [0, N], N)
+        subs = [oracle.subspace(ratio, F, SEED_CLS + i) for i in range(L)]
+        assert_forest_equal(forest, oracle_forest(X, y, counts, subs, depth, 32, cls))
+
+    ds = nat.DeviceDataset.synthetic(N, F, seed=5, num_classes=5, ctx=ctx)
+    X, y = ds.features(), ds.labels()
+    check(ds, X, y, 3, True, 1.0, 10)
+    check(ds, X, y, 3, False, 0.6, 9)
+    monkeypatch.setenv("SBAG_NO_LAYOUT_CACHE", "1")
+    check(ds, X, y, 3, True, 1.0, 10)
+    monkeypatch.delenv("SBAG_NO_LAYOUT_CACHE")
+    monkeypatch.setenv("SBAG_OVERLAP", "2")
+    ds2 = nat.DeviceDataset.synthetic(N, F, seed=6, num_classes=5, ctx=ctx)
+    check(ds2, ds2.features(), ds2.labels(), 4, True, 1.0, 10)
