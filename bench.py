@@ -28,7 +28,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
 LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
 # committed rocprofv3 PMC summaries of this command per workload (scripts/profile.sh +
 # scripts/pmc_summary.py); the newest one present is used
-PMC_SUMMARIES = {"c3": ["profiles/r02c/c3/summary.json", "profiles/r02/c3/summary.json",
+PMC_SUMMARIES = {"c3": ["profiles/r02d/c3/summary.json", "profiles/r02c/c3/summary.json",
                         "profiles/r01g/summary.json"],
                  "c4": ["profiles/r02/c4/summary.json"],
                  "c5": ["profiles/r02/c5/summary.json", "profiles/r01g_c5/summary.json"]}

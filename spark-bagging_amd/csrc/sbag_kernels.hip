@@ -2640,13 +2640,20 @@ void launch_zero_word(hipStream_t st, uint64_t* hist, const int32_t* d_slots, in
 // class sum, Gini.calculate = 1 - sum freq^2 in class order), and the block argmax
 // keeps Spark's first max (maxBy over splits, then over features).
 // stage the raw [g][NB][NS] u32 histogram of features [f0, f0 + g) (contiguous in the
-// slot) into LDS rows of NS + 1 words (odd pitch: the candidate threads of a wave read
-// rows (fl, sp) at one class c without bank conflicts), 16-byte loads with several in
-// flight per thread, then prefix sums over bins in place (a thread per (feature, class))
+// slot) into LDS rows of NS + 1 words, features split_fstride() words apart, 16-byte
+// loads with several in flight per thread, then prefix sums over bins in place (a
+// thread per (feature, class)).  Candidate q = fl * (NB - 1) + sp reads row (fl, sp) at
+// word q * (NS + 1) + c (mod 64): with NS + 1 odd the 64 candidates of a wave fall on 64
+// distinct banks (a plain NB * (NS + 1) feature stride put features 0 and 2 of a wave on
+// the same banks: 24 % of the kernel's LDS cycles were conflicts on C5)
+__host__ __device__ inline int split_fstride(int NB, int NS) {
+  const int NSP = NS + 1;
+  return NB * NSP + (((NB - 1) * NSP - NB * NSP) % 64 + 64) % 64;
+}
 __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ hs, int f0, int g,
                                                    int NB, int NS, uint32_t* pre) {
   const int tid = threadIdx.x;
-  const int NSP = NS + 1;
+  const int NSP = NS + 1, FS = split_fstride(NB, NS);
   const int64_t words = (int64_t)g * NB * NS;
   const uint32_t* src = hs + (int64_t)f0 * NB * NS;
   if ((NS & 3) == 0) {
@@ -2654,7 +2661,8 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
     const uint4* s4 = (const uint4*)src;
     auto put = [&](int q, const uint4& v) {
       const int row = q / ns4, c = (q - row * ns4) * 4;
-      uint32_t* d = pre + (size_t)row * NSP + c;
+      const int fl = row / NB;
+      uint32_t* d = pre + (size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c;
       d[0] = v.x;
       d[1] = v.y;
       d[2] = v.z;
@@ -2672,13 +2680,14 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
   } else {
     for (int64_t q = tid; q < words; q += 256) {
       const int row = (int)(q / NS), c = (int)(q - (int64_t)row * NS);
-      pre[(size_t)row * NSP + c] = src[q];
+      const int fl = row / NB;
+      pre[(size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c] = src[q];
     }
   }
   __syncthreads();
   for (int q = tid; q < g * NS; q += 256) {
     const int fl = q / NS, c = q - fl * NS;
-    uint32_t* o = pre + (size_t)fl * NB * NSP + c;
+    uint32_t* o = pre + (size_t)fl * FS + c;
     uint32_t acc = 0;
     for (int b = 0; b < NB; b++) {
       acc += o[(size_t)b * NSP];
@@ -2693,7 +2702,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   const int slot = A.slot_ids ? A.slot_ids[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x;
   const int r = A.slot_r[slot];
   const int Fr = A.Fr[r];
-  const int NB = A.NB, NS = A.NS, NSP = NS + 1;
+  const int NB = A.NB, NS = A.NS, NSP = NS + 1, FS = split_fstride(NB, NS);
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
   const uint32_t* hs = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
   const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
@@ -2729,7 +2738,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
       const int fl = q / (NB - 1), sp = q - fl * (NB - 1);
       const int nsp = nb_r[f0 + fl] - 1;
       if (sp >= nsp) continue;
-      const uint32_t* left = pre + ((size_t)fl * NB + sp) * NSP;
+      const uint32_t* left = pre + (size_t)fl * FS + (size_t)sp * NSP;
       // class sums of integers: exact in any order
       double lt = 0.0, rt = 0.0;
 #pragma unroll 8
@@ -2858,7 +2867,7 @@ void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
     // feature group: about one candidate per thread, and <= 40 KB of LDS in all so that
     // four blocks share a CU (the kernel waits on its staging loads; C5, 64 classes:
     // G = 4 -> 17.6 ms of splits per fit, G = 7 at two blocks per CU -> 21.5 ms)
-    const size_t per_f = (size_t)a.NB * (a.NS + 1) * 4;
+    const size_t per_f = (size_t)split_fstride(a.NB, a.NS) * 4;
     const size_t fixed = (size_t)a.NS * 8 + 256 * (8 + 4 + 4);
     const size_t budget = 40 * 1024 > fixed ? 40 * 1024 - fixed : 0;
     int G = (int)std::max<size_t>(1, std::min<size_t>(budget / per_f, (size_t)(256 / std::max(1, a.NB - 1))));
