@@ -2076,9 +2076,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     plane_nw32 = (N + 31) / 32;
     plane_nsp = NB - 1;
     // side-bit planes (bin > s) of the shared bins for the partition's gather, when
-    // they fit in 8 GB (NB - 1 planes of N/8 bytes per column)
+    // they fit in 24 GB (NB - 1 planes of N/8 bytes per column; C3 3.9 GB, C5 19.4 GB,
+    // C4's 99 GB are left to the column gather).  C5, serialized: partition 38 -> 32 ms
+    // per fit at levels with >= 1024 parents.
     auto planes_fit = [&](int nc, int nsp) {
-      static const double cap_gb = getenv("SBAG_PLANES_MAX_GB") ? atof(getenv("SBAG_PLANES_MAX_GB")) : 8.0;
+      static const double cap_gb = getenv("SBAG_PLANES_MAX_GB") ? atof(getenv("SBAG_PLANES_MAX_GB")) : 24.0;
       return nsp >= 1 && (double)nc * nsp * plane_nw32 * 4 <= cap_gb * (1ull << 30) &&
              !getenv("SBAG_NO_PLANES");
     };
@@ -2386,8 +2388,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       const int64_t piece = 8192;
       // the gathered object: a side-bit plane (column, split) once parents are many (with
       // few parents, finer groups would crowd the workgroups onto fewer cursors), else a
-      // column byte array
-      const bool lvl_planes = d_planes != nullptr && NP >= 1024;
+      // column byte array.  Crossover measured at 128-256 parents (C5 level 3 / 4: cols
+      // 2.21 / 2.49 ms, planes 2.38 / 2.23; C3 flat within 0.1 ms from 128)
+      static const int planes_min_np =
+          getenv("SBAG_PLANES_MIN_PARENTS") ? atoi(getenv("SBAG_PLANES_MIN_PARENTS")) : 256;
+      const bool lvl_planes = d_planes != nullptr && NP >= planes_min_np;
       auto colkey = [&](int q) {
         if (lvl_planes) return (int64_t)par[q].pos * plane_nsp + par[q].s;
         return (bins_rstride ? (int64_t)par[q].r * 65536 : 0) + (int64_t)par[q].pos;
