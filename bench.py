@@ -31,7 +31,8 @@ LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
 PMC_SUMMARIES = {"c3": ["profiles/r02d/c3/summary.json", "profiles/r02c/c3/summary.json",
                         "profiles/r01g/summary.json"],
                  "c4": ["profiles/r02/c4/summary.json"],
-                 "c5": ["profiles/r02/c5/summary.json", "profiles/r01g_c5/summary.json"]}
+                 "c5": ["profiles/r02d/c5/summary.json", "profiles/r02/c5/summary.json",
+                        "profiles/r01g_c5/summary.json"]}
 
 
 def pmc_traffic(workload):
@@ -236,10 +237,14 @@ def main():
                 "alg_bytes_per_launch": round(read_bytes / nl),
                 "alg_bytes_def": "entries the launch histograms x (F_r + 4): u8 bin per feature of "
                                  "the replica's subspace + 4-byte label word (DESIGN.md §4)",
-                "effective": {"achieved": round(effective, 1), "frac": round(effective / HBM_PEAK_GBS, 4),
+                # not a bandwidth (it counts bytes no kernel reads, and exceeds the peak on
+                # C4), so it carries a ratio, never a frac
+                "effective": {"work_rate": round(effective, 1),
+                              "work_rate_over_peak": round(effective / HBM_PEAK_GBS, 4),
                               "bytes_per_launch": round(work_bytes / nl),
                               "def": "SURVEY 8d: sum over histograms built (read or by subtraction) "
-                                     "of n(r,d)*(F_r+s_y) + 3N, s_y = 4 (regression) / 1 (class)"},
+                                     "of n(r,d)*(F_r+s_y) + 3N, s_y = 4 (regression) / 1 (class); "
+                                     "sibling histograms from k_subtract count as if read"},
                 "binding_limiter": "lds_atomic",
                 "lds_atomic": {"achieved": round(lds_rate / 1e9, 2),
                                "peak": round(LDS_ATOMIC_PEAK / 1e9, 2),

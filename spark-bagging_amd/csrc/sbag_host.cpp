@@ -1166,7 +1166,7 @@ static void build_work(const std::vector<std::pair<int64_t, int64_t>>& segs, int
   w.pieces.clear();
   for (size_t q = 0; q < segs.size(); q++)
     for (int64_t a = segs[q].first; a < segs[q].second; a += ps)
-      w.pieces.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + ps, segs[q].second)});
+      w.pieces.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + ps, segs[q].second), 0, 0, 0, 0});
   const int np = (int)w.pieces.size();
   w.nwg = std::max(1, std::min(np, nwg_max));
   w.wg.assign(w.nwg + 1, np);
@@ -1495,6 +1495,13 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   HistChunk* d_pieces;
   int32_t* d_wg;
   auto upload_work = [&](const std::vector<ParentInfo>& par) -> int {
+    for (HistChunk& pc : work.pieces) {
+      const ParentInfo& pi = par[pc.parent];
+      pc.r = pi.r;
+      pc.slot = pi.hist_slot;
+      pc.tile = pi.tile;
+      pc.fr = h_Fr[pi.r];
+    }
     TRY(ws_typed(c, "par", std::max<size_t>(par.size(), 1), &d_par));
     TRY(h2d(c, d_par, par.data(), par.size()));
     TRY(ws_typed(c, "pieces", std::max<size_t>(work.pieces.size(), 1), &d_pieces));
@@ -1538,7 +1545,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     constexpr int64_t kPiece = 1 << 16;
     for (size_t q = 0; q < segs.size(); q++)
       for (int64_t a = segs[q].first; a < segs[q].second; a += kPiece) {
-        pcs.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + kPiece, segs[q].second)});
+        pcs.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + kPiece, segs[q].second), 0, 0, 0, 0});
         pseg.push_back((int)q);
       }
     const int np = (int)pcs.size();
@@ -1596,6 +1603,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     }
     return SBAG_OK;
   };
+  // class tile of the gini histogram layout (gini_cell): the grouped kernels' tile when it
+  // divides the classes, so each (node, tile) flush is one contiguous block; else NS
+  auto hist_layout_tile = [&](const HistGeom& g) -> int32_t {
+    if (!gini || getenv("SBAG_NO_TILE_LAYOUT")) return NS;
+    return (g.grouped && g.CT < NS && NS % g.CT == 0) ? g.CT : NS;
+  };
   auto launch = [&](const HistGeom& g, int mode, int cat,
                     const std::vector<std::pair<int64_t, int64_t>>& segs_in,
                     const std::vector<ParentInfo>& par_in) -> int {
@@ -1613,6 +1626,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       ntiles = g.ntf;
     }
     ha.grouped = grouped ? 1 : 0;
+    // k_hist gathers aligned 4-byte words (SBAG_HIST_GW=1: single bytes, as before round 2e;
+    // 8-byte words were slower on C5, 134 vs 98 ms per fit)
+    static const int hist_gw = getenv("SBAG_HIST_GW") ? atoi(getenv("SBAG_HIST_GW")) : 4;
+    ha.dw = hist_gw == 1 ? 1 : 4;
     const std::vector<std::pair<int64_t, int64_t>>& segs = grouped ? gsegs : segs_in;
     const std::vector<ParentInfo>& par = grouped ? gpar : par_in;
     build_work(segs, flush_limit, 256 * wpc * (grouped ? 2 : 1), g.T, work);
@@ -1690,6 +1707,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     if (!hist_geometry(ds->S, Fmax, ncmax, NS, gini, g0, rl_mode_for(h_pos_codes, ds->S)))
       return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
     TRY(maybe_grouped(g0, ds->S, ncmax));
+    ha.hct = hist_layout_tile(g0);
     HIP_TRY(hipMemsetAsync(hist_cur, 0, (size_t)R * Fmax * ncmax * NS * word_bytes, c->stream));
     ha.bins = (const uint8_t*)ds->d_codes;
     ha.bins_rstride = 0;
@@ -1711,7 +1729,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
           const int64_t wi = (((int64_t)r * Fmax + fl) * ncmax + (int64_t)k) * NS;
           uint64_t cnt = 0;
           if (gini) {
-            for (int q = 0; q < NS; q++) cnt += ((const uint32_t*)tmp.data())[wi + q];
+            const uint32_t* hs = (const uint32_t*)tmp.data() + (int64_t)r * Fmax * ncmax * NS;
+            for (int q = 0; q < NS; q++) cnt += hs[gini_cell(fl, (int)k, q, ncmax, Fmax, ha.hct)];
           } else {
             cnt = ((const uint64_t*)tmp.data())[wi];
           }
@@ -1735,7 +1754,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       ha.hist = d_vch;
       ha.NB = ncmax;
       ha.NS = 1;
-        ha.count_only = 1;
+      ha.hct = 1;
+      ha.count_only = 1;
       TRY(launch(g, kHistGini, T_VC, seg, h_par));
       ha = save;
       std::vector<uint32_t> tmp((size_t)R * slot_words);
@@ -2135,6 +2155,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode_for(h_pos, S)))
     return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
   TRY(maybe_grouped(g, S, NB));
+  if (ha.hct == 0) ha.hct = hist_layout_tile(g);  // else the optimistic root's layout
   const int64_t slot_words = (int64_t)Fmax * NB * NS;
   std::vector<std::vector<HNode>> trees(R);
   std::vector<std::pair<int, int>> slots(R);  // (replica, node index)
@@ -2190,6 +2211,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     TRY(ws_typed(c, "sstats", (size_t)M * 3 * NS, &d_sstats));
     TRY(h2d(c, d_slot_r, h_slot_r.data(), (size_t)M));
     SplitArgs sa{};
+    sa.hct = ha.hct;
     sa.hist = hist_cur;
     sa.Fmax = Fmax;
     sa.NB = NB;

@@ -18,6 +18,9 @@ struct HistChunk {  // one workgroup: entries [a, b) of one parent segment
   int32_t parent;
   int32_t excl;      // the whole segment lies in this workgroup's pieces: flush with stores
   int64_t a, b;
+  // the histogram kernels' copy of the parent's ParentInfo fields (set by the host, so a
+  // piece is one load): replica, histogram slot, class tile, replica's feature count
+  int32_t r, slot, tile, fr;
 };
 
 struct ParentInfo {  // a node of level d whose rows are routed to level d+1
@@ -56,7 +59,16 @@ struct HistArgs {
   int32_t rl;            // k_hist_rl (identity byte layout): 1 = 64-bit row addresses, 2 = 32-bit
   int32_t grouped;       // gini: entries grouped by class tile, ParentInfo.tile per segment;
                          // blockIdx.y walks feature tiles only
+  int32_t dw;            // k_hist gather width: 1 (byte loads) or 4 (aligned words + extract)
+  int32_t hct;           // gini layout class tile: hist[slot][NS / hct][Fmax][NB][hct]
 };
+
+// Gini histogram cell (f, b, c) of one slot: class-tile-major, so that a class tile's
+// flush writes one contiguous block (hct = NS: the plain [f][b][NS] layout)
+__host__ __device__ inline int64_t gini_cell(int f, int b, int c, int NB, int Fmax, int hct) {
+  const int t = c / hct;
+  return (((int64_t)t * Fmax + f) * NB + b) * hct + (c - t * hct);
+}
 
 // k_partition: entries of each split node -> left block (from the segment start,
 // cursors[2p] grows) and right block (from the segment end, cursors[2p+1] shrinks)
@@ -113,6 +125,8 @@ struct SplitArgs {
   int64_t plane;                  // M * NS
   const int32_t* slot_ids;        // block -> slot (NULL: identity)
   const uint64_t* node_sq;        // screen: [M] exact sum of count*k^2 of each node
+  int32_t hct;                    // gini layout class tile (HistArgs.hct)
+  int32_t pad;
 };
 
 struct DevNode {  // packed tree node for predict

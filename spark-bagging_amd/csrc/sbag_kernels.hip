@@ -1366,8 +1366,11 @@ constexpr int kHistWaves = kHistThreads / 64;
 // entries per pipeline group: row bytes of the next group are loaded while the current
 // one is added, so a wave keeps up to 2 groups of row gathers in flight (k_hist is bound
 // by their latency when the atomics are few: 16 for up to two 64-feature lane groups)
-template <int NJ>
-constexpr int hist_group() { return NJ <= 2 ? 16 : 8; }
+// (gini with one lane group: 8, so that the kernel fits 64 VGPRs at 8 waves per SIMD)
+template <int MODE, int NJ, int GW>
+constexpr int hist_group() {
+  return (MODE == kHistGini && NJ == 1) || NJ > 2 ? 8 : 16;
+}
 
 static __host__ __device__ inline uint32_t hist_plane_bytes(int NB, int FPH, bool gini) {
   return (uint32_t)(NB * FPH + 64) * (gini ? 4u : 8u);
@@ -1387,12 +1390,15 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
     // class planes [0, nct) of the LDS hold classes [c0, c0 + nct).  Lane q takes one
     // (feature, bin): features fastest, so the LDS reads of a class plane hit distinct
     // banks (planes and bin rows are multiples of 64 words apart), and the lane writes
-    // its nct classes -- contiguous in the global [f][b][NS] row -- as 16-byte stores
+    // its classes -- runs of 4 contiguous in the class-tile-major global layout
+    // (gini_cell) -- as 16-byte stores.  With the workgroup's tile equal to the layout
+    // tile (grouped C5) the flush writes one contiguous block that no other workgroup
+    // shares a line of.
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
-    const bool vec = store && ((NS | c0) & 3) == 0;
+    const int hct = A.hct;
+    const bool vec = store && ((hct | c0) & 3) == 0;
     for (int q = tid; q < ftn * NB; q += blockDim.x) {
       const int f = q % ftn, b = q / ftn;
-      uint32_t* dst = &gh[((int64_t)(ft0 + f) * NB + b) * NS + c0];
       const unsigned char* src = smem + ((size_t)b * FPH + f) * 4;
       int cl = 0;
       if (vec)
@@ -1402,15 +1408,16 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
           v.y = *(const uint32_t*)(src + (size_t)(cl + 1) * plane);
           v.z = *(const uint32_t*)(src + (size_t)(cl + 2) * plane);
           v.w = *(const uint32_t*)(src + (size_t)(cl + 3) * plane);
-          *(uint4*)(dst + cl) = v;
+          *(uint4*)(gh + gini_cell(ft0 + f, b, c0 + cl, NB, A.Fmax, hct)) = v;
         }
       for (; cl < nct; cl++) {
         const uint32_t v = *(const uint32_t*)(src + (size_t)cl * plane);
         if (v) {
+          uint32_t* dst = gh + gini_cell(ft0 + f, b, c0 + cl, NB, A.Fmax, hct);
           if (store)
-            dst[cl] = v;
+            *dst = v;
           else
-            atomicAdd(dst + cl, v);
+            atomicAdd(dst, v);
         }
       }
     }
@@ -1447,8 +1454,11 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
-// bytes of the NJ feature columns of entries [u0, u0 + KG) of the batch
-template <int NJ, int KG>
+// bytes of the NJ feature columns of entries [u0, u0 + KG) of the batch.  DW: each lane
+// loads the aligned dword holding its byte (posr is then pos & ~3; the add extracts the
+// byte): a wave's 64 lanes touch ~1/4 as many distinct addresses as with byte loads, which
+// for a subspace's scattered columns is what the vector memory path is paced by
+template <int NJ, int KG, int GW>
 __device__ __forceinline__ void hist_load_group(const uint8_t* __restrict__ binsr, uint32_t S,
                                                 uint32_t row, int u0, const uint32_t (&posr)[NJ],
                                                 uint32_t (&buf)[KG][NJ]) {
@@ -1459,18 +1469,25 @@ __device__ __forceinline__ void hist_load_group(const uint8_t* __restrict__ bins
     for (int jj = 0; jj < NJ; jj++) {
       uint32_t off = posr[jj];
       asm volatile("" : "+v"(off));  // keep the column a 32-bit VGPR offset: saddr form
-      buf[t][jj] = rp[off];
+      if (GW == 4)
+        buf[t][jj] = *(const uint32_t*)(rp + off);
+      else
+        buf[t][jj] = rp[off];
     }
   }
 }
 
 // one LDS atomic per entry and lane group: GINI adds count wl into class plane
 // (offset wh); the u64 modes add (wh:wl)
-template <int MODE, int NJ, int KG>
+template <int MODE, int NJ, int KG, int GW>
 __device__ __forceinline__ void hist_add_group(unsigned char* smem, int u0,
                                                const uint32_t (&buf)[KG][NJ], uint32_t wl,
                                                uint32_t wh, const uint32_t (&amul)[NJ],
-                                               const uint32_t (&abase)[NJ]) {
+                                               const uint32_t (&abase)[NJ],
+                                               const uint32_t (&bsh)[NJ]) {
+  auto bin = [&](int t, int jj) -> uint32_t {
+    return GW == 4 ? __builtin_amdgcn_ubfe(buf[t][jj], bsh[jj], 8) : buf[t][jj];
+  };
 #pragma unroll
   for (int t = 0; t < KG; t++) {
     const int u = u0 + t;
@@ -1478,25 +1495,32 @@ __device__ __forceinline__ void hist_add_group(unsigned char* smem, int u0,
       const uint32_t cu = rdlane(wl, u), cou = rdlane(wh, u);
 #pragma unroll
       for (int jj = 0; jj < NJ; jj++) {
-        const uint32_t addr = __umul24(buf[t][jj], amul[jj]) + abase[jj] + cou;
+        const uint32_t addr = __umul24(bin(t, jj), amul[jj]) + abase[jj] + cou;
         atomicAdd((uint32_t*)(smem + addr), cu);
       }
     } else {
       const unsigned long long a0 = ((unsigned long long)rdlane(wh, u) << 32) | rdlane(wl, u);
 #pragma unroll
       for (int jj = 0; jj < NJ; jj++) {
-        const uint32_t addr = __umul24(buf[t][jj], amul[jj]) + abase[jj];
+        const uint32_t addr = __umul24(bin(t, jj), amul[jj]) + abase[jj];
         atomicAdd((unsigned long long*)(smem + addr), a0);
       }
     }
   }
 }
 
-template <int MODE, int NJ>
-__global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
+// The second bound is waves per SIMD.  Gini with one lane group (C5's class tiles, ~34 KB
+// of LDS, four workgroups per CU) needs 8 waves per SIMD, i.e. <= 64 VGPRs: at 85 VGPRs only
+// two of the four workgroups were resident.
+template <int MODE, int NJ, int GW>
+__global__ __launch_bounds__(kHistThreads, MODE == kHistGini && NJ == 1 ? 8 : 4) void k_hist(HistArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
   constexpr bool GINI = MODE == kHistGini;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave-uniform for the compiler too: batch bounds and the group loop's exits stay scalar
+  // branches, so the row-byte loads of the next group stay in flight across them (with a
+  // VGPR wave index the branches were exec-masked and each group waited for the next)
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int NB = A.NB, FPH = A.FPH;
   const uint32_t S = (uint32_t)A.S;
   const int ft0 = (int)(blockIdx.y % (unsigned)A.ntf) * A.FT;
@@ -1520,24 +1544,33 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
   int cur_slot = -1, cur_ftn = 0, cur_r = -1, cur_tile = -1;
   bool cur_store = false;  // the current node run is this workgroup's alone and not yet flushed
   int64_t acc = 0;
-  uint32_t posr[NJ], amul[NJ], abase[NJ];
+  uint32_t posr[NJ], amul[NJ], abase[NJ], bsh[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; j++) {
     posr[j] = 0;
+    bsh[j] = 0;
     amul[j] = 0;
     abase[j] = dump;
   }
   __syncthreads();
 
+  // pieces carry their parent's replica, slot, tile and feature count (HistChunk), and the
+  // next piece is loaded while this one runs; the first entries of a piece are loaded before
+  // the flush of the previous node.  Deep levels are thousands of short pieces per
+  // workgroup, where these dependent loads were most of the time.
+  HistChunk pn = p0 < p1 ? A.chunks[p0] : HistChunk{};
   for (int p = p0; p < p1; p++) {
-    const HistChunk pc = A.chunks[p];
-    const ParentInfo pi = A.parents[pc.parent];
-    const int r = pi.r;
-    const int ftn = min(A.FT, A.Fr[r] - ft0);
-    const int slot = pi.hist_slot;
+    const HistChunk pc = pn;
+    if (p + 1 < p1) pn = A.chunks[p + 1];
+    const int r = pc.r;
+    const int ftn = min(A.FT, pc.fr - ft0);
+    const int slot = pc.slot;
     if (ftn <= 0 || slot < 0) continue;
     const int64_t a = pc.a, b = pc.b;
-    const int tile = A.grouped ? pi.tile : 0;
+    const int tile = A.grouped ? pc.tile : 0;
+    // entries of the wave's next batch are loaded one batch ahead
+    int64_t q0 = a + (int64_t)wave * 64;
+    uint64_t e_next = (q0 + lane < b) ? A.ent_in[q0 + lane] : 0ull;
     if (slot != cur_slot || tile != cur_tile || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
@@ -1564,7 +1597,9 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
       for (int j = 0; j < NJ; j++) {
         const int fl = lane + 64 * j;
         const bool ok = fl < ftn;
-        posr[j] = ok ? (uint32_t)A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0u;
+        const uint32_t pb = ok ? (uint32_t)A.pos[(int64_t)r * A.Fmax + ft0 + fl] : 0u;
+        posr[j] = pb & ~(uint32_t)(GW - 1);
+        bsh[j] = (pb & (uint32_t)(GW - 1)) * 8u;
         amul[j] = ok ? (uint32_t)FPH * WB : 0u;
         abase[j] = ok ? (uint32_t)fl * WB : dump;
       }
@@ -1574,9 +1609,6 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
     const int cs = A.cshift;
     const int64_t K0 = A.K0;
     const uint32_t cstride = A.count_only ? 0u : plane;
-    // entries of the wave's next batch are loaded one batch ahead
-    int64_t q0 = a + (int64_t)wave * 64;
-    uint64_t e_next = (q0 + lane < b) ? A.ent_in[q0 + lane] : 0ull;
     for (; q0 < b; q0 += (int64_t)kHistWaves * 64) {
       int n = (int)min((int64_t)64, b - q0);
       uint64_t e = e_next;
@@ -1610,17 +1642,17 @@ __global__ __launch_bounds__(kHistThreads, 4) void k_hist(HistArgs A) {
         wl = (uint32_t)w;
         wh = (uint32_t)(w >> 32);
       }
-      constexpr int kG = hist_group<NJ>();
+      constexpr int kG = hist_group<MODE, NJ, GW>();
       uint32_t bA[kG][NJ], bB[kG][NJ];
-      hist_load_group<NJ, kG>(binsr, S, row, 0, posr, bA);
+      hist_load_group<NJ, kG, GW>(binsr, S, row, 0, posr, bA);
 #pragma unroll
       for (int g = 0; g < 64 / kG; g += 2) {
-        if ((g + 1) * kG < n) hist_load_group<NJ, kG>(binsr, S, row, (g + 1) * kG, posr, bB);
-        hist_add_group<MODE, NJ, kG>(smem, g * kG, bA, wl, wh, amul, abase);
+        if ((g + 1) * kG < n) hist_load_group<NJ, kG, GW>(binsr, S, row, (g + 1) * kG, posr, bB);
+        hist_add_group<MODE, NJ, kG, GW>(smem, g * kG, bA, wl, wh, amul, abase, bsh);
         if ((g + 1) * kG >= n) break;
         if (g + 2 < 64 / kG && (g + 2) * kG < n)
-          hist_load_group<NJ, kG>(binsr, S, row, (g + 2) * kG, posr, bA);
-        hist_add_group<MODE, NJ, kG>(smem, (g + 1) * kG, bB, wl, wh, amul, abase);
+          hist_load_group<NJ, kG, GW>(binsr, S, row, (g + 2) * kG, posr, bA);
+        hist_add_group<MODE, NJ, kG, GW>(smem, (g + 1) * kG, bB, wl, wh, amul, abase, bsh);
         if ((g + 2) * kG >= n) break;
       }
     }
@@ -1788,15 +1820,16 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
   RlLane L{A.bins, 0u, 0u, (uint32_t)(s * K) * WB};
   __syncthreads();
 
+  HistChunk pn = p0 < p1 ? A.chunks[p0] : HistChunk{};  // next piece prefetched (k_hist)
   for (int p = p0; p < p1; p++) {
-    const HistChunk pc = A.chunks[p];
-    const ParentInfo pi = A.parents[pc.parent];
-    const int r = pi.r;
-    const int ftn = min(A.FT, A.Fr[r] - ft0);
-    const int slot = pi.hist_slot;
+    const HistChunk pc = pn;
+    if (p + 1 < p1) pn = A.chunks[p + 1];
+    const int r = pc.r;
+    const int ftn = min(A.FT, pc.fr - ft0);
+    const int slot = pc.slot;
     if (ftn <= 0 || slot < 0) continue;
     const int64_t a = pc.a, b = pc.b;
-    const int tile = A.grouped ? pi.tile : 0;
+    const int tile = A.grouped ? pc.tile : 0;
     if (slot != cur_slot || tile != cur_tile || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
@@ -1910,8 +1943,13 @@ size_t hist_stage_bytes() { return (size_t)kHistWaves * 64 * 8; }
 
 template <int MODE, int NJ>
 static void launch_hist_t(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds_bytes) {
-  set_max_lds((const void*)k_hist<MODE, NJ>, 160 * 1024);
-  hipLaunchKernelGGL((k_hist<MODE, NJ>), grid, dim3(kHistThreads), lds_bytes, st, a);
+  if (a.dw == 4) {
+    set_max_lds((const void*)k_hist<MODE, NJ, 4>, 160 * 1024);
+    hipLaunchKernelGGL((k_hist<MODE, NJ, 4>), grid, dim3(kHistThreads), lds_bytes, st, a);
+  } else {
+    set_max_lds((const void*)k_hist<MODE, NJ, 1>, 160 * 1024);
+    hipLaunchKernelGGL((k_hist<MODE, NJ, 1>), grid, dim3(kHistThreads), lds_bytes, st, a);
+  }
 }
 
 template <int MODE>
@@ -2275,7 +2313,7 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
     const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
     for (int c = tid; c < NS; c += 256) {
       int64_t t = 0;
-      for (int b = 0; b < NB; b++) t += h[(int64_t)b * NS + c];
+      for (int b = 0; b < NB; b++) t += h[gini_cell(0, b, c, NB, A.Fmax, A.hct)];
       s_tot[c] = t;
     }
   } else {
@@ -2307,14 +2345,14 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
     for (int fl = tid; fl < Fr; fl += 256) {
       const int nsp = nb_r[fl] - 1;
       if (nsp <= 0) continue;
-      const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words + (int64_t)fl * NB * NS;
+      const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
       for (int c = 0; c < NS; c++) left[c * 256] = 0;
       double fg = 0.0;
       int fs = -1, fv = 0;
       for (int s = 0; s < nsp; s++) {
         double lt = 0.0;
         for (int c = 0; c < NS; c++) {
-          const uint32_t v = left[c * 256] + h[(int64_t)s * NS + c];
+          const uint32_t v = left[c * 256] + h[gini_cell(fl, s, c, NB, A.Fmax, A.hct)];
           left[c * 256] = v;
           lt += (double)v;
         }
@@ -2454,8 +2492,8 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
     int64_t l = 0;
     if (bf != INT_MAX) {
       if (GINI) {
-        const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words + (int64_t)bf * NB * NS;
-        for (int s = 0; s <= bsp; s++) l += h[(int64_t)s * NS + c];
+        const uint32_t* h = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
+        for (int s = 0; s <= bsp; s++) l += h[gini_cell(bf, s, c, NB, A.Fmax, A.hct)];
       } else {
         const uint64_t* h = (const uint64_t*)A.hist + (int64_t)slot * slot_words + (int64_t)bf * NB * 3;
         for (int s = 0; s <= bsp; s++) l += (int64_t)h[s * 3 + c];
@@ -2651,16 +2689,23 @@ __host__ __device__ inline int split_fstride(int NB, int NS) {
   return NB * NSP + (((NB - 1) * NSP - NB * NSP) % 64 + 64) % 64;
 }
 __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ hs, int f0, int g,
-                                                   int NB, int NS, uint32_t* pre) {
+                                                   int NB, int NS, int Fmax, int hct,
+                                                   uint32_t* pre) {
+  // features [f0, f0 + g) of each layout class tile t are one contiguous run of g*NB*hct
+  // words (gini_cell); staged as pre[fl][b][c] with the class row padded to NS + 1
   const int tid = threadIdx.x;
   const int NSP = NS + 1, FS = split_fstride(NB, NS);
-  const int64_t words = (int64_t)g * NB * NS;
-  const uint32_t* src = hs + (int64_t)f0 * NB * NS;
-  if ((NS & 3) == 0) {
-    const int n4 = (int)(words >> 2), ns4 = NS >> 2;
-    const uint4* s4 = (const uint4*)src;
+  const int ntc = NS / hct;
+  const int64_t per_t = (int64_t)g * NB * hct;
+  if ((hct & 3) == 0) {
+    const int hct4 = hct >> 2, per_t4 = (int)(per_t >> 2), n4 = ntc * per_t4;
+    auto src4 = [&](int q) {
+      const int t = q / per_t4, rem = q - t * per_t4;
+      return ((const uint4*)(hs + ((int64_t)t * Fmax + f0) * NB * hct))[rem];
+    };
     auto put = [&](int q, const uint4& v) {
-      const int row = q / ns4, c = (q - row * ns4) * 4;
+      const int t = q / per_t4, rem = q - t * per_t4;
+      const int row = rem / hct4, c = t * hct + (rem - row * hct4) * 4;
       const int fl = row / NB;
       uint32_t* d = pre + (size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c;
       d[0] = v.x;
@@ -2670,18 +2715,22 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
     };
     int q = tid;
     for (; q + 3 * 256 < n4; q += 4 * 256) {
-      const uint4 v0 = s4[q], v1 = s4[q + 256], v2 = s4[q + 512], v3 = s4[q + 768];
+      const uint4 v0 = src4(q), v1 = src4(q + 256), v2 = src4(q + 512), v3 = src4(q + 768);
       put(q, v0);
       put(q + 256, v1);
       put(q + 512, v2);
       put(q + 768, v3);
     }
-    for (; q < n4; q += 256) put(q, s4[q]);
+    for (; q < n4; q += 256) put(q, src4(q));
   } else {
+    const int64_t words = (int64_t)ntc * per_t;
     for (int64_t q = tid; q < words; q += 256) {
-      const int row = (int)(q / NS), c = (int)(q - (int64_t)row * NS);
+      const int t = (int)(q / per_t);
+      const int64_t rem = q - (int64_t)t * per_t;
+      const int row = (int)(rem / hct), c = t * hct + (int)(rem - (int64_t)row * hct);
       const int fl = row / NB;
-      pre[(size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c] = src[q];
+      pre[(size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c] =
+          hs[((int64_t)t * Fmax + f0) * NB * hct + rem];
     }
   }
   __syncthreads();
@@ -2712,7 +2761,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   int* s_valid = s_key + 256;                           // [256]
   uint32_t* pre = (uint32_t*)(s_valid + 256);           // [G][NB][NS + 1] prefix over bins
   // group 0 first: the node totals are feature 0's last prefix
-  split_stage_prefix(hs, 0, min(G, Fr), NB, NS, pre);
+  split_stage_prefix(hs, 0, min(G, Fr), NB, NS, A.Fmax, A.hct, pre);
   for (int c = tid; c < NS; c += 256) s_tot[c] = (int64_t)pre[(size_t)(NB - 1) * NSP + c];
   __syncthreads();
   double ttot = 0.0;
@@ -2732,7 +2781,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
     const int g = min(G, Fr - f0);
     if (f0 > 0) {
       __syncthreads();  // previous group's prefix no longer read
-      split_stage_prefix(hs, f0, g, NB, NS, pre);
+      split_stage_prefix(hs, f0, g, NB, NS, A.Fmax, A.hct, pre);
     }
     for (int q = tid; q < g * (NB - 1); q += 256) {
       const int fl = q / (NB - 1), sp = q - fl * (NB - 1);
@@ -2821,16 +2870,18 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   for (int c = tid; c < NS; c += 256) {
     int64_t l = 0;
     if (bf >= 0) {
-      const uint32_t* h = hs + (int64_t)bf * NB * NS + c;
+      // bins of (bf, c) are hct words apart (gini_cell)
+      const int hct = A.hct;
+      const uint32_t* h = hs + gini_cell(bf, 0, c, NB, A.Fmax, hct);
       int sb = 0;
       for (; sb + 8 <= bsp + 1; sb += 8) {
         uint32_t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = h[(int64_t)(sb + u) * NS];
+        for (int u = 0; u < 8; u++) v[u] = h[(int64_t)(sb + u) * hct];
 #pragma unroll
         for (int u = 0; u < 8; u++) l += v[u];
       }
-      for (; sb <= bsp; sb++) l += h[(int64_t)sb * NS];
+      for (; sb <= bsp; sb++) l += h[(int64_t)sb * hct];
     }
     so[c] = s_tot[c];
     so[A.plane + c] = l;
