@@ -198,6 +198,8 @@ typedef struct {
   double fix_ms;           /* exact-split fallback of screened variance nodes */
   int64_t exact_fallbacks; /* nodes that needed it                                      */
   double hist_lds_atomics; /* LDS atomic wave-instructions issued by the hist launches   */
+  double group_ms;         /* gini class tiles: entries regrouped by tile before the
+                              histogram (k_tile_count / k_tile_scatter), not in hist_ms   */
 } sbag_timing;
 int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
 

@@ -647,7 +647,7 @@ struct EventTimer {
     }
   }
 };
-enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_FIX, T_NCAT };
+enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_FIX, T_GROUP, T_NCAT };
 
 // ---------------------------------------------------------------- C ABI
 extern "C" {
@@ -1238,6 +1238,7 @@ static void merge_forests(sbag_forest* fa, sbag_forest* fb) {
   T.fix_ms += U.fix_ms;
   T.exact_fallbacks += U.exact_fallbacks;
   T.hist_lds_atomics += U.hist_lds_atomics;
+  T.group_ms += U.group_ms;
 }
 
 // one context: fit_range, or halves of the learner range when per-replica bins exceed
@@ -1617,11 +1618,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     const int wpc = std::max(1, std::min(grouped ? 4 : 2, (int)((160 * 1024) / g.lds)));
     const uint64_t* ent_saved = ha.ent_in;
     int ntiles = g.ntiles;
-    int hg = -1;
-    if (grouped) {
-      hg = tm.begin(cat);
+    if (grouped) {  // timed apart from the histogram kernel (group_ms)
+      const int hg = tm.begin(cat == T_HIST ? T_GROUP : cat);
       uint64_t* d_entg = nullptr;
       TRY(group_tiles(g, segs_in, par_in, &d_entg));
+      tm.end(hg);
       ha.ent_in = d_entg;
       ntiles = g.ntf;
     }
@@ -1642,7 +1643,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     ha.CT = g.CT;
     ha.ntf = g.ntf;
     ha.rl = g.rl;
-    int h = hg >= 0 ? hg : tm.begin(cat);
+    int h = tm.begin(cat);
     launch_hist(c->stream, ha, work.nwg, ntiles, mode, g.lds);
     HIP_TRY(hipGetLastError());
     tm.end(h);
@@ -2650,10 +2651,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       it->second[tm.ev[i].first] += ms;
     }
     for (auto& kv : per) {
-      fprintf(stderr, "[sbag] level %d ms: sample %.2f vc %.2f bin %.2f compact %.2f hist %.2f split %.2f "
-              "sub %.2f part %.2f fix %.2f\n", kv.first, kv.second[T_SAMPLE], kv.second[T_VC],
-              kv.second[T_BIN], kv.second[T_COMPACT], kv.second[T_HIST], kv.second[T_SPLIT],
-              kv.second[T_SUB], kv.second[T_PART], kv.second[T_FIX]);
+      fprintf(stderr, "[sbag] level %d ms: sample %.2f vc %.2f bin %.2f compact %.2f group %.2f hist %.2f "
+              "split %.2f sub %.2f part %.2f fix %.2f\n", kv.first, kv.second[T_SAMPLE], kv.second[T_VC],
+              kv.second[T_BIN], kv.second[T_COMPACT], kv.second[T_GROUP], kv.second[T_HIST],
+              kv.second[T_SPLIT], kv.second[T_SUB], kv.second[T_PART], kv.second[T_FIX]);
     }
   }
   float total_ms = 0;
@@ -2672,6 +2673,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   T.partition_ms = cats[T_PART];
   T.hist_work_bytes = hist_work;
   T.fix_ms = cats[T_FIX];
+  T.group_ms = cats[T_GROUP];
   T.exact_fallbacks = fallbacks;
   T.hist_launches = hist_launches;
   T.hist_alg_bytes = hist_alg_bytes;
