@@ -2759,7 +2759,8 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   double* s_gain = (double*)(s_tot + NS);               // [256]
   int* s_key = (int*)(s_gain + 256);                    // [256] fl * 65536 + s (INT_MAX: none)
   int* s_valid = s_key + 256;                           // [256]
-  uint32_t* pre = (uint32_t*)(s_valid + 256);           // [G][NB][NS + 1] prefix over bins
+  double* s_wmax = (double*)(s_valid + 256);            // [2][4] per-wave best, by group parity
+  uint32_t* pre = (uint32_t*)(s_wmax + 8);              // [G][NB][NS + 1] prefix over bins
   // group 0 first: the node totals are feature 0's last prefix
   split_stage_prefix(hs, 0, min(G, Fr), NB, NS, A.Fmax, A.hct, pre);
   for (int c = tid; c < NS; c += 256) s_tot[c] = (int64_t)pre[(size_t)(NB - 1) * NSP + c];
@@ -2777,10 +2778,21 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   const int64_t tcount = (int64_t)ttot;
   double bgain = -INFINITY;
   int bkey = INT_MAX, bvalid = 0;
-  for (int f0 = 0; f0 < Fr; f0 += G) {
+  // Screen: a candidate whose cheap gain (1 - sum l^2 / lt^2: two divisions instead of
+  // two per class) lies below the block's best exact gain of the earlier feature groups by
+  // more than kGiniScreen cannot be the argmax or tie it (the two formulas differ by
+  // rounding only, < 1e-11 for up to 4096 classes), so only the others run Spark's
+  // per-class Gini.calculate.  thr is exact, so the chosen split is unchanged.
+  constexpr double kGiniScreen = 1e-9;
+  double thr = -INFINITY;
+  int grp = 0;
+  for (int f0 = 0; f0 < Fr; f0 += G, grp++) {
     const int g = min(G, Fr - f0);
     if (f0 > 0) {
-      __syncthreads();  // previous group's prefix no longer read
+      // per-wave maxima of the running best, written after the previous group
+      const double* wm = s_wmax + ((grp - 1) & 1) * 4;
+      __syncthreads();  // previous group's prefix no longer read; wm visible
+      thr = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
       split_stage_prefix(hs, f0, g, NB, NS, A.Fmax, A.hct, pre);
     }
     for (int q = tid; q < g * (NB - 1); q += 256) {
@@ -2800,6 +2812,21 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
       const int64_t rc = tcount - lc;
       double gain;
       int valid;
+      const double lw = (double)lc / (double)(lc + rc);
+      const double rw = (double)rc / (double)(lc + rc);
+      bool screened = false;
+      if (lc >= A.min_inst && rc >= A.min_inst && thr > -DBL_MAX) {
+        double sl = 0.0, sr = 0.0;
+#pragma unroll 8
+        for (int c = 0; c < NS; c++) {
+          const double l = (double)left[c], r = (double)(s_tot[c] - (int64_t)left[c]);
+          sl = fma(l, l, sl);
+          sr = fma(r, r, sr);
+        }
+        const double apx = imp - lw * (1.0 - sl / (lt * lt)) - rw * (1.0 - sr / (rt * rt));
+        screened = apx < thr - kGiniScreen;
+      }
+      if (screened) continue;
       if (lc < A.min_inst || rc < A.min_inst) {
         gain = -DBL_MAX;
         valid = 0;
@@ -2814,8 +2841,6 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
           if (lt != 0) li -= fl_ * fl_;
           if (rt != 0) ri -= fr_ * fr_;
         }
-        const double lw = (double)lc / (double)(lc + rc);
-        const double rw = (double)rc / (double)(lc + rc);
         gain = imp - lw * li - rw * ri;
         valid = 1;
         if (gain < A.min_gain) {
@@ -2830,6 +2855,10 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
         bvalid = valid;
       }
     }
+    double wmx = bgain;  // this wave's best exact gain so far -> the next group's screen
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wmx = fmax(wmx, __shfl_xor(wmx, o));
+    if ((tid & 63) == 0) s_wmax[(grp & 1) * 4 + (tid >> 6)] = wmx;
   }
   s_gain[tid] = bgain;
   s_key[tid] = bkey;
@@ -2919,7 +2948,7 @@ void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini) {
     // four blocks share a CU (the kernel waits on its staging loads; C5, 64 classes:
     // G = 4 -> 17.6 ms of splits per fit, G = 7 at two blocks per CU -> 21.5 ms)
     const size_t per_f = (size_t)split_fstride(a.NB, a.NS) * 4;
-    const size_t fixed = (size_t)a.NS * 8 + 256 * (8 + 4 + 4);
+    const size_t fixed = (size_t)a.NS * 8 + 256 * (8 + 4 + 4) + 64;
     const size_t budget = 40 * 1024 > fixed ? 40 * 1024 - fixed : 0;
     int G = (int)std::max<size_t>(1, std::min<size_t>(budget / per_f, (size_t)(256 / std::max(1, a.NB - 1))));
     if (const char* e = getenv("SBAG_SPLIT_G")) G = atoi(e);
