@@ -1503,8 +1503,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       pc.tile = pi.tile;
       pc.fr = h_Fr[pi.r];
     }
-    TRY(ws_typed(c, "par", std::max<size_t>(par.size(), 1), &d_par));
-    TRY(h2d(c, d_par, par.data(), par.size()));
+    // (the parent list itself stays on the host: the kernels read the pieces' copies)
     TRY(ws_typed(c, "pieces", std::max<size_t>(work.pieces.size(), 1), &d_pieces));
     TRY(h2d(c, d_pieces, work.pieces.data(), work.pieces.size()));
     TRY(ws_typed(c, "wgp", work.wg.size(), &d_wg));
@@ -1637,7 +1636,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     TRY(upload_work(par));
     ha.chunks = d_pieces;
     ha.wg_piece = d_wg;
-    ha.parents = d_par;
+    ha.parents = nullptr;
     ha.FT = g.FT;
     ha.FPH = g.FPH;
     ha.CT = g.CT;
@@ -2194,6 +2193,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   std::vector<uint64_t> slot_sq(R);
   for (int r = 0; r < R; r++) slot_sq[r] = inbag[3 * R + r];
   int64_t fallbacks = 0;
+  std::unique_ptr<int64_t[]> sst_buf;  // split stats planes copied back per level
+  size_t sst_cap = 0;
   for (int level = 0; level <= D; level++) {
     const int M = (int)slots.size();
     if (M == 0) break;
@@ -2246,7 +2247,13 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     // stats planes [total][left][right] x [M][NS]; the host needs the left plane (a
     // node's total is known from its parent's split, right = total - left) and, at the
     // root, the totals
-    std::vector<int64_t> sst((size_t)M * 3 * NS);
+    // not value-initialized: at C5's deep levels M * 3 * NS words are ~50 MB, whose zero
+    // fill was most of the host's per-level split setup (14 ms per fit)
+    if (sst_cap < (size_t)M * 3 * NS) {
+      sst_cap = (size_t)M * 3 * NS;
+      sst_buf.reset(new int64_t[sst_cap]);
+    }
+    int64_t* sst = sst_buf.get();
     hmark(0);
     TRY(d2h(c, sout.data(), d_sout, (size_t)M));
     hmark(1);
@@ -2286,9 +2293,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       }
     }
     if (level == 0)
-      TRY(d2h(c, sst.data(), d_sstats, (size_t)2 * M * NS));
+      TRY(d2h(c, sst, d_sstats, (size_t)2 * M * NS));
     else
-      TRY(d2h(c, sst.data() + (size_t)M * NS, d_sstats + (size_t)M * NS, (size_t)M * NS));
+      TRY(d2h(c, sst + (size_t)M * NS, d_sstats + (size_t)M * NS, (size_t)M * NS));
     // --- node updates (RandomForest.findBestSplits, host part)
     struct Split {
       int slot, r, ni, li;
@@ -2587,7 +2594,24 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     // --- histograms of level+1: the smaller (or only) child of each split node
     void* hist_nxt;
     TRY(ws_get(c, hist_nxt_name, (size_t)Mn * slot_words * word_bytes, &hist_nxt));
-    HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * slot_words * word_bytes, c->stream));
+    {
+      // only the slots histogrammed below start from zero (the subtraction overwrites the
+      // rest): C5's deep levels memset ~10 GB per level otherwise.  A slot's u32 word
+      // count is a multiple of 4 (16-byte aligned slots) when slot_words * word_bytes is.
+      std::vector<int32_t> zs;
+      zs.reserve(hpar.size());
+      for (const ParentInfo& p : hpar) zs.push_back(p.hist_slot);
+      const int64_t u32w = slot_words * (int64_t)word_bytes / 4;
+      if ((u32w & 3) == 0 && !zs.empty()) {
+        int32_t* d_zs;
+        TRY(ws_typed(c, "zslots", zs.size(), &d_zs));
+        TRY(h2d(c, d_zs, zs.data(), zs.size()));
+        launch_zero_slots(c->stream, hist_nxt, d_zs, (int)zs.size(), u32w);
+        HIP_TRY(hipGetLastError());
+      } else if (!zs.empty()) {
+        HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * slot_words * word_bytes, c->stream));
+      }
+    }
     ha.ent_in = ent_nxt;
     ha.hist = hist_nxt;
     TRY(launch(g, gini ? kHistGini : kHistVar, T_HIST, hseg, hpar));

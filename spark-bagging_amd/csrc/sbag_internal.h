@@ -45,7 +45,7 @@ struct HistArgs {
   const int32_t* Fr;     // [R]
   const HistChunk* chunks;   // pieces: slices of node segments, in node order
   const int32_t* wg_piece;   // [nwg + 1]: workgroup w walks pieces [wg_piece[w], wg_piece[w+1])
-  const ParentInfo* parents; // per segment: replica (r) and histogram slot (hist_slot)
+  const ParentInfo* parents; // unused by the histogram kernels (HistChunk carries r/slot/tile)
   const uint64_t* ent_in;
   void* hist;            // [slot][Fmax][NB][NS] u64 (variance) or u32 (gini / counts)
   int32_t NB, NS;
@@ -219,6 +219,8 @@ void launch_split(hipStream_t st, const SplitArgs& a, int M, bool gini);
 void launch_split_screen(hipStream_t st, const SplitArgs& a, int M);
 void launch_zero_word(hipStream_t st, uint64_t* hist, const int32_t* d_slots, int nslots,
                       int64_t slot_words, int stride, int word);
+void launch_zero_slots(hipStream_t st, void* hist, const int32_t* d_slots, int nslots,
+                       int64_t u32_words_per_slot);
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words);
 void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,

@@ -2978,6 +2978,26 @@ __global__ __launch_bounds__(256) void k_subtract(W* __restrict__ dst_hist,
     dst_hist[d * words + w] = par_hist[p * words + w] - dst_hist[s * words + w];
 }
 
+// zero the listed histogram slots (u32 words): the slots the next level's histogram kernel
+// accumulates; the subtraction writes every word of the others
+__global__ __launch_bounds__(256) void k_zero_slots(uint32_t* __restrict__ hist,
+                                                    const int32_t* __restrict__ slots,
+                                                    int64_t words) {
+  uint4* h = (uint4*)(hist + (int64_t)slots[blockIdx.y] * words);
+  for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < words / 4; w += (int64_t)gridDim.x * 256)
+    h[w] = make_uint4(0, 0, 0, 0);
+  if (blockIdx.x == 0 && threadIdx.x < (words & 3))
+    hist[(int64_t)slots[blockIdx.y] * words + (words & ~3ll) + threadIdx.x] = 0u;
+}
+
+void launch_zero_slots(hipStream_t st, void* hist, const int32_t* d_slots, int nslots,
+                       int64_t u32_words_per_slot) {
+  if (nslots <= 0) return;
+  const unsigned gx = (unsigned)std::min<int64_t>((u32_words_per_slot / 4 + 255) / 256, 64);
+  hipLaunchKernelGGL(k_zero_slots, dim3(std::max(gx, 1u), (unsigned)nslots), dim3(256), 0, st,
+                     (uint32_t*)hist, d_slots, u32_words_per_slot);
+}
+
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words) {
   if (ntriples <= 0) return;
