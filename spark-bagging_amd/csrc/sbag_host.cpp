@@ -201,12 +201,16 @@ static int h2d(sbag_ctx* c, T* dst, const T* src, size_t count) {
     const size_t need = (bytes + 255) & ~(size_t)255;
     if (c->pin_used + need > c->pin_cap) {
       HIP_TRY(hipStreamSynchronize(c->stream));  // earlier uploads have been consumed
+      // an arena that ran out between two synchronizations grows (x2, to 256 MB), so a
+      // level's uploads (C5's deep levels: ~10 MB of pieces and tile bases) fit in it and
+      // the next level does not pay this synchronization again
+      const bool grow = need > c->pin_cap || (c->pin_used > 0 && c->pin_cap < ((size_t)256 << 20));
       c->pin_used = 0;
-      if (need > c->pin_cap) {
+      if (grow) {
         if (c->pin) HIP_TRY(hipHostFree(c->pin));
         c->pin = nullptr;
+        const size_t cap = std::max<size_t>({need, (size_t)8 << 20, std::min<size_t>(2 * c->pin_cap, (size_t)256 << 20)});
         c->pin_cap = 0;
-        const size_t cap = std::max<size_t>(need, (size_t)8 << 20);
         HIP_TRY(hipHostMalloc((void**)&c->pin, cap, hipHostMallocDefault));
         c->pin_cap = cap;
       }
@@ -1164,6 +1168,7 @@ static void build_work(const std::vector<std::pair<int64_t, int64_t>>& segs, int
   int64_t ps = tot / std::max<int64_t>(1, 2 * (int64_t)nwg_max);
   ps = std::max<int64_t>(T, std::min<int64_t>(ps_max, (ps + T - 1) / T * T));
   w.pieces.clear();
+  w.pieces.reserve(segs.size() + (size_t)(tot / ps) + 1);
   for (size_t q = 0; q < segs.size(); q++)
     for (int64_t a = segs[q].first; a < segs[q].second; a += ps)
       w.pieces.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + ps, segs[q].second), 0, 0, 0, 0});
@@ -1378,7 +1383,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   HIP_TRY(hipEventRecord(ev_start, c->stream));
   // host-side phase timing (SBAG_PROFILE_HOST=1 prints it): where the GPU waits
   const bool hprof = getenv("SBAG_PROFILE_HOST") != nullptr;
-  double hp[16] = {0};
+  double hp[20] = {0};  // [16..19]: inside histogram launches (grouping, work lists, launch)
   auto hnow = [] {
     return std::chrono::duration<double, std::milli>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -1561,12 +1566,20 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     launch_tile_count(c->stream, d_pcs, np, ha.ent_in, CT, ntc, d_cnt);
     HIP_TRY(hipGetLastError());
     std::vector<uint32_t> cnt((size_t)np * ntc);
+    double gt0 = hprof ? hnow() : 0.0;
     TRY(d2h(c, cnt.data(), d_cnt, cnt.size()));
+    if (hprof) {
+      const double t = hnow();
+      hp[18] += t - gt0;  // waiting for the counts (and the queue ahead of them)
+      gt0 = t;
+    }
     // sub-segment of (q, t) at segs[q].first + sum of the tiles before t; pieces of q
     // fill it in piece order
     std::vector<int64_t> base((size_t)np * ntc);
     gsegs.clear();
     gpar.clear();
+    gsegs.reserve((size_t)segs.size() * ntc);
+    gpar.reserve((size_t)segs.size() * ntc);
     for (int p0 = 0; p0 < np;) {
       int p1 = p0;
       while (p1 < np && pseg[p1] == pseg[p0]) p1++;
@@ -1587,6 +1600,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       }
       p0 = p1;
     }
+    if (hprof) hp[19] += hnow() - gt0;  // host prefix and sub-segment lists
     TRY(h2d(c, d_base, base.data(), base.size()));
     launch_tile_scatter(c->stream, d_pcs, np, ha.ent_in, CT, ntc, d_base, d_entg);
     HIP_TRY(hipGetLastError());
@@ -1617,6 +1631,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     const int wpc = std::max(1, std::min(grouped ? 4 : 2, (int)((160 * 1024) / g.lds)));
     const uint64_t* ent_saved = ha.ent_in;
     int ntiles = g.ntiles;
+    double lt0 = hprof ? hnow() : 0.0;
     if (grouped) {  // timed apart from the histogram kernel (group_ms)
       const int hg = tm.begin(cat == T_HIST ? T_GROUP : cat);
       uint64_t* d_entg = nullptr;
@@ -1624,6 +1639,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       tm.end(hg);
       ha.ent_in = d_entg;
       ntiles = g.ntf;
+    }
+    if (hprof) {
+      const double t = hnow();
+      hp[16] += t - lt0;
+      lt0 = t;
     }
     ha.grouped = grouped ? 1 : 0;
     // k_hist gathers aligned 4-byte words (SBAG_HIST_GW=1: single bytes, as before round 2e;
@@ -1634,6 +1654,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     const std::vector<ParentInfo>& par = grouped ? gpar : par_in;
     build_work(segs, flush_limit, 256 * wpc * (grouped ? 2 : 1), g.T, work);
     TRY(upload_work(par));
+    if (hprof) {
+      const double t = hnow();
+      hp[17] += t - lt0;
+      lt0 = t;
+    }
     ha.chunks = d_pieces;
     ha.wg_piece = d_wg;
     ha.parents = nullptr;
@@ -2709,9 +2734,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   if (hprof)
     fprintf(stderr, "host ms: setup+sample-launch %.2f compact-wait %.2f valuecounts %.2f thresholds %.2f "
                     "bins %.2f | split-prep %.2f split-wait %.2f nodes %.2f part-cursors %.2f part-sort %.2f "
-                    "part-upload %.2f part-wait %.2f children %.2f hist-prep %.2f loop %.2f | emit %.2f\n",
+                    "part-upload %.2f part-wait %.2f children %.2f hist-prep %.2f loop %.2f | emit %.2f"
+                    " | in hist launches: grouping %.2f (count wait %.2f, prefix %.2f) work lists %.2f\n",
             hp[8], hp[9], hp[10], hp[11], hp[12], hp[0], hp[1], hp[2], hp[13], hp[14], hp[3], hp[4], hp[5],
-            hp[6], hp[7], hp[15]);
+            hp[6], hp[7], hp[15], hp[16], hp[18], hp[19], hp[17]);
   *out = forest.release();
   return SBAG_OK;
 }
