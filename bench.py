@@ -28,11 +28,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
 LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
 # committed rocprofv3 PMC summaries of this command per workload (scripts/profile.sh +
 # scripts/pmc_summary.py); the newest one present is used
-PMC_SUMMARIES = {"c3": ["profiles/r02d/c3/summary.json", "profiles/r02c/c3/summary.json",
-                        "profiles/r01g/summary.json"],
+PMC_SUMMARIES = {"c3": ["profiles/r02f/c3/summary.json", "profiles/r02e/c3/summary.json",
+                        "profiles/r02d/c3/summary.json", "profiles/r01g/summary.json"],
                  "c4": ["profiles/r02/c4/summary.json"],
-                 "c5": ["profiles/r02d/c5/summary.json", "profiles/r02/c5/summary.json",
-                        "profiles/r01g_c5/summary.json"]}
+                 "c5": ["profiles/r02f/c5/summary.json", "profiles/r02e/c5/summary.json",
+                        "profiles/r02d/c5/summary.json", "profiles/r01g_c5/summary.json"]}
 
 
 def pmc_traffic(workload):
@@ -76,7 +76,7 @@ def hist_kernel_name(F, cls, N):
     hist_geometry): row lanes when roundup(F, 16) < roundup(F, 64)."""
     if cls:
         # gini tiles shrink features and classes to fit the LDS target; the variant is
-        # not predicted here (C5 runs sbag::k_hist<0, 1>: profiles/r01g_c5/)
+        # not predicted here (C5 runs sbag::k_hist<0, 1, 4>: profiles/r02e/c5/)
         return "sbag::k_hist* (kHistGini, class tiles; variant per hist_geometry)"
     ft = min(F, 256)
     mode = "0" if cls else "1"
