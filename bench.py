@@ -26,11 +26,13 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
 # ds_add_u64 throughput measured on MI355X by scripts/micro/lds_atomic.hip:
 # 7.16 cycles per wave-instruction per CU (4 x 512-thread workgroups per CU), 256 CUs, 2.4 GHz
 LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
+# ds_add_u32 (the gini class counts): 5.97 cycles per wave-instruction, same micro-benchmark
+LDS_ATOMIC_PEAK_U32 = 256 * 2.4e9 / 5.97
 # committed rocprofv3 PMC summaries of this command per workload (scripts/profile.sh +
 # scripts/pmc_summary.py); the newest one present is used
 PMC_SUMMARIES = {"c3": ["profiles/r02f/c3/summary.json", "profiles/r02e/c3/summary.json",
                         "profiles/r02d/c3/summary.json", "profiles/r01g/summary.json"],
-                 "c4": ["profiles/r02/c4/summary.json"],
+                 "c4": ["profiles/r02f/c4/summary.json"],
                  "c5": ["profiles/r02f/c5/summary.json", "profiles/r02e/c5/summary.json",
                         "profiles/r02d/c5/summary.json", "profiles/r01g_c5/summary.json"]}
 
@@ -226,6 +228,7 @@ def main():
     # packed (count, sum) word after the screening of DESIGN.md §5; gini: ds_add_u32)
     lds_instr = sum(t["hist_lds_atomics"] for t in timings)
     lds_rate = lds_instr / (hist_ms / 1e3) if hist_ms > 0 else 0.0
+    lds_peak = LDS_ATOMIC_PEAK_U32 if cls else LDS_ATOMIC_PEAK
     traffic, traffic_src, traffic_kernel = pmc_traffic(args.workload)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -247,9 +250,10 @@ def main():
                                      "sibling histograms from k_subtract count as if read"},
                 "binding_limiter": "lds_atomic",
                 "lds_atomic": {"achieved": round(lds_rate / 1e9, 2),
-                               "peak": round(LDS_ATOMIC_PEAK / 1e9, 2),
-                               "unit": "G wave-instr/s (ds_add_u64 peak, scripts/micro/lds_atomic.hip)",
-                               "frac": round(lds_rate / LDS_ATOMIC_PEAK, 4)}}
+                               "peak": round(lds_peak / 1e9, 2),
+                               "unit": "G wave-instr/s (%s peak, scripts/micro/lds_atomic.hip)"
+                                       % ("ds_add_u32" if cls else "ds_add_u64"),
+                               "frac": round(lds_rate / lds_peak, 4)}}
     breakdown = {k: round(v, 3) for k, v in timings[-1].items() if k.endswith("_ms")}
     # the sampler's cost depends on rows per partition stream (Poisson.scala:53-56 reseeds
     # per partition): one extra fit, outside the timed region, at P = nproc
