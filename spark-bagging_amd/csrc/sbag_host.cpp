@@ -1628,7 +1628,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
                     const std::vector<ParentInfo>& par_in) -> int {
     const bool grouped = g.grouped && mode == kHistGini && !ha.count_only;
     // 16 waves per CU (two 512-thread workgroups), 32 for grouped class tiles
-    const int wpc = std::max(1, std::min(grouped ? 4 : 2, (int)((160 * 1024) / g.lds)));
+    static const int wpc_env = getenv("SBAG_HIST_WPC") ? atoi(getenv("SBAG_HIST_WPC")) : 0;
+    const int wpc = std::max(1, std::min(wpc_env > 0 ? wpc_env : (grouped ? 4 : 2),
+                                         (int)((160 * 1024) / g.lds)));
     const uint64_t* ent_saved = ha.ent_in;
     int ntiles = g.ntiles;
     double lt0 = hprof ? hnow() : 0.0;
@@ -1650,6 +1652,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     // 8-byte words were slower on C5, 134 vs 98 ms per fit)
     static const int hist_gw = getenv("SBAG_HIST_GW") ? atoi(getenv("SBAG_HIST_GW")) : 4;
     ha.dw = hist_gw == 1 ? 1 : 4;
+    // k_hist_rl row prefetch distance in passes of 4 entries (C3, ms per fit: 2 -> hist 92.1,
+    // 3 -> 90.2 and step 134, 4 -> hist 89.7 and step 130; SBAG_HIST_RL_PD=5 for the next)
+    static const int rlpd = getenv("SBAG_HIST_RL_PD") ? atoi(getenv("SBAG_HIST_RL_PD")) : 4;
+    ha.rlpd = rlpd;
     const std::vector<std::pair<int64_t, int64_t>>& segs = grouped ? gsegs : segs_in;
     const std::vector<ParentInfo>& par = grouped ? gpar : par_in;
     build_work(segs, flush_limit, 256 * wpc * (grouped ? 2 : 1), g.T, work);

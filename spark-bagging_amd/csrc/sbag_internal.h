@@ -61,6 +61,8 @@ struct HistArgs {
                          // blockIdx.y walks feature tiles only
   int32_t dw;            // k_hist gather width: 1 (byte loads) or 4 (aligned words + extract)
   int32_t hct;           // gini layout class tile: hist[slot][NS / hct][Fmax][NB][hct]
+  int32_t rlpd;          // k_hist_rl: rows loaded this many passes ahead (2 or 3)
+  int32_t pad2_;
 };
 
 // Gini histogram cell (f, b, c) of one slot: class-tile-major, so that a class tile's

@@ -1754,40 +1754,42 @@ struct RlLane {  // per-lane constants of the current (replica, tile)
 // one batch of n <= 64 entries (16 passes of 4 entries), row bytes two passes ahead and
 // entries three passes ahead.  FULL: n == 64 from global memory, no bounds checks.
 // src: the batch's entries, global (ent_in + q0) or the wave's LDS stage.
-template <int MODE, int K, bool OFF32, bool FULL>
+template <int MODE, int K, bool OFF32, bool FULL, int PD>
 __device__ __forceinline__ void rl_batch(unsigned char* smem, const uint64_t* src, int n,
                                          int eo, const RlLane& L, uint32_t S, uint32_t amul,
                                          int csh, int32_t K0, int c0, uint32_t cstride) {
+  // rows PD passes ahead, entries PD + 1
   const int npass = FULL ? 16 : (n + kRlEP - 1) / kRlEP;
   auto fetch = [&](int t) -> uint64_t {
     const int i = t * kRlEP + eo;
     if (FULL) return src[i];
     return i < n ? src[i] : 0ull;
   };
-  // rows two passes ahead, entries three
-  uint64_t e0 = fetch(0), e1 = 0, e2 = 0, e3 = 0;
-  if (FULL || 1 < npass) e1 = fetch(1);
-  if (FULL || 2 < npass) e2 = fetch(2);
-  RlRaw<K> r0, r1, r2;
-  rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)e0, r0);
-  if (FULL || 1 < npass) rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)e1, r1);
+  uint64_t ev[PD + 2];
+  RlRaw<K> rb[PD + 1];
+#pragma unroll
+  for (int j = 0; j <= PD; j++) ev[j] = (FULL || j < npass) ? fetch(j) : 0ull;
+  ev[PD + 1] = 0;
+#pragma unroll
+  for (int j = 0; j < PD; j++)
+    if (FULL || j < npass) rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)ev[j], rb[j]);
 #pragma unroll
   for (int t = 0; t < 16; t++) {
     if (!FULL && t >= npass) break;
-    if (FULL ? t + 3 < 16 : t + 3 < npass) e3 = fetch(t + 3);
-    if (FULL ? t + 2 < 16 : t + 2 < npass) rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)e2, r2);
+    if (FULL ? t + PD + 1 < 16 : t + PD + 1 < npass) ev[PD + 1] = fetch(t + PD + 1);
+    if (FULL ? t + PD < 16 : t + PD < npass)
+      rl_load<K, OFF32>(L.binsr, L.loff, S, (uint32_t)ev[PD], rb[PD]);
     uint32_t wl, wh, lb = L.lb;
-    rl_words<MODE>(e0, csh, K0, c0, cstride, wl, wh, lb);
-    rl_add<MODE, K>(smem, r0, L.sh, amul, lb, wl, wh);
-    e0 = e1;
-    e1 = e2;
-    e2 = e3;
-    r0 = r1;
-    r1 = r2;
+    rl_words<MODE>(ev[0], csh, K0, c0, cstride, wl, wh, lb);
+    rl_add<MODE, K>(smem, rb[0], L.sh, amul, lb, wl, wh);
+#pragma unroll
+    for (int j = 0; j <= PD; j++) ev[j] = ev[j + 1];
+#pragma unroll
+    for (int j = 0; j < PD; j++) rb[j] = rb[j + 1];
   }
 }
 
-template <int MODE, int K, bool OFF32>
+template <int MODE, int K, bool OFF32, int PD>
 __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
   constexpr bool GINI = MODE == kHistGini;
@@ -1872,12 +1874,12 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         if (nm > 0)
-          rl_batch<MODE, K, OFF32, false>(smem, stage, nm, eo, L, S, amul, csh, K0, c0, plane);
+          rl_batch<MODE, K, OFF32, false, PD>(smem, stage, nm, eo, L, S, amul, csh, K0, c0, plane);
         __builtin_amdgcn_wave_barrier();
       } else if (n == 64) {
-        rl_batch<MODE, K, OFF32, true>(smem, A.ent_in + q0, 64, eo, L, S, amul, csh, K0, c0, plane);
+        rl_batch<MODE, K, OFF32, true, PD>(smem, A.ent_in + q0, 64, eo, L, S, amul, csh, K0, c0, plane);
       } else {
-        rl_batch<MODE, K, OFF32, false>(smem, A.ent_in + q0, n, eo, L, S, amul, csh, K0, c0, plane);
+        rl_batch<MODE, K, OFF32, false, PD>(smem, A.ent_in + q0, n, eo, L, S, amul, csh, K0, c0, plane);
       }
     }
   }
@@ -1887,18 +1889,26 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
   }
 }
 
-template <int K, bool OFF32>
-static void launch_hist_rl_ko(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
-  for (const void* f : {(const void*)k_hist_rl<kHistGini, K, OFF32>,
-                        (const void*)k_hist_rl<kHistVar, K, OFF32>,
-                        (const void*)k_hist_rl<kHistSq, K, OFF32>})
+template <int K, bool OFF32, int PD>
+static void launch_hist_rl_kop(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
+  for (const void* f : {(const void*)k_hist_rl<kHistGini, K, OFF32, PD>,
+                        (const void*)k_hist_rl<kHistVar, K, OFF32, PD>,
+                        (const void*)k_hist_rl<kHistSq, K, OFF32, PD>})
     set_max_lds(f, 160 * 1024);
   if (mode == kHistGini)
-    hipLaunchKernelGGL((k_hist_rl<kHistGini, K, OFF32>), grid, dim3(kHistThreads), lds, st, a);
+    hipLaunchKernelGGL((k_hist_rl<kHistGini, K, OFF32, PD>), grid, dim3(kHistThreads), lds, st, a);
   else if (mode == kHistVar)
-    hipLaunchKernelGGL((k_hist_rl<kHistVar, K, OFF32>), grid, dim3(kHistThreads), lds, st, a);
+    hipLaunchKernelGGL((k_hist_rl<kHistVar, K, OFF32, PD>), grid, dim3(kHistThreads), lds, st, a);
   else
-    hipLaunchKernelGGL((k_hist_rl<kHistSq, K, OFF32>), grid, dim3(kHistThreads), lds, st, a);
+    hipLaunchKernelGGL((k_hist_rl<kHistSq, K, OFF32, PD>), grid, dim3(kHistThreads), lds, st, a);
+}
+
+template <int K, bool OFF32>
+static void launch_hist_rl_ko(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
+  if (a.rlpd >= 5)
+    launch_hist_rl_kop<K, OFF32, 5>(st, a, grid, lds, mode);
+  else
+    launch_hist_rl_kop<K, OFF32, 4>(st, a, grid, lds, mode);
 }
 
 template <int K>
