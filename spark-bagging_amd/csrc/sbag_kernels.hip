@@ -1272,13 +1272,38 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
   uint64_t* er = ent + (int64_t)r * cap;
   unsigned long long mysum = 0, mysq = 0;
   unsigned int mymax = 0;
+  // all 8 iterations' count words and labels are loaded up front (one dword and one
+  // 16-byte load each when the rows are whole and aligned): the loop's barriers and cursor
+  // atomic then no longer wait on them one iteration at a time
+  const bool vec = ((N | (int64_t)(uintptr_t)cr) & 3) == 0 && ((uintptr_t)labk & 15) == 0;
+  uint32_t cw[8];
+  int4 lk[8];
+#pragma unroll
+  for (int it = 0; it < 8; it++) {
+    const int64_t row0 = chunk * 8192 + (int64_t)it * 1024 + (int64_t)tid * 4;
+    if (vec && row0 + 3 < N) {
+      cw[it] = *(const uint32_t*)(cr + row0);
+      lk[it] = *(const int4*)(labk + row0);
+    } else {
+      cw[it] = 0;
+      int l4[4] = {0, 0, 0, 0};
+      for (int j = 0; j < 4; j++)
+        if (row0 + j < N) {
+          cw[it] |= (uint32_t)cr[row0 + j] << (8 * j);
+          l4[j] = labk[row0 + j];
+        }
+      lk[it] = make_int4(l4[0], l4[1], l4[2], l4[3]);
+    }
+  }
+#pragma unroll
   for (int it = 0; it < 8; it++) {
     const int64_t row0 = chunk * 8192 + (int64_t)it * 1024 + (int64_t)tid * 4;
     uint32_t c[4];
+    const int32_t kk[4] = {lk[it].x, lk[it].y, lk[it].z, lk[it].w};
     int n = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      c[j] = (row0 + j < N) ? cr[row0 + j] : 0u;
+      c[j] = (cw[it] >> (8 * j)) & 0xffu;
       n += c[j] ? 1 : 0;
       mysum += c[j];
       mymax = max(mymax, c[j]);
@@ -1297,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
 #pragma unroll
     for (int j = 0; j < 4; j++)
       if (c[j]) {
-        const int32_t k = labk[row0 + j];
+        const int32_t k = kk[j];
         mysq += (unsigned long long)c[j] * (unsigned long long)((int64_t)k * k);
         er[pos++] = pack_entry((uint32_t)(row0 + j), k, c[j]);
       }
