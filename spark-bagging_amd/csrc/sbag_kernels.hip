@@ -2075,8 +2075,8 @@ void launch_hist(hipStream_t st, const HistArgs& a, int nwg, int ntiles, int mod
 
 size_t hist_lds_limit() { return 160 * 1024; }
 
-// ---- partition: 8 entries per lane per step, one cursor atomic per workgroup and
-// side for 2048 entries.  Pieces are handed out dynamically in split-column order
+// ---- partition: kPartK entries per lane per step, one cursor atomic per workgroup and
+// side for 64 * 4 * kPartK entries.  Pieces are handed out dynamically in split-column order
 // (parents of one column interleaved), so at any time the whole GPU gathers from
 // one or two columns of the column-major bins copy: a column (N bytes) stays in
 // the MALL / L2 while every node that splits on it is routed, instead of each
