@@ -2446,7 +2446,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       // 8192 entries interleaved round-robin across the parents of a group, so the
       // concurrent workgroups spread over the group's cursors while the GPU reads
       // one column
-      const int64_t piece = 8192;
+      static const int64_t piece =
+          getenv("SBAG_PART_PIECE") ? std::max<int64_t>(1024, atoll(getenv("SBAG_PART_PIECE"))) : 8192;
       // the gathered object: a side-bit plane (column, split) once parents are many (with
       // few parents, finer groups would crowd the workgroups onto fewer cursors), else a
       // column byte array.  Crossover measured at 128-256 parents (C5 level 3 / 4: cols
