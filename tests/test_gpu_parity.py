@@ -255,6 +255,36 @@ def test_gini_class_tiles_forced(ctx, monkeypatch):
     assert_forest_equal(forest, orf)
 
 
+@pytest.mark.parametrize("min_gain", [0.0, 0.02])
+def test_gini_screen_exact_ties_and_min_gain(ctx, min_gain):
+    """The gini split screen (cheap 1 - sum l^2/lt^2 against the block's best exact gain of
+    earlier feature groups) must keep Spark's choice: duplicated columns in later feature
+    groups tie the earlier ones exactly (first feature wins), and minInfoGain near the
+    gains decides leaves on the exact fp64 gain.  64 classes: grouped class tiles and the
+    class-tile-major histogram layout."""
+    ds0 = nat.DeviceDataset.synthetic(20000, 40, seed=29, num_classes=64, ctx=ctx)
+    X0, y = ds0.features(), ds0.labels()
+    X = np.ascontiguousarray(np.concatenate([X0, X0[:, :12], X0[:, 5:9]], axis=1))
+    forest, orf, _ = _fit_both(ctx, X, y, 3, replacement=False, ratio=1.0, seed=SEED_CLS,
+                               depth=9, bins=32, cls=True, min_gain=min_gain, min_inst=2)
+    assert_forest_equal(forest, orf)
+
+
+@pytest.mark.parametrize("classes,lds_kb,layout", [(64, None, "1"), (10, "29", None),
+                                                   (12, "29", None), (12, "12", None)])
+def test_gini_tile_layouts(ctx, monkeypatch, classes, lds_kb, layout):
+    """Class tiles that divide the classes store the histogram class-tile-major (12 classes
+    in tiles of 3: scalar flush and staging paths; tiles of 1); tiles that do not (10
+    classes in tiles of 3) keep the [f][b][NS] layout; SBAG_NO_TILE_LAYOUT=1 forces the
+    plain layout.  Every case bit-exact against the oracle."""
+    if lds_kb:
+        monkeypatch.setenv("SBAG_HIST_GROUPED_LDS_KB", lds_kb)
+    if layout:
+        monkeypatch.setenv("SBAG_NO_TILE_LAYOUT", layout)
+    ds, X, forest, orf = _synthetic_cls(ctx, 16000, 60, classes, 3, 9, seed_data=31)
+    assert_forest_equal(forest, orf)
+
+
 def test_transform_batches_nan_and_signed_zero(ctx, cpusmall, monkeypatch):
     """Batched host-row transform (rows binned on the device against the forest's
     thresholds): several upload batches, NaN (Spark: `NaN <= t` is false -> right),
