@@ -1623,6 +1623,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     if (!gini || getenv("SBAG_NO_TILE_LAYOUT")) return NS;
     return (g.grouped && g.CT < NS && NS % g.CT == 0) ? g.CT : NS;
   };
+  std::function<int()> pre_hist;  // queued by launch() right before the histogram kernel
   auto launch = [&](const HistGeom& g, int mode, int cat,
                     const std::vector<std::pair<int64_t, int64_t>>& segs_in,
                     const std::vector<ParentInfo>& par_in) -> int {
@@ -1673,6 +1674,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     ha.CT = g.CT;
     ha.ntf = g.ntf;
     ha.rl = g.rl;
+    if (pre_hist) TRY(pre_hist());
     int h = tm.begin(cat);
     launch_hist(c->stream, ha, work.nwg, ntiles, mode, g.lds);
     HIP_TRY(hipGetLastError());
@@ -2626,10 +2628,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     // --- histograms of level+1: the smaller (or only) child of each split node
     void* hist_nxt;
     TRY(ws_get(c, hist_nxt_name, (size_t)Mn * slot_words * word_bytes, &hist_nxt));
-    {
-      // only the slots histogrammed below start from zero (the subtraction overwrites the
-      // rest): C5's deep levels memset ~10 GB per level otherwise.  A slot's u32 word
-      // count is a multiple of 4 (16-byte aligned slots) when slot_words * word_bytes is.
+    // only the slots histogrammed below start from zero (the subtraction overwrites the
+    // rest): C5's deep levels memset ~10 GB per level otherwise.  A slot's u32 word count
+    // is a multiple of 4 (16-byte aligned slots) when slot_words * word_bytes is.  Queued
+    // by launch() after the class-tile grouping's count pass, so the host's wait for the
+    // counts does not include the zeroing.
+    pre_hist = [&, hist_nxt, Mn]() -> int {
       std::vector<int32_t> zs;
       zs.reserve(hpar.size());
       for (const ParentInfo& p : hpar) zs.push_back(p.hist_slot);
@@ -2643,10 +2647,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       } else if (!zs.empty()) {
         HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * slot_words * word_bytes, c->stream));
       }
-    }
+      return SBAG_OK;
+    };
     ha.ent_in = ent_nxt;
     ha.hist = hist_nxt;
     TRY(launch(g, gini ? kHistGini : kHistVar, T_HIST, hseg, hpar));
+    pre_hist = nullptr;
     if (!triples.empty()) {
       int32_t* d_tri;
       TRY(ws_typed(c, "triples", triples.size(), &d_tri));
