@@ -1369,9 +1369,10 @@ void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, con
 // per (workgroup, node run).  Inside a run the waves are independent (no
 // barrier): each takes batches of 64 consecutive entries; lane i loads entry i
 // and computes its stat words, then for every entry of the batch the wave
-// broadcasts row and words (readlane), lane fl loads byte pos[fl] of that row
-// straight from the row's cache line (global_load_ubyte, SGPR row base + VGPR
-// column) one group of 8 entries ahead, and adds the words into
+// broadcasts row and words (readlane), lane fl loads the aligned 4-byte word holding
+// byte pos[fl] of that row straight from the row's cache line (SGPR row base + VGPR
+// column; HistArgs.dw = 1: the byte itself) one group of entries ahead, extracts the
+// byte, and adds the words into
 // [plane][bin][feature] with one LDS atomic per plane.  The LDS atomic pipe is
 // the only shared resource, and it only carries the atomics.
 //
