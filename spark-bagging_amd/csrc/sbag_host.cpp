@@ -1654,10 +1654,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     static const int hist_gw = getenv("SBAG_HIST_GW") ? atoi(getenv("SBAG_HIST_GW")) : 4;
     ha.dw = hist_gw == 1 ? 1 : 4;
     // k_hist_rl row prefetch distance in passes of 4 entries (C3, ms per fit: 2 -> hist 92.1,
-    // 3 -> 90.2 and step 134, 4 -> hist 89.7 and step 130, 5 -> flat; built: 4 and 5,
-    // SBAG_HIST_RL_PD >= 5 selects 5)
-    static const int rlpd = getenv("SBAG_HIST_RL_PD") ? atoi(getenv("SBAG_HIST_RL_PD")) : 4;
-    ha.rlpd = rlpd;
+    // 3 -> 90.2 and step 134, 4 -> hist 89.7 and step 130, 5 -> flat); only 4 is built
+    ha.rlpd = 4;
     const std::vector<std::pair<int64_t, int64_t>>& segs = grouped ? gsegs : segs_in;
     const std::vector<ParentInfo>& par = grouped ? gpar : par_in;
     build_work(segs, flush_limit, 256 * wpc * (grouped ? 2 : 1), g.T, work);

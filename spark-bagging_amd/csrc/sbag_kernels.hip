@@ -1931,10 +1931,9 @@ static void launch_hist_rl_kop(hipStream_t st, const HistArgs& a, dim3 grid, siz
 
 template <int K, bool OFF32>
 static void launch_hist_rl_ko(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds, int mode) {
-  if (a.rlpd >= 5)
-    launch_hist_rl_kop<K, OFF32, 5>(st, a, grid, lds, mode);
-  else
-    launch_hist_rl_kop<K, OFF32, 4>(st, a, grid, lds, mode);
+  // rows four passes ahead (HistArgs.rlpd documents it; 2, 3 and 5 were measured, 4 is
+  // the one built)
+  launch_hist_rl_kop<K, OFF32, 4>(st, a, grid, lds, mode);
 }
 
 template <int K>
