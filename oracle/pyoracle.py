@@ -79,8 +79,13 @@ def bytes_hash(data, seed):
 
 
 def hash_seed(seed):
-    """XORShiftRandom.hashSeed"""
-    b = struct.pack(">q", _i64(seed))
+    """XORShiftRandom.hashSeed (Spark 2.4.3).
+
+    `ByteBuffer.allocate(java.lang.Long.SIZE).putLong(seed)`: Long.SIZE = 64 is a bit count
+    used as a byte count, so 64 bytes are hashed -- the big-endian seed and 56 zero bytes
+    (Spark 3.0 hashes 8). Anchors: tests/test_oracle.py::test_xorshift_spark2_anchors.
+    """
+    b = struct.pack(">q", _i64(seed)) + bytes(56)
     lo = bytes_hash(b, 0x3C074A61)
     hi = bytes_hash(b, lo)
     return ((hi << 32) | lo) & M64

@@ -66,12 +66,20 @@ static uint32_t mm3_bytes_hash(const uint8_t* d, int len, uint32_t seed) {
   return mm3_finalize(h, (uint32_t)len);
 }
 
+/* Spark 2.4.3 XORShiftRandom.hashSeed:
+ *   ByteBuffer.allocate(java.lang.Long.SIZE).putLong(seed).array()
+ * Long.SIZE is 64 (bits) but allocate() takes bytes, so the hashed buffer is 64 bytes: the
+ * big-endian seed followed by 56 zero bytes (Spark 3.0 changed this to Long.BYTES = 8).
+ * Pinned by tests/test_oracle.py: XORShiftRandom(0|30|5419823303878592871).nextDouble()
+ * = 0.8446490682263027 | 0.31429268272540556 | 0.2304755080444375 (published 2.x values). */
+#define OR_HASH_SEED_BYTES 64
 uint64_t or_hash_seed(int64_t seed) {
-  uint8_t b[8];
+  uint8_t b[OR_HASH_SEED_BYTES];
+  memset(b, 0, sizeof b);
   uint64_t u = (uint64_t)seed;
   for (int i = 0; i < 8; i++) b[i] = (uint8_t)(u >> (56 - 8 * i)); /* ByteBuffer.putLong: big endian */
-  uint32_t lo = mm3_bytes_hash(b, 8, 0x3c074a61u);                  /* MurmurHash3.arraySeed */
-  uint32_t hi = mm3_bytes_hash(b, 8, lo);
+  uint32_t lo = mm3_bytes_hash(b, OR_HASH_SEED_BYTES, 0x3c074a61u); /* MurmurHash3.arraySeed */
+  uint32_t hi = mm3_bytes_hash(b, OR_HASH_SEED_BYTES, lo);
   return ((uint64_t)hi << 32) | (uint64_t)lo;
 }
 

@@ -248,14 +248,18 @@ static uint32_t h_mix(uint32_t h, uint32_t k) {
   h = h_rotl(h, 13);
   return h * 5u + 0xe6546b64u;
 }
-static uint32_t h_hash8(const uint8_t* d, uint32_t seed) {
+// Spark 2.4.3 hashes ByteBuffer.allocate(java.lang.Long.SIZE).putLong(seed): Long.SIZE is 64
+// bits used as a byte count, so the buffer is 64 bytes (big-endian seed + 56 zero bytes).
+// Spark 3.0 switched to Long.BYTES; the reference pins 2.4.3 (build.sbt:1).
+static constexpr int kHashSeedBytes = 64;
+static uint32_t h_hash_buf(const uint8_t* d, uint32_t seed) {
   uint32_t h = seed;
-  for (int i = 0; i < 8; i += 4) {
+  for (int i = 0; i < kHashSeedBytes; i += 4) {
     const uint32_t k = (uint32_t)d[i] | ((uint32_t)d[i + 1] << 8) | ((uint32_t)d[i + 2] << 16) |
                        ((uint32_t)d[i + 3] << 24);
     h = h_mix(h, k);
   }
-  h ^= 8u;
+  h ^= (uint32_t)kHashSeedBytes;
   h ^= h >> 16;
   h *= 0x85ebca6bu;
   h ^= h >> 13;
@@ -264,11 +268,11 @@ static uint32_t h_hash8(const uint8_t* d, uint32_t seed) {
   return h;
 }
 static uint64_t h_hash_seed(int64_t seed) {
-  uint8_t b[8];
+  uint8_t b[kHashSeedBytes] = {};
   const uint64_t u = (uint64_t)seed;
   for (int i = 0; i < 8; i++) b[i] = (uint8_t)(u >> (56 - 8 * i));
-  const uint32_t lo = h_hash8(b, 0x3c074a61u);
-  const uint32_t hi = h_hash8(b, lo);
+  const uint32_t lo = h_hash_buf(b, 0x3c074a61u);
+  const uint32_t hi = h_hash_buf(b, lo);
   return ((uint64_t)hi << 32) | lo;
 }
 static uint64_t h_xs_step(uint64_t s) {

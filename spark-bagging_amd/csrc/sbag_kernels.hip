@@ -1134,9 +1134,14 @@ __device__ __forceinline__ uint32_t d_mix(uint32_t h, uint32_t k) {
   h = d_rotl(h, 13);
   return h * 5u + 0xe6546b64u;
 }
-__device__ uint32_t d_hash8(uint32_t k0, uint32_t k1, uint32_t seed) {
+// MurmurHash3.bytesHash of Spark 2.4.3's 64-byte hashSeed buffer
+// (ByteBuffer.allocate(java.lang.Long.SIZE): the seed's 8 big-endian bytes, then 56 zeros).
+// A zero block leaves mix_last's h unchanged, so those 14 blocks are plain mix(h, 0).
+__device__ uint32_t d_hash64(uint32_t k0, uint32_t k1, uint32_t seed) {
   uint32_t h = d_mix(d_mix(seed, k0), k1);
-  h ^= 8u;
+#pragma unroll
+  for (int i = 0; i < 14; i++) h = d_rotl(h, 13) * 5u + 0xe6546b64u;
+  h ^= 64u;
   h ^= h >> 16;
   h *= 0x85ebca6bu;
   h ^= h >> 13;
@@ -1144,7 +1149,7 @@ __device__ uint32_t d_hash8(uint32_t k0, uint32_t k1, uint32_t seed) {
   h ^= h >> 16;
   return h;
 }
-__device__ uint64_t d_hash_seed(int64_t seed) {  // XORShiftRandom.hashSeed
+__device__ uint64_t d_hash_seed(int64_t seed) {  // XORShiftRandom.hashSeed (Spark 2.4.3)
   const uint64_t u = (uint64_t)seed;
   // big-endian bytes b0..b7; little-endian 4-byte blocks of that array
   const uint32_t b0 = (uint32_t)(u >> 56) & 0xff, b1 = (uint32_t)(u >> 48) & 0xff;
@@ -1153,8 +1158,8 @@ __device__ uint64_t d_hash_seed(int64_t seed) {  // XORShiftRandom.hashSeed
   const uint32_t b6 = (uint32_t)(u >> 8) & 0xff, b7 = (uint32_t)u & 0xff;
   const uint32_t k0 = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
   const uint32_t k1 = b4 | (b5 << 8) | (b6 << 16) | (b7 << 24);
-  const uint32_t lo = d_hash8(k0, k1, 0x3c074a61u);
-  const uint32_t hi = d_hash8(k0, k1, lo);
+  const uint32_t lo = d_hash64(k0, k1, 0x3c074a61u);
+  const uint32_t hi = d_hash64(k0, k1, lo);
   return ((uint64_t)hi << 32) | (uint64_t)lo;
 }
 __device__ __forceinline__ uint64_t xs_step(uint64_t s) {

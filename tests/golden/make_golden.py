@@ -46,6 +46,11 @@ def rng_fixtures():
                                      for s in seeds[:6]}
         g = po.poisson_stream(lam, SEED_REG)
         assert out["poisson"][repr(lam)][str(SEED_REG)] == [next(g) for _ in range(64)]
+    # published Spark 2.x XORShiftRandom(seed).nextDouble() values (hashSeed over 64 bytes)
+    out["spark2_anchors"] = {"0": 0.8446490682263027, "30": 0.31429268272540556,
+                             "5419823303878592871": 0.2304755080444375}
+    for s, want in out["spark2_anchors"].items():
+        assert oracle.xorshift_doubles(int(s), 1)[0] == want, s
     with open(os.path.join(OUT, "rng.json"), "w") as fh:
         json.dump(out, fh, indent=0)
 

@@ -55,6 +55,14 @@ def test_host_subspace_matches_oracle(seed, ratio):
     assert list(nat.subspace(ratio, 30, seed)) == list(oracle.subspace(ratio, 30, seed))
 
 
+def test_host_subspace_spark2_anchor():
+    """sbag_subspace (host code, no GPU) follows Spark 2.4.3's 64-byte hashSeed:
+    XORShiftRandom(0).nextDouble() = 0.8446490682263027, so mkSubspace(u, 1, 0) is []."""
+    u = 0.8446490682263027
+    assert list(nat.subspace(u, 1, 0)) == []
+    assert list(nat.subspace(float(np.nextafter(u, 1.0)), 1, 0)) == [0]
+
+
 def test_null_arguments_are_rejected():
     lib = nat.lib()
     assert lib.sbag_subspace(1.0, 4, 0, None, None) == nat.SBAG_EINVAL

@@ -79,6 +79,23 @@ def test_bernoulli_bag_bit_exact(ctx, seed, ratio):
     assert (got == want).all()
 
 
+def test_spark2_hash_seed_anchor_through_c_abi(ctx):
+    """Spark 2.4.3's XORShiftRandom(0).nextDouble() is 0.8446490682263027 (64-byte
+    hashSeed). rand(seed + i) on partition 0 row 0 and mkSubspace both take that draw with a
+    strict `<`: ratio == u gives 0 / [], the next double up 1 / [0]."""
+    u = 0.8446490682263027
+    up = float(np.nextafter(u, 1.0))
+    assert list(nat.subspace(u, 1, 0)) == []
+    assert list(nat.subspace(up, 1, 0)) == [0]
+    assert nat.sample(ctx, False, u, 0, 0, 1, 1, [0, 1])[0, 0] == 0
+    assert nat.sample(ctx, False, up, 0, 0, 1, 1, [0, 1])[0, 0] == 1
+    # the other two published anchors: seed 30 and 5419823303878592871 (SQL Int wrap does not
+    # apply above Int range; learner 0, partition 0)
+    for seed, v in [(30, 0.31429268272540556), (5419823303878592871, 0.2304755080444375)]:
+        assert nat.sample(ctx, False, v, seed, 0, 1, 1, [0, 1])[0, 0] == 0
+        assert nat.sample(ctx, False, float(np.nextafter(v, 1.0)), seed, 0, 1, 1, [0, 1])[0, 0] == 1
+
+
 def test_all_ones_bag(ctx):
     got = nat.sample(ctx, False, 1.0, SEED_REG, 0, 4, 1000)
     assert (got == 1).all()

@@ -37,6 +37,36 @@ def test_murmur3_x86_32_smhasher_verification():
         assert po.bytes_hash(key[:i], 256 - i) == oracle.mm3_bytes_hash(key[:i], 256 - i)
 
 
+SPARK2_XORSHIFT_ANCHORS = [
+    # seed, XORShiftRandom(seed).nextDouble() under Spark 2.x (published values):
+    (0, 0.8446490682263027),                     # Spark 2.x `rand(0)` docstring example
+    (30, 0.31429268272540556),                   # Spark 2.x RandomSuite
+    (5419823303878592871, 0.2304755080444375),   # SPARK-9127 test
+]
+
+
+@pytest.mark.parametrize("seed,want", SPARK2_XORSHIFT_ANCHORS)
+def test_xorshift_spark2_anchors(seed, want):
+    """Spark 2.4.3's hashSeed hashes ByteBuffer.allocate(java.lang.Long.SIZE) = 64 bytes
+    (Spark 3.x: 8). These published 2.x values pin that; the 8-byte form gives
+    0.7604953758285915 for seed 0."""
+    assert oracle.xorshift_doubles(seed, 1)[0] == want
+    assert po.XORShiftRandom(seed).next_double() == want
+
+
+def test_subspace_anchor_boundary():
+    """mkSubspace keeps f iff nextDouble() < ratio (strict): with seed 0 the first draw is
+    0.8446490682263027, so ratio == that value drops feature 0 and the next double up keeps
+    it (ml/ensemble/HasSubBag.scala:97-103)."""
+    u = SPARK2_XORSHIFT_ANCHORS[0][1]
+    assert list(oracle.subspace(u, 1, 0)) == []
+    assert list(oracle.subspace(float(np.nextafter(u, 1.0)), 1, 0)) == [0]
+    assert po.subspace(u, 1, 0) == [] and po.subspace(float(np.nextafter(u, 1.0)), 1, 0) == [0]
+    # the same draw is row 0 of learner 0's Bernoulli bag on partition 0 (seed + 0 + 0)
+    assert oracle.bag(False, u, 0, 1, 0, [0, 1], 1)[0, 0] == 0
+    assert oracle.bag(False, float(np.nextafter(u, 1.0)), 0, 1, 0, [0, 1], 1)[0, 0] == 1
+
+
 @pytest.mark.parametrize("seed", [0, 1, -1, 12345, -1395689524, 2**62 + 11, -(2**63)])
 def test_rng_streams_c_vs_python(seed):
     assert oracle.hash_seed(seed) == po.hash_seed(seed)
