@@ -229,7 +229,8 @@ int sbag_aggregate(sbag_ctx* ctx, const double* votes, int32_t num_learners, int
  * Pointers named d_* are device memory on the context's device (e.g. a torch tensor's
  * data_ptr()); both calls return after their work is complete on the device.       */
 #define SBAG_OUT_SUM 2   /* fp64 [num_rows]: in-order sum of the forest's tree predictions */
-#define SBAG_OUT_VOTES 3 /* [trees x num_rows] class ids, vote_bytes 1 (u8) or 2 (u16)    */
+#define SBAG_OUT_VOTES 3 /* [trees x num_rows] class ids, vote_bytes 1 (u8) or 2 (u16), or
+                            vote_bytes 8: every tree's fp64 prediction (any impurity)  */
 int sbag_predict_dataset_device(sbag_ctx* ctx, const sbag_forest* f, const sbag_dataset* ds,
                                 int32_t out_kind, int32_t vote_bytes, void* d_out);
 /* d_in [K x num_rows]: in_bytes 8 -> fp64 values, MEAN: out = (in-order sum of the K

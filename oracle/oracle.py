@@ -68,6 +68,8 @@ def lib():
         L.or_fit_x.argtypes = [P, i32, P, i64, i32, P, i32, P, P, ctypes.POINTER(TreeParams), i32,
                                P, i32, P, i32, P, P, P]
         L.or_synth.argtypes = [i64, i64, i32, ctypes.c_uint64, i32, i32, P, P]
+        L.or_fastmath_exp_neg.restype = dbl
+        L.or_fastmath_exp_neg.argtypes = [dbl]
         L.or_mm3_bytes_hash.restype = ctypes.c_uint32
         L.or_mm3_bytes_hash.argtypes = [P, i32, ctypes.c_uint32]
         _lib = L
@@ -172,6 +174,11 @@ def split_sample(counts_row, part_off, dt_seed, fraction):
     return mult
 
 
+def fastmath_exp_neg(x):
+    """commons-math3 FastMath.exp(x) for -41 < x < 0 (or_fastmath.h)."""
+    return float(lib().or_fastmath_exp_neg(float(x)))
+
+
 def mm3_bytes_hash(data, seed):
     """scala.util.hashing.MurmurHash3.bytesHash (= MurmurHash3_x86_32) of a bytes object."""
     buf = np.frombuffer(bytes(data), np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
@@ -203,7 +210,8 @@ def fit(X, y, counts, subspaces, max_depth=5, max_bins=32, min_instances_per_nod
     for l, s in enumerate(subspaces):
         sub[l, : len(s)] = s
         nsub[l] = len(s)
-    max_nodes = (1 << (max_depth + 1)) - 1
+    # a leaf holds at least one distinct row: <= 2N - 1 nodes whatever the depth
+    max_nodes = min((1 << (max_depth + 1)) - 1, 2 * N + 1)
     if max_stats is None:
         max_stats = 3 if not classification else int(y.max()) + 1
     nodes = np.zeros((L, max_nodes), NODE_DTYPE)

@@ -17,6 +17,8 @@ Upstream arithmetic restated from SURVEY.md Appendix A.
 import math
 import struct
 
+import fastmath
+
 M32 = 0xFFFFFFFF
 M64 = 0xFFFFFFFFFFFFFFFF
 DOUBLE_MIN_VALUE = -1.7976931348623157e308  # Scala Double.MinValue
@@ -152,7 +154,7 @@ class Well19937c:
 def poisson_stream(mean, seed):
     """PoissonDistribution(mean) reseeded with `seed`; yields sample() values."""
     rng = Well19937c(seed)
-    p = math.exp(-mean)
+    p = fastmath.exp(-mean)  # FastMath.exp, not libm (oracle/fastmath.py)
     while True:
         n = 0
         r = 1.0

@@ -12,6 +12,7 @@
  * Java integer semantics are reproduced with unsigned arithmetic.
  */
 #include "sbag_oracle.h"
+#include "or_fastmath.h"
 
 #include <math.h>
 #include <stdlib.h>
@@ -164,7 +165,8 @@ static double well_next_double(well_t* w) {
 }
 
 /* PoissonDistribution.sample() -> nextPoisson(mean) for mean < 40.
-   p = FastMath.exp(-mean); restated with libm exp (SURVEY.md A.2 [verify]). */
+   p = FastMath.exp(-mean), restated table for table in or_fastmath.h (FastMath is not
+   correctly rounded: at mean 0.052 it is one ulp above libm's exp). */
 static int poisson_sample(well_t* w, double mean, double p) {
   int64_t n = 0;
   double r = 1.0;
@@ -193,7 +195,7 @@ void or_well_doubles(int64_t seed, int n, double* out) {
 void or_poisson(double lambda, int64_t seed, int n, int32_t* out) {
   well_t w;
   well_seed(&w, seed);
-  const double p = exp(-lambda);
+  const double p = or_fm_exp_neg(-lambda);
   for (int i = 0; i < n; i++) out[i] = poisson_sample(&w, lambda, p);
 }
 
@@ -212,7 +214,7 @@ int or_bag(int replacement, double ratio, int lb, int le, int64_t seed, const in
   if (!replacement && ratio > 1) return -1;
   if (replacement && ratio >= 40.0) return -2; /* large-mean Poisson branch not restated */
   if (off[0] != 0 || off[P] != N) return -3;
-  const double p = exp(-ratio);
+  const double p = replacement ? or_fm_exp_neg(-ratio) : 0.0;
   for (int i = lb; i < le; i++) {
     uint8_t* c = counts + (int64_t)(i - lb) * N;
     for (int part = 0; part < P; part++) {
@@ -447,6 +449,7 @@ int or_find_splits(const double* X, int64_t N, int F, int feature, const uint8_t
 
 /* MurmurHash3_x86_32 (= scala.util.hashing.MurmurHash3.bytesHash), exported so the tests
    can pin it to SMHasher's published verification value. */
+double or_fastmath_exp_neg(double x) { return (x < 0 && x > -41) ? or_fm_exp_neg(x) : NAN; }
 uint32_t or_mm3_bytes_hash(const uint8_t* data, int len, uint32_t seed) {
   return mm3_bytes_hash(data, len, seed);
 }
@@ -505,11 +508,28 @@ typedef struct { /* ImpurityStats of the chosen candidate */
   double calc[MAXS], left[MAXS], right[MAXS];
 } istats_t;
 
-typedef struct { /* LearningNode */
+typedef struct { /* LearningNode; children are nodes[child] and nodes[child + 1] */
   int exists, is_leaf, has_split, split_f, split_bin, processed;
+  int64_t child;
   double threshold;
   istats_t st;
 } lnode_t;
+
+/* the tree's LearningNodes in creation order (level by level, heap order within a level:
+   Spark's node ids 2h, 2h+1 are only ever compared within a level, so indices replace them
+   and depth 30 needs no 2^31-entry heap) */
+typedef struct {
+  lnode_t* v;
+  int64_t n, cap;
+} lnodes_t;
+static int64_t lnodes_push(lnodes_t* a) {
+  if (a->n == a->cap) {
+    a->cap = a->cap ? 2 * a->cap : 64;
+    a->v = (lnode_t*)realloc(a->v, sizeof(lnode_t) * (size_t)a->cap);
+  }
+  memset(&a->v[a->n], 0, sizeof(lnode_t));
+  return a->n++;
+}
 
 static double calc_count_d(const double* s, int ns, int gini) {
   if (!gini) return s[0];
@@ -614,8 +634,8 @@ static tn_ret to_node(const lnode_t* ln, int64_t hid, emit_t* e, int gini, int* 
   if (n->has_split) {
     const int mark = e->count;
     int lid, rid;
-    tn_ret l = to_node(ln, 2 * hid, e, gini, &lid);
-    tn_ret r = to_node(ln, 2 * hid + 1, e, gini, &rid);
+    tn_ret l = to_node(ln, n->child, e, gini, &lid);
+    tn_ret r = to_node(ln, n->child + 1, e, gini, &rid);
     if (l.is_leaf && r.is_leaf && l.prediction == r.prediction) {
       /* pruned: LeafNode(l.prediction, stats.impurity, stats.impurityCalculator) */
       e->count = mark;
@@ -663,7 +683,7 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
                    int32_t* out_ns, int32_t* out_exact, int inner) {
   const int gini = p->impurity == 1;
   const int D = p->max_depth;
-  if (D < 0 || D > 20 || p->max_bins < 2 || Fr <= 0) return -1;
+  if (D < 0 || D > 30 || p->max_bins < 2 || Fr <= 0) return -1;
   int64_t n = 0, nrows = 0;
   double maxlab = -1;
   for (int64_t r = 0; r < N; r++)
@@ -733,17 +753,17 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
       bins[k * Fr + fl] = (uint16_t)lo;
     }
   }
-  const int64_t H = (int64_t)1 << (D + 1);
-  lnode_t* ln = (lnode_t*)calloc((size_t)(H + 2), sizeof(lnode_t));
+  lnodes_t tree = {NULL, 0, 0};
+  lnodes_push(&tree); /* root: LearningNode.emptyNode(1), stats == null */
+  tree.v[0].exists = 1;
   int64_t* node_of = (int64_t*)malloc(sizeof(int64_t) * (size_t)nrows);
-  for (int64_t k = 0; k < nrows; k++) node_of[k] = 1;
-  ln[1].exists = 1; /* LearningNode.emptyNode(1): stats == null */
+  for (int64_t k = 0; k < nrows; k++) node_of[k] = 0;
   const int nb = p->max_bins;
-  for (int level = 0; level <= D; level++) {
-    const int64_t first = (int64_t)1 << level, last = ((int64_t)1 << (level + 1)) - 1;
+  int64_t first = 0, last = 0; /* this level's nodes: tree.v[first .. last] */
+  for (int level = 0; level <= D && first <= last; level++) {
     int64_t nact = 0;
     for (int64_t h = first; h <= last; h++)
-      if (ln[h].exists && !ln[h].is_leaf) nact++;
+      if (tree.v[h].exists && !tree.v[h].is_leaf) nact++;
     if (nact == 0) break;
     const int64_t per_node = (int64_t)Fr * nb * ns;
     /* process active nodes in groups bounded by memory (mirrors selectNodesToSplit) */
@@ -756,7 +776,7 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
       int64_t g = 0, h = h0;
       int64_t* members = (int64_t*)malloc(sizeof(int64_t) * (size_t)group);
       for (; h <= last && g < group; h++)
-        if (ln[h].exists && !ln[h].is_leaf) {
+        if (tree.v[h].exists && !tree.v[h].is_leaf) {
           slot[h - first] = g;
           members[g++] = h;
         }
@@ -829,7 +849,7 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
       }
       /* binsToBestSplit for each node of the group */
       for (int64_t gi = 0; gi < g; gi++) {
-        lnode_t* node = &ln[members[gi]];
+        lnode_t* node = &tree.v[members[gi]];
         double* a = agg + gi * per_node;
         int chain_set = 0;
         double chain_calc[MAXS], chain_imp = 0.0;
@@ -898,9 +918,13 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
           node->split_bin = best_s;
           node->threshold = thr[(int64_t)best_f * p->max_bins + best_s];
           const int child_leaf = (level + 1) == D;
-          const int64_t hid = members[gi];
-          lnode_t* L = &ln[2 * hid];
-          lnode_t* R = &ln[2 * hid + 1];
+          const int64_t ci = lnodes_push(&tree);
+          lnodes_push(&tree);
+          node = &tree.v[members[gi]]; /* the push may have moved the array */
+          best = &node->st;
+          node->child = ci;
+          lnode_t* L = &tree.v[ci];
+          lnode_t* R = &tree.v[ci + 1];
           L->exists = R->exists = 1;
           /* LearningNode(child, isLeaf, getEmptyImpurityStats(calculator)) */
           L->st.impurity = calc_impurity(best->left, ns, gini);
@@ -923,10 +947,12 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
     for (int64_t k = 0; k < nrows; k++) {
       const int64_t nd = node_of[k];
       if (nd < first || nd > last) continue;
-      const lnode_t* node = &ln[nd];
+      const lnode_t* node = &tree.v[nd];
       if (!node->has_split) continue;
-      node_of[k] = (bins[k * Fr + node->split_f] <= node->split_bin) ? 2 * nd : 2 * nd + 1;
+      node_of[k] = (bins[k * Fr + node->split_f] <= node->split_bin) ? node->child : node->child + 1;
     }
+    first = last + 1;
+    last = tree.n - 1;
   }
   emit_t e;
   e.nodes = out_nodes;
@@ -937,12 +963,12 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
   e.max_nodes = max_nodes;
   e.overflow = 0;
   int rid;
-  to_node(ln, 1, &e, gini, &rid);
+  to_node(tree.v, 0, &e, gini, &rid);
   *out_num_nodes = e.count;
   *out_ns = ns;
   free(mult);
   *out_exact = all_exact;
-  free(ln);
+  free(tree.v);
   free(node_of);
   free(rows);
   free(thr);

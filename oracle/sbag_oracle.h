@@ -75,6 +75,8 @@ int or_fit_x(const void* X, int xkind, const double* y, int64_t N, int F, const 
 void or_synth(int64_t row_begin, int64_t n, int F, uint64_t seed, int C, int nthreads, uint8_t* X,
               double* y);
 uint32_t or_mm3_bytes_hash(const uint8_t* data, int len, uint32_t seed);
+/* commons-math3 FastMath.exp(x), -41 < x < 0 (NaN outside) */
+double or_fastmath_exp_neg(double x);
 
 /* ensemble prediction: agg 0 = mean (BaggingRegressionModel.predict),
    1 = breeze mode (BaggingClassificationModel.predict).                  */

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "sbag.h"
+#include "sbag_fastmath.h"
 #include "sbag_internal.h"
 
 using namespace sbag;
@@ -155,6 +156,9 @@ struct sbag_ctx {
   // learner range on the two contexts from two host threads, so one half's host work
   // (split bookkeeping between levels) overlaps the other half's kernels
   std::vector<sbag_ctx*> twins;
+  // learner parts fitting concurrently on this device (sbag_fit's overlap): each part's
+  // per-replica bins get 1/concurrent_parts of the device budget
+  int concurrent_parts = 1;
 };
 #define CTX_LOCK(c) std::lock_guard<std::recursive_mutex> ctx_lock_((c)->mu)
 
@@ -422,13 +426,22 @@ struct sbag_forest {
   std::vector<HTree> trees;
   int32_t impurity = 0;
   sbag_timing timing{};
-  int dev_id = -1;
-  DevNode* d_nodes = nullptr;
-  int64_t* d_off = nullptr;
+  // device copies of the node arrays for the global-memory walk, one per device, built on
+  // first use: contexts on different devices (or threads predicting with one forest) each
+  // read their own copy, and a copy is never freed while the forest lives
+  struct DevCopy {
+    DevNode* nodes = nullptr;
+    int64_t* off = nullptr;
+  };
+  std::mutex dev_mu;
+  std::map<int, DevCopy> dev;
   int32_t nclasses = 0;
   ~sbag_forest() {
-    if (d_nodes) (void)hipFree(d_nodes);
-    if (d_off) (void)hipFree(d_off);
+    for (auto& kv : dev) {
+      (void)hipSetDevice(kv.first);
+      if (kv.second.nodes) (void)hipFree(kv.second.nodes);
+      if (kv.second.off) (void)hipFree(kv.second.off);
+    }
   }
 };
 
@@ -688,6 +701,14 @@ int sbag_ctx_create(int32_t device_ordinal, sbag_ctx** out) {
   return SBAG_OK;
 }
 
+// frees the context's workspace (the caller holds its lock; the stream is drained first)
+static void ws_release(sbag_ctx* c) {
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->ws)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  c->ws.clear();
+}
+
 int sbag_ctx_destroy(sbag_ctx* c) {
   if (!c) return SBAG_OK;
   { CTX_LOCK(c); }  // no call is in flight on it any more
@@ -739,7 +760,9 @@ static int run_sampler(sbag_ctx* c, const sbag_sampler_params* p, const std::vec
     int* d_err;
     TRY(ws_typed(c, "err", 1 + 16, &d_err));  // flag + 64-byte store sink for k_poisson
     HIP_TRY(hipMemsetAsync(d_err, 0, 4, c->stream));
-    const double p_exp = std::exp(-p->sample_ratio);  // PoissonDistribution: FastMath.exp(-mean)
+    // PoissonDistribution.nextPoisson: p = FastMath.exp(-mean), restated table for table
+    // (sbag_fastmath.h): FastMath is not correctly rounded (mean 0.052: one ulp above libm).
+    const double p_exp = sbag_fm_exp_neg(-p->sample_ratio);
     launch_poisson(c->stream, d_counts, N, d_poff, P, R, p->learner_begin, p->seed, p->sample_ratio,
                    p_exp, d_err);
     HIP_TRY(hipGetLastError());
@@ -1210,13 +1233,14 @@ static constexpr int kSplitRange = -1000;
 
 // device bytes per-replica bins may take: SBAG_BINS_BUDGET_MB, else 40 % of the device
 static double bins_budget(sbag_ctx* c) {
-  if (const char* e = getenv("SBAG_BINS_BUDGET_MB")) return atof(e) * (1 << 20);
+  if (const char* e = getenv("SBAG_BINS_BUDGET_MB"))
+    return atof(e) * (1 << 20) / std::max(1, c->concurrent_parts);
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
     (void)hipGetLastError();
     return 48.0 * (1ull << 30);
   }
-  return 0.4 * (double)tot;
+  return 0.4 * (double)tot / std::max(1, c->concurrent_parts);
 }
 
 static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out);
@@ -1305,6 +1329,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   std::vector<std::string> errs(parts);
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
+  // the parts share the device: each one's per-replica bins take a 1/parts budget
+  c->concurrent_parts = parts;
+  for (int k = 1; k < parts; k++) c->twins[k - 1]->concurrent_parts = parts;
   for (int k = 1; k < parts; k++)
     th.emplace_back([&, k] {
       sbag_ctx* t = c->twins[k - 1];
@@ -1315,8 +1342,24 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     });
   sts[0] = fit_learners(c, ds, &hp[0], &fs[0]);
   for (auto& t : th) t.join();
+  c->concurrent_parts = 1;
+  for (int k = 1; k < parts; k++) c->twins[k - 1]->concurrent_parts = 1;
   std::vector<std::unique_ptr<sbag_forest>> own;
   for (auto* f : fs) own.emplace_back(f);
+  bool oom = false;
+  for (int k = 0; k < parts; k++) oom = oom || sts[k] == SBAG_ENOMEM;
+  if (oom) {
+    // two workspaces did not fit next to each other: release the twins' device memory and
+    // fit the whole range serially on this context (the result is the same forest)
+    for (int k = 1; k < parts; k++) {
+      sbag_ctx* t = c->twins[k - 1];
+      CTX_LOCK(t);
+      (void)hipSetDevice(c->device);
+      ws_release(t);
+    }
+    own.clear();
+    return fit_learners(c, ds, fp, out);
+  }
   if (sts[0] != SBAG_OK) return sts[0];
   for (int k = 1; k < parts; k++)
     if (sts[k] != SBAG_OK) return fail(sts[k], errs[k]);
@@ -1333,7 +1376,6 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   TRY(check_sampler(&fp->sampler));
   if (tp.max_depth < 0 || tp.max_depth > 30)
     return fail(SBAG_EINVAL, "maxDepth given invalid value (must be in [0, 30])");
-  if (tp.max_depth > 24) return fail(SBAG_EUNSUPPORTED, "maxDepth > 24");
   if (tp.max_bins < 2 || tp.max_bins > 256)
     return fail(SBAG_EINVAL, "maxBins given invalid value (must be in [2, 256])");
   if (tp.min_instances_per_node < 1)
@@ -2844,13 +2886,17 @@ int sbag_forest_free(sbag_forest* f) {
 }
 
 // ---------------------------------------------------------------- predict
-static int upload_forest(sbag_ctx* c, const sbag_forest* fc) {
+// this device's copy of the forest's nodes (built once per device under the forest's lock)
+static int upload_forest(sbag_ctx* c, const sbag_forest* fc, const DevNode** d_nodes,
+                         const int64_t** d_off) {
   sbag_forest* f = const_cast<sbag_forest*>(fc);
-  if (f->d_nodes && f->dev_id == c->device) return SBAG_OK;
-  if (f->d_nodes) (void)hipFree(f->d_nodes);
-  if (f->d_off) (void)hipFree(f->d_off);
-  f->d_nodes = nullptr;
-  f->d_off = nullptr;
+  std::lock_guard<std::mutex> lk(f->dev_mu);
+  auto it = f->dev.find(c->device);
+  if (it != f->dev.end()) {
+    *d_nodes = it->second.nodes;
+    *d_off = it->second.off;
+    return SBAG_OK;
+  }
   std::vector<DevNode> dn;
   std::vector<int64_t> off;
   for (const HTree& t : f->trees) {
@@ -2864,11 +2910,18 @@ static int upload_forest(sbag_ctx* c, const sbag_forest* fc) {
       dn.push_back(d);
     }
   }
-  HIP_TRY(hipMalloc(&f->d_nodes, std::max<size_t>(dn.size(), 1) * sizeof(DevNode)));
-  HIP_TRY(hipMalloc(&f->d_off, std::max<size_t>(off.size(), 1) * 8));
-  HIP_TRY(hipMemcpy(f->d_nodes, dn.data(), dn.size() * sizeof(DevNode), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(f->d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
-  f->dev_id = c->device;
+  sbag_forest::DevCopy cp;
+  HIP_TRY(hipMalloc(&cp.nodes, std::max<size_t>(dn.size(), 1) * sizeof(DevNode)));
+  if (hipMalloc(&cp.off, std::max<size_t>(off.size(), 1) * 8) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(cp.nodes);
+    return fail(SBAG_ENOMEM, "device allocation of the forest failed");
+  }
+  f->dev[c->device] = cp;  // owned by the forest from here on
+  HIP_TRY(hipMemcpy(cp.nodes, dn.data(), dn.size() * sizeof(DevNode), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(cp.off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+  *d_nodes = cp.nodes;
+  *d_off = cp.off;
   return SBAG_OK;
 }
 
@@ -3053,7 +3106,9 @@ int sbag_predict(sbag_ctx* c, const sbag_forest* f, const double* X, int64_t N, 
     TRY(d2h(c, out, d_out, (size_t)N));
     return SBAG_OK;
   }
-  TRY(upload_forest(c, f));
+  const DevNode* f_nodes = nullptr;
+  const int64_t* f_off = nullptr;
+  TRY(upload_forest(c, f, &f_nodes, &f_off));
   double* d_X;
   TRY(ws_typed(c, "pX", (size_t)N * F, &d_X));
   if (per_tree) TRY(ws_typed(c, "ppt", (size_t)N * L, &d_pt));
@@ -3061,7 +3116,7 @@ int sbag_predict(sbag_ctx* c, const sbag_forest* f, const double* X, int64_t N, 
   uint16_t* d_gcnt = nullptr;
   int64_t gcnt_rows = 0;
   TRY(mode_counters(c, agg, f->nclasses, N, &d_gcnt, &gcnt_rows));
-  launch_predict(c->stream, d_X, nullptr, 1, nullptr, nullptr, N, F, F, f->d_nodes, f->d_off, L, agg,
+  launch_predict(c->stream, d_X, nullptr, 1, nullptr, nullptr, N, F, F, f_nodes, f_off, L, agg,
                  std::max(f->nclasses, 1), d_out, d_pt, nullptr, 0, d_gcnt, gcnt_rows);
   HIP_TRY(hipGetLastError());
   TRY(d2h(c, out, d_out, (size_t)N));
@@ -3109,12 +3164,14 @@ static int predict_dataset_dev(sbag_ctx* c, const sbag_forest* f, const sbag_dat
     pa.votes = d_votes;
     launch_predict_tiled(c->stream, pa);
   } else {  // very deep trees, very wide rows or many classes: node walk from global memory
-    TRY(upload_forest(c, f));
+    const DevNode* f_nodes = nullptr;
+    const int64_t* f_off = nullptr;
+    TRY(upload_forest(c, f, &f_nodes, &f_off));
     uint16_t* d_gcnt = nullptr;
     int64_t gcnt_rows = 0;
     TRY(mode_counters(c, agg, f->nclasses, ds->N, &d_gcnt, &gcnt_rows));
     launch_predict(c->stream, nullptr, ds->d_codes, ds->code_bytes, ds->d_dict, ds->d_dict_off, ds->N,
-                   ds->F, ds->S, f->d_nodes, f->d_off, L, agg, std::max(f->nclasses, 1), d_o, nullptr,
+                   ds->F, ds->S, f_nodes, f_off, L, agg, std::max(f->nclasses, 1), d_o, nullptr,
                    d_votes, vote_bytes, d_gcnt, gcnt_rows);
   }
   HIP_TRY(hipGetLastError());
@@ -3138,10 +3195,10 @@ int sbag_predict_dataset_device(sbag_ctx* c, const sbag_forest* f, const sbag_da
   if (out_kind != SBAG_OUT_SUM && out_kind != SBAG_OUT_VOTES)
     return fail(SBAG_EINVAL, "unknown output kind");
   CTX_LOCK(c);
-  if (out_kind == SBAG_OUT_VOTES) {
+  if (out_kind == SBAG_OUT_VOTES && vote_bytes != 8) {
     if (f->impurity != SBAG_IMPURITY_GINI || f->nclasses <= 0)
       return fail(SBAG_EINVAL, "votes need class-valued trees");
-    if (vote_bytes != 1 && vote_bytes != 2) return fail(SBAG_EINVAL, "vote_bytes must be 1 or 2");
+    if (vote_bytes != 1 && vote_bytes != 2) return fail(SBAG_EINVAL, "vote_bytes must be 1, 2 or 8");
     if (f->nclasses > (vote_bytes == 1 ? 256 : 4096))
       return fail(SBAG_EINVAL, std::to_string(f->nclasses) + " classes do not fit " +
                                    std::to_string(vote_bytes) + "-byte votes");
@@ -3406,7 +3463,6 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
     return fail(SBAG_EINVAL, "the booster engine fits DecisionTreeRegressor (impurity variance)");
   if (tp.max_depth < 0 || tp.max_depth > 30)
     return fail(SBAG_EINVAL, "maxDepth given invalid value (must be in [0, 30])");
-  if (tp.max_depth > 24) return fail(SBAG_EUNSUPPORTED, "maxDepth > 24");
   if (tp.max_bins < 2 || tp.max_bins > 256)
     return fail(SBAG_EINVAL, "maxBins given invalid value (must be in [2, 256])");
   if (tp.min_instances_per_node < 1)

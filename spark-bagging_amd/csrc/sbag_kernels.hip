@@ -3264,8 +3264,10 @@ __global__ __launch_bounds__(256) void k_predict(const double* __restrict__ X,
     if (agg == kAggVotes) {
       if (vote_bytes == 1)
         ((uint8_t*)votes)[(int64_t)l * N + row] = (uint8_t)pred;
-      else
+      else if (vote_bytes == 2)
         ((uint16_t*)votes)[(int64_t)l * N + row] = (uint16_t)pred;
+      else
+        ((double*)votes)[(int64_t)l * N + row] = pred;
     } else if (agg == kAggMode) {
       const int k = ++cnt[(int64_t)(int)pred * cstride];
       if (k > maxc) {
@@ -3375,6 +3377,9 @@ __global__ __launch_bounds__(kPredThreads) void k_predict_tiled(PredictArgs A) {
         if (A.vote_bytes == 1) {
           if (row0 + tid < A.N) ((uint8_t*)A.votes)[v0] = (uint8_t)p0;
           if (row0 + tid + kPredThreads < A.N) ((uint8_t*)A.votes)[v1] = (uint8_t)p1;
+        } else if (A.vote_bytes == 8) {  // per-tree fp64 predictions (any impurity)
+          if (row0 + tid < A.N) ((double*)A.votes)[v0] = p0;
+          if (row0 + tid + kPredThreads < A.N) ((double*)A.votes)[v1] = p1;
         } else {
           if (row0 + tid < A.N) ((uint16_t*)A.votes)[v0] = (uint16_t)p0;
           if (row0 + tid + kPredThreads < A.N) ((uint16_t*)A.votes)[v1] = (uint16_t)p1;

@@ -57,12 +57,20 @@ def exchange_rows(local, dist):
     shards = [row_range(N, s, world) for s in range(world)]
     a, b = shards[rank]
     n_me = b - a
-    send = torch.cat([local[:, s0:s1].reshape(-1) for s0, s1 in shards]) if K else \
-        torch.empty(0, dtype=local.dtype, device=local.device)
-    recv = torch.empty(sum(ks) * n_me, dtype=local.dtype, device=local.device)
-    dist.all_to_all_single(recv, send, output_split_sizes=[k * n_me for k in ks],
-                           input_split_sizes=[K * (s1 - s0) for s0, s1 in shards])
-    return recv.view(sum(ks), n_me)
+    # torch's NCCL binding converts only float/half/double/bf16/int8/uint8/int32/int64/bool:
+    # u16 votes (> 256 classes) cross the links as bytes, every column range scaled by 2
+    w = 1
+    src = local
+    if local.dtype in (torch.int16, torch.uint16):
+        w = local.element_size()
+        src = local.contiguous().view(torch.uint8)  # [K x w N]
+    send = torch.cat([src[:, w * s0:w * s1].reshape(-1) for s0, s1 in shards]) if K else \
+        torch.empty(0, dtype=src.dtype, device=src.device)
+    recv = torch.empty(sum(ks) * n_me * w, dtype=src.dtype, device=src.device)
+    dist.all_to_all_single(recv, send, output_split_sizes=[k * n_me * w for k in ks],
+                           input_split_sizes=[K * (s1 - s0) * w for s0, s1 in shards])
+    out = recv.view(sum(ks), n_me * w)
+    return out.view(local.dtype) if w > 1 else out
 
 
 def gather_rows(part, num_rows, dist):

@@ -16,6 +16,7 @@ DecisionTreeRegressor and DecisionTreeClassifier (param holders with Spark's
 names and defaults; their fit only happens inside the ensemble).
 """
 import json
+import logging
 import os
 import threading
 import uuid
@@ -34,6 +35,14 @@ def java_string_hash(s):
     for ch in s:
         h = (31 * h + ord(ch)) & 0xFFFFFFFF
     return h - (1 << 32) if h & 0x80000000 else h
+
+
+_log = logging.getLogger("spark_bagging_amd")
+
+# Instrumentation.logParams list of BaggingRegressor/-Classifier.train
+# (ml/regression/BaggingRegressor.scala:121-135, ml/classification/BaggingClassifier.scala:121-135)
+_LOGGED_PARAMS = ("labelCol", "weightCol", "featuresCol", "predictionCol", "numBaseLearners",
+                  "sampleRatio", "replacement", "subspaceRatio", "seed")
 
 
 def _uid(prefix):
@@ -380,11 +389,31 @@ class _BaggingEstimator(_BaggingParams):
             est.devices = devices
         return est._train(dataset, bug_compat, (learner_begin, learner_end))
 
+    def _instrument(self, dataset):
+        """Instrumentation.instrumented's records (BaggingRegressor.scala:121-135):
+        logPipelineStage, logDataset, logParams -- logged at INFO on the
+        "spark_bagging_amd" logger with Spark's "<uid>: " prefix, and returned."""
+        part = getattr(dataset, "partition_offsets", None)
+        rec = {"stage": type(self).__name__, "uid": self.uid,
+               "numPartitions": (len(part) - 1) if part is not None else 1,
+               "params": {k: self.get(k) for k in _LOGGED_PARAMS if self.isDefined(k)}}
+        _log.info("%s: Stage class: %s", self.uid, rec["stage"])
+        _log.info("%s: Stage uid: %s", self.uid, self.uid)
+        _log.info("%s: training: numPartitions=%d", self.uid, rec["numPartitions"])
+        _log.info("%s: %s", self.uid, json.dumps(rec["params"], sort_keys=True, default=str))
+        return rec
+
     def _train(self, dataset, bug_compat, learner_range=None):
         bl = self._base()
+        if not isinstance(dataset, (Frame, nat.DeviceDataset)):
+            X, y = dataset
+            return self._train(Frame(X, y), bug_compat, learner_range)
+        train_log = self._instrument(dataset)
         if self.get("weightCol"):
             # DecisionTree has no HasWeightCol in Spark 2.4 (BaggingRegressor.scala:137-144, H10)
-            warnings.warn(f"weightCol is ignored, as it is not supported by {type(bl).__name__} now.")
+            msg = f"weightCol is ignored, as it is not supported by {type(bl).__name__} now."
+            _log.warning("%s: %s", self.uid, msg)
+            warnings.warn(msg)
         L = self.get("numBaseLearners")
         lb0, le0 = learner_range if learner_range is not None else (0, L)
         if not (0 <= lb0 < le0 <= L):
@@ -404,9 +433,6 @@ class _BaggingEstimator(_BaggingParams):
                     nat.SBAG_EINVAL, f"a DeviceDataset lives on device {dataset.ctx.device} only")
             devices = [dataset.ctx.device]
             make_ds = [lambda ctx, d=dataset: d]
-        else:
-            X, y = dataset
-            return self._train(Frame(X, y), bug_compat, learner_range)
         shards = [(lb0 + a, lb0 + b) for a, b in _learner_shards(le0 - lb0, len(devices))]
         results = [None] * len(devices)
         errors = []
@@ -449,6 +475,7 @@ class _BaggingEstimator(_BaggingParams):
         model = self._model_cls(subspaces, models)
         model._copy_params_from(self)
         model.fit_timing = timings
+        model.train_log = train_log
         return model
 
 
@@ -465,6 +492,7 @@ class _BaggingModel(_BaggingParams):
         self.models = list(models)
         self._forest = None
         self.fit_timing = []
+        self.train_log = None
 
     @property
     def numBaseModels(self):
@@ -486,19 +514,35 @@ class _BaggingModel(_BaggingParams):
     def transform(self, dataset, device=0, per_tree=False):
         """PredictionModel.transform: one prediction per row (HIP kernel)."""
         if isinstance(dataset, nat.DeviceDataset):  # on the dataset's own device
-            return nat.predict_dataset(dataset.ctx, self.native_forest(), dataset, self._agg)
+            return self._transform_dataset(dataset, per_tree)
         ctx = nat.default_context(device)
         X = dataset.features if isinstance(dataset, Frame) else dataset
         if is_sparse(X):  # SparseVector rows: binned on the device from CSR, no dense copy
             ds = nat.DeviceDataset.from_csr(X, np.zeros(X.shape[0]), ctx)
             try:
-                return nat.predict_dataset(ctx, self.native_forest(), ds, self._agg)
+                return self._transform_dataset(ds, per_tree)
             finally:
                 ds.free()
         X = np.asarray(X, np.float64)
         if X.ndim == 1:
             X = X[None, :]
         return nat.predict(ctx, self.native_forest(), X, self._agg, per_tree=per_tree)
+
+    def _transform_dataset(self, ds, per_tree):
+        """Predictions of a device dataset; with per_tree also every tree's prediction
+        [L x N] (fp64, learner order), as the host-row path returns them."""
+        forest = self.native_forest()
+        pred = nat.predict_dataset(ds.ctx, forest, ds, self._agg)
+        if not per_tree:
+            return pred
+        import torch
+
+        dev = torch.device("cuda", ds.ctx.device)
+        buf = torch.empty((len(self.models), ds.shape[0]), dtype=torch.float64, device=dev)
+        torch.cuda.synchronize(dev)  # the allocation is complete before the library's stream writes
+        nat.predict_dataset_device(ds.ctx, forest, ds, nat.OUT_VOTES, 8, buf.data_ptr())
+        torch.cuda.synchronize(dev)
+        return pred, buf.cpu().numpy()
 
     def predict(self, features):
         """Single-vector predict (BaggingRegressor.scala:248-256 / BaggingClassifier.scala:248-257)."""

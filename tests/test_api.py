@@ -133,3 +133,23 @@ def test_frame_keeps_sparse_rows():
     fr = sb.Frame(S, np.zeros(3))
     assert fr.num_rows == 3 and fr.num_features == 5
     assert fr.features is S
+
+
+def test_train_logs_params_like_instrumentation(caplog):
+    """BaggingRegressor.train's instr.logPipelineStage / logDataset / logParams
+    (ml/regression/BaggingRegressor.scala:121-135): the same param list, INFO records."""
+    import logging
+
+    est = sb.BaggingRegressor().setNumBaseLearners(7).setSampleRatio(0.5).setReplacement(True)
+    frame = sb.Frame(np.zeros((10, 2)), np.zeros(10), partition_offsets=[0, 4, 10])
+    with caplog.at_level(logging.INFO, logger="spark_bagging_amd"):
+        rec = est._instrument(frame)
+    assert rec["stage"] == "BaggingRegressor" and rec["numPartitions"] == 2
+    assert rec["params"]["numBaseLearners"] == 7 and rec["params"]["sampleRatio"] == 0.5
+    assert rec["params"]["seed"] == -1395689524
+    assert set(rec["params"]) <= {"labelCol", "weightCol", "featuresCol", "predictionCol",
+                                  "numBaseLearners", "sampleRatio", "replacement",
+                                  "subspaceRatio", "seed"}
+    text = caplog.text
+    assert "Stage class: BaggingRegressor" in text and "numPartitions=2" in text
+    assert '"numBaseLearners": 7' in text

@@ -160,3 +160,61 @@ def test_learner_ranges_partition_in_order():
             rs = [learner_range(L, r, world) for r in range(world)]
             assert rs[0][0] == 0 and rs[-1][1] == L
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+
+
+def _votes16_worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import sbag_loader
+
+    sbag_loader.load()
+    from spark_bagging_amd import distributed as D
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        lb, le = D.learner_range(11, rank, world)
+        # votes of learners lb..le-1 for 777 rows, class ids up to 400 (> 256: u16)
+        l = torch.arange(lb, le, dtype=torch.int32)[:, None]
+        r = torch.arange(777, dtype=torch.int32)[None, :]
+        local = ((l * 131 + r * 7) % 401).to(torch.int16)
+        out = D.exchange_rows(local, dist)
+        q.put((rank, out.dtype, out.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_rows_u16_votes_as_bytes(world):
+    """Above 256 classes the votes are int16, which torch's NCCL binding cannot move; they
+    cross as bytes. Every rank gets all 11 learners' votes of its row shard,
+    in learner order, as int16."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_votes16_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            r, dt, arr = q.get(timeout=180)
+            got[r] = (dt, arr)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0
+    import torch
+
+    from spark_bagging_amd.distributed import row_range
+    full = ((np.arange(11)[:, None] * 131 + np.arange(777)[None, :] * 7) % 401).astype(np.int16)
+    for r in range(world):
+        a, b = row_range(777, r, world)
+        dt, arr = got[r]
+        assert dt == torch.int16
+        assert (arr == full[:, a:b]).all()

@@ -59,3 +59,29 @@ def test_classifier_fit_transform_save_load(tmp_path, vehicle):
     model.save(path)
     back = sb.BaggingClassificationModel.load(path)
     assert (back.transform(X) == pred).all()
+
+
+@pytest.mark.parametrize("cls", [False, True])
+def test_transform_per_tree_for_sparse_and_device_inputs(cls):
+    """transform(per_tree=True) returns (pred, per_tree [L x N]) for SparseVector rows and
+    device datasets too, equal to the host-row path."""
+    from spark_bagging_amd import _native as nat
+
+    path = os.path.join(DATA, "vehicle.svm" if cls else "cpusmall.svm")
+    dense = sb.Frame.from_libsvm(path, sparse=False)
+    sparse = sb.Frame.from_libsvm(path, sparse=True)
+    est = (sb.BaggingClassifier() if cls else sb.BaggingRegressor()).setNumBaseLearners(5)
+    est = est.setReplacement(True).setSampleRatio(0.8)
+    model = est.fit(dense)
+    want, want_pt = model.transform(dense.features, per_tree=True)
+    got, got_pt = model.transform(sparse, per_tree=True)
+    assert got_pt.shape == (5, dense.num_rows)
+    np.testing.assert_array_equal(got_pt, want_pt)
+    np.testing.assert_array_equal(got, want)
+    ds = nat.DeviceDataset.from_numpy(dense.features, dense.label, sb.default_context(0))
+    try:
+        got, got_pt = model.transform(ds, per_tree=True)
+    finally:
+        ds.free()
+    np.testing.assert_array_equal(got_pt, want_pt)
+    np.testing.assert_array_equal(got, want)

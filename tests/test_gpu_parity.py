@@ -165,6 +165,29 @@ def test_cpusmall_reference_grid_point(ctx, cpusmall):
                                rtol=1e-5, atol=0)
 
 
+@pytest.mark.parametrize("cls,depth", [(False, 30), (True, 30), (False, 26)])
+def test_max_depth_up_to_30(ctx, cpusmall, vehicle, cls, depth):
+    """Spark's DecisionTree allows maxDepth <= 30 (fitBaseLearner passes it through,
+    ml/ensemble/ensembleParams.scala:99-117). cpusmall / vehicle grown without a depth
+    bound in practice (cpusmall's trees reach levels 25-27, vehicle's 15-16), bit-exact
+    against the oracle."""
+    X, y = vehicle if cls else cpusmall
+    forest, orf, _ = _fit_both(ctx, X, y, 3, replacement=True, ratio=1.0,
+                               seed=SEED_CLS if cls else SEED_REG, depth=depth, bins=64, cls=cls)
+    assert_forest_equal(forest, orf)
+
+    def tree_depth(nodes, i=0):
+        n = nodes[i]
+        return 0 if n["left"] < 0 else 1 + max(tree_depth(nodes, n["left"]),
+                                               tree_depth(nodes, n["right"]))
+    deepest = max(tree_depth(forest.tree(t)[0]) for t in range(3))
+    assert deepest <= depth and (cls or deepest > 24)
+    agg = nat.AGG_MODE if cls else nat.AGG_MEAN
+    got = nat.predict(ctx, forest, X, agg)
+    want = oracle.predict(orf, X, classification=cls)
+    assert (got == want).all() if cls else np.allclose(got, want, rtol=1e-5, atol=0)
+
+
 def test_vehicle_c2_parity(ctx, vehicle):
     """BASELINE config 2: BaggingClassifier on vehicle, 32 learners, subspaceRatio 0.7 (H1: no-op)."""
     X, y = vehicle
