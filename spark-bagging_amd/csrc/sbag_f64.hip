@@ -1,0 +1,547 @@
+// sbag_f64.hip — gfx950 kernels for bagging regression on arbitrary fp64 labels.
+//
+// The integer engine (sbag_kernels.hip) needs dyadic labels: its histogram sums are exact
+// integers, so their order does not matter.  For any other double the reference's result
+// depends on the order: Spark's DTStatsAggregator.update adds every exploded row (a row
+// drawn c times is c consecutive rows, sql/bfunctions.scala:42-44) to its (node, feature,
+// bin) cell in row order, in fp64 (count += 1, sum += 1 * y, sumSq += 1 * y * y).  These
+// kernels reproduce those sums bit for bit:
+//
+//   k_chunk_inbag / k_chunk_scan / k_compact_ordered  in-bag entries of each replica in
+//                                                      row order (a stable compaction)
+//   k_f64_hist        one wave per (node, group of <= 64 features); lane = feature owns
+//                     that feature's NB cells in LDS and walks the node's entries in row
+//                     order, adding each row's label with LDS fp64 atomics (ds_add_f64):
+//                     one lane's adds to one cell execute in issue order, so the sum is
+//                     the sequential fp64 sum, while the wave never waits on a result
+//   k_f64_split       RandomForest.binsToBestSplit in Spark's operation order, one wave
+//                     per node, lane = feature (mergeForFeature prefixes, right = total -
+//                     left, calculateImpurityStats, first max over splits then features)
+//   k_sp_count / k_sp_scan / k_sp_scatter   stable partition of every split node's
+//                     entries into its children (row order kept), reading the split
+//                     column from the column-major bins copy
+//
+// Reference call sites: ml/ensemble/ensembleParams.scala:113-115 (fitBaseLearner ->
+// DecisionTreeRegressor.train), ml/regression/BaggingRegressor.scala:146-150,179-185.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "sbag_internal.h"
+
+namespace sbag {
+
+namespace {
+
+__device__ __forceinline__ int f64_wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// block-wide exclusive scan of one int per thread (256 threads); returns the exclusive
+// prefix and writes the block total to *total
+__device__ __forceinline__ int block_excl_scan256(int v, int* s_wave, int* total) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int incl = f64_wave_incl_scan(v, lane);
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    if (w < wave) before += s_wave[w];
+    tot += s_wave[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return before + incl - v;
+}
+
+__device__ __forceinline__ void lds_add_f64(double* p, double v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+constexpr int kChunkRows = 8192;
+
+}  // namespace
+
+// ---------------------------------------------------------------- ordered compaction
+// per (replica, 8192-row chunk): in-bag rows, and per replica Σ count and max count
+__global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__ counts, int64_t N,
+                                                     int R, int64_t chunks,
+                                                     uint32_t* __restrict__ ncnt,
+                                                     unsigned long long* __restrict__ wsum,
+                                                     unsigned int* __restrict__ cmax) {
+  const int r = blockIdx.x % R;
+  const int64_t chunk = blockIdx.x / R;
+  const uint8_t* cr = counts + (int64_t)r * N;
+  int n = 0;
+  unsigned int s = 0, m = 0;
+  for (int it = 0; it < kChunkRows / 256; it++) {
+    const int64_t row = chunk * kChunkRows + it * 256 + threadIdx.x;
+    if (row < N) {
+      const unsigned int c = cr[row];
+      n += c ? 1 : 0;
+      s += c;
+      m = max(m, c);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    n += __shfl_down(n, o);
+    s += __shfl_down(s, o);
+    m = max(m, (unsigned int)__shfl_down((int)m, o));
+  }
+  __shared__ int s_n[4];
+  __shared__ unsigned int s_s[4], s_m[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_n[wave] = n;
+    s_s[wave] = s;
+    s_m[wave] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ncnt[(int64_t)r * chunks + chunk] = (uint32_t)(s_n[0] + s_n[1] + s_n[2] + s_n[3]);
+    const unsigned long long t = (unsigned long long)s_s[0] + s_s[1] + s_s[2] + s_s[3];
+    if (t) atomicAdd(&wsum[r], t);
+    const unsigned int mm = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+    if (mm) atomicMax(&cmax[r], mm);
+  }
+}
+
+// per replica: exclusive prefix of the chunks' in-bag counts; cursor[r] = the total
+__global__ __launch_bounds__(256) void k_chunk_scan(const uint32_t* __restrict__ ncnt, int64_t chunks,
+                                                    unsigned long long* __restrict__ base,
+                                                    unsigned long long* __restrict__ cursor) {
+  __shared__ int s_wave[4];
+  const int r = blockIdx.x;
+  unsigned long long carry = 0;
+  for (int64_t k0 = 0; k0 < chunks; k0 += 256) {
+    const int64_t k = k0 + threadIdx.x;
+    const int v = k < chunks ? (int)ncnt[(int64_t)r * chunks + k] : 0;
+    int tot;
+    const int ex = block_excl_scan256(v, s_wave, &tot);
+    if (k < chunks) base[(int64_t)r * chunks + k] = carry + (unsigned long long)ex;
+    carry += (unsigned long long)tot;
+  }
+  if (threadIdx.x == 0) cursor[r] = carry;
+}
+
+// entries (row | count << 32) of every in-bag row, in row order
+__global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restrict__ counts, int64_t N,
+                                                         int R, int64_t chunks,
+                                                         const unsigned long long* __restrict__ base,
+                                                         uint64_t* __restrict__ ent, int64_t cap) {
+  __shared__ int s_wave[4];
+  const int r = blockIdx.x % R;
+  const int64_t chunk = blockIdx.x / R;
+  const uint8_t* cr = counts + (int64_t)r * N;
+  uint64_t* er = ent + (int64_t)r * cap;
+  unsigned long long pos0 = base[(int64_t)r * chunks + chunk];
+  for (int it = 0; it < kChunkRows / 1024; it++) {
+    const int64_t row0 = chunk * kChunkRows + (int64_t)it * 1024 + (int64_t)threadIdx.x * 4;
+    uint32_t c[4];
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      c[j] = row0 + j < N ? cr[row0 + j] : 0u;
+      n += c[j] ? 1 : 0;
+    }
+    int tot;
+    const int ex = block_excl_scan256(n, s_wave, &tot);
+    unsigned long long pos = pos0 + (unsigned long long)ex;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (c[j]) er[pos++] = pack_entry((uint32_t)(row0 + j), 0, c[j]);
+    pos0 += (unsigned long long)tot;
+  }
+}
+
+void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint64_t* ent,
+                            int64_t cap, uint32_t* d_ncnt, unsigned long long* d_base,
+                            unsigned long long* d_cursor, unsigned long long* d_wsum,
+                            unsigned int* d_cmax) {
+  const int64_t chunks = (N + kChunkRows - 1) / kChunkRows;
+  hipLaunchKernelGGL(k_chunk_inbag, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, R,
+                     chunks, d_ncnt, d_wsum, d_cmax);
+  hipLaunchKernelGGL(k_chunk_scan, dim3(R), dim3(256), 0, st, d_ncnt, chunks, d_base, d_cursor);
+  hipLaunchKernelGGL(k_compact_ordered, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, R,
+                     chunks, d_base, ent, cap);
+}
+
+int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunkRows; }
+
+// ---------------------------------------------------------------- row-order fp64 histogram
+// LDS per wave: sum [NB][64] f64, sumSq [NB][64] f64, count [NB][64] u32.  Lane fl < Fr
+// owns feature fl's cells, lane Fr (when in this group) the node total (one bin).  The
+// wave walks the node's entries in batches of 64: lane i loads entry i and its label;
+// the bins of batch k + 1 are gathered (one byte per lane and entry, the row's line
+// shared by the wave) while batch k is added, so the gathers' latency overlaps the
+// atomics.  A row of count c adds its label c times (the reference's explode).
+constexpr int kF64Batch = 64;
+
+__global__ __launch_bounds__(64) void k_f64_hist(F64HistArgs A) {
+  extern __shared__ double lds[];
+  const F64Node nd = A.nodes[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int Fr = A.Fr[nd.r];
+  const int f0 = blockIdx.y * A.FPW;
+  if (f0 > Fr) return;  // this feature group lies past the node's features and total
+  const int fl = f0 + lane;
+  const bool feat = lane < A.FPW && fl < Fr;
+  const bool tot = lane < A.FPW && fl == Fr;
+  const bool on = feat || tot;
+  const int NB = A.NB;
+  double* s1 = lds;
+  double* s2 = lds + (size_t)NB * 64;
+  uint32_t* cn = (uint32_t*)(lds + (size_t)2 * NB * 64);
+  for (int k = lane; k < NB * 64; k += 64) {
+    s1[k] = 0.0;
+    s2[k] = 0.0;
+    cn[k] = 0u;
+  }
+  __syncthreads();
+  const uint8_t* bcol =
+      A.bins + (int64_t)nd.r * A.bins_rstride + (feat ? (int64_t)A.pos[(int64_t)nd.r * A.Fmax + fl] : 0);
+  const int64_t S = A.S;
+  const int64_t a = nd.a, b = nd.b;
+  // batch registers: entry, label (lane i = entry i of the batch), bins (per entry)
+  uint64_t e0 = 0, e1 = 0;
+  double y0 = 0.0, y1 = 0.0;
+  uint32_t b0[kF64Batch], b1[kF64Batch];
+  auto load_batch = [&](int64_t base, uint64_t& e, double& y) {
+    const int64_t i = base + lane;
+    if (i < b) {
+      e = A.ent[i];
+      y = A.y[(uint32_t)e];
+    }
+  };
+  auto load_bins = [&](int64_t base, uint64_t e, uint32_t* bb) {
+    const int n = (int)min((int64_t)kF64Batch, b - base);
+#pragma unroll
+    for (int j = 0; j < kF64Batch; j++) {
+      const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, j);
+      bb[j] = (feat && j < n) ? (uint32_t)bcol[(int64_t)row * S] : 0u;
+    }
+  };
+  if (a < b) {
+    load_batch(a, e0, y0);
+    load_bins(a, e0, b0);
+    if (a + kF64Batch < b) load_batch(a + kF64Batch, e1, y1);
+  }
+  for (int64_t base = a; base < b; base += kF64Batch) {
+    const int64_t nb = base + kF64Batch;
+    // gather the next batch's bins and the one after's entries before adding this one
+    if (nb < b) load_bins(nb, e1, b1);
+    uint64_t e2 = 0;
+    double y2 = 0.0;
+    if (nb + kF64Batch < b) load_batch(nb + kF64Batch, e2, y2);
+    const int n = (int)min((int64_t)kF64Batch, b - base);
+#pragma unroll
+    for (int j = 0; j < kF64Batch; j++) {
+      if (j < n) {
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(e0 >> 32), j);
+        const uint32_t c = hi & 0xffu;
+        const int ylo = __builtin_amdgcn_readlane((int)(uint32_t)__double_as_longlong(y0), j);
+        const int yhi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)__double_as_longlong(y0) >> 32), j);
+        const double v = __longlong_as_double((long long)(((uint64_t)(uint32_t)yhi << 32) | (uint32_t)ylo));
+        const double w = 1.0 * v;  // instanceWeight * label
+        const double w2 = w * v;   // instanceWeight * label * label
+        if (on) {
+          const int cell = (int)b0[j] * 64 + lane;
+          for (uint32_t k = 0; k < c; k++) {
+            lds_add_f64(s1 + cell, w);
+            lds_add_f64(s2 + cell, w2);
+          }
+          atomicAdd(cn + cell, c);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kF64Batch; j++) b0[j] = b1[j];
+    e0 = e1;
+    y0 = y1;
+    e1 = e2;
+    y1 = y2;
+  }
+  __syncthreads();
+  if (on) {
+    double* out = A.hist + ((int64_t)blockIdx.x * (A.Fmax + 1) + fl) * NB * 3;
+    const int nbk = tot ? 1 : NB;
+    for (int k = 0; k < nbk; k++) {
+      out[3 * k] = (double)cn[k * 64 + lane];
+      out[3 * k + 1] = s1[k * 64 + lane];
+      out[3 * k + 2] = s2[k * 64 + lane];
+    }
+  }
+}
+
+size_t f64_hist_lds_bytes(int NB) { return (size_t)NB * 64 * (8 + 8 + 4); }
+
+void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups) {
+  const size_t lds = f64_hist_lds_bytes(a.NB);
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)k_f64_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(k_f64_hist, dim3(nnodes, ngroups), dim3(64), lds, st, a);
+}
+
+// ---------------------------------------------------------------- split (binsToBestSplit)
+namespace {
+__device__ __forceinline__ double var_impurity(double count, double sum, double sumsq) {
+  if (count == 0) return 0.0;  // Variance.calculate
+  const double squared_loss = sumsq - (sum * sum) / count;
+  return squared_loss / count;
+}
+constexpr double kMinValue = -1.7976931348623157e308;  // Double.MinValue
+}  // namespace
+
+// hist [q][Fmax + 1][NB][3]: the node's per-feature bin stats (and its total at Fmax... at
+// local index Fr).  Each lane takes features fl = lane, lane + 64, ...; per feature it
+// forms the prefixes in bin order (mergeForFeature), evaluates every split against the
+// node's chain state and keeps the first max; the wave then takes the first max over
+// features (lowest index on ties).  At the root the chain state is the first candidate's
+// left + right of the first feature with splits (calculateImpurityStats, stats == null).
+__global__ __launch_bounds__(64) void k_f64_split(F64SplitArgs A) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const F64Node nd = A.nodes[q];
+  const int r = nd.r;
+  const int Fr = A.Fr[r];
+  const int NB = A.NB;
+  const double* h = A.hist + (int64_t)q * (A.Fmax + 1) * NB * 3;
+  const int32_t* nbins = A.nbins + (int64_t)r * A.Fmax;
+  const F64Chain ch = A.chain[q];
+  double pc0 = ch.calc[0], pc1 = ch.calc[1], pc2 = ch.calc[2], pimp = ch.impurity;
+  if (!ch.set) {
+    // first feature with splits; its first candidate fixes the parent
+    int f0 = -1;
+    for (int k = 0; k < Fr; k++)
+      if (nbins[k] > 1) {
+        f0 = k;
+        break;
+      }
+    if (f0 >= 0) {
+      const double* fa = h + (int64_t)f0 * NB * 3;
+      const int nsp = nbins[f0] - 1;
+      double t0 = 0, t1 = 0, t2 = 0;  // prefix through bin nsp, in bin order
+      for (int s = 0; s <= nsp; s++) {
+        if (s == 0) {
+          t0 = fa[0];
+          t1 = fa[1];
+          t2 = fa[2];
+        } else {
+          t0 += fa[3 * s];
+          t1 += fa[3 * s + 1];
+          t2 += fa[3 * s + 2];
+        }
+      }
+      const double l0 = fa[0], l1 = fa[1], l2 = fa[2];
+      const double r0 = t0 - l0, r1 = t1 - l1, r2 = t2 - l2;
+      pc0 = l0 + r0;
+      pc1 = l1 + r1;
+      pc2 = l2 + r2;
+      pimp = var_impurity(pc0, pc1, pc2);
+    }
+  }
+  double best_gain = 0.0;
+  int best_f = -1, best_s = -1, best_valid = 0;
+  for (int fl = lane; fl < Fr; fl += 64) {
+    const int nsp = nbins[fl] - 1;
+    if (nsp <= 0) continue;
+    const double* fa = h + (int64_t)fl * NB * 3;
+    double t0 = fa[0], t1 = fa[1], t2 = fa[2];
+    for (int s = 1; s <= nsp; s++) {
+      t0 += fa[3 * s];
+      t1 += fa[3 * s + 1];
+      t2 += fa[3 * s + 2];
+    }
+    double c0 = 0, c1 = 0, c2 = 0;
+    double fg = 0.0;
+    int fs = -1, fv = 0;
+    for (int s = 0; s < nsp; s++) {
+      if (s == 0) {
+        c0 = fa[0];
+        c1 = fa[1];
+        c2 = fa[2];
+      } else {
+        c0 += fa[3 * s];
+        c1 += fa[3 * s + 1];
+        c2 += fa[3 * s + 2];
+      }
+      const double r0 = t0 - c0, r1 = t1 - c1, r2 = t2 - c2;
+      const int64_t lc = (int64_t)c0, rc = (int64_t)r0;
+      double gain;
+      int valid;
+      if (lc < A.min_inst || rc < A.min_inst) {
+        gain = kMinValue;
+        valid = 0;
+      } else {
+        const int64_t total = lc + rc;
+        const double li = var_impurity(c0, c1, c2), ri = var_impurity(r0, r1, r2);
+        const double lw = (double)lc / (double)total, rw = (double)rc / (double)total;
+        gain = pimp - lw * li - rw * ri;
+        valid = 1;
+        if (gain < A.min_gain) {
+          gain = kMinValue;
+          valid = 0;
+        }
+      }
+      if (fs < 0 || gain > fg) {
+        fg = gain;
+        fs = s;
+        fv = valid;
+      }
+    }
+    if (best_f < 0 || fg > best_gain) {  // features visited in increasing order per lane
+      best_gain = fg;
+      best_f = fl;
+      best_s = fs;
+      best_valid = fv;
+    }
+  }
+  // wave: first max over features (the larger gain, on ties the lower feature index)
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(best_gain, o);
+    const int of = __shfl_xor(best_f, o);
+    const int os = __shfl_xor(best_s, o);
+    const int ov = __shfl_xor(best_valid, o);
+    const bool take = of >= 0 && (best_f < 0 || og > best_gain || (og == best_gain && of < best_f));
+    if (take) {
+      best_gain = og;
+      best_f = of;
+      best_s = os;
+      best_valid = ov;
+    }
+  }
+  if (lane != 0) return;
+  F64SplitOut o{};
+  o.f = best_f;
+  o.s = best_s;
+  if (best_f < 0) {  // no feature has a split: invalid stats on the node's total
+    const double* par = h + (int64_t)Fr * NB * 3;
+    o.calc[0] = par[0];
+    o.calc[1] = par[1];
+    o.calc[2] = par[2];
+    o.gain = kMinValue;
+    o.impurity = var_impurity(par[0], par[1], par[2]);
+    o.valid = 0;
+    A.out[q] = o;
+    return;
+  }
+  o.calc[0] = pc0;
+  o.calc[1] = pc1;
+  o.calc[2] = pc2;
+  o.gain = best_gain;
+  o.impurity = pimp;
+  o.valid = best_valid;
+  const double* fa = h + (int64_t)best_f * NB * 3;
+  const int nsp = nbins[best_f] - 1;
+  double c0 = 0, c1 = 0, c2 = 0, t0 = 0, t1 = 0, t2 = 0;
+  for (int s = 0; s <= nsp; s++) {
+    if (s == 0) {
+      t0 = fa[0];
+      t1 = fa[1];
+      t2 = fa[2];
+    } else {
+      t0 += fa[3 * s];
+      t1 += fa[3 * s + 1];
+      t2 += fa[3 * s + 2];
+    }
+    if (s == best_s) {
+      c0 = t0;
+      c1 = t1;
+      c2 = t2;
+    }
+  }
+  o.left[0] = c0;
+  o.left[1] = c1;
+  o.left[2] = c2;
+  o.right[0] = t0 - c0;
+  o.right[1] = t1 - c1;
+  o.right[2] = t2 - c2;
+  A.out[q] = o;
+}
+
+void launch_f64_split(hipStream_t st, const F64SplitArgs& a, int nnodes) {
+  hipLaunchKernelGGL(k_f64_split, dim3(nnodes), dim3(64), 0, st, a);
+}
+
+// ---------------------------------------------------------------- stable partition
+// pieces of kSpPiece entries of every split node; left iff bin <= s (shouldGoLeft)
+namespace {
+__device__ __forceinline__ bool sp_left(const F64PartArgs& A, const F64PartNode& p, uint64_t e) {
+  const uint32_t row = (uint32_t)e;
+  const uint8_t bin = A.cols[(int64_t)p.r * A.cols_rstride + (int64_t)p.col * A.npad + row];
+  return bin <= p.s;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_sp_count(F64PartArgs A) {
+  const F64PartPiece pc = A.pieces[blockIdx.x];
+  const F64PartNode p = A.nodes[pc.node];
+  int n = 0;
+  for (int64_t i = pc.a + threadIdx.x; i < pc.b; i += 256) n += sp_left(A, p, A.ent_in[i]) ? 1 : 0;
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
+  __shared__ int s_n[4];
+  if ((threadIdx.x & 63) == 0) s_n[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) A.piece_left[blockIdx.x] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+}
+
+// per split node: left entries before each of its pieces, and the node's left total
+__global__ __launch_bounds__(64) void k_sp_scan(F64PartArgs A, int nnodes) {
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= nnodes) return;
+  const F64PartNode p = A.nodes[q];
+  int64_t acc = 0;
+  for (int64_t k = p.piece0; k < p.piece1; k++) {
+    A.piece_base[k] = acc;
+    acc += A.piece_left[k];
+  }
+  A.nleft[q] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_sp_scatter(F64PartArgs A) {
+  __shared__ int s_wave[4];
+  const F64PartPiece pc = A.pieces[blockIdx.x];
+  const F64PartNode p = A.nodes[pc.node];
+  const int64_t nl = A.nleft[pc.node];
+  int64_t lpos = p.a + A.piece_base[blockIdx.x];
+  // right entries before this piece = entries before it - left entries before it
+  int64_t rpos = p.a + nl + (pc.a - p.a) - A.piece_base[blockIdx.x];
+  for (int64_t i0 = pc.a; i0 < pc.b; i0 += 256) {
+    const int64_t i = i0 + threadIdx.x;
+    const bool valid = i < pc.b;
+    uint64_t e = 0;
+    bool left = false;
+    if (valid) {
+      e = A.ent_in[i];
+      left = sp_left(A, p, e);
+    }
+    int ltot;
+    const int lex = block_excl_scan256(valid && left ? 1 : 0, s_wave, &ltot);
+    const int nvalid = (int)min((int64_t)256, pc.b - i0);
+    // right rank = entries before me in this round - left entries before me
+    const int rex = (int)threadIdx.x - lex;
+    if (valid) A.ent_out[left ? lpos + lex : rpos + rex] = e;
+    lpos += ltot;
+    rpos += nvalid - ltot;
+  }
+}
+
+void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int64_t npieces) {
+  if (npieces <= 0) return;
+  hipLaunchKernelGGL(k_sp_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_sp_scan, dim3((nnodes + 63) / 64), dim3(64), 0, st, a, nnodes);
+  hipLaunchKernelGGL(k_sp_scatter, dim3((unsigned)npieces), dim3(256), 0, st, a);
+}
+
+}  // namespace sbag

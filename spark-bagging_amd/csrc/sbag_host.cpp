@@ -329,6 +329,7 @@ struct sbag_dataset {
   std::vector<int32_t> zero_code;         // code of 0.0, -1 when absent
   std::vector<double> y;
   int32_t* d_labk = nullptr;              // labels as fixed point k = y * 2^shift
+  double* d_y64 = nullptr;                // fp64 labels on the device (f64 fits; built lazily)
   int shift = 0;
   bool label_ok = false;                  // representable as |k| < 2^23
   int64_t kmin = 0, kmax = 0;
@@ -1095,6 +1096,7 @@ int sbag_dataset_free(sbag_dataset* ds) {
   (void)hipStreamSynchronize(ds->ctx->stream);
   if (ds->d_codes) (void)hipFree(ds->d_codes);
   if (ds->d_labk) (void)hipFree(ds->d_labk);
+  if (ds->d_y64) (void)hipFree(ds->d_y64);
   if (ds->d_dict) (void)hipFree(ds->d_dict);
   if (ds->d_dict_off) (void)hipFree(ds->d_dict_off);
   if (ds->d_cols) (void)hipFree(ds->d_cols);
@@ -1371,6 +1373,322 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   return SBAG_OK;
 }
 
+// ---------------------------------------------------------------- fp64-stat trees
+// LearningNode with fp64 ImpurityStats: the booster engine (sbag_fit_booster) and the
+// bagging engine's row-order path for labels that are not dyadic (fit_range, f64 mode)
+namespace {
+struct BtNode {  // LearningNode with fp64 ImpurityStats
+  int left = -1, right = -1;
+  bool is_leaf = false, has_split = false, valid = true;
+  int fl = -1, s = -1;
+  double thr = 0.0;
+  double calc[3] = {0, 0, 0};  // stats.impurityCalculator (count, sum, sumSq)
+  double impurity = 0.0, gain = NAN;
+};
+
+double bt_count(const double* s) { return s[0]; }
+// Variance.calculate (count, sum, sumSq)
+double bt_impurity(const double* s) {
+  const double count = s[0], sum = s[1], sumsq = s[2];
+  if (count == 0) return 0.0;
+  const double squared_loss = sumsq - (sum * sum) / count;
+  return squared_loss / count;
+}
+// VarianceCalculator.predict: sum / count (count as a Long)
+double bt_predict(const double* s) {
+  const int64_t cnt = (int64_t)s[0];
+  if (cnt == 0) return 0.0;
+  return s[1] / (double)cnt;
+}
+
+// LearningNode.toNode(prune = true), NodeData pre-order
+struct BtRet {
+  bool leaf;
+  double pred;
+};
+BtRet bt_emit(const std::vector<BtNode>& nodes, int idx, HTree& t) {
+  const BtNode& n = nodes[idx];
+  const int my = (int)t.nodes.size();
+  t.nodes.push_back(sbag_node{});
+  t.stats.resize((size_t)(my + 1) * 3);
+  auto fill = [&](int at) {
+    for (int i = 0; i < 3; i++) t.stats[(size_t)at * 3 + i] = n.calc[i];
+  };
+  if (n.has_split) {
+    const size_t mark = t.nodes.size();
+    const int lid = (int)t.nodes.size();
+    BtRet l = bt_emit(nodes, n.left, t);
+    const int rid = (int)t.nodes.size();
+    BtRet r = bt_emit(nodes, n.right, t);
+    if (l.leaf && r.leaf && l.pred == r.pred) {
+      t.nodes.resize(mark);
+      t.stats.resize(mark * 3);
+      sbag_node& p = t.nodes[my];
+      p = sbag_node{};
+      p.id = my;
+      p.left = p.right = -1;
+      p.feature = -1;
+      p.split_bin = -1;
+      p.prediction = l.pred;
+      p.impurity = n.impurity;
+      p.gain = -1.0;
+      fill(my);
+      return {true, l.pred};
+    }
+    sbag_node& o = t.nodes[my];
+    o.id = my;
+    o.left = lid;
+    o.right = rid;
+    o.feature = n.fl;
+    o.split_bin = n.s;
+    o.threshold = n.thr;
+    o.prediction = bt_predict(n.calc);
+    o.impurity = n.impurity;
+    o.gain = n.gain;
+    fill(my);
+    return {false, o.prediction};
+  }
+  sbag_node& o = t.nodes[my];
+  o.id = my;
+  o.left = o.right = -1;
+  o.feature = -1;
+  o.split_bin = -1;
+  o.prediction = bt_predict(n.calc);
+  o.impurity = n.valid ? n.impurity : -1.0;
+  o.gain = -1.0;
+  fill(my);
+  return {true, o.prediction};
+}
+
+}  // namespace
+
+// fp64 labels: level-wise growth whose histograms are Spark's row-order fp64 sums
+// (sbag_f64.hip).  Every node is histogrammed from its own rows (the reference builds
+// both children's aggregates; a sibling by subtraction would round differently), split
+// search runs on the device in binsToBestSplit's order, and a stable partition keeps
+// each child's entries in row order for the next level.
+struct F64Grow {
+  sbag_ctx* c;
+  sbag_dataset* ds;
+  const sbag_tree_params& tp;
+  int R;
+  int64_t N;
+  int Fmax, NB, S;
+  const std::vector<int32_t>& h_Fr;
+  const std::vector<std::vector<int32_t>>& sub;
+  const std::vector<std::vector<double>>& thr;  // [R * Fmax]
+  const uint8_t* d_bins;
+  int64_t bins_rstride;
+  const int16_t* d_pos;
+  const int32_t* d_Fr;
+  const int32_t* d_nbins;
+  const std::vector<int16_t>& h_pos;
+  const uint8_t* d_cols;
+  int64_t cols_rstride, npad;
+  uint64_t* entA;
+  uint64_t* entB;
+  int64_t cap;
+  const std::vector<unsigned long long>& inbag;
+  EventTimer& tm;
+  int64_t hist_launches = 0;
+  double hist_entries = 0, hist_alg_bytes = 0;
+  int levels = 0;
+};
+
+static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
+  sbag_ctx* c = G.c;
+  const int R = G.R, Fmax = G.Fmax, NB = G.NB, D = G.tp.max_depth;
+  // the labels on the device, once per dataset
+  {
+    std::lock_guard<std::mutex> lk(G.ds->layout_mu);
+    if (!G.ds->d_y64) {
+      HIP_TRY(hipMalloc(&G.ds->d_y64, (size_t)std::max<int64_t>(G.N, 1) * 8));
+      HIP_TRY(hipMemcpy(G.ds->d_y64, G.ds->y.data(), (size_t)G.N * 8, hipMemcpyHostToDevice));
+    }
+  }
+  struct LNode {
+    int r, node;
+    int64_t a, b;
+  };
+  trees.assign(R, {});
+  std::vector<LNode> cur;
+  for (int r = 0; r < R; r++) {
+    trees[r].push_back(BtNode{});
+    cur.push_back(LNode{r, 0, (int64_t)r * G.cap, (int64_t)r * G.cap + (int64_t)G.inbag[r]});
+  }
+  uint64_t* ent_cur = G.entA;
+  uint64_t* ent_nxt = G.entB;
+  const int FPW = 64;
+  const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
+  const size_t node_words = (size_t)(Fmax + 1) * NB * 3;
+  // nodes per histogram batch: the level's fp64 histograms within 4 GB
+  const int64_t batch = std::max<int64_t>(1, ((int64_t)4 << 30) / (int64_t)(node_words * 8));
+  for (int level = 0; level <= D && !cur.empty(); level++) {
+    G.levels++;
+    G.tm.level = level;
+    const int A = (int)cur.size();
+    std::vector<F64Node> hn(A);
+    std::vector<F64Chain> chain(A);
+    for (int q = 0; q < A; q++) {
+      hn[q] = F64Node{cur[q].a, cur[q].b, cur[q].r, 0};
+      const BtNode& n = trees[cur[q].r][cur[q].node];
+      F64Chain ch{};
+      if (level > 0) {
+        for (int i = 0; i < 3; i++) ch.calc[i] = n.calc[i];
+        ch.impurity = n.impurity;
+        ch.set = 1;
+      }
+      chain[q] = ch;
+      G.hist_entries += (double)(cur[q].b - cur[q].a);
+      G.hist_alg_bytes += (double)(cur[q].b - cur[q].a) * (G.h_Fr[cur[q].r] + 8 + 8);
+    }
+    F64Node* d_nodes;
+    F64Chain* d_chain;
+    F64SplitOut* d_out;
+    double* d_hist;
+    TRY(ws_typed(c, "f64_nodes", (size_t)A, &d_nodes));
+    TRY(ws_typed(c, "f64_chain", (size_t)A, &d_chain));
+    TRY(ws_typed(c, "f64_sout", (size_t)A, &d_out));
+    TRY(ws_typed(c, "f64_hist", (size_t)std::min<int64_t>(A, batch) * node_words, &d_hist));
+    TRY(h2d(c, d_nodes, hn.data(), (size_t)A));
+    TRY(h2d(c, d_chain, chain.data(), (size_t)A));
+    for (int64_t q0 = 0; q0 < A; q0 += batch) {
+      const int nq = (int)std::min<int64_t>(batch, A - q0);
+      F64HistArgs ha{};
+      ha.ent = ent_cur;
+      ha.nodes = d_nodes + q0;
+      ha.y = G.ds->d_y64;
+      ha.bins = G.d_bins;
+      ha.bins_rstride = G.bins_rstride;
+      ha.S = G.S;
+      ha.Fmax = Fmax;
+      ha.pos = G.d_pos;
+      ha.Fr = G.d_Fr;
+      ha.NB = NB;
+      ha.FPW = FPW;
+      ha.hist = d_hist;
+      int h = G.tm.begin(T_HIST);
+      launch_f64_hist(c->stream, ha, nq, ngroups);
+      HIP_TRY(hipGetLastError());
+      G.tm.end(h);
+      G.hist_launches++;
+      F64SplitArgs sa{};
+      sa.hist = d_hist;
+      sa.nodes = d_nodes + q0;
+      sa.chain = d_chain + q0;
+      sa.Fr = G.d_Fr;
+      sa.nbins = G.d_nbins;
+      sa.Fmax = Fmax;
+      sa.NB = NB;
+      sa.min_inst = G.tp.min_instances_per_node;
+      sa.min_gain = G.tp.min_info_gain;
+      sa.out = d_out + q0;
+      h = G.tm.begin(T_SPLIT);
+      launch_f64_split(c->stream, sa, nq);
+      HIP_TRY(hipGetLastError());
+      G.tm.end(h);
+    }
+    std::vector<F64SplitOut> so(A);
+    TRY(d2h(c, so.data(), d_out, (size_t)A));
+    // node updates (RandomForest.findBestSplits, host part)
+    struct Split {
+      int q, li;
+    };
+    std::vector<Split> splits;
+    std::vector<F64PartNode> pn;
+    std::vector<F64PartPiece> pieces;
+    for (int q = 0; q < A; q++) {
+      const int r = cur[q].r;
+      const F64SplitOut& o = so[q];
+      {
+        BtNode& n = trees[r][cur[q].node];
+        for (int i = 0; i < 3; i++) n.calc[i] = o.calc[i];
+        n.gain = o.gain;
+        n.impurity = o.impurity;
+        n.valid = o.f >= 0 && o.valid != 0;
+        n.is_leaf = (n.gain <= 0) || (level == D);
+        if (n.is_leaf) continue;
+        n.has_split = true;
+        n.fl = o.f;
+        n.s = o.s;
+        n.thr = G.thr[(size_t)r * Fmax + o.f][o.s];
+      }
+      const bool child_leaf = (level + 1) == D;
+      BtNode L, Rn;
+      for (int i = 0; i < 3; i++) {
+        L.calc[i] = o.left[i];
+        Rn.calc[i] = o.right[i];
+      }
+      // LearningNode(child, isLeaf, ImpurityStats.getEmptyImpurityStats(calculator))
+      L.impurity = bt_impurity(L.calc);
+      Rn.impurity = bt_impurity(Rn.calc);
+      L.is_leaf = child_leaf || L.impurity == 0.0;
+      Rn.is_leaf = child_leaf || Rn.impurity == 0.0;
+      const int li = (int)trees[r].size();
+      trees[r][cur[q].node].left = li;
+      trees[r][cur[q].node].right = li + 1;
+      trees[r].push_back(L);
+      trees[r].push_back(Rn);
+      if (L.is_leaf && Rn.is_leaf) continue;  // nothing to route
+      F64PartNode p{};
+      p.a = cur[q].a;
+      p.b = cur[q].b;
+      p.piece0 = (int64_t)pieces.size();
+      for (int64_t x = p.a; x < p.b; x += kF64PartPiece)
+        pieces.push_back(F64PartPiece{x, std::min(x + kF64PartPiece, p.b), (int32_t)pn.size(), 0});
+      p.piece1 = (int64_t)pieces.size();
+      p.r = r;
+      p.col = G.h_pos[(size_t)r * Fmax + o.f];
+      p.s = o.s;
+      pn.push_back(p);
+      splits.push_back(Split{q, li});
+    }
+    if (pn.empty()) break;
+    const int NP = (int)pn.size();
+    F64PartNode* d_pn;
+    F64PartPiece* d_pc;
+    int32_t* d_pleft;
+    int64_t *d_pbase, *d_nl;
+    TRY(ws_typed(c, "f64_pn", (size_t)NP, &d_pn));
+    TRY(ws_typed(c, "f64_pc", std::max<size_t>(pieces.size(), 1), &d_pc));
+    TRY(ws_typed(c, "f64_pleft", std::max<size_t>(pieces.size(), 1), &d_pleft));
+    TRY(ws_typed(c, "f64_pbase", std::max<size_t>(pieces.size(), 1), &d_pbase));
+    TRY(ws_typed(c, "f64_nl", (size_t)NP, &d_nl));
+    TRY(h2d(c, d_pn, pn.data(), (size_t)NP));
+    TRY(h2d(c, d_pc, pieces.data(), pieces.size()));
+    F64PartArgs pa{};
+    pa.cols = G.d_cols;
+    pa.cols_rstride = G.cols_rstride;
+    pa.npad = G.npad;
+    pa.nodes = d_pn;
+    pa.pieces = d_pc;
+    pa.ent_in = ent_cur;
+    pa.ent_out = ent_nxt;
+    pa.piece_left = d_pleft;
+    pa.piece_base = d_pbase;
+    pa.nleft = d_nl;
+    {
+      int h = G.tm.begin(T_PART);
+      launch_f64_partition(c->stream, pa, NP, (int64_t)pieces.size());
+      HIP_TRY(hipGetLastError());
+      G.tm.end(h);
+    }
+    std::vector<int64_t> nl(NP);
+    TRY(d2h(c, nl.data(), d_nl, (size_t)NP));
+    std::vector<LNode> next;
+    for (int k = 0; k < NP; k++) {
+      const LNode& p = cur[splits[k].q];
+      const int li = splits[k].li;
+      const int64_t m = pn[k].a + nl[k];
+      if (!trees[p.r][li].is_leaf) next.push_back(LNode{p.r, li, pn[k].a, m});
+      if (!trees[p.r][li + 1].is_leaf) next.push_back(LNode{p.r, li + 1, m, pn[k].b});
+    }
+    cur.swap(next);
+    std::swap(ent_cur, ent_nxt);
+  }
+  return SBAG_OK;
+}
+
 static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
   const sbag_tree_params& tp = fp->tree;
   TRY(check_sampler(&fp->sampler));
@@ -1386,9 +1704,15 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   const bool gini = tp.impurity == SBAG_IMPURITY_GINI;
   if (tp.impurity != SBAG_IMPURITY_GINI && tp.impurity != SBAG_IMPURITY_VARIANCE)
     return fail(SBAG_EINVAL, "unknown impurity");
-  if (!ds->label_ok)
-    return fail(SBAG_EUNSUPPORTED,
-                "labels are not dyadic fixed-point values (|y * 2^s| < 2^23 for some s <= 40)");
+  // Regression labels that are not dyadic fixed point (|y * 2^s| < 2^23, s <= 40) take the
+  // row-order fp64 path (f64 mode, sbag_f64.hip): Spark's sums depend on their order
+  // there. SBAG_F64=1 forces it on dyadic labels too (both paths then agree bit for bit).
+  const bool force_f64 = getenv("SBAG_F64") && atoi(getenv("SBAG_F64")) != 0;
+  const bool f64 = !gini && (!ds->label_ok || force_f64);
+  if (f64) {
+    for (double v : ds->y)
+      if (!std::isfinite(v)) return fail(SBAG_EINVAL, "labels must be finite");
+  }
   if (gini && !ds->integral)
     return fail(SBAG_EINVAL, "Classifier was given dataset with invalid label: labels must be "
                              "integers in [0, 2^23)");
@@ -1462,8 +1786,18 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 32, c->stream));
   {
     int h = tm.begin(T_COMPACT);
-    launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
-                   d_sqsum);
+    if (f64) {  // row order inside every replica (the fp64 sums follow it)
+      const int64_t chunks = compact_ordered_chunks(N);
+      uint32_t* d_ncnt;
+      unsigned long long* d_cbase;
+      TRY(ws_typed(c, "f64_ncnt", (size_t)R * chunks, &d_ncnt));
+      TRY(ws_typed(c, "f64_cbase", (size_t)R * chunks, &d_cbase));
+      launch_compact_ordered(c->stream, d_counts, N, R, entA, cap, d_ncnt, d_cbase, d_inbag, d_wsum,
+                             d_cmax);
+    } else {
+      launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
+                     d_sqsum);
+    }
     HIP_TRY(hipGetLastError());
     tm.end(h);
   }
@@ -1492,7 +1826,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     if (flush_limit < 256)
       return fail(SBAG_EUNSUPPORTED, "label range too wide for the packed LDS histogram");
     const double wmax = (double)flush_limit * cmax;
-    if (gini) {
+    if (gini || f64) {  // f64: only the u32 value-count histograms use the packing
       if (wmax < 4294967295.0) break;
       continue;
     }
@@ -1502,8 +1836,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   }
   // the row-lane histogram builds the word as (c << cshift) + c*(k + K0) with a 32-bit
   // low half: raise cshift to 32 when the count field keeps room for flush_limit * cmax
-  if (!gini && cshift < 32 && (double)flush_limit * cmax < 4294967296.0) cshift = 32;
-  if (!gini && (double)N * cmax * kabs * kabs >= std::ldexp(1.0, 53))
+  if (!gini && !f64 && cshift < 32 && (double)flush_limit * cmax < 4294967296.0) cshift = 32;
+  if (!gini && !f64 && (double)N * cmax * kabs * kabs >= std::ldexp(1.0, 53))
     return fail(SBAG_EUNSUPPORTED, "sum of squared labels would exceed 2^53 (not exact in fp64)");
 
   // ---- per-replica tables
@@ -1768,7 +2102,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   TRY(ws_typed(c, "pos", h_pos_codes.size(), &d_pos));
   TRY(h2d(c, d_pos, h_pos_codes.data(), h_pos_codes.size()));
   std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1), 0);
-  const bool optimistic = ds->code_bytes == 1 && ncmax <= tp.max_bins;
+  const bool optimistic = ds->code_bytes == 1 && ncmax <= tp.max_bins && !f64;
   // row-lane histogram: identity byte layout, packed variance words with cshift >= 32
   // (SBAG_HIST_RL: 0 = never, 1 = always 64-bit row addresses; tests pin both paths)
   const int rl_env = getenv("SBAG_HIST_RL") ? atoi(getenv("SBAG_HIST_RL")) : -1;
@@ -2228,6 +2562,44 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   TRY(h2d(c, d_nbins, h_nbins.data(), h_nbins.size()));
 
   hmark(12);
+  if (f64) {
+    F64Grow G{c, ds, tp, R, N, Fmax, NB, S, h_Fr, sub, thr, d_bins, bins_rstride, d_pos, d_Fr, d_nbins,
+              h_pos, d_cols, cols_rstride, npad, entA, entB, cap, inbag, tm};
+    std::vector<std::vector<BtNode>> ftrees;
+    TRY(grow_f64(G, ftrees));
+    HIP_TRY(hipEventRecord(ev_stop, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    forest->trees.resize(R);
+    for (int r = 0; r < R; r++) {
+      HTree& t = forest->trees[r];
+      t.sub = sub[r];
+      t.exact = exact[r];
+      t.ns = 3;
+      bt_emit(ftrees[r], 0, t);
+    }
+    forest->nclasses = 0;
+    double cats[T_NCAT] = {0};
+    tm.collect(cats, nullptr, -1);
+    float total_ms = 0;
+    (void)hipEventElapsedTime(&total_ms, ev_start, ev_stop);
+    (void)hipEventDestroy(ev_start);
+    (void)hipEventDestroy(ev_stop);
+    sbag_timing& T = forest->timing;
+    T.total_ms = total_ms;
+    T.sample_ms = cats[T_SAMPLE];
+    T.valuecount_ms = cats[T_VC];
+    T.bin_ms = cats[T_BIN];
+    T.compact_ms = cats[T_COMPACT];
+    T.hist_ms = cats[T_HIST];
+    T.split_ms = cats[T_SPLIT];
+    T.partition_ms = cats[T_PART];
+    T.hist_launches = G.hist_launches;
+    T.hist_entries = G.hist_entries;
+    T.hist_alg_bytes = G.hist_alg_bytes;
+    T.levels = G.levels;
+    *out = forest.release();
+    return SBAG_OK;
+  }
   // ---- 6. level-wise growth
   HistGeom g;
   if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode_for(h_pos, S)))
@@ -3277,89 +3649,6 @@ int sbag_aggregate_device(sbag_ctx* c, const void* d_in, int32_t in_bytes, int32
 // on the host in Spark's operation order.  Thresholds are Spark's findSplits of the
 // subbag, with the split-finding sample (k_split_sample) above max(maxBins^2, 1e4) rows.
 namespace {
-struct BtNode {  // LearningNode with fp64 ImpurityStats
-  int left = -1, right = -1;
-  bool is_leaf = false, has_split = false, valid = true;
-  int fl = -1, s = -1;
-  double thr = 0.0;
-  double calc[3] = {0, 0, 0};  // stats.impurityCalculator (count, sum, sumSq)
-  double impurity = 0.0, gain = NAN;
-};
-
-double bt_count(const double* s) { return s[0]; }
-// Variance.calculate (count, sum, sumSq)
-double bt_impurity(const double* s) {
-  const double count = s[0], sum = s[1], sumsq = s[2];
-  if (count == 0) return 0.0;
-  const double squared_loss = sumsq - (sum * sum) / count;
-  return squared_loss / count;
-}
-// VarianceCalculator.predict: sum / count (count as a Long)
-double bt_predict(const double* s) {
-  const int64_t cnt = (int64_t)s[0];
-  if (cnt == 0) return 0.0;
-  return s[1] / (double)cnt;
-}
-
-// LearningNode.toNode(prune = true), NodeData pre-order
-struct BtRet {
-  bool leaf;
-  double pred;
-};
-BtRet bt_emit(const std::vector<BtNode>& nodes, int idx, HTree& t) {
-  const BtNode& n = nodes[idx];
-  const int my = (int)t.nodes.size();
-  t.nodes.push_back(sbag_node{});
-  t.stats.resize((size_t)(my + 1) * 3);
-  auto fill = [&](int at) {
-    for (int i = 0; i < 3; i++) t.stats[(size_t)at * 3 + i] = n.calc[i];
-  };
-  if (n.has_split) {
-    const size_t mark = t.nodes.size();
-    const int lid = (int)t.nodes.size();
-    BtRet l = bt_emit(nodes, n.left, t);
-    const int rid = (int)t.nodes.size();
-    BtRet r = bt_emit(nodes, n.right, t);
-    if (l.leaf && r.leaf && l.pred == r.pred) {
-      t.nodes.resize(mark);
-      t.stats.resize(mark * 3);
-      sbag_node& p = t.nodes[my];
-      p = sbag_node{};
-      p.id = my;
-      p.left = p.right = -1;
-      p.feature = -1;
-      p.split_bin = -1;
-      p.prediction = l.pred;
-      p.impurity = n.impurity;
-      p.gain = -1.0;
-      fill(my);
-      return {true, l.pred};
-    }
-    sbag_node& o = t.nodes[my];
-    o.id = my;
-    o.left = lid;
-    o.right = rid;
-    o.feature = n.fl;
-    o.split_bin = n.s;
-    o.threshold = n.thr;
-    o.prediction = bt_predict(n.calc);
-    o.impurity = n.impurity;
-    o.gain = n.gain;
-    fill(my);
-    return {false, o.prediction};
-  }
-  sbag_node& o = t.nodes[my];
-  o.id = my;
-  o.left = o.right = -1;
-  o.feature = -1;
-  o.split_bin = -1;
-  o.prediction = bt_predict(n.calc);
-  o.impurity = n.valid ? n.impurity : -1.0;
-  o.gain = -1.0;
-  fill(my);
-  return {true, o.prediction};
-}
-
 // RandomForest.binsToBestSplit for one node over its fp64 histogram [Fr+1][NB][3]
 // (in place: mergeForFeature turns each feature's bins into prefixes).  `level > 0`:
 // the chain starts from the node's stats (set when its parent split); at the root from

@@ -271,4 +271,73 @@ void launch_bt_partition(hipStream_t st, const uint32_t* in, uint32_t* out, cons
                          int nsplit, const void* codes, int code_bytes, int32_t S,
                          const uint8_t* lut, int64_t* nleft);
 
+// ---- fp64 labels (sbag_f64.hip): bagging regression on labels that are not dyadic,
+// Spark's row-order fp64 histogram sums reproduced bit for bit
+struct F64Node {      // a node of the level: its entries [a, b) (row order) of replica r
+  int64_t a, b;
+  int32_t r, pad;
+};
+struct F64HistArgs {
+  const uint64_t* ent;     // entries row | count << 32, row order inside every node
+  const F64Node* nodes;    // [A]
+  const double* y;         // [N] labels
+  const uint8_t* bins;     // [R?][N][S]
+  int64_t bins_rstride;
+  int32_t S, Fmax;
+  const int16_t* pos;      // [R][Fmax] byte of local feature fl in a bins row
+  const int32_t* Fr;       // [R]
+  int32_t NB, FPW;         // bins; features per wave (<= 64; local index Fr = node total)
+  double* hist;            // [A][Fmax + 1][NB][3]: count, sum, sumSq
+};
+struct F64Chain {     // calculateImpurityStats' chain state: the node's stats (set) or none
+  double calc[3];
+  double impurity;
+  int32_t set, pad;
+};
+struct F64SplitOut {
+  double gain, impurity;   // Double.MinValue when invalid; the chain's parent impurity
+  double calc[3];          // parent calculator
+  double left[3], right[3];
+  int32_t f, s, valid, pad;  // f = -1: no feature has splits (calc = the node total)
+};
+struct F64SplitArgs {
+  const double* hist;
+  const F64Node* nodes;
+  const F64Chain* chain;
+  const int32_t* Fr;       // [R]
+  const int32_t* nbins;    // [R][Fmax] numSplits + 1
+  int32_t Fmax, NB, min_inst, pad;
+  double min_gain;
+  F64SplitOut* out;
+};
+struct F64PartNode {  // a split node: entries [a, b), pieces [piece0, piece1)
+  int64_t a, b, piece0, piece1;
+  int32_t r, col, s, pad;  // replica, split column of the column-major bins, split bin
+};
+struct F64PartPiece {
+  int64_t a, b;
+  int32_t node, pad;
+};
+struct F64PartArgs {
+  const uint8_t* cols;     // [R?][C][npad]
+  int64_t cols_rstride, npad;
+  const F64PartNode* nodes;
+  const F64PartPiece* pieces;
+  const uint64_t* ent_in;
+  uint64_t* ent_out;
+  int32_t* piece_left;     // [pieces]
+  int64_t* piece_base;     // [pieces]
+  int64_t* nleft;          // [nodes]
+};
+constexpr int64_t kF64PartPiece = 4096;
+void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint64_t* ent,
+                            int64_t cap, uint32_t* d_ncnt /*[R][chunks]*/,
+                            unsigned long long* d_base /*[R][chunks]*/, unsigned long long* d_cursor,
+                            unsigned long long* d_wsum, unsigned int* d_cmax);
+int64_t compact_ordered_chunks(int64_t N);
+size_t f64_hist_lds_bytes(int NB);
+void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups);
+void launch_f64_split(hipStream_t st, const F64SplitArgs& a, int nnodes);
+void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int64_t npieces);
+
 }  // namespace sbag

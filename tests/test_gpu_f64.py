@@ -1,0 +1,156 @@
+"""GPU: bagging regression on arbitrary fp64 labels.
+
+The reference accepts any Double label (ml/regression/BaggingRegressor.scala:146-150 selects
+the label column as is; DecisionTreeRegressor sums count, y, y^2 per exploded row in row
+order, RandomForest's DTStatsAggregator.update).  Labels that are not dyadic fixed point
+take the engine's row-order fp64 path (sbag_f64.hip).  At P = 1 the oracle's sums are
+Spark's, so the trees must be bit-exact in every field; with P > 1 Spark merges the
+partitions' aggregates in shuffle order (not deterministic), and the engine keeps the
+one-partition order -- leaves within 1e-5 relative (north_star's regression tolerance).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import DATA
+from parity_utils import assert_forest_equal, oracle_forest
+
+import spark_bagging_amd as sb
+from spark_bagging_amd import _native as nat
+
+pytestmark = pytest.mark.gpu
+
+SEED_REG = oracle.DEFAULT_SEED_REGRESSOR
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return sb.default_context(0)
+
+
+@pytest.fixture(scope="module")
+def cpusmall():
+    return sb.load_libsvm(os.path.join(DATA, "cpusmall.svm"))
+
+
+def _fit_both(ctx, X, y, L, *, replacement=True, ratio=1.0, seed=SEED_REG, depth=5, bins=32,
+              part=None, min_inst=1, min_gain=0.0):
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        forest = nat.fit(ctx, ds, replacement=replacement, sample_ratio=ratio, seed=seed,
+                         learner_begin=0, learner_end=L, partition_offsets=part, max_depth=depth,
+                         max_bins=bins, min_instances_per_node=min_inst, min_info_gain=min_gain,
+                         impurity=nat.IMPURITY_VARIANCE)
+    finally:
+        ds.free()
+    N, F = X.shape
+    off = part if part is not None else [0, N]
+    counts = oracle.bag(replacement, ratio, 0, L, seed, off, N)
+    subs = [oracle.subspace(ratio, F, seed + i) for i in range(L)]
+    orf = oracle_forest(X, y, counts, subs, depth, bins, False, min_inst, min_gain, part=part)
+    return forest, orf
+
+
+@pytest.mark.parametrize("label", ["y/10", "y*pi"])
+@pytest.mark.parametrize("depth", [5, 10])
+def test_cpusmall_nondyadic_labels_bit_exact(ctx, cpusmall, label, depth):
+    """cpusmall with labels y/10 and y*pi, 10 learners, P = 1."""
+    X, y = cpusmall
+    y2 = y / 10 if label == "y/10" else y * np.pi
+    forest, orf = _fit_both(ctx, X, y2, 10, depth=depth)
+    assert_forest_equal(forest, orf)
+    pred = nat.predict(ctx, forest, X, nat.AGG_MEAN)
+    want = oracle.predict(orf, X)
+    np.testing.assert_allclose(pred, want, rtol=1e-5, atol=0)
+    assert (pred == want).all()  # the same sums in the same order: bit-exact in practice
+
+
+def test_cpusmall_nondyadic_subspace_bernoulli(ctx, cpusmall):
+    """Without replacement at ratio 0.7: Bernoulli bags and a 0.7 subspace (H1)."""
+    X, y = cpusmall
+    forest, orf = _fit_both(ctx, X, y * 0.1 + 1e-3, 6, replacement=False, ratio=0.7, depth=7)
+    assert_forest_equal(forest, orf)
+
+
+def test_min_instances_and_gain_nondyadic(ctx, cpusmall):
+    X, y = cpusmall
+    y2 = np.sqrt(y + 1.0)
+    forest, orf = _fit_both(ctx, X, y2, 4, depth=8, min_inst=5, min_gain=0.01)
+    assert_forest_equal(forest, orf)
+
+
+def test_partitions_p3_leaves_within_tolerance(ctx):
+    """P = 3 partitions: structure and thresholds equal to the oracle's, leaves within
+    1e-5 relative (Spark's partition merge order is not deterministic)."""
+    rng = np.random.default_rng(7)
+    N, F = 9000, 6
+    X = np.round(rng.normal(size=(N, F)), 2)
+    y = rng.normal(size=N) * 3.7 + 0.1
+    part = [0, 2500, 6100, N]
+    forest, orf = _fit_both(ctx, X, y, 5, depth=6, part=part)
+    assert_forest_equal(forest, orf, rel_tol_pred=1e-5)
+
+
+def test_sampled_split_finding_nondyadic(ctx):
+    """Subbags above max(maxBins^2, 10^4) rows: thresholds from Spark's split-finding
+    sample, row-order fp64 sums."""
+    rng = np.random.default_rng(11)
+    N, F = 26000, 4
+    X = np.round(rng.normal(size=(N, F)), 3)
+    X[rng.random((N, F)) < 0.15] = 0.0
+    y = np.exp(rng.normal(size=N))
+    forest, orf = _fit_both(ctx, X, y, 3, depth=6, bins=16, part=[0, 12000, N])
+    assert_forest_equal(forest, orf)
+
+
+def test_forced_f64_path_equals_integer_path_on_dyadic_labels(ctx, cpusmall, monkeypatch):
+    """On dyadic labels both engines' sums are exact, so the row-order fp64 path
+    (SBAG_F64=1) must give the integer engine's trees bit for bit."""
+    X, y = cpusmall
+    a, _ = _fit_both(ctx, X, y, 6, depth=9)
+    monkeypatch.setenv("SBAG_F64", "1")
+    import importlib  # noqa: F401  (the env var is read per process by the library)
+    b, orf = _fit_both(ctx, X, y, 6, depth=9)
+    assert_forest_equal(b, orf)
+    for t in range(6):
+        (na, sa), (nb, sb_) = a.tree(t), b.tree(t)
+        assert na.tobytes() == nb.tobytes() and (sa == sb_).all()
+
+
+def test_synthetic_u8_codes_nondyadic(ctx):
+    """The bench workload's shape (32-level u8 features, shared bins) with real-valued
+    labels, 8 learners over 8 partitions."""
+    N, F = 200_000, 20
+    X, yk = oracle.synth(N, F, 20261015, 0)
+    y = yk * 1.1 + 0.3
+    part = [i * N // 8 for i in range(9)]
+    forest, orf = _fit_both(ctx, X.astype(np.float64), y, 8, depth=8, part=part)
+    assert_forest_equal(forest, orf)
+
+
+def test_api_accepts_real_labels(cpusmall):
+    """BaggingRegressor.fit on a real-valued label column through the Python API."""
+    X, y = cpusmall
+    y2 = y / 7.0
+    model = (sb.BaggingRegressor().setNumBaseLearners(4).setReplacement(True)
+             .setSampleRatio(0.9)).fit(sb.Frame(X, y2))
+    seed = SEED_REG
+    counts = oracle.bag(True, 0.9, 0, 4, seed, [0, len(y)], len(y))
+    subs = [oracle.subspace(0.9, X.shape[1], seed + i) for i in range(4)]
+    orf = oracle.fit(X, y2, counts, subs, max_depth=5, max_bins=32)
+    np.testing.assert_allclose(model.transform(X), oracle.predict(orf, X), rtol=1e-5, atol=0)
+
+
+def test_nonfinite_labels_rejected(ctx, cpusmall):
+    X, y = cpusmall
+    y2 = y / 10
+    y2[5] = np.inf
+    ds = nat.DeviceDataset.from_numpy(X, y2, ctx)
+    try:
+        with pytest.raises(sb.IllegalArgumentException):
+            nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=1, learner_begin=0,
+                    learner_end=2, max_depth=3, impurity=nat.IMPURITY_VARIANCE)
+    finally:
+        ds.free()

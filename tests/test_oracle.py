@@ -354,3 +354,22 @@ def test_oracle_u8_codes_equal_fp64_rows():
     # rows of a later range are the same rows (row_begin offsets the generator)
     Xt, yt = oracle.synth(1000, 7, 99, 0, row_begin=2000, nthreads=2)
     assert (Xt == X[2000:]).all() and (yt == y[2000:]).all()
+
+
+def test_nondyadic_labels_c_vs_python():
+    """Real-valued labels (the row-order fp64 path): the C oracle's trees equal the
+    pure-Python restatement's, every field -- both sum count, y, y*y per exploded row in
+    row order (DTStatsAggregator.update)."""
+    X, y = synthetic.generate(900, 6, seed=12)
+    y = y * np.pi + 0.1
+    counts = oracle.bag(True, 1.0, 0, 2, 21, [0, 900], 900)
+    subs = [oracle.subspace(1.0, 6, 21 + i) for i in range(2)]
+    f = oracle.fit(X, y, counts, subs, max_depth=6, max_bins=8)
+    for t in range(2):
+        nodes, _ = f.tree(t)
+        pt = po.fit_tree(X.tolist(), y.tolist(), counts[t].tolist(), list(subs[t]), max_depth=6,
+                         max_bins=8)
+        assert len(pt) == len(nodes)
+        for a, b in zip(nodes, pt):
+            for k in ("left", "right", "feature", "threshold", "prediction", "impurity", "gain"):
+                assert a[k] == b[k], (t, k)
