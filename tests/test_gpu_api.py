@@ -70,7 +70,8 @@ def test_transform_per_tree_for_sparse_and_device_inputs(cls):
     path = os.path.join(DATA, "vehicle.svm" if cls else "cpusmall.svm")
     dense = sb.Frame.from_libsvm(path, sparse=False)
     sparse = sb.Frame.from_libsvm(path, sparse=True)
-    est = (sb.BaggingClassifier() if cls else sb.BaggingRegressor()).setNumBaseLearners(5)
+    est = (sb.BaggingClassifier().setBaseLearner(sb.DecisionTreeClassifier()) if cls else
+           sb.BaggingRegressor().setBaseLearner(sb.DecisionTreeRegressor())).setNumBaseLearners(5)
     est = est.setReplacement(True).setSampleRatio(0.8)
     model = est.fit(dense)
     want, want_pt = model.transform(dense.features, per_tree=True)

@@ -134,7 +134,8 @@ def test_api_accepts_real_labels(cpusmall):
     """BaggingRegressor.fit on a real-valued label column through the Python API."""
     X, y = cpusmall
     y2 = y / 7.0
-    model = (sb.BaggingRegressor().setNumBaseLearners(4).setReplacement(True)
+    model = (sb.BaggingRegressor().setBaseLearner(sb.DecisionTreeRegressor())
+             .setNumBaseLearners(4).setReplacement(True)
              .setSampleRatio(0.9)).fit(sb.Frame(X, y2))
     seed = SEED_REG
     counts = oracle.bag(True, 0.9, 0, 4, seed, [0, len(y)], len(y))
