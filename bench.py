@@ -108,6 +108,9 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-learners", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-nondyadic", action="store_true",
+                    help="skip the extra timing of the same fit on real-valued (non-dyadic) labels")
+    ap.add_argument("--nondyadic-steps", type=int, default=2)
     a = ap.parse_args()
     w = WORKLOADS[a.workload]
     for k in ("rows", "features", "learners", "depth"):
@@ -166,7 +169,27 @@ def main():
     ctx = nat.Context(local)
     N, F, L = args.rows, args.features, args.learners
     cls = args.classes > 0
-    ds = nat.DeviceDataset.synthetic(N, F, seed=args.seed, num_classes=args.classes, ctx=ctx)
+    replication = None
+    if world == 1:
+        ds = nat.DeviceDataset.synthetic(N, F, seed=args.seed, num_classes=args.classes, ctx=ctx)
+    else:
+        # rank 0 ingests (here: generates) the dataset, the other ranks receive the
+        # binned matrix over RCCL (distributed.replicate_dataset); timed apart from the fits
+        from spark_bagging_amd import distributed as D
+        dist.barrier()
+        torch.cuda.synchronize()
+        t_r = time.perf_counter()
+        ds0 = (nat.DeviceDataset.synthetic(N, F, seed=args.seed, num_classes=args.classes, ctx=ctx)
+               if rank == 0 else None)
+        ds = D.replicate_dataset(ds0, dist, ctx)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t_rep = torch.tensor([time.perf_counter() - t_r], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t_rep, op=dist.ReduceOp.MAX)
+        replication = {"seconds": round(float(t_rep.item()), 4), "bytes": ds.codes_nbytes() + 8 * N,
+                       "how": "rank 0 generates the synthetic dataset; ranks > 0 import its value "
+                              "codes, dictionaries and labels after RCCL broadcasts "
+                              "(distributed.replicate_dataset)"}
     part = [int(round(i * N / args.partitions)) for i in range(args.partitions + 1)]
     lb = rank * L
 
@@ -276,6 +299,31 @@ def main():
         os.environ.pop("SBAG_OVERLAP", None)
     else:
         os.environ["SBAG_OVERLAP"] = prev
+    # The same fit on real-valued labels: y' = 1.1 y + 0.3 is not dyadic,
+    # so sbag_fit takes the row-order fp64 path (Spark's DTStatsAggregator sums, sbag_f64.hip).
+    # Reported beside the headline; not part of `value`.
+    nondyadic = None
+    if not cls and world == 1 and not args.no_nondyadic:
+        y0 = ds.labels()
+        ds.set_labels(y0 * 1.1 + 0.3)
+        step().free()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        tl = []
+        for _ in range(args.nondyadic_steps):
+            f = step()
+            tl.append(f.timing())
+            f.free()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t1
+        ds.set_labels(y0)
+        nondyadic = {"labels": "1.1 * y + 0.3 (fp64, not dyadic)", "steps": args.nondyadic_steps,
+                     "ms_per_step": round(1000.0 * el / args.nondyadic_steps, 3),
+                     "value": round(L * N * args.nondyadic_steps / el, 1),
+                     "unit": "estimator*rows/s",
+                     "breakdown_ms": {k: round(v, 3) for k, v in tl[-1].items() if k.endswith("_ms")},
+                     "engine": "row-order fp64 histograms (LDS fp64 atomics), device "
+                               "binsToBestSplit, stable partition (DESIGN.md §4.7)"}
     out = {
         "metric": "estimator×rows trained/sec", "value": round(value, 1),
         "unit": "estimator*rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -289,6 +337,9 @@ def main():
                    "classes": args.classes, "replacement": args.replacement,
                    "sample_ratio": args.ratio, "parallelism": f"learner-shard x{world}"},
         "roofline": roofline, "breakdown_ms": breakdown, "sampler_at_nproc_partitions": sampler_p,
+        "nondyadic_labels": nondyadic, "replication": replication,
+        "value_incl_replication": (round(world * L * N * args.steps / (elapsed + replication["seconds"]), 1)
+                                   if replication else None),
         "kernel_timing": "roofline and breakdown_ms: one extra fit after the timed steps with "
                          "the learner halves serialized (SBAG_OVERLAP=0), so each launch runs "
                          "alone; the timed steps overlap the two halves on two streams",

@@ -109,6 +109,26 @@ int sbag_dataset_info(const sbag_dataset* ds, int64_t* num_rows, int32_t* num_fe
 int sbag_dataset_labels(const sbag_dataset* ds, double* y_out);
 int sbag_dataset_features(const sbag_dataset* ds, int64_t row_begin, int64_t row_end,
                           double* X_out /* [(row_end-row_begin) x F] */);
+/* Replaces the label column (y [num_rows], host).  The reference selects whatever Double
+   label column the DataFrame holds (ml/regression/BaggingRegressor.scala:146-150): labels
+   that are not dyadic fixed point are fitted with Spark's row-order fp64 sums.          */
+int sbag_dataset_set_labels(sbag_dataset* ds, const double* y);
+/* Replication of an ingested dataset (every GPU holds the full binned matrix;
+   the reference's learners share one persisted DataFrame, BaggingRegressor.scala:158-189):
+   one rank ingests, exports the value codes (num_rows x row_stride x code_bytes bytes, into
+   device memory of the dataset's device when codes_on_device, else host memory), the
+   per-feature dictionaries (dict [dict_values], dict_off [num_features + 1]) and the labels;
+   the others import them (after an RCCL broadcast of the codes, or a host copy) instead of
+   re-ingesting rows.  Any of the export outputs may be NULL.  Import validates the
+   dictionaries, the code width and every code on the device.                            */
+int sbag_dataset_layout(const sbag_dataset* ds, int64_t* num_rows, int32_t* num_features,
+                        int32_t* row_stride, int32_t* code_bytes, int64_t* dict_values);
+int sbag_dataset_export(const sbag_dataset* ds, void* codes, int32_t codes_on_device, double* dict,
+                        int64_t* dict_off, double* y);
+int sbag_dataset_import(sbag_ctx* ctx, int64_t num_rows, int32_t num_features, int32_t row_stride,
+                        int32_t code_bytes, const void* codes, int32_t codes_on_device,
+                        const double* dict, const int64_t* dict_off, const double* y,
+                        sbag_dataset** out);
 /* datasets reference their context: free every dataset before sbag_ctx_destroy */
 int sbag_dataset_free(sbag_dataset* ds);
 

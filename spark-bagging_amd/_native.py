@@ -25,6 +25,7 @@ EXPORTED = [
     "sbag_sample", "sbag_subspace", "sbag_dataset_create", "sbag_dataset_create_csr",
     "sbag_dataset_create_columns", "sbag_dataset_synthetic",
     "sbag_dataset_info", "sbag_dataset_labels", "sbag_dataset_features", "sbag_dataset_free",
+    "sbag_dataset_set_labels", "sbag_dataset_layout", "sbag_dataset_export", "sbag_dataset_import",
     "sbag_fit", "sbag_fit_booster", "sbag_forest_num_trees", "sbag_forest_tree_info", "sbag_forest_subspace",
     "sbag_forest_nodes", "sbag_forest_create", "sbag_forest_free", "sbag_forest_timing",
     "sbag_predict", "sbag_predict_dataset", "sbag_aggregate", "sbag_predict_dataset_device",
@@ -129,6 +130,10 @@ def lib():
             "sbag_dataset_labels": [P, P],
             "sbag_dataset_features": [P, i64, i64, P],
             "sbag_dataset_free": [P],
+            "sbag_dataset_set_labels": [P, P],
+            "sbag_dataset_layout": [P, P, P, P, P, P],
+            "sbag_dataset_export": [P, P, i32, P, P, P],
+            "sbag_dataset_import": [P, i64, i32, i32, i32, P, i32, P, P, P, P],
             "sbag_fit": [P, P, ctypes.POINTER(FitParams), P],
             "sbag_fit_booster": [P, P, P, ctypes.POINTER(BoosterParams), P],
             "sbag_forest_num_trees": [P, P],
@@ -287,6 +292,52 @@ class DeviceDataset:
         y = np.zeros(self.shape[0], np.float64)
         check(lib().sbag_dataset_labels(self._h, ptr(y)))
         return y
+
+    def set_labels(self, y):
+        """Replace the label column (sbag_dataset_set_labels); non-dyadic regression labels
+        are then fitted with Spark's row-order fp64 sums."""
+        y = np.ascontiguousarray(y, np.float64)
+        if y.shape != (self.shape[0],):
+            raise IllegalArgumentException(SBAG_EINVAL, "labels do not match the row count")
+        check(lib().sbag_dataset_set_labels(self._h, ptr(y)))
+
+    def layout(self):
+        """(num_rows, num_features, row_stride, code_bytes, dict_values) of the codes."""
+        n, f, s, cb, dv = (ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(),
+                           ctypes.c_int64())
+        check(lib().sbag_dataset_layout(self._h, ctypes.byref(n), ctypes.byref(f), ctypes.byref(s),
+                                        ctypes.byref(cb), ctypes.byref(dv)))
+        return n.value, f.value, s.value, cb.value, dv.value
+
+    def codes_nbytes(self):
+        n, _, s, cb, _ = self.layout()
+        return n * s * cb
+
+    def export(self, codes_ptr=None, codes_on_device=False):
+        """Export for replication: the codes into `codes_ptr` (device memory of this
+        dataset's device when codes_on_device, else host memory of codes_nbytes() bytes;
+        None: skipped), and (dict, dict_off, labels) as numpy arrays."""
+        n, f, _, _, dv = self.layout()
+        d = np.zeros(max(dv, 1), np.float64)
+        off = np.zeros(f + 1, np.int64)
+        y = np.zeros(n, np.float64)
+        check(lib().sbag_dataset_export(self._h, ctypes.c_void_p(codes_ptr) if codes_ptr else None,
+                                        1 if codes_on_device else 0, ptr(d), ptr(off), ptr(y)))
+        return d[:dv], off, y
+
+    @classmethod
+    def import_codes(cls, ctx, layout, codes_ptr, codes_on_device, dict_values, dict_off, y):
+        """A dataset from exported pieces (sbag_dataset_import): `layout` as layout()
+        returns it, the codes at codes_ptr (device memory of ctx's device or host)."""
+        n, f, s, cb, _ = layout
+        d = np.ascontiguousarray(dict_values, np.float64)
+        off = np.ascontiguousarray(dict_off, np.int64)
+        y = np.ascontiguousarray(y, np.float64)
+        h = ctypes.c_void_p()
+        check(lib().sbag_dataset_import(ctx.handle, n, f, s, cb, ctypes.c_void_p(codes_ptr),
+                                        1 if codes_on_device else 0, ptr(d), ptr(off), ptr(y),
+                                        ctypes.byref(h)))
+        return cls(ctx, h)
 
     def features(self, row_begin=0, row_end=None):
         n, f = self.shape

@@ -544,4 +544,32 @@ void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int6
   hipLaunchKernelGGL(k_sp_scatter, dim3((unsigned)npieces), dim3(256), 0, st, a);
 }
 
+// ---------------------------------------------------------------- imported codes
+// sbag_dataset_import checks a received code matrix before any kernel indexes a table
+// with it: feature columns hold codes < their dictionary size, the row padding is zero.
+__global__ __launch_bounds__(256) void k_check_codes(const void* __restrict__ codes, int code_bytes,
+                                                     int64_t N, int32_t S, int32_t F,
+                                                     const int64_t* __restrict__ dict_off,
+                                                     int* __restrict__ bad) {
+  const int64_t total = N * (int64_t)S;
+  int b = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(i % S);
+    const uint32_t v = code_bytes == 1   ? ((const uint8_t*)codes)[i]
+                       : code_bytes == 2 ? ((const uint16_t*)codes)[i]
+                                         : ((const uint32_t*)codes)[i];
+    if (f < F ? (int64_t)v >= dict_off[f + 1] - dict_off[f] : v != 0u) b = 1;
+  }
+  if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+}
+
+void launch_check_codes(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S,
+                        int32_t F, const int64_t* d_dict_off, int* d_bad) {
+  const int64_t total = N * (int64_t)S;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 256 * 16));
+  hipLaunchKernelGGL(k_check_codes, dim3(blocks), dim3(256), 0, st, codes, code_bytes, N, S, F,
+                     d_dict_off, d_bad);
+}
+
 }  // namespace sbag

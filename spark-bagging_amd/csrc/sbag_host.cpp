@@ -1070,6 +1070,132 @@ int sbag_dataset_labels(const sbag_dataset* ds, double* y) {
   return SBAG_OK;
 }
 
+// The label column replaced in place (Spark: a new DataFrame whose labelCol differs; the
+// features' codes and dictionaries are kept)
+int sbag_dataset_set_labels(sbag_dataset* ds, const double* y) {
+  if (!ds || !y) return fail(SBAG_EINVAL, "bad arguments");
+  sbag_ctx* c = ds->ctx;
+  CTX_LOCK(c);
+  HIP_TRY(hipSetDevice(c->device));
+  std::lock_guard<std::mutex> lk(ds->layout_mu);
+  HIP_TRY(hipStreamSynchronize(c->stream));  // no fit of this context still reads the labels
+  ds->y.assign(y, y + ds->N);
+  analyze_labels(ds);
+  if (ds->d_labk) HIP_TRY(hipFree(ds->d_labk));
+  ds->d_labk = nullptr;
+  TRY(upload_labels(ds));
+  if (!ds->label_ok) HIP_TRY(hipMemset(ds->d_labk, 0, (size_t)std::max<int64_t>(ds->N, 1) * 4));
+  if (ds->d_y64) HIP_TRY(hipFree(ds->d_y64));
+  ds->d_y64 = nullptr;
+  return SBAG_OK;
+}
+
+// ---- replication of an ingested dataset to another device: the value codes
+// (device), the dictionaries and the labels, so that one rank ingests and the others
+// receive the binned matrix over RCCL (or a host copy) instead of re-ingesting rows
+int sbag_dataset_layout(const sbag_dataset* ds, int64_t* num_rows, int32_t* num_features,
+                        int32_t* row_stride, int32_t* code_bytes, int64_t* dict_values) {
+  if (!ds) return fail(SBAG_EINVAL, "dataset is NULL");
+  if (num_rows) *num_rows = ds->N;
+  if (num_features) *num_features = ds->F;
+  if (row_stride) *row_stride = ds->S;
+  if (code_bytes) *code_bytes = ds->code_bytes;
+  if (dict_values) {
+    int64_t t = 0;
+    for (const auto& d : ds->dict) t += (int64_t)d.size();
+    *dict_values = t;
+  }
+  return SBAG_OK;
+}
+
+int sbag_dataset_export(const sbag_dataset* ds, void* codes, int32_t codes_on_device, double* dict,
+                        int64_t* dict_off, double* y) {
+  if (!ds) return fail(SBAG_EINVAL, "dataset is NULL");
+  sbag_ctx* c = ds->ctx;
+  CTX_LOCK(c);
+  HIP_TRY(hipSetDevice(c->device));
+  if (codes) {
+    const size_t bytes = (size_t)ds->N * ds->S * ds->code_bytes;
+    HIP_TRY(hipMemcpyAsync(codes, ds->d_codes, bytes,
+                           codes_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  if (dict_off) {
+    dict_off[0] = 0;
+    for (int f = 0; f < ds->F; f++) dict_off[f + 1] = dict_off[f] + (int64_t)ds->dict[f].size();
+  }
+  if (dict) {
+    int64_t o = 0;
+    for (const auto& d : ds->dict) {
+      std::copy(d.begin(), d.end(), dict + o);
+      o += (int64_t)d.size();
+    }
+  }
+  if (y) std::copy(ds->y.begin(), ds->y.end(), y);
+  return SBAG_OK;
+}
+
+int sbag_dataset_import(sbag_ctx* c, int64_t N, int32_t F, int32_t S, int32_t cb, const void* codes,
+                        int32_t codes_on_device, const double* dict, const int64_t* dict_off,
+                        const double* y, sbag_dataset** out) {
+  if (!c || !out || !codes || !dict || !dict_off || !y || N <= 0 || F <= 0)
+    return fail(SBAG_EINVAL, "bad arguments");
+  if (N >= (int64_t)1 << 32) return fail(SBAG_EUNSUPPORTED, "more than 2^32 rows");
+  if (S != row_stride(F)) return fail(SBAG_EINVAL, "row stride does not match the engine's layout");
+  if (dict_off[0] != 0) return fail(SBAG_EINVAL, "dictionary offsets must start at 0");
+  size_t maxd = 0;
+  for (int f = 0; f < F; f++) {
+    if (dict_off[f + 1] <= dict_off[f]) return fail(SBAG_EINVAL, "every feature needs a dictionary");
+    maxd = std::max(maxd, (size_t)(dict_off[f + 1] - dict_off[f]));
+    for (int64_t k = dict_off[f]; k < dict_off[f + 1]; k++) {
+      const double v = dict[k];
+      if (std::isnan(v) || (v == 0.0 && std::signbit(v)) || (k > dict_off[f] && !(dict[k - 1] < v)))
+        return fail(SBAG_EINVAL, "dictionaries must be strictly increasing, without NaN or -0.0");
+    }
+  }
+  if (cb != (maxd <= 256 ? 1 : maxd <= 65536 ? 2 : 4))
+    return fail(SBAG_EINVAL, "code width does not match the dictionaries");
+  CTX_LOCK(c);
+  HIP_TRY(hipSetDevice(c->device));
+  auto ds = std::make_unique<sbag_dataset>();
+  ds->ctx = c;
+  ds->N = N;
+  ds->F = F;
+  ds->S = S;
+  ds->code_bytes = cb;
+  ds->dict.resize(F);
+  ds->zero_code.assign(F, -1);
+  for (int f = 0; f < F; f++) {
+    ds->dict[f].assign(dict + dict_off[f], dict + dict_off[f + 1]);
+    const auto& d = ds->dict[f];
+    const auto z = std::lower_bound(d.begin(), d.end(), 0.0);
+    if (z != d.end() && *z == 0.0) ds->zero_code[f] = (int)(z - d.begin());
+  }
+  const size_t bytes = (size_t)N * S * cb;
+  HIP_TRY(hipMalloc(&ds->d_codes, bytes + 256));
+  HIP_TRY(hipMemsetAsync((uint8_t*)ds->d_codes + bytes, 0, 256, c->stream));
+  HIP_TRY(hipMemcpyAsync(ds->d_codes, codes, bytes,
+                         codes_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+  TRY(upload_dict(ds.get()));
+  int* d_bad;
+  TRY(ws_typed(c, "import_bad", 1, &d_bad));
+  HIP_TRY(hipMemsetAsync(d_bad, 0, 4, c->stream));
+  launch_check_codes(c->stream, ds->d_codes, cb, N, S, F, ds->d_dict_off, d_bad);
+  HIP_TRY(hipGetLastError());
+  int bad = 0;
+  TRY(d2h(c, &bad, d_bad, 1));
+  if (bad) return fail(SBAG_EINVAL, "imported codes exceed their dictionaries (or padding is not zero)");
+  if (cb == 4) {
+    ds->h_codes.resize((size_t)N * S);
+    HIP_TRY(hipMemcpy(ds->h_codes.data(), ds->d_codes, bytes, hipMemcpyDeviceToHost));
+  }
+  ds->y.assign(y, y + N);
+  analyze_labels(ds.get());
+  TRY(upload_labels(ds.get()));
+  *out = ds.release();
+  return SBAG_OK;
+}
+
 int sbag_dataset_features(const sbag_dataset* ds, int64_t r0, int64_t r1, double* X) {
   if (!ds || !X || r0 < 0 || r1 > ds->N || r1 < r0) return fail(SBAG_EINVAL, "bad arguments");
   sbag_ctx* c = ds->ctx;

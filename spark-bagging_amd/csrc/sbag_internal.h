@@ -339,5 +339,8 @@ size_t f64_hist_lds_bytes(int NB);
 void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups);
 void launch_f64_split(hipStream_t st, const F64SplitArgs& a, int nnodes);
 void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int64_t npieces);
+// sbag_dataset_import: *d_bad != 0 when a code is past its dictionary or padding is nonzero
+void launch_check_codes(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S,
+                        int32_t F, const int64_t* d_dict_off, int* d_bad);
 
 }  // namespace sbag

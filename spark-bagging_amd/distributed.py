@@ -22,6 +22,14 @@ tensors in the CPU tests):
                   and breeze's mode with its first-to-reach-the-max tie rule
                   (BaggingClassifier.scala:248-257) runs there -- bit-exact.
   Both finish with an all-gather of the N fp64 predictions by row shard.
+
+Dataset replication (every GPU holds the full binned matrix; the reference's
+learners share one persisted DataFrame, ml/regression/BaggingRegressor.scala:158-189):
+replicate_dataset has rank 0 ingest once and broadcast the value codes -- device memory
+over RCCL with backend "nccl", host memory with "gloo" -- plus dictionaries and labels;
+the other ranks import them (sbag_dataset_import validates every code) instead of
+re-ingesting rows.  Under gloo the collectives stage device tensors through host memory,
+so the CPU tests and a one-GPU multi-rank run share the code path.
 """
 import numpy as np
 
@@ -36,9 +44,16 @@ def row_range(num_rows, rank, world):
     return (rank * num_rows // world, (rank + 1) * num_rows // world)
 
 
+def _staged(dist, t):
+    """gloo moves host tensors: a device tensor goes through host memory."""
+    return dist.get_backend() == "gloo" and t.is_cuda
+
+
 def _all_gather_ints(value, dist, device):
     import torch
 
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     world = dist.get_world_size()
     t = torch.tensor([int(value)], dtype=torch.int64, device=device)
     out = [torch.zeros_like(t) for _ in range(world)]
@@ -51,6 +66,8 @@ def exchange_rows(local, dist):
     the rows of every rank's block stacked in rank order (= learner order)."""
     import torch
 
+    if _staged(dist, local):
+        return exchange_rows(local.cpu(), dist).to(local.device)
     world, rank = dist.get_world_size(), dist.get_rank()
     K, N = local.shape
     ks = _all_gather_ints(K, dist, local.device)
@@ -77,6 +94,8 @@ def gather_rows(part, num_rows, dist):
     """All-gather the row shards' predictions [n_rank] -> [N] in row order."""
     import torch
 
+    if _staged(dist, part):
+        return gather_rows(part.cpu(), num_rows, dist).to(part.device)
     world = dist.get_world_size()
     sizes = [row_range(num_rows, s, world) for s in range(world)]
     sizes = [s1 - s0 for s0, s1 in sizes]
@@ -110,6 +129,46 @@ def gather_model(shard, dist):
     full = type(shard)(subs, models, uid=shard.uid)
     full._values = dict(shard._values)
     return full
+
+
+def replicate_dataset(dataset, dist, ctx):
+    """Rank 0's DeviceDataset on every rank: rank 0 passes its ingested dataset, the others
+    None.  The codes (N x row_stride x code_bytes bytes) cross as one broadcast -- in device
+    memory over RCCL (backend "nccl"), through host memory with gloo -- with the
+    dictionaries and labels; ranks > 0 import them on `ctx`'s device.  Returns this rank's
+    dataset (rank 0: `dataset` itself)."""
+    import torch
+
+    from . import _native as nat
+
+    rank = dist.get_rank()
+    on_dev = dist.get_backend() == "nccl"
+    dev = torch.device("cuda", ctx.device) if on_dev else torch.device("cpu")
+    lay = torch.zeros(5, dtype=torch.int64, device=dev)
+    if rank == 0:
+        lay.copy_(torch.tensor(dataset.layout(), dtype=torch.int64))
+    dist.broadcast(lay, 0)
+    n, f, s, cb, dv = (int(v) for v in lay.cpu().tolist())
+    codes = torch.empty(n * s * cb, dtype=torch.uint8, device=dev)
+    dvals = torch.zeros(max(dv, 1), dtype=torch.float64, device=dev)
+    doff = torch.zeros(f + 1, dtype=torch.int64, device=dev)
+    y = torch.zeros(n, dtype=torch.float64, device=dev)
+    if rank == 0:
+        if on_dev:
+            torch.cuda.synchronize(dev)  # the allocation precedes the library's copy into it
+        d, off, yy = dataset.export(codes.data_ptr(), codes_on_device=on_dev)
+        dvals[:dv].copy_(torch.from_numpy(d))
+        doff.copy_(torch.from_numpy(off))
+        y.copy_(torch.from_numpy(yy))
+    for t in (codes, dvals, doff, y):
+        dist.broadcast(t, 0)
+    if rank == 0:
+        return dataset
+    if on_dev:
+        torch.cuda.synchronize(dev)  # the broadcast has landed before the library reads it
+    return nat.DeviceDataset.import_codes(ctx, (n, f, s, cb, dv), codes.data_ptr(), on_dev,
+                                          dvals[:dv].cpu().numpy(), doff.cpu().numpy(),
+                                          y.cpu().numpy())
 
 
 def fit_shard(estimator, frame, dist, devices=None):
