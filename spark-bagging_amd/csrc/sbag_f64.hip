@@ -184,6 +184,28 @@ int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunk
 // atomics.  A row of count c adds its label c times (the reference's explode).
 constexpr int kF64Batch = 64;
 
+// one entry of the batch: c consecutive adds of its label (the reference's explode) to the
+// lane's cell of the entry's bin; every operand but the bin is wave-uniform
+__device__ __forceinline__ void f64_add_entry(double* s1, double* s2, uint32_t* cn, uint32_t bin,
+                                              int lane, bool on, uint64_t e0, double y0, int j) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(e0 >> 32), j);
+  const uint32_t c = hi & 0xffu;
+  const uint64_t yb = (uint64_t)__double_as_longlong(y0);
+  const int ylo = __builtin_amdgcn_readlane((int)(uint32_t)yb, j);
+  const int yhi = __builtin_amdgcn_readlane((int)(uint32_t)(yb >> 32), j);
+  const double v = __longlong_as_double((long long)(((uint64_t)(uint32_t)yhi << 32) | (uint32_t)ylo));
+  const double w = 1.0 * v;  // instanceWeight * label
+  const double w2 = w * v;   // instanceWeight * label * label
+  if (on) {
+    const int cell = (int)bin * 64 + lane;
+    for (uint32_t k = 0; k < c; k++) {
+      lds_add_f64(s1 + cell, w);
+      lds_add_f64(s2 + cell, w2);
+    }
+    atomicAdd(cn + cell, c);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_f64_hist(F64HistArgs A) {
   extern __shared__ double lds[];
   const F64Node nd = A.nodes[blockIdx.x];
@@ -205,68 +227,56 @@ __global__ __launch_bounds__(64) void k_f64_hist(F64HistArgs A) {
     cn[k] = 0u;
   }
   __syncthreads();
-  const uint8_t* bcol =
-      A.bins + (int64_t)nd.r * A.bins_rstride + (feat ? (int64_t)A.pos[(int64_t)nd.r * A.Fmax + fl] : 0);
-  const int64_t S = A.S;
   const int64_t a = nd.a, b = nd.b;
-  // batch registers: entry, label (lane i = entry i of the batch), bins (per entry)
-  uint64_t e0 = 0, e1 = 0;
-  double y0 = 0.0, y1 = 0.0;
-  uint32_t b0[kF64Batch], b1[kF64Batch];
-  auto load_batch = [&](int64_t base, uint64_t& e, double& y) {
-    const int64_t i = base + lane;
-    if (i < b) {
+  if (a < b) {
+    // lanes without a feature read column 0 (valid memory) and add nothing
+    const uint8_t* bcol =
+        A.bins + (int64_t)nd.r * A.bins_rstride + (feat ? (int64_t)A.pos[(int64_t)nd.r * A.Fmax + fl] : 0);
+    const int64_t S = A.S;
+    const int64_t last = b - 1;
+    // Every load is unconditional (indexes clamped to the node's last entry), so the loop is
+    // straight-line and the compiler waits only for the loads each step consumes: the bins
+    // of batch k + 1 and the entries of batch k + 2 stay in flight while batch k is added.
+    auto ld_entries = [&](int64_t base, uint64_t& e, double& y) {
+      const int64_t i = min(base + lane, last);
       e = A.ent[i];
       y = A.y[(uint32_t)e];
-    }
-  };
-  auto load_bins = [&](int64_t base, uint64_t e, uint32_t* bb) {
-    const int n = (int)min((int64_t)kF64Batch, b - base);
+    };
+    auto ld_bins = [&](uint64_t e, uint32_t* bb) {
 #pragma unroll
-    for (int j = 0; j < kF64Batch; j++) {
-      const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, j);
-      bb[j] = (feat && j < n) ? (uint32_t)bcol[(int64_t)row * S] : 0u;
-    }
-  };
-  if (a < b) {
-    load_batch(a, e0, y0);
-    load_bins(a, e0, b0);
-    if (a + kF64Batch < b) load_batch(a + kF64Batch, e1, y1);
-  }
-  for (int64_t base = a; base < b; base += kF64Batch) {
-    const int64_t nb = base + kF64Batch;
-    // gather the next batch's bins and the one after's entries before adding this one
-    if (nb < b) load_bins(nb, e1, b1);
-    uint64_t e2 = 0;
-    double y2 = 0.0;
-    if (nb + kF64Batch < b) load_batch(nb + kF64Batch, e2, y2);
-    const int n = (int)min((int64_t)kF64Batch, b - base);
-#pragma unroll
-    for (int j = 0; j < kF64Batch; j++) {
-      if (j < n) {
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(e0 >> 32), j);
-        const uint32_t c = hi & 0xffu;
-        const int ylo = __builtin_amdgcn_readlane((int)(uint32_t)__double_as_longlong(y0), j);
-        const int yhi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)__double_as_longlong(y0) >> 32), j);
-        const double v = __longlong_as_double((long long)(((uint64_t)(uint32_t)yhi << 32) | (uint32_t)ylo));
-        const double w = 1.0 * v;  // instanceWeight * label
-        const double w2 = w * v;   // instanceWeight * label * label
-        if (on) {
-          const int cell = (int)b0[j] * 64 + lane;
-          for (uint32_t k = 0; k < c; k++) {
-            lds_add_f64(s1 + cell, w);
-            lds_add_f64(s2 + cell, w2);
-          }
-          atomicAdd(cn + cell, c);
-        }
+      for (int j = 0; j < kF64Batch; j++) {
+        const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, j);
+        bb[j] = (uint32_t)bcol[(int64_t)row * S];
       }
-    }
+    };
+    uint64_t e0, e1;
+    double y0, y1;
+    uint32_t b0[kF64Batch], b1[kF64Batch];
+    ld_entries(a, e0, y0);
+    ld_bins(e0, b0);
+    ld_entries(a + kF64Batch, e1, y1);
+    for (int64_t base = a; base < b; base += kF64Batch) {
+      ld_bins(e1, b1);
+      uint64_t e2;
+      double y2;
+      ld_entries(base + 2 * kF64Batch, e2, y2);
+      const int n = (int)min((int64_t)kF64Batch, b - base);
+      if (n == kF64Batch) {
 #pragma unroll
-    for (int j = 0; j < kF64Batch; j++) b0[j] = b1[j];
-    e0 = e1;
-    y0 = y1;
-    e1 = e2;
-    y1 = y2;
+        for (int j = 0; j < kF64Batch; j++)
+          f64_add_entry(s1, s2, cn, feat ? b0[j] : 0u, lane, on, e0, y0, j);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kF64Batch; j++)
+          if (j < n) f64_add_entry(s1, s2, cn, feat ? b0[j] : 0u, lane, on, e0, y0, j);
+      }
+#pragma unroll
+      for (int j = 0; j < kF64Batch; j++) b0[j] = b1[j];
+      e0 = e1;
+      y0 = y1;
+      e1 = e2;
+      y1 = y2;
+    }
   }
   __syncthreads();
   if (on) {

@@ -1644,8 +1644,6 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
   }
   uint64_t* ent_cur = G.entA;
   uint64_t* ent_nxt = G.entB;
-  const int FPW = 64;
-  const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
   const size_t node_words = (size_t)(Fmax + 1) * NB * 3;
   // nodes per histogram batch: the level's fp64 histograms within 4 GB
   const int64_t batch = std::max<int64_t>(1, ((int64_t)4 << 30) / (int64_t)(node_words * 8));
@@ -1653,6 +1651,11 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
     G.levels++;
     G.tm.level = level;
     const int A = (int)cur.size();
+    // features per wave: a wave walks its node's entries serially (the row order), so
+    // few, long nodes (the shallow levels) get narrower feature groups and more waves
+    int FPW = 64;
+    while (FPW > 8 && (int64_t)A * ((Fmax + 1 + FPW - 1) / FPW) < 2048) FPW /= 2;
+    const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
     std::vector<F64Node> hn(A);
     std::vector<F64Chain> chain(A);
     for (int q = 0; q < A; q++) {
@@ -2045,6 +2048,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   static const bool group_off = getenv("SBAG_NO_TILE_GROUPING") != nullptr;
   std::vector<std::pair<int64_t, int64_t>> gsegs;
   std::vector<ParentInfo> gpar;
+  // the last grouping's per-segment tile bounds [segs][ntc + 1], its class tile and buffer
+  // (tile-resident entries start from the root's grouping, see the level loop)
+  std::vector<int64_t> gtile_bounds;
+  int gtile_ct = 0;
+  uint64_t* gtile_ent = nullptr;
+  bool hist_pregrouped = false;  // launch(): segments are (node, tile) sub-segments already
   // Gini class tiles: regroup the entries to be histogrammed so that each (segment,
   // class tile) is contiguous (k_tile_count / k_tile_scatter into "entG"), and hand the
   // histogram one sub-segment per (segment, tile) with ParentInfo.tile.
@@ -2084,6 +2093,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     std::vector<int64_t> base((size_t)np * ntc);
     gsegs.clear();
     gpar.clear();
+    gtile_bounds.assign(segs.size() * (ntc + 1), 0);
+    gtile_ct = CT;
     gsegs.reserve((size_t)segs.size() * ntc);
     gpar.reserve((size_t)segs.size() * ntc);
     for (int p0 = 0; p0 < np;) {
@@ -2093,6 +2104,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       int64_t o = segs[q].first;
       for (int t = 0; t < ntc; t++) {
         const int64_t start = o;
+        gtile_bounds[(size_t)q * (ntc + 1) + t] = o;
         for (int p = p0; p < p1; p++) {
           base[(size_t)p * ntc + t] = o;
           o += cnt[(size_t)p * ntc + t];
@@ -2104,6 +2116,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
           gpar.push_back(pi);
         }
       }
+      gtile_bounds[(size_t)q * (ntc + 1) + ntc] = o;
       p0 = p1;
     }
     if (hprof) hp[19] += hnow() - gt0;  // host prefix and sub-segment lists
@@ -2111,6 +2124,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     launch_tile_scatter(c->stream, d_pcs, np, ha.ent_in, CT, ntc, d_base, d_entg);
     HIP_TRY(hipGetLastError());
     *ent_out = d_entg;
+    gtile_ent = d_entg;
     return SBAG_OK;
   };
   // class tiles of a gini histogram: group the entries by tile (k_hist only)
@@ -2141,7 +2155,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     const uint64_t* ent_saved = ha.ent_in;
     int ntiles = g.ntiles;
     double lt0 = hprof ? hnow() : 0.0;
-    if (grouped) {  // timed apart from the histogram kernel (group_ms)
+    if (grouped && hist_pregrouped) {
+      ntiles = g.ntf;  // (node, tile) sub-segments of tile-resident entries: nothing to group
+    } else if (grouped) {  // timed apart from the histogram kernel (group_ms)
       const int hg = tm.begin(cat == T_HIST ? T_GROUP : cat);
       uint64_t* d_entg = nullptr;
       TRY(group_tiles(g, segs_in, par_in, &d_entg));
@@ -2162,8 +2178,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     // k_hist_rl row prefetch distance in passes of 4 entries (C3, ms per fit: 2 -> hist 92.1,
     // 3 -> 90.2 and step 134, 4 -> hist 89.7 and step 130, 5 -> flat); only 4 is built
     ha.rlpd = 4;
-    const std::vector<std::pair<int64_t, int64_t>>& segs = grouped ? gsegs : segs_in;
-    const std::vector<ParentInfo>& par = grouped ? gpar : par_in;
+    const bool regrouped = grouped && !hist_pregrouped;
+    const std::vector<std::pair<int64_t, int64_t>>& segs = regrouped ? gsegs : segs_in;
+    const std::vector<ParentInfo>& par = regrouped ? gpar : par_in;
     build_work(segs, flush_limit, 256 * wpc * (grouped ? 2 : 1), g.T, work);
     TRY(upload_work(par));
     if (hprof) {
@@ -2763,6 +2780,26 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   const double inv_scale = std::ldexp(1.0, -ds->shift), inv_scale2 = std::ldexp(1.0, -2 * ds->shift);
   uint64_t* ent_cur = entA;
   uint64_t* ent_nxt = entB;
+  // Tile-resident gini entries (C5's class tiles): the root's class-tile grouping is kept
+  // for the whole fit.  Every node is a list of ntc (node, class tile) sub-segments; the
+  // partition splits each sub-segment in place (left from its front, right from its back:
+  // k_partition with one parent per (node, tile)), so the children's entries are grouped
+  // for their histograms and no level regroups -- k_tile_count / k_tile_scatter and their
+  // host round trip ran before every histogram (18.9 ms per C5 shard fit, round 2).
+  const int ntc_t = g.CT > 0 ? (NS + g.CT - 1) / g.CT : 1;
+  const bool tile_res = gini && g.grouped && !group_off && !getenv("SBAG_NO_TILE_RESIDENT") &&
+                        gtile_ent != nullptr && gtile_ct == g.CT &&
+                        gtile_bounds.size() == (size_t)R * (ntc_t + 1);
+  std::vector<std::pair<int64_t, int64_t>> tseg;  // [slot][ntc_t] sub-segments (tile_res)
+  if (tile_res) {
+    tseg.resize((size_t)R * ntc_t);
+    for (int r = 0; r < R; r++)
+      for (int t = 0; t < ntc_t; t++)
+        tseg[(size_t)r * ntc_t + t] = {gtile_bounds[(size_t)r * (ntc_t + 1) + t],
+                                       gtile_bounds[(size_t)r * (ntc_t + 1) + t + 1]};
+    ent_cur = gtile_ent;
+    hist_pregrouped = true;
+  }
   std::string hist_nxt_name = "histB", hist_cur_name = "histA";
   int levels = 0;
   // exact sum of count*k^2 of every slot's node (variance screening): root from k_compact
@@ -2970,6 +3007,28 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     }
     hmark(2);
     if (par.empty()) break;
+    // tile-resident entries: one partition parent per (split node, non-empty class tile)
+    const int NPn = (int)par.size();  // split nodes
+    std::vector<int32_t> tq_first, tq_tile;
+    if (tile_res) {
+      std::vector<ParentInfo> tpar;
+      std::vector<std::pair<int64_t, int64_t>> tps;
+      tq_first.assign((size_t)NPn + 1, 0);
+      for (int q = 0; q < NPn; q++) {
+        tq_first[q] = (int)tpar.size();
+        const size_t i = (size_t)psplit[q].slot;
+        for (int t = 0; t < ntc_t; t++) {
+          const auto& sub = tseg[i * ntc_t + t];
+          if (sub.second <= sub.first) continue;
+          tpar.push_back(par[q]);
+          tps.push_back(sub);
+          tq_tile.push_back(t);
+        }
+      }
+      tq_first[NPn] = (int)tpar.size();
+      par.swap(tpar);
+      pseg.swap(tps);
+    }
     // --- partition the rows of every split node into its children (and, for
     // variance, the exact sum of squares of each left child)
     const int NP = (int)par.size();
@@ -3102,7 +3161,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     std::vector<int32_t> triples;
     std::vector<std::pair<int64_t, int64_t>> hseg;
     std::vector<ParentInfo> hpar;
-    for (int q = 0; q < NP; q++) {
+    std::vector<std::pair<int64_t, int64_t>> ntseg;  // next slots' tile sub-segments
+    for (int q = 0; q < NPn; q++) {
       const Split& sp = psplit[q];
       HNode& L = trees[sp.r][sp.li];
       HNode& Rn = trees[sp.r][sp.li + 1];
@@ -3132,17 +3192,39 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       Rn.is_leaf = child_leaf || Rn.impurity == 0.0;
       const bool wl = !L.is_leaf, wr = !Rn.is_leaf;
       int sl = -1, sr = -1;
-      if (wl) {
-        sl = (int)next_slots.size();
-        next_slots.push_back({sp.r, sp.li});
-        nseg.push_back({pseg[q].first, (int64_t)cur[2 * q]});
-        next_sq.push_back(gini ? 0 : (uint64_t)L.stats[2]);
-      }
-      if (wr) {
-        sr = (int)next_slots.size();
-        next_slots.push_back({sp.r, sp.li + 1});
-        nseg.push_back({(int64_t)cur[2 * q + 1], pseg[q].second});
-        next_sq.push_back(gini ? 0 : (uint64_t)Rn.stats[2]);
+      if (tile_res) {
+        // child tile t: [sub.first, left cursor) and [right cursor, sub.second) of the
+        // (node, tile) sub-segment; nseg keeps each child's entry count only
+        for (int side = 0; side < 2; side++) {
+          if (side == 0 ? !wl : !wr) continue;
+          (side == 0 ? sl : sr) = (int)next_slots.size();
+          next_slots.push_back({sp.r, sp.li + side});
+          next_sq.push_back(0);
+          const size_t b0 = ntseg.size();
+          ntseg.resize(b0 + ntc_t, {0, 0});
+          int64_t n = 0;
+          for (int k = tq_first[q]; k < tq_first[q + 1]; k++) {
+            const std::pair<int64_t, int64_t> sub =
+                side == 0 ? std::make_pair(pseg[k].first, (int64_t)cur[2 * k])
+                          : std::make_pair((int64_t)cur[2 * k + 1], pseg[k].second);
+            ntseg[b0 + tq_tile[k]] = sub;
+            n += sub.second - sub.first;
+          }
+          nseg.push_back({0, n});
+        }
+      } else {
+        if (wl) {
+          sl = (int)next_slots.size();
+          next_slots.push_back({sp.r, sp.li});
+          nseg.push_back({pseg[q].first, (int64_t)cur[2 * q]});
+          next_sq.push_back(gini ? 0 : (uint64_t)L.stats[2]);
+        }
+        if (wr) {
+          sr = (int)next_slots.size();
+          next_slots.push_back({sp.r, sp.li + 1});
+          nseg.push_back({(int64_t)cur[2 * q + 1], pseg[q].second});
+          next_sq.push_back(gini ? 0 : (uint64_t)Rn.stats[2]);
+        }
       }
       int hs = -1;
       if (wl && wr) {
@@ -3155,7 +3237,14 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       } else if (wl || wr) {
         hs = wl ? sl : sr;
       }
-      if (hs >= 0) {
+      if (hs >= 0 && tile_res) {
+        for (int t = 0; t < ntc_t; t++) {
+          const auto& sub = ntseg[(size_t)hs * ntc_t + t];
+          if (sub.second <= sub.first) continue;
+          hseg.push_back(sub);
+          hpar.push_back(ParentInfo{sp.r, -1, 0, 0, 0, hs, 0, t});
+        }
+      } else if (hs >= 0) {
         hseg.push_back(nseg[hs]);
         hpar.push_back(ParentInfo{sp.r, -1, 0, 0, 0, hs, 0, 0});
       }
@@ -3179,7 +3268,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     pre_hist = [&, hist_nxt, Mn]() -> int {
       std::vector<int32_t> zs;
       zs.reserve(hpar.size());
-      for (const ParentInfo& p : hpar) zs.push_back(p.hist_slot);
+      for (const ParentInfo& p : hpar)  // (a tile-resident slot's sub-segments are adjacent)
+        if (zs.empty() || zs.back() != p.hist_slot) zs.push_back(p.hist_slot);
       const int64_t u32w = slot_words * (int64_t)word_bytes / 4;
       if ((u32w & 3) == 0 && !zs.empty()) {
         int32_t* d_zs;
@@ -3206,6 +3296,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       tm.end(h);
     }
     seg = nseg;
+    if (tile_res) tseg.swap(ntseg);
     slots = next_slots;
     slot_sq = next_sq;
     std::swap(hist_cur_name, hist_nxt_name);
