@@ -1402,6 +1402,24 @@ static void merge_forests(sbag_forest* fa, sbag_forest* fb) {
   T.group_ms += U.group_ms;
 }
 
+// Two learner parts run side by side only when both workspaces fit the device next to what
+// is already allocated: per replica the counts (N bytes) and the two entry buffers (16 N),
+// plus the histogram slots.  C4's shard (10^8 rows, 64 learners: 2 x 54 GB) qualifies on a
+// 288-GB MI355X; the context's own workspace is reused by its part.
+static bool overlap_fits(sbag_ctx* c, const sbag_dataset* ds, int learners) {
+  size_t fr = 0, tot = 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  double mine = 0;  // this context's and its twins' workspaces are reused by the parts
+  for (const auto& kv : c->ws) mine += (double)kv.second.cap;
+  for (const sbag_ctx* t : c->twins)
+    for (const auto& kv : t->ws) mine += (double)kv.second.cap;
+  const double part = (double)((learners + 1) / 2) * (double)ds->N * 17.0 + (double)(1ull << 30);
+  return 2.0 * part <= 0.9 * ((double)fr + mine);
+}
+
 // one context: fit_range, or halves of the learner range when per-replica bins exceed
 // the device budget (learners are independent, so concatenation is exact)
 static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
@@ -1438,7 +1456,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   // rows with at least 16 learners overlap; SBAG_OVERLAP=0/1
   // forces it off / on; SBAG_OVERLAP=k runs k parts (3 and 4 were slower on C3: 151, 152 ms).
   const char* ov = getenv("SBAG_OVERLAP");
-  int parts = ov ? atoi(ov) : ((le - lb >= 16 && ds->N >= (1 << 20) && ds->N <= (1 << 26)) ? 2 : 0);
+  int parts = ov ? atoi(ov) : ((le - lb >= 16 && ds->N >= (1 << 20) && overlap_fits(c, ds, le - lb)) ? 2 : 0);
   if (parts == 1) parts = 2;  // SBAG_OVERLAP=1: on, two parts
   parts = std::min(parts, le - lb);
   if (parts < 2) return fit_learners(c, ds, fp, out);
