@@ -506,17 +506,21 @@ __global__ __launch_bounds__(256) void k_sp_count(F64PartArgs A) {
   if (threadIdx.x == 0) A.piece_left[blockIdx.x] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
 }
 
-// per split node: left entries before each of its pieces, and the node's left total
+// per split node (one wave each): left entries before each of its pieces, and the node's
+// left total -- 64 pieces per step with a wave prefix scan
 __global__ __launch_bounds__(64) void k_sp_scan(F64PartArgs A, int nnodes) {
-  const int q = blockIdx.x * 64 + threadIdx.x;
-  if (q >= nnodes) return;
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
   const F64PartNode p = A.nodes[q];
   int64_t acc = 0;
-  for (int64_t k = p.piece0; k < p.piece1; k++) {
-    A.piece_base[k] = acc;
-    acc += A.piece_left[k];
+  for (int64_t k0 = p.piece0; k0 < p.piece1; k0 += 64) {
+    const int64_t k = k0 + lane;
+    const int v = k < p.piece1 ? A.piece_left[k] : 0;
+    const int incl = f64_wave_incl_scan(v, lane);
+    if (k < p.piece1) A.piece_base[k] = acc + (int64_t)(incl - v);
+    acc += (int64_t)__shfl(incl, 63);
   }
-  A.nleft[q] = acc;
+  if (lane == 0) A.nleft[q] = acc;
 }
 
 __global__ __launch_bounds__(256) void k_sp_scatter(F64PartArgs A) {
@@ -550,7 +554,7 @@ __global__ __launch_bounds__(256) void k_sp_scatter(F64PartArgs A) {
 void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int64_t npieces) {
   if (npieces <= 0) return;
   hipLaunchKernelGGL(k_sp_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_sp_scan, dim3((nnodes + 63) / 64), dim3(64), 0, st, a, nnodes);
+  hipLaunchKernelGGL(k_sp_scan, dim3(nnodes), dim3(64), 0, st, a, nnodes);
   hipLaunchKernelGGL(k_sp_scatter, dim3((unsigned)npieces), dim3(256), 0, st, a);
 }
 

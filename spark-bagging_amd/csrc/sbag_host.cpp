@@ -1669,10 +1669,11 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
     G.levels++;
     G.tm.level = level;
     const int A = (int)cur.size();
-    // features per wave: a wave walks its node's entries serially (the row order), so
-    // few, long nodes (the shallow levels) get narrower feature groups and more waves
-    int FPW = 64;
-    while (FPW > 8 && (int64_t)A * ((Fmax + 1 + FPW - 1) / FPW) < 2048) FPW /= 2;
+    // features per wave (SBAG_F64_FPW, default 64).  Narrower groups give the shallow
+    // levels more waves but multiply the LDS atomic instructions: FPW down to 8 at < 2048
+    // waves made the C3-shape fit 1.7x slower (gpurun_out/r03c).
+    const int fpw_env = getenv("SBAG_F64_FPW") ? atoi(getenv("SBAG_F64_FPW")) : 64;
+    const int FPW = std::max(1, std::min(64, fpw_env));
     const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
     std::vector<F64Node> hn(A);
     std::vector<F64Chain> chain(A);
@@ -2805,7 +2806,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   // for their histograms and no level regroups -- k_tile_count / k_tile_scatter and their
   // host round trip ran before every histogram (18.9 ms per C5 shard fit, round 2).
   const int ntc_t = g.CT > 0 ? (NS + g.CT - 1) / g.CT : 1;
-  const bool tile_res = gini && g.grouped && !group_off && !getenv("SBAG_NO_TILE_RESIDENT") &&
+  // Off by default (SBAG_TILE_RESIDENT=1 turns it on): measured on the C5 shard it removed
+  // the per-level grouping (18.9 -> 4.1 ms per fit) but the partition's (node, tile) pieces
+  // cost as much (25.7 -> 40.2 ms) and their host setup more (serialized fit 181 -> 223 ms).
+  const bool tile_res_env = getenv("SBAG_TILE_RESIDENT") && atoi(getenv("SBAG_TILE_RESIDENT")) != 0;
+  const bool tile_res = tile_res_env && gini && g.grouped && !group_off &&
                         gtile_ent != nullptr && gtile_ct == g.CT &&
                         gtile_bounds.size() == (size_t)R * (ntc_t + 1);
   std::vector<std::pair<int64_t, int64_t>> tseg;  // [slot][ntc_t] sub-segments (tile_res)

@@ -286,6 +286,17 @@ def test_many_classes_c5_shape(ctx):
             oracle.predict(orf, X, classification=True)).all()
 
 
+@pytest.mark.parametrize("replacement", [False, True])
+def test_tile_resident_entries_opt_in(ctx, monkeypatch, replacement):
+    """SBAG_TILE_RESIDENT=1: the root's class-tile grouping kept for the whole fit, the
+    partition splitting every (node, tile) sub-segment in place -- same trees (the option
+    is off by default: slower on the C5 shard)."""
+    monkeypatch.setenv("SBAG_TILE_RESIDENT", "1")
+    ds, X, forest, orf = _synthetic_cls(ctx, 24000, 100, 64, 3, 12, seed_data=19,
+                                        replacement=replacement, ratio=0.6)
+    assert_forest_equal(forest, orf)
+
+
 def test_gini_class_tiles_forced(ctx, monkeypatch):
     """A tiny LDS budget forces one-class tiles on a 7-class problem (k_hist class
     tiling + per-wave entry staging), bit-exact against the oracle."""
