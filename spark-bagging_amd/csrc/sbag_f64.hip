@@ -7,8 +7,8 @@
 // bin) cell in row order, in fp64 (count += 1, sum += 1 * y, sumSq += 1 * y * y).  These
 // kernels reproduce those sums bit for bit:
 //
-//   k_chunk_inbag / k_chunk_scan / k_compact_ordered  in-bag entries of each replica in
-//                                                      row order (a stable compaction)
+//   k_chunk_inbag / k_chunk_scan / k_compact_ordered  the exploded bootstrap of each
+//                     replica: one entry per draw, in row order (a stable compaction)
 //   k_f64_hist        one wave per (node, group of <= 64 features); lane = feature owns
 //                     that feature's NB cells in LDS and walks the node's entries in row
 //                     order, adding each row's label with LDS fp64 atomics (ds_add_f64):
@@ -61,16 +61,15 @@ __device__ __forceinline__ int block_excl_scan256(int v, int* s_wave, int* total
   return before + incl - v;
 }
 
-__device__ __forceinline__ void lds_add_f64(double* p, double v) {
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 constexpr int kChunkRows = 8192;
 
 }  // namespace
 
 // ---------------------------------------------------------------- ordered compaction
-// per (replica, 8192-row chunk): in-bag rows, and per replica Σ count and max count
+// The fp64 path explodes the bootstrap (sql/bfunctions.scala:42-44: a row drawn c times is
+// c consecutive rows): every draw is its own entry (row | 1 << 32), in row order, so the
+// histogram walk adds one label per entry without a per-entry loop.
+// per (replica, 8192-row chunk): draws; per replica Σ count and max count
 __global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__ counts, int64_t N,
                                                      int R, int64_t chunks,
                                                      uint32_t* __restrict__ ncnt,
@@ -79,41 +78,36 @@ __global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__
   const int r = blockIdx.x % R;
   const int64_t chunk = blockIdx.x / R;
   const uint8_t* cr = counts + (int64_t)r * N;
-  int n = 0;
   unsigned int s = 0, m = 0;
   for (int it = 0; it < kChunkRows / 256; it++) {
     const int64_t row = chunk * kChunkRows + it * 256 + threadIdx.x;
     if (row < N) {
       const unsigned int c = cr[row];
-      n += c ? 1 : 0;
       s += c;
       m = max(m, c);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
-    n += __shfl_down(n, o);
     s += __shfl_down(s, o);
     m = max(m, (unsigned int)__shfl_down((int)m, o));
   }
-  __shared__ int s_n[4];
   __shared__ unsigned int s_s[4], s_m[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
-    s_n[wave] = n;
     s_s[wave] = s;
     s_m[wave] = m;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    ncnt[(int64_t)r * chunks + chunk] = (uint32_t)(s_n[0] + s_n[1] + s_n[2] + s_n[3]);
-    const unsigned long long t = (unsigned long long)s_s[0] + s_s[1] + s_s[2] + s_s[3];
-    if (t) atomicAdd(&wsum[r], t);
+    const unsigned int t = s_s[0] + s_s[1] + s_s[2] + s_s[3];  // <= 8192 * 255
+    ncnt[(int64_t)r * chunks + chunk] = t;
+    if (t) atomicAdd(&wsum[r], (unsigned long long)t);
     const unsigned int mm = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
     if (mm) atomicMax(&cmax[r], mm);
   }
 }
 
-// per replica: exclusive prefix of the chunks' in-bag counts; cursor[r] = the total
+// per replica: exclusive prefix of the chunks' draws; cursor[r] = the total
 __global__ __launch_bounds__(256) void k_chunk_scan(const uint32_t* __restrict__ ncnt, int64_t chunks,
                                                     unsigned long long* __restrict__ base,
                                                     unsigned long long* __restrict__ cursor) {
@@ -131,7 +125,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(const uint32_t* __restrict__
   if (threadIdx.x == 0) cursor[r] = carry;
 }
 
-// entries (row | count << 32) of every in-bag row, in row order
+// one entry (row | 1 << 32) per draw, in row order
 __global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restrict__ counts, int64_t N,
                                                          int R, int64_t chunks,
                                                          const unsigned long long* __restrict__ base,
@@ -149,25 +143,29 @@ __global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restri
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       c[j] = row0 + j < N ? cr[row0 + j] : 0u;
-      n += c[j] ? 1 : 0;
+      n += (int)c[j];
     }
     int tot;
     const int ex = block_excl_scan256(n, s_wave, &tot);
     unsigned long long pos = pos0 + (unsigned long long)ex;
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if (c[j]) er[pos++] = pack_entry((uint32_t)(row0 + j), 0, c[j]);
+      for (uint32_t k = 0; k < c[j]; k++) er[pos++] = pack_entry((uint32_t)(row0 + j), 0, 1u);
     pos0 += (unsigned long long)tot;
   }
 }
 
-void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint64_t* ent,
-                            int64_t cap, uint32_t* d_ncnt, unsigned long long* d_base,
-                            unsigned long long* d_cursor, unsigned long long* d_wsum,
-                            unsigned int* d_cmax) {
-  const int64_t chunks = (N + kChunkRows - 1) / kChunkRows;
+void launch_chunk_draws(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint32_t* d_ncnt,
+                        unsigned long long* d_wsum, unsigned int* d_cmax) {
+  const int64_t chunks = compact_ordered_chunks(N);
   hipLaunchKernelGGL(k_chunk_inbag, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, R,
                      chunks, d_ncnt, d_wsum, d_cmax);
+}
+
+void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint64_t* ent,
+                            int64_t cap, const uint32_t* d_ncnt, unsigned long long* d_base,
+                            unsigned long long* d_cursor) {
+  const int64_t chunks = compact_ordered_chunks(N);
   hipLaunchKernelGGL(k_chunk_scan, dim3(R), dim3(256), 0, st, d_ncnt, chunks, d_base, d_cursor);
   hipLaunchKernelGGL(k_compact_ordered, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, R,
                      chunks, d_base, ent, cap);
@@ -176,131 +174,197 @@ void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, in
 int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunkRows; }
 
 // ---------------------------------------------------------------- row-order fp64 histogram
-// LDS per wave: sum [NB][64] f64, sumSq [NB][64] f64, count [NB][64] u32.  Lane fl < Fr
-// owns feature fl's cells, lane Fr (when in this group) the node total (one bin).  The
-// wave walks the node's entries in batches of 64: lane i loads entry i and its label;
-// the bins of batch k + 1 are gathered (one byte per lane and entry, the row's line
-// shared by the wave) while batch k is added, so the gathers' latency overlaps the
-// atomics.  A row of count c adds its label c times (the reference's explode).
+// LDS per wave: count u32 [NB][W] at byte 0, then sum and sumSq interleaved as f64
+// [NB][2][W] (sum of lane l at bin k: 16·W·k + 8·l, its sumSq 8·W bytes further), W = 64
+// lanes (32 when NB > 128 would not fit 160 KB).  Lane fl < Fr owns feature fl's cells,
+// lane Fr (when in this group) the node total at bin 0, lanes past the group their own
+// bin-0 cells (never read back).  A cell address is one 24-bit multiply-add, bin · M +
+// lane offset, M = 0 for the total and the idle lanes.
+//
+// The wave walks the node's entries (one per draw, compaction above) two batches of 64
+// at a time: lane i holds entry i and its label, and the bins of the next batch are
+// gathered one per entry of the current one, right after that entry's atomics, so each
+// gather has ~63 entries of work to land in (the most the 6-bit vmcnt counter tracks).
+// Both batches of an iteration are one basic block and the bins are consumed exactly as
+// loaded: any operation between a gather and its use (a mask, a widening the compiler
+// sinks to the use or folds through the loop phi, a rotation copy) would wait on every
+// gather in flight.  Per entry: two readlanes (the label), its square, two cell
+// addresses, the LDS atomics and the next gather.  The node's last iteration runs whole:
+// entries past the end repeat the last entry with label y[N] = +0.0 (an exact no-op for
+// the sums, which start at +0.0 and so never become -0.0), and their count increments are
+// taken back from the last row's cells after the walk.
+//
+// Parts: at shallow levels (few nodes, few waves) a (node, group) is split over two
+// waves, one adding count and sum, the other sumSq: the two walks run in parallel and
+// each issues part of the LDS atomics (the walk is the level's critical path there).
 constexpr int kF64Batch = 64;
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) double lds_double;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-// one entry of the batch: c consecutive adds of its label (the reference's explode) to the
-// lane's cell of the entry's bin; every operand but the bin is wave-uniform
-__device__ __forceinline__ void f64_add_entry(double* s1, double* s2, uint32_t* cn, uint32_t bin,
-                                              int lane, bool on, uint64_t e0, double y0, int j) {
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(e0 >> 32), j);
-  const uint32_t c = hi & 0xffu;
-  const uint64_t yb = (uint64_t)__double_as_longlong(y0);
+template <int PART, int W>
+__device__ __forceinline__ void f64_add_entry(lds_char* L, double y, uint32_t bin, int j,
+                                              uint32_t M1, uint32_t lo1, uint32_t M2, uint32_t lo2,
+                                              bool act) {
+  const uint64_t yb = (uint64_t)__double_as_longlong(y);
   const int ylo = __builtin_amdgcn_readlane((int)(uint32_t)yb, j);
   const int yhi = __builtin_amdgcn_readlane((int)(uint32_t)(yb >> 32), j);
   const double v = __longlong_as_double((long long)(((uint64_t)(uint32_t)yhi << 32) | (uint32_t)ylo));
-  const double w = 1.0 * v;  // instanceWeight * label
-  const double w2 = w * v;   // instanceWeight * label * label
-  if (on) {
-    const int cell = (int)bin * 64 + lane;
-    for (uint32_t k = 0; k < c; k++) {
-      lds_add_f64(s1 + cell, w);
-      lds_add_f64(s2 + cell, w2);
-    }
-    atomicAdd(cn + cell, c);
-  }
+  const double w = 1.0 * v;   // instanceWeight * label
+  if (W < 64 && !act) return;  // lanes past W hold no cells
+  lds_double* s = (lds_double*)(L + (__umul24(bin, M1) + lo1));
+  if (PART != 2) __hip_atomic_fetch_add(s, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (PART != 1)  // instanceWeight * label * label (its own array in part 2)
+    __hip_atomic_fetch_add(PART == 2 ? s : s + W, w * v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (PART != 2)
+    __hip_atomic_fetch_add((lds_u32*)(L + (__umul24(bin, M2) + lo2)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__global__ __launch_bounds__(64) void k_f64_hist(F64HistArgs A) {
+template <int PART, int W, bool BUF>
+__device__ __forceinline__ void f64_hist_body(const F64HistArgs& A, const F64Node& nd, int group) {
   extern __shared__ double lds[];
-  const F64Node nd = A.nodes[blockIdx.x];
+  lds_char* L = (lds_char*)lds;
   const int lane = threadIdx.x;
   const int Fr = A.Fr[nd.r];
-  const int f0 = blockIdx.y * A.FPW;
-  if (f0 > Fr) return;  // this feature group lies past the node's features and total
+  const int f0 = group * A.FPW;
   const int fl = f0 + lane;
-  const bool feat = lane < A.FPW && fl < Fr;
-  const bool tot = lane < A.FPW && fl == Fr;
-  const bool on = feat || tot;
+  const bool feat = lane < A.FPW && lane < W && fl < Fr;
+  const bool tot = lane < A.FPW && lane < W && fl == Fr;
   const int NB = A.NB;
-  double* s1 = lds;
-  double* s2 = lds + (size_t)NB * 64;
-  uint32_t* cn = (uint32_t*)(lds + (size_t)2 * NB * 64);
-  for (int k = lane; k < NB * 64; k += 64) {
-    s1[k] = 0.0;
-    s2[k] = 0.0;
-    cn[k] = 0u;
-  }
+  // part 0: counts, then sum and sumSq interleaved; part 1: counts, then sums; part 2:
+  // sumSq only
+  const uint32_t B1 = PART == 2 ? 0u : (uint32_t)NB * W * 4;
+  const uint32_t F64W = PART == 0 ? 2u : 1u;  // f64 arrays per bin row
+  for (uint32_t k = lane * 4; k < B1 + (uint32_t)NB * W * 8 * F64W; k += 256) *(lds_u32*)(L + k) = 0u;
   __syncthreads();
   const int64_t a = nd.a, b = nd.b;
   if (a < b) {
-    // lanes without a feature read column 0 (valid memory) and add nothing
-    const uint8_t* bcol =
-        A.bins + (int64_t)nd.r * A.bins_rstride + (feat ? (int64_t)A.pos[(int64_t)nd.r * A.Fmax + fl] : 0);
-    const int64_t S = A.S;
+    const bool act = lane < W;
+    const uint32_t M1 = feat ? 8u * F64W * W : 0u, M2 = feat ? 4u * W : 0u;
+    const uint32_t lo1 = B1 + 8u * (uint32_t)lane, lo2 = 4u * (uint32_t)lane;
+    const uint8_t* bins_r = A.bins + (int64_t)nd.r * A.bins_rstride;
+    // lanes without a feature read column 0 (valid memory) and multiply it by 0
+    const uint32_t posl = feat ? (uint32_t)A.pos[(int64_t)nd.r * A.Fmax + fl] : 0u;
+    const uint64_t S = (uint64_t)A.S;
+    const uint32_t S32 = (uint32_t)A.S;
     const int64_t last = b - 1;
-    // Every load is unconditional (indexes clamped to the node's last entry), so the loop is
-    // straight-line and the compiler waits only for the loads each step consumes: the bins
-    // of batch k + 1 and the entries of batch k + 2 stay in flight while batch k is added.
-    auto ld_entries = [&](int64_t base, uint64_t& e, double& y) {
-      const int64_t i = min(base + lane, last);
-      e = A.ent[i];
-      y = A.y[(uint32_t)e];
+    // BUF: a replica's bins below 4 GB, a buffer load with the row offset in a scalar
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)bins_r, (short)0, (int)A.bins_bytes, 0x00020000);
+    auto ld_row_bin = [&](uint32_t row) -> uint32_t {
+      if (BUF) return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, posl, row * S32, 0);
+      return (uint32_t)bins_r[(uint64_t)row * S + posl];
     };
-    auto ld_bins = [&](uint64_t e, uint32_t* bb) {
+    auto ld_bin = [&](uint64_t e, int j) -> uint32_t {
+      return ld_row_bin((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, j));
+    };
+    auto ld_entry = [&](int64_t base) -> uint64_t { return A.ent[min(base + lane, last)]; };
+    auto ld_y = [&](int64_t base, uint64_t e) -> double {
+      return A.y[base + lane <= last ? (uint32_t)e : A.yzero];
+    };
+    // even batches: eE, yE, bE; odd batches: eO, yO, bO -- each updated in place
+    uint64_t eE = ld_entry(a), eO = ld_entry(a + kF64Batch);
+    double yE = ld_y(a, eE), yO = ld_y(a + kF64Batch, eO);
+    uint32_t bE[kF64Batch], bO[kF64Batch];
+    // (the prologue's bins pass through an opaque xor, so the loop phi is not a widening
+    // the compiler could fold to the top of the loop)
+#pragma unroll
+    for (int j = 0; j < kF64Batch; j++) bE[j] = ld_bin(eE, j) ^ A.zero;
+    int64_t base = a;
+    for (;; base += 2 * kF64Batch) {
+      // batch k (bE, yE): gather batch k + 1's bins, fetch batch k + 2's entries
+      eE = ld_entry(base + 2 * kF64Batch);
 #pragma unroll
       for (int j = 0; j < kF64Batch; j++) {
-        const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, j);
-        bb[j] = (uint32_t)bcol[(int64_t)row * S];
+        f64_add_entry<PART, W>(L, yE, bE[j], j, M1, lo1, M2, lo2, act);
+        bO[j] = ld_bin(eO, j);
+        __builtin_amdgcn_sched_barrier(0);  // keep each gather next to its entry
       }
-    };
-    uint64_t e0, e1;
-    double y0, y1;
-    uint32_t b0[kF64Batch], b1[kF64Batch];
-    ld_entries(a, e0, y0);
-    ld_bins(e0, b0);
-    ld_entries(a + kF64Batch, e1, y1);
-    for (int64_t base = a; base < b; base += kF64Batch) {
-      ld_bins(e1, b1);
-      uint64_t e2;
-      double y2;
-      ld_entries(base + 2 * kF64Batch, e2, y2);
-      const int n = (int)min((int64_t)kF64Batch, b - base);
-      if (n == kF64Batch) {
+      yE = ld_y(base + 2 * kF64Batch, eE);
+      // batch k + 1 (bO, yO): gather batch k + 2's bins, fetch batch k + 3's entries
+      eO = ld_entry(base + 3 * kF64Batch);
 #pragma unroll
-        for (int j = 0; j < kF64Batch; j++)
-          f64_add_entry(s1, s2, cn, feat ? b0[j] : 0u, lane, on, e0, y0, j);
-      } else {
-#pragma unroll
-        for (int j = 0; j < kF64Batch; j++)
-          if (j < n) f64_add_entry(s1, s2, cn, feat ? b0[j] : 0u, lane, on, e0, y0, j);
+      for (int j = 0; j < kF64Batch; j++) {
+        f64_add_entry<PART, W>(L, yO, bO[j], j, M1, lo1, M2, lo2, act);
+        bE[j] = ld_bin(eE, j);
+        __builtin_amdgcn_sched_barrier(0);
       }
-#pragma unroll
-      for (int j = 0; j < kF64Batch; j++) b0[j] = b1[j];
-      e0 = e1;
-      y0 = y1;
-      e1 = e2;
-      y1 = y2;
+      yO = ld_y(base + 3 * kF64Batch, eO);
+      if (base + 2 * kF64Batch >= b) break;
+    }
+    // the padding [b, base + 128) was counted in the last row's cells
+    const uint32_t pad = (uint32_t)(base + 2 * kF64Batch - b);
+    if (PART != 2 && pad != 0u && act) {
+      const uint32_t bl = ld_row_bin((uint32_t)A.ent[last]);
+      __hip_atomic_fetch_sub((lds_u32*)(L + (__umul24(bl, M2) + lo2)), pad, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   __syncthreads();
-  if (on) {
+  if (feat || tot) {
     double* out = A.hist + ((int64_t)blockIdx.x * (A.Fmax + 1) + fl) * NB * 3;
     const int nbk = tot ? 1 : NB;
+    const lds_u32* cn = (const lds_u32*)L;
+    const lds_double* s12 = (const lds_double*)(L + B1);
     for (int k = 0; k < nbk; k++) {
-      out[3 * k] = (double)cn[k * 64 + lane];
-      out[3 * k + 1] = s1[k * 64 + lane];
-      out[3 * k + 2] = s2[k * 64 + lane];
+      if (PART != 2) {
+        out[3 * k] = (double)cn[k * W + lane];
+        out[3 * k + 1] = s12[F64W * k * W + lane];
+      }
+      if (PART != 1) out[3 * k + 2] = s12[(F64W * k + F64W - 1) * W + lane];
     }
   }
 }
 
-size_t f64_hist_lds_bytes(int NB) { return (size_t)NB * 64 * (8 + 8 + 4); }
+// grid (nodes, groups * parts): blockIdx.y = group * parts + part
+template <int W, bool BUF>
+__global__ __launch_bounds__(64) void k_f64_hist(F64HistArgs A) {
+  const F64Node nd = A.nodes[blockIdx.x];
+  const int group = (int)blockIdx.y / A.parts;
+  const int part = (int)blockIdx.y % A.parts;
+  if (group * A.FPW > A.Fr[nd.r]) return;  // past the node's features and total
+  if (A.parts == 1)
+    f64_hist_body<0, W, BUF>(A, nd, group);
+  else if (part == 0)
+    f64_hist_body<1, W, BUF>(A, nd, group);
+  else
+    f64_hist_body<2, W, BUF>(A, nd, group);
+}
 
-void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups) {
-  const size_t lds = f64_hist_lds_bytes(a.NB);
+int f64_hist_width(int NB) { return (size_t)NB * 64 * 20 <= 160 * 1024 ? 64 : 32; }
+// per wave: 20 B a cell (count, sum, sumSq), 12 B when split in parts (count + sum | sumSq)
+size_t f64_hist_lds_bytes(int NB, int parts) {
+  return (size_t)NB * f64_hist_width(NB) * (parts == 1 ? 20 : 12);
+}
+
+template <int W, bool BUF>
+static void launch_f64_hist_t(hipStream_t st, const F64HistArgs& a, dim3 grid, size_t lds) {
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)k_f64_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_f64_hist<W, BUF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
-  hipLaunchKernelGGL(k_f64_hist, dim3(nnodes, ngroups), dim3(64), lds, st, a);
+  hipLaunchKernelGGL((k_f64_hist<W, BUF>), grid, dim3(64), lds, st, a);
+}
+
+void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups) {
+  const size_t lds = f64_hist_lds_bytes(a.NB, a.parts);
+  const dim3 grid(nnodes, ngroups * a.parts);
+  const bool buf = a.bins_bytes != 0;
+  if (f64_hist_width(a.NB) == 64) {
+    if (buf)
+      launch_f64_hist_t<64, true>(st, a, grid, lds);
+    else
+      launch_f64_hist_t<64, false>(st, a, grid, lds);
+  } else {
+    if (buf)
+      launch_f64_hist_t<32, true>(st, a, grid, lds);
+    else
+      launch_f64_hist_t<32, false>(st, a, grid, lds);
+  }
 }
 
 // ---------------------------------------------------------------- split (binsToBestSplit)

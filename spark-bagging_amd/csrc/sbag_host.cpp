@@ -1646,8 +1646,10 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
   {
     std::lock_guard<std::mutex> lk(G.ds->layout_mu);
     if (!G.ds->d_y64) {
-      HIP_TRY(hipMalloc(&G.ds->d_y64, (size_t)std::max<int64_t>(G.N, 1) * 8));
+      // + one +0.0 at index N: the label of the histogram walk's padding entries
+      HIP_TRY(hipMalloc(&G.ds->d_y64, (size_t)(G.N + 1) * 8));
       HIP_TRY(hipMemcpy(G.ds->d_y64, G.ds->y.data(), (size_t)G.N * 8, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemset(G.ds->d_y64 + G.N, 0, 8));
     }
   }
   struct LNode {
@@ -1673,8 +1675,12 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
     // levels more waves but multiply the LDS atomic instructions: FPW down to 8 at < 2048
     // waves made the C3-shape fit 1.7x slower (gpurun_out/r03c).
     const int fpw_env = getenv("SBAG_F64_FPW") ? atoi(getenv("SBAG_F64_FPW")) : 64;
-    const int FPW = std::max(1, std::min(64, fpw_env));
+    const int FPW = std::max(1, std::min(f64_hist_width(NB), fpw_env));
     const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
+    // levels with fewer waves than SIMDs split each (node, group) walk over two waves
+    // (count + sum, sumSq): the walk is the level's critical path there
+    const int split_below = getenv("SBAG_F64_SPLIT") ? atoi(getenv("SBAG_F64_SPLIT")) : 1024;
+    const int parts = (int64_t)A * ngroups < split_below ? 2 : 1;
     std::vector<F64Node> hn(A);
     std::vector<F64Chain> chain(A);
     for (int q = 0; q < A; q++) {
@@ -1714,6 +1720,9 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
       ha.Fr = G.d_Fr;
       ha.NB = NB;
       ha.FPW = FPW;
+      ha.parts = parts;
+      ha.bins_bytes = (double)G.N * G.S < 4294967295.0 ? (uint32_t)(G.N * G.S) : 0u;
+      ha.yzero = (uint32_t)G.N;
       ha.hist = d_hist;
       int h = G.tm.begin(T_HIST);
       launch_f64_hist(c->stream, ha, nq, ngroups);
@@ -1921,27 +1930,36 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     TRY(run_sampler(c, &fp->sampler, poff, N, d_counts));
     tm.end(h);
   }
-  // ---- 2. in-bag entry lists (two ping-pong buffers, capacity N per replica)
-  const int64_t cap = N;
-  uint64_t *entA, *entB;
-  TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
-  TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
+  // ---- 2. in-bag entry lists (two ping-pong buffers per replica): capacity N, or for the
+  // fp64 path, which keeps one entry per draw, the largest replica's draws
   unsigned long long* d_inbag;
   TRY(ws_typed(c, "inbag", (size_t)R * 4, &d_inbag));
   unsigned long long* d_wsum = d_inbag + R;
   unsigned int* d_cmax = (unsigned int*)(d_inbag + 2 * R);
   unsigned long long* d_sqsum = d_inbag + 3 * R;
   HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 32, c->stream));
+  int64_t cap = N;
+  uint32_t* d_ncnt = nullptr;
+  if (f64) {
+    int h = tm.begin(T_COMPACT);
+    TRY(ws_typed(c, "f64_ncnt", (size_t)R * compact_ordered_chunks(N), &d_ncnt));
+    launch_chunk_draws(c->stream, d_counts, N, R, d_ncnt, d_wsum, d_cmax);
+    HIP_TRY(hipGetLastError());
+    tm.end(h);
+    std::vector<unsigned long long> ws(R);
+    TRY(d2h(c, ws.data(), d_wsum, (size_t)R));
+    cap = 1;
+    for (unsigned long long w : ws) cap = std::max<int64_t>(cap, (int64_t)w);
+  }
+  uint64_t *entA, *entB;
+  TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
+  TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
   {
     int h = tm.begin(T_COMPACT);
     if (f64) {  // row order inside every replica (the fp64 sums follow it)
-      const int64_t chunks = compact_ordered_chunks(N);
-      uint32_t* d_ncnt;
       unsigned long long* d_cbase;
-      TRY(ws_typed(c, "f64_ncnt", (size_t)R * chunks, &d_ncnt));
-      TRY(ws_typed(c, "f64_cbase", (size_t)R * chunks, &d_cbase));
-      launch_compact_ordered(c->stream, d_counts, N, R, entA, cap, d_ncnt, d_cbase, d_inbag, d_wsum,
-                             d_cmax);
+      TRY(ws_typed(c, "f64_cbase", (size_t)R * compact_ordered_chunks(N), &d_cbase));
+      launch_compact_ordered(c->stream, d_counts, N, R, entA, cap, d_ncnt, d_cbase, d_inbag);
     } else {
       launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
                      d_sqsum);
@@ -2741,7 +2759,14 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     }
     forest->nclasses = 0;
     double cats[T_NCAT] = {0};
-    tm.collect(cats, nullptr, -1);
+    std::vector<double> hist_each;
+    tm.collect(cats, &hist_each, T_HIST);
+    if (getenv("SBAG_LEVEL_TRACE")) {  // diagnostics: each fp64 histogram launch
+      size_t k = 0;
+      for (size_t i = 0; i < tm.ev.size(); i++)
+        if (tm.ev[i].first == T_HIST && k < hist_each.size())
+          fprintf(stderr, "[sbag] f64 level %d hist ms %.3f\n", tm.lv[i], hist_each[k++]);
+    }
     float total_ms = 0;
     (void)hipEventElapsedTime(&total_ms, ev_start, ev_stop);
     (void)hipEventDestroy(ev_start);

@@ -286,7 +286,10 @@ struct F64HistArgs {
   int32_t S, Fmax;
   const int16_t* pos;      // [R][Fmax] byte of local feature fl in a bins row
   const int32_t* Fr;       // [R]
-  int32_t NB, FPW;         // bins; features per wave (<= 64; local index Fr = node total)
+  int32_t NB, FPW;         // bins; features per wave (<= f64_hist_width; local Fr = total)
+  int32_t parts;           // 1, or 2: count + sum and sumSq on separate waves
+  uint32_t bins_bytes;     // one replica's bins (N·S) when below 4 GB (buffer loads), else 0
+  uint32_t yzero, zero;    // y[yzero] = +0.0 (padding label); zero = 0 (opaque to the compiler)
   double* hist;            // [A][Fmax + 1][NB][3]: count, sum, sumSq
 };
 struct F64Chain {     // calculateImpurityStats' chain state: the node's stats (set) or none
@@ -330,12 +333,17 @@ struct F64PartArgs {
   int64_t* nleft;          // [nodes]
 };
 constexpr int64_t kF64PartPiece = 4096;
+// the exploded bootstrap: draws per (replica, chunk) and per replica (Σ, max), then one
+// entry per draw in row order
+void launch_chunk_draws(hipStream_t st, const uint8_t* counts, int64_t N, int R,
+                        uint32_t* d_ncnt /*[R][chunks]*/, unsigned long long* d_wsum,
+                        unsigned int* d_cmax);
 void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint64_t* ent,
-                            int64_t cap, uint32_t* d_ncnt /*[R][chunks]*/,
-                            unsigned long long* d_base /*[R][chunks]*/, unsigned long long* d_cursor,
-                            unsigned long long* d_wsum, unsigned int* d_cmax);
+                            int64_t cap, const uint32_t* d_ncnt,
+                            unsigned long long* d_base /*[R][chunks]*/, unsigned long long* d_cursor);
 int64_t compact_ordered_chunks(int64_t N);
-size_t f64_hist_lds_bytes(int NB);
+int f64_hist_width(int NB);
+size_t f64_hist_lds_bytes(int NB, int parts);
 void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups);
 void launch_f64_split(hipStream_t st, const F64SplitArgs& a, int nnodes);
 void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int64_t npieces);
