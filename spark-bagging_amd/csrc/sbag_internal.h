@@ -180,6 +180,9 @@ constexpr int kLdsModeClasses = 320;
 // ---- launchers (sbag_kernels.hip) ----
 void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
                     int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err);
+void launch_poisson4(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
+                     int R, int learner0, int64_t seed, double p_exp, int icap, bool cap, int lanes,
+                     int* d_err);
 void launch_bernoulli(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off,
                       const int64_t* d_chunk_pre, int P, int64_t chunks_total, int R,
                       int learner0, int64_t seed, double ratio, const uint64_t* d_jump);

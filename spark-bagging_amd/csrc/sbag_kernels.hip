@@ -33,6 +33,7 @@
 #include <utility>
 
 #include "sbag_internal.h"
+#include "sbag_well.h"
 
 namespace sbag {
 
@@ -68,7 +69,6 @@ static void set_max_lds(const void* fn, int bytes) {
 // window from one wave-uniform base with immediate offsets (no per-read wrap).
 constexpr int kWB = 16;
 
-__device__ __forceinline__ int wrap624(int x) { return x < 0 ? x + 624 : (x >= 624 ? x - 624 : x); }
 
 struct WellOut {
   uint32_t o[kWB];  // next(26) of each step
@@ -301,12 +301,6 @@ __device__ __forceinline__ bool well_window_ok(int p, int len) {  // [p, p+len) 
   return w + len <= 624;
 }
 
-__device__ __forceinline__ uint32_t well_temper26(uint32_t z4) {
-  z4 ^= (z4 << 7) & 0xe46e1700u;
-  z4 ^= (z4 << 15) & 0x9b868000u;
-  return z4 >> 6;  // next(26)
-}
-
 __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, int64_t N,
                                                   const int64_t* __restrict__ part_off, int P,
                                                   int R, int learner0, int64_t seed, double mean,
@@ -458,54 +452,6 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
 // the e-th count the batch emits, then the lanes store the batch's counts together.
 // tests/test_sampler_algebra.py replays this schedule on the CPU against the
 // sequential generator.
-namespace wellsp {
-__host__ __device__ constexpr uint32_t L1(uint32_t x) {
-  return (x << 9) ^ (x >> 21) ^ ((x & 0x7Fu) << 4);
-}
-struct Masks {
-  uint32_t m[63];  // m[s + 31]: input bits i with output bit i + s
-};
-constexpr Masks lpow_masks(int k) {
-  Masks r{};
-  for (int i = 0; i < 32; i++) {
-    uint32_t x = 1u << i;
-    for (int s = 0; s < k; s++) x = L1(x);
-    for (int j = 0; j < 32; j++)
-      if ((x >> j) & 1u) r.m[j - i + 31] |= 1u << i;
-  }
-  return r;
-}
-template <int K>
-struct LP {
-  static constexpr Masks M = lpow_masks(K);
-};
-// L^K(x) as a XOR of shifted, masked copies of x (zero terms vanish at compile time)
-template <int K, int S = 0>
-__device__ __forceinline__ uint32_t lpow(uint32_t x) {
-  if constexpr (S == 63) {
-    return 0u;
-  } else {
-    constexpr uint32_t m = LP<K>::M.m[S];
-    constexpr int sh = S - 31;
-    if constexpr (m == 0u)
-      return lpow<K, S + 1>(x);
-    else if constexpr (sh >= 0)
-      return ((x & m) << sh) ^ lpow<K, S + 1>(x);
-    else
-      return ((x & m) >> (-sh)) ^ lpow<K, S + 1>(x);
-  }
-}
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp(uint32_t x) {  // lanes without a source read 0
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
-}
-template <int LANE>
-__device__ __forceinline__ double row_bcast(double x) {  // DPP row_newbcast:LANE
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + LANE, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + LANE, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-}  // namespace wellsp
 
 constexpr int kSpLanes = 16;                             // lanes per stream
 constexpr int kSpStreams = 256 / kSpLanes;               // streams per 256-thread block
@@ -770,13 +716,23 @@ void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d
                     int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err) {
   const int64_t streams = (int64_t)R * P;
   const int blocks = (int)((streams + 63) / 64);
-  // A/B knobs, read per launch so tests can switch them: SBAG_POISSON_V (3 = k_poisson3,
+  // A/B knobs, read per launch so tests can switch them: SBAG_POISSON_V (4 = k_poisson4,
+  // the default; 3 = k_poisson3,
   // 2 = the two-wave k_poisson2, 1 = one wave), SBAG_POISSON_SPL (steps per lane, 2 or 4),
   // SBAG_POISSON_PAR (1 = lane-parallel relaxation parse, 0 = serial parse)
   const char* ev = getenv("SBAG_POISSON_V");
   const char* es = getenv("SBAG_POISSON_SPL");
-  const int ver = ev ? atoi(ev) : 3;
+  const int ver = ev ? atoi(ev) : 4;
   const int spl = es ? atoi(es) : 4;
+  if (ver == 4) {
+    // k_poisson4 (sbag_poisson.hip); SBAG_POISSON_LANES: lanes per stream (8, 16 or 4; default
+    // by stream count)
+    const int icap = (int)std::min(ceil(1000.0 * mean), 1e9);
+    const char* el = getenv("SBAG_POISSON_LANES");
+    launch_poisson4(st, counts, N, d_part_off, P, R, learner0, seed, p_exp, icap, icap <= 255,
+                    el ? atoi(el) : 0, d_err);
+    return;
+  }
   if (ver == 3) {
     // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean);
     // the cap is only checked when it can end a row below the 255 limit

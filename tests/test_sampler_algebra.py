@@ -53,11 +53,11 @@ def temper26(z4):
     return z4 >> 6
 
 
-def step_parallel_outputs(seed, nsteps, spl):
-    """next(26) outputs of the stream seeded `seed`, batch by batch as the kernel does."""
+def step_parallel_outputs(seed, nsteps, spl, lanes=16):
+    """next(26) outputs of the stream seeded `seed`, batch by batch as the kernel does
+    (k_poisson3: 16 lanes; k_poisson4: 8 lanes x 8 steps, 16 x 4, 4 x 16)."""
     g = pyoracle.Well19937c(seed)  # only for the seeded initial ring
     st = list(g.v)
-    lanes = 16
     B = lanes * spl
     T = {k: lpow_terms(k) for k in (spl * (1 << d) for d in range(5))}
     carry = st[0]  # z4 "before" step 0 is v[0]
@@ -87,7 +87,7 @@ def step_parallel_outputs(seed, nsteps, spl):
                 x = L1(x) ^ c[t][q]
             C.append(x)
         C[0] ^= lpow(T[spl], carry)
-        for d in (1, 2, 4, 8):
+        for d in (d for d in (1, 2, 4, 8) if d < lanes):
             C = [C[t] ^ (lpow(T[spl * d], C[t - d]) if t >= d else 0) for t in range(lanes)]
         for t in range(lanes):
             y = carry if t == 0 else C[t - 1]
@@ -102,11 +102,11 @@ def step_parallel_outputs(seed, nsteps, spl):
     return out[:nsteps]
 
 
-@pytest.mark.parametrize("spl", [1, 2, 4])
+@pytest.mark.parametrize("lanes,spl", [(16, 1), (16, 2), (16, 4), (8, 8), (4, 16)])
 @pytest.mark.parametrize("seed", [0, 42, -1395689524 + 7, (1 << 40) + 3])
-def test_step_parallel_well_matches_sequential(seed, spl):
+def test_step_parallel_well_matches_sequential(seed, lanes, spl):
     n = 3 * 624 + 100  # several trips round the ring, both wrap cases of every window
-    got = step_parallel_outputs(seed, n, spl)
+    got = step_parallel_outputs(seed, n, spl, lanes)
     g = pyoracle.Well19937c(seed)
     want = [g.next(26) for _ in range(n)]
     assert got == want
