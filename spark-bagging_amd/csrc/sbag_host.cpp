@@ -2228,6 +2228,13 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     ha.chunks = d_pieces;
     ha.wg_piece = d_wg;
     ha.parents = nullptr;
+    // short (node, class tile) sub-segments (deep gini levels): the 256-thread k_hist with
+    // 32-entry gather groups; SBAG_HIST_SMALL = mean entries per sub-segment below which it
+    // is used (0: never)
+    static const double small_seg =
+        getenv("SBAG_HIST_SMALL") ? atof(getenv("SBAG_HIST_SMALL")) : 4096.0;
+    ha.small = (grouped && !segs.empty() && work.entries < small_seg * (double)segs.size()) ? 1 : 0;
+    ha.ablate = 0;
     ha.FT = g.FT;
     ha.FPH = g.FPH;
     ha.CT = g.CT;
@@ -2248,6 +2255,26 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       fprintf(stderr, "[sbag] level %d cat %d mode %d grouped %d segs %zu entries %lld pieces %zu nwg %d ms %.3f\n",
               trace_level, cat, mode, grouped ? 1 : 0, segs.size(), (long long)ne, work.pieces.size(),
               work.nwg, ms);
+    }
+    if (trace && getenv("SBAG_HIST_ABLATE")) {
+      // diagnostics: relaunch the same histogram with phases skipped (flushes always
+      // skipped, so the real result stays intact) and time each relaunch
+      for (int m : {1, 1 | 2, 1 | 4, 1 | 8, 1 | 2 | 4 | 8}) {
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        ha.ablate = m;
+        (void)hipEventRecord(e0, c->stream);
+        launch_hist(c->stream, ha, work.nwg, ntiles, mode, g.lds);
+        (void)hipEventRecord(e1, c->stream);
+        (void)hipEventSynchronize(e1);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        fprintf(stderr, "[sbag] ablate level %d mode %d ms %.3f\n", trace_level, m, ms);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+      }
+      ha.ablate = 0;
     }
     ha.ent_in = ent_saved;
     ha.grouped = 0;

@@ -62,7 +62,11 @@ struct HistArgs {
   int32_t dw;            // k_hist gather width: 1 (byte loads) or 4 (aligned words + extract)
   int32_t hct;           // gini layout class tile: hist[slot][NS / hct][Fmax][NB][hct]
   int32_t rlpd;          // k_hist_rl: rows loaded this many passes ahead (2 or 3)
-  int32_t pad2_;
+  int32_t small;         // k_hist: short segments (deep levels): 256-thread workgroups with
+                         // 32-entry gather groups (k_hist<.., 256, 32>)
+  int32_t ablate;        // diagnostics only (SBAG_HIST_ABLATE, wrong results): 1 skips the
+                         // flushes, 2 the LDS zeroing, 4 the row gathers, 8 the LDS atomics
+  int32_t pad3_;
 };
 
 // Gini histogram cell (f, b, c) of one slot: class-tile-major, so that a class tile's

@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <set>
+#include <type_traits>
 #include <utility>
 
 #include "sbag_internal.h"
@@ -1451,22 +1452,27 @@ __device__ __forceinline__ void hist_load_group(const uint8_t* __restrict__ bins
                                                 uint32_t (&buf)[KG][NJ]) {
 #pragma unroll
   for (int t = 0; t < KG; t++) {
-    const uint8_t* rp = binsr + (size_t)rdlane(row, u0 + t) * S;  // wave-uniform (SGPRs)
+    // a buffer load per row: the resource's base is the row (SGPRs: the row index is
+    // wave-uniform), the column the VGPR offset -- no VALU for the address (a global load
+    // took a v_mov of the column or a 64-bit v_lshl_add per load)
+    const uint8_t* rp = binsr + (size_t)rdlane(row, u0 + t) * S;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)rp, (short)0, (int)S, 0x00020000);
 #pragma unroll
     for (int jj = 0; jj < NJ; jj++) {
-      uint32_t off = posr[jj];
-      asm volatile("" : "+v"(off));  // keep the column a 32-bit VGPR offset: saddr form
       if (GW == 4)
-        buf[t][jj] = *(const uint32_t*)(rp + off);
+        buf[t][jj] = __builtin_amdgcn_raw_buffer_load_b32(rs, posr[jj], 0, 0);
       else
-        buf[t][jj] = rp[off];
+        buf[t][jj] = __builtin_amdgcn_raw_buffer_load_b8(rs, posr[jj], 0, 0);
     }
   }
 }
 
 // one LDS atomic per entry and lane group: GINI adds count wl into class plane
 // (offset wh); the u64 modes add (wh:wl)
-template <int MODE, int NJ, int KG, int GW>
+// ONES (gini): every count of the batch is 1 (Bernoulli bags, C5): the added value is the
+// constant 1 and the count readlane and its VGPR copy go away (5 VALU per entry, not 7)
+template <int MODE, int NJ, int KG, int GW, bool ONES = false>
 __device__ __forceinline__ void hist_add_group(unsigned char* smem, int u0,
                                                const uint32_t (&buf)[KG][NJ], uint32_t wl,
                                                uint32_t wh, const uint32_t (&amul)[NJ],
@@ -1478,7 +1484,14 @@ __device__ __forceinline__ void hist_add_group(unsigned char* smem, int u0,
 #pragma unroll
   for (int t = 0; t < KG; t++) {
     const int u = u0 + t;
-    if (MODE == kHistGini) {
+    if (MODE == kHistGini && ONES) {
+      const uint32_t cou = rdlane(wh, u);
+#pragma unroll
+      for (int jj = 0; jj < NJ; jj++) {
+        const uint32_t addr = __umul24(bin(t, jj), amul[jj]) + abase[jj] + cou;
+        atomicAdd((uint32_t*)(smem + addr), 1u);
+      }
+    } else if (MODE == kHistGini) {
       const uint32_t cu = rdlane(wl, u), cou = rdlane(wh, u);
 #pragma unroll
       for (int jj = 0; jj < NJ; jj++) {
@@ -1499,8 +1512,14 @@ __device__ __forceinline__ void hist_add_group(unsigned char* smem, int u0,
 // The second bound is waves per SIMD.  Gini with one lane group (C5's class tiles, ~34 KB
 // of LDS, four workgroups per CU) needs 8 waves per SIMD, i.e. <= 64 VGPRs: at 85 VGPRs only
 // two of the four workgroups were resident.
-template <int MODE, int NJ, int GW>
-__global__ __launch_bounds__(kHistThreads, MODE == kHistGini && NJ == 1 ? 8 : 4) void k_hist(HistArgs A) {
+// NT threads per workgroup, KG entries per gather group.  The default (512, 8 or 16) keeps
+// 8 waves per SIMD; the short-segment form (256, 32) is for deep levels, where a (node,
+// class tile) sub-segment is a few hundred entries: each wave then holds one or two
+// batches, the barriers around every sub-segment's flush expose the whole chain of gather
+// groups, and 32-entry groups (4 waves per SIMD, 128 VGPRs) cut that chain by 4.
+template <int MODE, int NJ, int GW, int NT = kHistThreads, int KG = hist_group<MODE, NJ, GW>()>
+__global__ __launch_bounds__(NT, NT == kHistThreads ? (MODE == kHistGini && NJ == 1 ? 8 : 4) : 4) void k_hist(HistArgs A) {
+  constexpr int kWaves = NT / 64;
   extern __shared__ __align__(16) unsigned char smem[];
   constexpr bool GINI = MODE == kHistGini;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1524,7 +1543,7 @@ __global__ __launch_bounds__(kHistThreads, MODE == kHistGini && NJ == 1 ? 8 : 4)
   uint64_t* stage = (uint64_t*)(smem + hist_bytes) + wave * 64;
   const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 
-  for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
+  for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += NT * 16)
     *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 
   const int p0 = A.wg_piece[blockIdx.x], p1 = A.wg_piece[blockIdx.x + 1];
@@ -1561,10 +1580,11 @@ __global__ __launch_bounds__(kHistThreads, MODE == kHistGini && NJ == 1 ? 8 : 4)
     if (slot != cur_slot || tile != cur_tile || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
         __syncthreads();
-        hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
+        if (!(A.ablate & 1)) hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
         __syncthreads();
-        for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
-          *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+        if (!(A.ablate & 2))
+          for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += NT * 16)
+            *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
         __syncthreads();
       }
       // a node split over several flushes by this workgroup adds from the second on
@@ -1596,10 +1616,10 @@ __global__ __launch_bounds__(kHistThreads, MODE == kHistGini && NJ == 1 ? 8 : 4)
     const int cs = A.cshift;
     const int64_t K0 = A.K0;
     const uint32_t cstride = A.count_only ? 0u : plane;
-    for (; q0 < b; q0 += (int64_t)kHistWaves * 64) {
+    for (; q0 < b; q0 += (int64_t)kWaves * 64) {
       int n = (int)min((int64_t)64, b - q0);
       uint64_t e = e_next;
-      const int64_t qn = q0 + (int64_t)kHistWaves * 64 + lane;
+      const int64_t qn = q0 + (int64_t)kWaves * 64 + lane;
       e_next = (qn < b) ? A.ent_in[qn] : 0ull;
       if (ctile) {  // keep the batch entries of classes [c0, c0 + nct), packed to the front
         const int32_t eh = (int32_t)(e >> 32);
@@ -1629,19 +1649,31 @@ __global__ __launch_bounds__(kHistThreads, MODE == kHistGini && NJ == 1 ? 8 : 4)
         wl = (uint32_t)w;
         wh = (uint32_t)(w >> 32);
       }
-      constexpr int kG = hist_group<MODE, NJ, GW>();
-      uint32_t bA[kG][NJ], bB[kG][NJ];
-      hist_load_group<NJ, kG, GW>(binsr, S, row, 0, posr, bA);
+      constexpr int kG = KG;
+      const uint32_t rowa = (A.ablate & 4) ? 0u : row;  // diagnostics: every gather hits row 0
+      // the batch's group loop; ONES: a full batch whose counts are all 1 (lanes past a
+      // piece have c = 0, so a partial batch takes the general path, which adds 0 for them)
+      auto groups = [&](auto ones) {
+        constexpr bool O = decltype(ones)::value;
+        uint32_t bA[kG][NJ], bB[kG][NJ];
+        hist_load_group<NJ, kG, GW>(binsr, S, rowa, 0, posr, bA);
 #pragma unroll
-      for (int g = 0; g < 64 / kG; g += 2) {
-        if ((g + 1) * kG < n) hist_load_group<NJ, kG, GW>(binsr, S, row, (g + 1) * kG, posr, bB);
-        hist_add_group<MODE, NJ, kG, GW>(smem, g * kG, bA, wl, wh, amul, abase, bsh);
-        if ((g + 1) * kG >= n) break;
-        if (g + 2 < 64 / kG && (g + 2) * kG < n)
-          hist_load_group<NJ, kG, GW>(binsr, S, row, (g + 2) * kG, posr, bA);
-        hist_add_group<MODE, NJ, kG, GW>(smem, (g + 1) * kG, bB, wl, wh, amul, abase, bsh);
-        if ((g + 2) * kG >= n) break;
-      }
+        for (int g = 0; g < 64 / kG; g += 2) {
+          if ((g + 1) * kG < n) hist_load_group<NJ, kG, GW>(binsr, S, rowa, (g + 1) * kG, posr, bB);
+          if (!(A.ablate & 8))
+            hist_add_group<MODE, NJ, kG, GW, O>(smem, g * kG, bA, wl, wh, amul, abase, bsh);
+          if ((g + 1) * kG >= n) break;
+          if (g + 2 < 64 / kG && (g + 2) * kG < n)
+            hist_load_group<NJ, kG, GW>(binsr, S, rowa, (g + 2) * kG, posr, bA);
+          if (!(A.ablate & 8))
+            hist_add_group<MODE, NJ, kG, GW, O>(smem, (g + 1) * kG, bB, wl, wh, amul, abase, bsh);
+          if ((g + 2) * kG >= n) break;
+        }
+      };
+      if (GINI && __all(c == 1u))
+        groups(std::true_type{});
+      else
+        groups(std::false_type{});
     }
   }
   if (cur_slot >= 0) {
@@ -1939,6 +1971,13 @@ size_t hist_stage_bytes() { return (size_t)kHistWaves * 64 * 8; }
 
 template <int MODE, int NJ>
 static void launch_hist_t(hipStream_t st, const HistArgs& a, dim3 grid, size_t lds_bytes) {
+  if constexpr (MODE == kHistGini && NJ == 1) {
+    if (a.small && a.dw == 4) {
+      set_max_lds((const void*)k_hist<MODE, NJ, 4, 256, 32>, 160 * 1024);
+      hipLaunchKernelGGL((k_hist<MODE, NJ, 4, 256, 32>), grid, dim3(256), lds_bytes, st, a);
+      return;
+    }
+  }
   if (a.dw == 4) {
     set_max_lds((const void*)k_hist<MODE, NJ, 4>, 160 * 1024);
     hipLaunchKernelGGL((k_hist<MODE, NJ, 4>), grid, dim3(kHistThreads), lds_bytes, st, a);
