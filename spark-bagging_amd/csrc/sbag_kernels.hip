@@ -1385,6 +1385,25 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
     uint32_t* gh = (uint32_t*)A.hist + (int64_t)slot * slot_words;
     const int hct = A.hct;
     const bool vec = store && ((hct | c0) & 3) == 0;
+    if (vec && nct == 4 && hct == 4 && ftn <= 64) {
+      // the workgroup's class tile is the layout tile (grouped C5): its block
+      // [Fmax][NB][4] is contiguous; lane = feature, waves step the bins -- no index
+      // division per (feature, bin) (the general loop below spent ~60 instructions on
+      // each, which made the flush a third of the deep levels' histogram time)
+      uint4* blk = (uint4*)(gh + (int64_t)(c0 >> 2) * A.Fmax * NB * 4) + (int64_t)ft0 * NB;
+      const int f = tid & 63;
+      if (f < ftn)
+        for (int b = tid >> 6; b < NB; b += (int)(blockDim.x >> 6)) {
+          const unsigned char* src = smem + ((size_t)b * FPH + f) * 4;
+          uint4 v;
+          v.x = *(const uint32_t*)(src);
+          v.y = *(const uint32_t*)(src + plane);
+          v.z = *(const uint32_t*)(src + 2 * (size_t)plane);
+          v.w = *(const uint32_t*)(src + 3 * (size_t)plane);
+          blk[f * NB + b] = v;
+        }
+      return;
+    }
     for (int q = tid; q < ftn * NB; q += blockDim.x) {
       const int f = q % ftn, b = q / ftn;
       const unsigned char* src = smem + ((size_t)b * FPH + f) * 4;
@@ -1676,7 +1695,7 @@ __global__ __launch_bounds__(NT, NT == kHistThreads ? (MODE == kHistGini && NJ =
         groups(std::false_type{});
     }
   }
-  if (cur_slot >= 0) {
+  if (cur_slot >= 0 && !(A.ablate & 1)) {
     __syncthreads();
     hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
   }
