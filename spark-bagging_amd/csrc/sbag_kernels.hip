@@ -3571,6 +3571,20 @@ __global__ void k_bt_valuecount(const uint32_t* __restrict__ rows, int64_t nrows
 // LDS (count times: the reference's explode), exactly DTStatsAggregator.update's fp64
 // sequence for that (feature, bin).  fl == Fr is the node's total (its parent stats,
 // one bin).  hist: [q][Fr + 1][NB][3] fp64.
+// One wave per (node, feature chunk); lane = feature (lane Fr: the node total).  Rows are
+// taken 64 at a time: lane j loads row i0 + j's id, count and label (coalesced), the wave
+// then walks the batch in row order, each row broadcast by readlane, and every lane adds
+// the row into its feature's bin with LDS fp64 atomics.  One lane's adds to one cell are
+// executed in issue order, so each cell is the sequential fp64 sum over the node's rows
+// in row order, `count` times per row -- DTStatsAggregator.update on the exploded rows.
+// The bin of row t + 8 is gathered while row t is added (the code, then the LUT lookup
+// one group later), so the walk is not paced by two dependent global loads per row.
+constexpr int kBtG = 8;  // rows per gather group
+// CB: code bytes (1, 2, 4) as a template parameter, and every lane loads (lanes without a
+// feature read local feature 0's code and LUT and discard the bin): with bt_code's width
+// branches under a per-lane condition each load sat in its own exec-masked block behind a
+// vmcnt(0), and the walk ran ~650 cycles per row
+template <int CB>
 __global__ __launch_bounds__(64) void k_bt_hist(const uint32_t* __restrict__ rows,
                                                 const int64_t* __restrict__ seg, /*[q][2]*/
                                                 const uint8_t* __restrict__ cnt,
@@ -3587,29 +3601,79 @@ __global__ __launch_bounds__(64) void k_bt_hist(const uint32_t* __restrict__ row
   const bool on = lane < FL && fl <= Fr;
   for (int k = lane; k < NB * 3 * FL; k += 64) acc[k] = 0.0;
   __syncthreads();
-  if (on) {
-    const int64_t a = seg[2 * q], b = seg[2 * q + 1];
-    const bool total = fl == Fr;
-    const int g = total ? 0 : sub[fl];
-    const uint8_t* lt = total ? nullptr : lut + lutoff[fl];
-    for (int64_t i = a; i < b; i++) {
-      const uint32_t r = rows[i];
-      const int c = cnt[r];
-      const double v = y[r];
-      const double w = 1.0 * v;  // instanceWeight * label
-      const double w2 = w * v;   // instanceWeight * label * label
-      const int bin = total ? 0 : lt[bt_code(codes, code_bytes, (int64_t)r * S + g)];
-      double* cell = acc + (size_t)bin * 3 * FL + lane;
-      double s0 = cell[0], s1 = cell[FL], s2 = cell[2 * FL];
-      for (int k = 0; k < c; k++) {
-        s0 += 1.0;
-        s1 += w;
-        s2 += w2;
+  const int64_t a = seg[2 * q], b = seg[2 * q + 1];
+  const bool total = fl == Fr;
+  const bool gat = on && !total;  // lanes whose code decides the bin (the total lane: bin 0)
+  const int fg = gat ? fl : 0;
+  const int g = sub[fg];
+  const uint8_t* lt = lut + lutoff[fg];
+  double* const cell0 = acc + lane;
+  for (int64_t i0 = a; i0 < b; i0 += 64) {
+    const int n = (int)min((int64_t)64, b - i0);
+    // lane j: row i0 + j (rows past the node: count 0, label +0.0)
+    const uint32_t rj = lane < n ? rows[i0 + lane] : 0u;
+    const uint32_t cj = lane < n ? (uint32_t)cnt[rj] : 0u;
+    const double vj = lane < n ? y[rj] : 0.0;
+    const int vhi = __double2hiint(vj), vlo = __double2loint(vj);
+    // codes of a group of rows (lane = feature), then their bins through the LUT
+    auto codes_of = [&](int t0, uint32_t (&cd)[kBtG]) {
+#pragma unroll
+      for (int u = 0; u < kBtG; u++) {
+        // groups past the batch read lane 63's row (valid; their bins are never added)
+        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rj, min(t0 + u, 63));
+        const int64_t at = (int64_t)r * S + g;
+        cd[u] = CB == 1 ? (uint32_t)((const uint8_t*)codes)[at]
+                        : (CB == 2 ? (uint32_t)((const uint16_t*)codes)[at] : ((const uint32_t*)codes)[at]);
       }
-      cell[0] = s0;
-      cell[FL] = s1;
-      cell[2 * FL] = s2;
+    };
+    auto bins_of = [&](const uint32_t (&cd)[kBtG], uint32_t (&bn)[kBtG]) {
+#pragma unroll
+      for (int u = 0; u < kBtG; u++) {
+        const uint32_t v = lt[cd[u]];
+        bn[u] = gat ? v : 0u;
+      }
+    };
+    // three-stage pipeline over groups of rows: codes of group g + 2, bins (LUT) of group
+    // g + 1, adds of group g
+    uint32_t cA[kBtG], cB[kBtG], bA[kBtG], bB[kBtG];
+    // loads issued unconditionally (no branch between issue and use, so the compiler's
+    // vmcnt counts stay exact and the stages overlap)
+    codes_of(0, cA);
+    codes_of(kBtG, cB);
+    bins_of(cA, bA);
+    for (int t0 = 0; t0 < n; t0 += kBtG) {
+      codes_of(t0 + 2 * kBtG, cA);
+      bins_of(cB, bB);
+      const uint32_t (&bn)[kBtG] = bA;
+#pragma unroll
+      for (int u = 0; u < kBtG; u++) {
+        const int t = t0 + u;
+        if (t >= n) break;  // wave-uniform
+        const int c = __builtin_amdgcn_readlane((int)cj, t);
+        const double v = __hiloint2double(__builtin_amdgcn_readlane(vhi, t),
+                                          __builtin_amdgcn_readlane(vlo, t));
+        const double w = 1.0 * v;  // instanceWeight * label
+        const double w2 = w * v;   // instanceWeight * label * label
+        if (on) {
+          double* cell = cell0 + (size_t)bn[u] * 3 * FL;
+          for (int k = 0; k < c; k++) {  // the row's c exploded copies, in order
+            atomicAdd(cell, 1.0);
+            atomicAdd(cell + FL, w);
+            atomicAdd(cell + 2 * FL, w2);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kBtG; u++) {
+        bA[u] = bB[u];
+        const uint32_t t = cA[u];  // codes of group g + 2 move to the middle stage
+        cA[u] = cB[u];
+        cB[u] = t;
+      }
     }
+  }
+  __syncthreads();
+  if (on) {
     double* out = hist + ((int64_t)q * (Fr + 1) + fl) * NB * 3;
     const int nb = total ? 1 : NB;
     for (int k = 0; k < nb; k++) {
@@ -3628,42 +3692,71 @@ struct BtSplit {
   int64_t lutoff;
   int32_t g, s;
 };
-__global__ __launch_bounds__(64) void k_bt_partition(const uint32_t* __restrict__ in,
-                                                     uint32_t* __restrict__ out,
-                                                     const BtSplit* __restrict__ sp,
-                                                     const void* __restrict__ codes, int code_bytes,
-                                                     int32_t S, const uint8_t* __restrict__ lut,
-                                                     int64_t* __restrict__ nleft) {
+// A workgroup of kBtPartT threads per split node: each pass takes kBtPartT consecutive
+// rows, ranks the left and the right rows of every wave with ballots and the waves with an
+// LDS prefix, so both children keep the node's row order (one wave per node walked the
+// root's 10^6 rows 64 at a time, each step behind two dependent loads).
+constexpr int kBtPartT = 512;
+__global__ __launch_bounds__(kBtPartT) void k_bt_partition(const uint32_t* __restrict__ in,
+                                                           uint32_t* __restrict__ out,
+                                                           const BtSplit* __restrict__ sp,
+                                                           const void* __restrict__ codes,
+                                                           int code_bytes, int32_t S,
+                                                           const uint8_t* __restrict__ lut,
+                                                           int64_t* __restrict__ nleft) {
+  constexpr int W = kBtPartT / 64;
+  __shared__ int s_l[W], s_r[W];
+  __shared__ unsigned long long s_tot;
   const BtSplit p = sp[blockIdx.x];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint8_t* lt = lut + p.lutoff;
-  int64_t nl = 0;
-  for (int64_t i0 = p.a; i0 < p.b; i0 += 64) {
-    const int64_t i = i0 + lane;
-    bool left = false;
-    if (i < p.b) left = lt[bt_code(codes, code_bytes, (int64_t)in[i] * S + p.g)] <= p.s;
-    nl += __popcll(__ballot(left));
-  }
+  auto goes_left = [&](uint32_t r) {
+    return lt[bt_code(codes, code_bytes, (int64_t)r * S + p.g)] <= p.s;
+  };
+  if (tid == 0) s_tot = 0;
+  __syncthreads();
+  int nl_mine = 0;  // this thread's left rows (pass 1)
+  for (int64_t i = p.a + tid; i < p.b; i += kBtPartT) nl_mine += goes_left(in[i]) ? 1 : 0;
+  // wave sum then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) nl_mine += __shfl_xor(nl_mine, o);
+  if (lane == 0) atomicAdd(&s_tot, (unsigned long long)nl_mine);
+  __syncthreads();
+  const int64_t nl = (int64_t)s_tot;
   int64_t lpos = p.a, rpos = p.a + nl;
-  for (int64_t i0 = p.a; i0 < p.b; i0 += 64) {
-    const int64_t i = i0 + lane;
+  for (int64_t i0 = p.a; i0 < p.b; i0 += kBtPartT) {
+    const int64_t i = i0 + tid;
     const bool valid = i < p.b;
     uint32_t r = 0;
     bool left = false;
     if (valid) {
       r = in[i];
-      left = lt[bt_code(codes, code_bytes, (int64_t)r * S + p.g)] <= p.s;
+      left = goes_left(r);
     }
     const uint64_t ml = __ballot(valid && left), mr = __ballot(valid && !left);
+    if (lane == 0) {
+      s_l[wave] = __popcll(ml);
+      s_r[wave] = __popcll(mr);
+    }
+    __syncthreads();
+    int bl = 0, br = 0, tl = 0, tr = 0;  // rows of the waves before this one; pass totals
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int cl = s_l[w], cr = s_r[w];
+      bl += w < wave ? cl : 0;
+      br += w < wave ? cr : 0;
+      tl += cl;
+      tr += cr;
+    }
     const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
     const uint32_t rank_r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mr >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mr, 0u));
-    if (valid) out[left ? lpos + rank_l : rpos + rank_r] = r;
-    lpos += __popcll(ml);
-    rpos += __popcll(mr);
+    if (valid) out[left ? lpos + bl + rank_l : rpos + br + rank_r] = r;
+    lpos += tl;
+    rpos += tr;
+    __syncthreads();  // s_l / s_r are rewritten by the next pass
   }
-  if (lane == 0) nleft[blockIdx.x] = nl;
+  if (tid == 0) nleft[blockIdx.x] = nl;
 }
 
 void launch_bt_valuecount(hipStream_t st, const uint32_t* rows, int64_t nrows, const uint8_t* cnt,
@@ -3686,15 +3779,25 @@ void launch_bt_hist(hipStream_t st, const uint32_t* rows, const int64_t* seg, in
                     const int64_t* lutoff, int NB, double* hist) {
   const int FL = bt_lanes(NB);
   const size_t lds = (size_t)NB * 3 * FL * 8;
-  set_max_lds((const void*)k_bt_hist, 64 * 1024);
-  hipLaunchKernelGGL(k_bt_hist, dim3(nnodes, (Fr + 1 + FL - 1) / FL), dim3(64), lds, st, rows, seg,
-                     cnt, y, codes, code_bytes, S, sub, Fr, lut, lutoff, NB, FL, hist);
+  const dim3 grid(nnodes, (Fr + 1 + FL - 1) / FL);
+#define SBAG_BTH(CB)                                                                      \
+  set_max_lds((const void*)k_bt_hist<CB>, 64 * 1024);                                     \
+  hipLaunchKernelGGL(k_bt_hist<CB>, grid, dim3(64), lds, st, rows, seg, cnt, y, codes, code_bytes, \
+                     S, sub, Fr, lut, lutoff, NB, FL, hist)
+  if (code_bytes == 1) {
+    SBAG_BTH(1);
+  } else if (code_bytes == 2) {
+    SBAG_BTH(2);
+  } else {
+    SBAG_BTH(4);
+  }
+#undef SBAG_BTH
 }
 
 void launch_bt_partition(hipStream_t st, const uint32_t* in, uint32_t* out, const void* splits,
                          int nsplit, const void* codes, int code_bytes, int32_t S,
                          const uint8_t* lut, int64_t* nleft) {
-  hipLaunchKernelGGL(k_bt_partition, dim3(nsplit), dim3(64), 0, st, in, out,
+  hipLaunchKernelGGL(k_bt_partition, dim3(nsplit), dim3(kBtPartT), 0, st, in, out,
                      (const BtSplit*)splits, codes, code_bytes, S, lut, nleft);
 }
 
