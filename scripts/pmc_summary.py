@@ -21,7 +21,7 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "")
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
 
 
 def read_counters(path):
