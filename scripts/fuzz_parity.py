@@ -1,0 +1,95 @@
+"""Randomized parity fuzzing at larger shapes than tests/test_gpu_random.py: every case a
+fresh random dataset and parameter draw (rows up to ~150k, up to 140 features, up to 80
+classes -- grouped class tiles --, 32-level u8 columns for the row-lane kernel, non-dyadic
+fp64 labels for the fp64 engine, depth up to 14, several partitions), each forest checked
+against the CPU oracle node by node.  Runs until the time budget is spent; prints one line
+per case so a failure names its seed and replays with --start SEED --cases 1.
+
+usage: python3 scripts/fuzz_parity.py [--start S] [--minutes M] [--cases K]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import sbag_loader  # noqa: E402
+
+sb = sbag_loader.load()
+nat = sb._native
+import oracle  # noqa: E402
+from parity_utils import assert_forest_equal, fuzz_case, oracle_forest  # noqa: E402
+
+
+draw = fuzz_case  # tests/parity_utils.py
+
+
+def run(ctx, seed):
+    X, y, cls, f64, part, p, kind = draw(seed)
+    sd = oracle.DEFAULT_SEED_CLASSIFIER if cls else oracle.DEFAULT_SEED_REGRESSOR
+    N, F = X.shape
+    desc = (f"seed {seed} N {N} F {F} {kind} {'cls C=%d' % (int(y.max()) + 1) if cls else ('f64' if f64 else 'reg')} "
+            f"P {len(part) - 1} {p}")
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        forest = nat.fit(ctx, ds, replacement=p["replacement"], sample_ratio=p["ratio"], seed=sd,
+                         learner_begin=0, learner_end=p["L"], partition_offsets=part,
+                         max_depth=p["depth"], max_bins=p["bins"],
+                         min_instances_per_node=p["min_inst"], min_info_gain=p["min_gain"],
+                         impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    except sb.SparkException as e:
+        ds.free()
+        counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, N)
+        ok = e.code == nat.SBAG_EEMPTY and (counts.sum(axis=1) == 0).any()
+        return ok, desc + f" -> {e}"
+    except sb.IllegalArgumentException as e:
+        ds.free()
+        ok = any(len(oracle.subspace(p["ratio"], F, sd + i)) == 0 for i in range(p["L"]))
+        return ok, desc + f" -> {e}"
+    counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, N)
+    subs = [oracle.subspace(p["ratio"], F, sd + i) for i in range(p["L"])]
+    orf = oracle_forest(X, y, counts, subs, p["depth"], p["bins"], cls, p["min_inst"], p["min_gain"],
+                        part=part)
+    try:
+        assert_forest_equal(forest, orf)
+        agg = nat.AGG_MODE if cls else nat.AGG_MEAN
+        want = oracle.predict(orf, X, classification=cls)
+        got = nat.predict(ctx, forest, X, agg)
+        np.testing.assert_array_equal(got, want)
+    except AssertionError as e:
+        return False, desc + " FAIL " + str(e)[:400]
+    finally:
+        forest.free()
+        ds.free()
+    return True, desc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--start", type=int, default=50_000)
+    ap.add_argument("--minutes", type=float, default=5.0)
+    ap.add_argument("--cases", type=int, default=10**9)
+    a = ap.parse_args()
+    ctx = sb.default_context(0)
+    t0 = time.time()
+    n = fails = 0
+    seed = a.start
+    while n < a.cases and time.time() - t0 < 60 * a.minutes:
+        t1 = time.time()
+        ok, desc = run(ctx, seed)
+        n += 1
+        fails += 0 if ok else 1
+        print(("ok   " if ok else "FAIL ") + f"{time.time() - t1:6.1f}s " + desc, flush=True)
+        seed += 1
+    print(f"fuzz: {n} cases, {fails} failures, seeds {a.start}..{seed - 1}", flush=True)
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -49,14 +49,14 @@ __device__ __forceinline__ int block_excl_scan256(int v, int* s_wave, int* total
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int incl = f64_wave_incl_scan(v, lane);
   if (lane == 63) s_wave[wave] = incl;
-  __syncthreads();
+  block_sync();
   int before = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) {
     if (w < wave) before += s_wave[w];
     tot += s_wave[w];
   }
-  __syncthreads();
+  block_sync();
   *total = tot;
   return before + incl - v;
 }
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__
     s_s[wave] = s;
     s_m[wave] = m;
   }
-  __syncthreads();
+  block_sync();
   if (threadIdx.x == 0) {
     const unsigned int t = s_s[0] + s_s[1] + s_s[2] + s_s[3];  // <= 8192 * 255
     ncnt[(int64_t)r * chunks + chunk] = t;
@@ -238,7 +238,7 @@ __device__ __forceinline__ void f64_hist_body(const F64HistArgs& A, const F64Nod
   const uint32_t B1 = PART == 2 ? 0u : (uint32_t)NB * W * 4;
   const uint32_t F64W = PART == 0 ? 2u : 1u;  // f64 arrays per bin row
   for (uint32_t k = lane * 4; k < B1 + (uint32_t)NB * W * 8 * F64W; k += 256) *(lds_u32*)(L + k) = 0u;
-  __syncthreads();
+  block_sync();
   const int64_t a = nd.a, b = nd.b;
   if (a < b) {
     const bool act = lane < W;
@@ -302,7 +302,7 @@ __device__ __forceinline__ void f64_hist_body(const F64HistArgs& A, const F64Nod
                              __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-  __syncthreads();
+  block_sync();
   if (feat || tot) {
     double* out = A.hist + ((int64_t)blockIdx.x * (A.Fmax + 1) + fl) * NB * 3;
     const int nbk = tot ? 1 : NB;
@@ -566,7 +566,7 @@ __global__ __launch_bounds__(256) void k_sp_count(F64PartArgs A) {
   for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
   __shared__ int s_n[4];
   if ((threadIdx.x & 63) == 0) s_n[threadIdx.x >> 6] = n;
-  __syncthreads();
+  block_sync();
   if (threadIdx.x == 0) A.piece_left[blockIdx.x] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
 }
 

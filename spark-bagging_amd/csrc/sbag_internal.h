@@ -7,6 +7,22 @@
 
 namespace sbag {
 
+// Workgroup barrier with the waits spelled out.  gfx950 has the back-off barrier, so the
+// compiler leaves the wait for a wave's outstanding LDS operations to the barrier's release
+// fence, and on some loop paths that wait was dropped: a wave crossed s_barrier with a
+// ds_write in flight and another wave read the old word (k_split_gini's per-wave maxima of
+// the previous feature group: nondeterministic splits, found by scripts/fuzz_parity.py).
+// block_sync: s_waitcnt lgkmcnt(0) first; block_sync_mem: vmcnt(0) too, for global
+// memory written by one thread of the block and read by another after the barrier.
+__device__ __forceinline__ void block_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt 63 (no wait), expcnt 7, lgkmcnt 0
+  __syncthreads();
+}
+__device__ __forceinline__ void block_sync_mem() {
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt 0, expcnt 7, lgkmcnt 0
+  __syncthreads();
+}
+
 // Entry of a replica's row list (one per in-bag row): low 32 bits row index,
 // high 32 bits (label_fixed << 8) | count.  Replaces the reference's
 // explode(array_repeat) replication (sql/bfunctions.scala:42-44) by a weight.

@@ -342,7 +342,7 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
       v0 = z4;
       ring[kPB * 64 + lane * 4 + (kPB - 1 - 4) + 256] = z4;  // slot 1, half 1, word 3
     }
-    __syncthreads();  // the parser takes the prologue output
+    block_sync();  // the parser takes the prologue output
     int index = 623;
     for (int k = 0;; k++) {
       // the parser's verdict after batch k-2 (its last barrier matched batch k-1's)
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
         uint32_t* slot = ring + (k & 1) * kPB * 64 + lane * 4;
 #pragma unroll
         for (int t = 0; t < kPB; t++) slot[(t >> 2) * 256 + (t & 3)] = v0 + t * 77777u;
-        __syncthreads();
+        block_sync();
         continue;
       }
       const bool fast = well_window_ok(index + 63 - 2, 12) && well_window_ok(index + 172 - 3, 12) &&
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
       uint4* slot = (uint4*)(ring + (k & 1) * kPB * 64) + lane;
       slot[0] = make_uint4(z4o[0], z4o[1], z4o[2], z4o[3]);
       slot[64] = make_uint4(z4o[4], z4o[5], z4o[6], z4o[7]);
-      __syncthreads();
+      block_sync();
     }
   } else {
     int64_t row = active ? part_off[p] : 0;
@@ -376,10 +376,10 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
     uint8_t* const sink = (uint8_t*)(err + 1) + lane;  // stores of lanes that finish no row
     int n = 0, bad = 0;
     double racc = 1.0;
-    __syncthreads();  // the prologue output: first half of the first double
+    block_sync();  // the prologue output: first half of the first double
     uint32_t pending = well_temper26(ring[kPB * 64 + lane * 4 + (kPB - 1 - 4) + 256]);
     for (int k = 0;; k++) {
-      __syncthreads();  // batch k is in ring slot k & 1
+      block_sync();  // batch k is in ring slot k & 1
       uint32_t* slot = ring + (k & 1) * kPB * 64;
       uint32_t o[kPB];
       {
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
         row = min(row + kPB / 2, row_end);
         if (lane == 0) slot[0] = !__any(row < row_end) ? 1u : 0u;
         if (!__any(row < row_end)) {
-          __syncthreads();
+          block_sync();
           break;
         }
         continue;
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, 
       // report in the consumed slot: the generator reads it before refilling the slot
       if (lane == 0) slot[0] = all_done ? 1u : 0u;
       if (all_done) {
-        __syncthreads();  // matches the generator's next barrier
+        block_sync();  // matches the generator's next barrier
         break;
       }
     }
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void k_poisson3(uint8_t* __restrict__ counts, 
       st[i] = x;
     }
   }
-  __syncthreads();
+  block_sync();
   int64_t row = active ? part_off[p] : 0;
   const int64_t row_end = active ? part_off[p + 1] : 0;
   uint8_t* out = counts + (int64_t)r * N;
@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_split_sample_vc(
   const bool use_lds = nw <= lds_words;
   if (use_lds)
     for (int i = threadIdx.x; i < nw; i += 256) s_vc[i] = 0u;
-  __syncthreads();
+  block_sync();
   // lane = feature within a 64-feature group, wave = every 4th sampled row: a row's
   // codes are read by one wave from its cache line
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_split_sample_vc(
     }
   }
   if (use_lds) {
-    __syncthreads();
+    block_sync();
     for (int i = threadIdx.x; i < nw; i += 256)
       if (s_vc[i]) atomicAdd(&vc[vbase + i], s_vc[i]);
   }
@@ -1272,14 +1272,14 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
     }
     const int incl = wave_incl_scan(n, lane);
     if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
+    block_sync();
     int before = 0, total = 0;
     for (int w = 0; w < 4; w++) {
       if (w < wave) before += s_wave[w];
       total += s_wave[w];
     }
     if (tid == 0) s_base = total ? atomicAdd(&cursor[r], (unsigned long long)total) : 0ull;
-    __syncthreads();
+    block_sync();
     unsigned long long pos = s_base + (unsigned long long)(before + incl - n);
 #pragma unroll
     for (int j = 0; j < 4; j++)
@@ -1288,7 +1288,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
         mysq += (unsigned long long)c[j] * (unsigned long long)((int64_t)k * k);
         er[pos++] = pack_entry((uint32_t)(row0 + j), k, c[j]);
       }
-    __syncthreads();
+    block_sync();
   }
   __shared__ unsigned long long s_sq[4];
   for (int o = 32; o > 0; o >>= 1) {
@@ -1301,7 +1301,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
     s_sq[wave] = mysq;
     s_max[wave] = mymax;
   }
-  __syncthreads();
+  block_sync();
   if (tid == 0) {
     const unsigned long long s = s_red[0] + s_red[1] + s_red[2] + s_red[3];
     const unsigned long long q = s_sq[0] + s_sq[1] + s_sq[2] + s_sq[3];
@@ -1577,7 +1577,7 @@ __global__ __launch_bounds__(NT, NT == kHistThreads ? (MODE == kHistGini && NJ =
     amul[j] = 0;
     abase[j] = dump;
   }
-  __syncthreads();
+  block_sync();
 
   // pieces carry their parent's replica, slot, tile and feature count (HistChunk), and the
   // next piece is loaded while this one runs; the first entries of a piece are loaded before
@@ -1598,13 +1598,13 @@ __global__ __launch_bounds__(NT, NT == kHistThreads ? (MODE == kHistGini && NJ =
     uint64_t e_next = (q0 + lane < b) ? A.ent_in[q0 + lane] : 0ull;
     if (slot != cur_slot || tile != cur_tile || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
-        __syncthreads();
+        block_sync();
         if (!(A.ablate & 1)) hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
-        __syncthreads();
+        block_sync();
         if (!(A.ablate & 2))
           for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += NT * 16)
             *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
-        __syncthreads();
+        block_sync();
       }
       // a node split over several flushes by this workgroup adds from the second on
       cur_store = (slot != cur_slot || tile != cur_tile) && pc.excl != 0;
@@ -1696,7 +1696,7 @@ __global__ __launch_bounds__(NT, NT == kHistThreads ? (MODE == kHistGini && NJ =
     }
   }
   if (cur_slot >= 0 && !(A.ablate & 1)) {
-    __syncthreads();
+    block_sync();
     hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
   }
 }
@@ -1858,7 +1858,7 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
   int64_t acc = 0;
   // this lane's byte range of the tile: [off, off + K)
   RlLane L{A.bins, 0u, 0u, (uint32_t)(s * K) * WB};
-  __syncthreads();
+  block_sync();
 
   HistChunk pn = p0 < p1 ? A.chunks[p0] : HistChunk{};  // next piece prefetched (k_hist)
   for (int p = p0; p < p1; p++) {
@@ -1872,12 +1872,12 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
     const int tile = A.grouped ? pc.tile : 0;
     if (slot != cur_slot || tile != cur_tile || acc + (b - a) > A.flush_limit) {
       if (cur_slot >= 0) {
-        __syncthreads();
+        block_sync();
         hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
-        __syncthreads();
+        block_sync();
         for (uint32_t i = (uint32_t)tid * 16; i < hist_bytes; i += kHistThreads * 16)
           *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
-        __syncthreads();
+        block_sync();
       }
       cur_store = (slot != cur_slot || tile != cur_tile) && pc.excl != 0;
       cur_slot = slot;
@@ -1922,7 +1922,7 @@ __global__ __launch_bounds__(kHistThreads, 2) void k_hist_rl(HistArgs A) {
     }
   }
   if (cur_slot >= 0) {
-    __syncthreads();
+    block_sync();
     hist_flush<MODE>(A, smem, plane, cur_slot, ft0, cur_ftn, c0, nct, cur_store);
   }
 }
@@ -2033,12 +2033,12 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_count(const HistChunk* __
   uint32_t* cnt = (uint32_t*)smem;
   const HistChunk pc = pieces[blockIdx.x];
   for (int t = threadIdx.x; t < ntc; t += kTileThreads) cnt[t] = 0;
-  __syncthreads();
+  block_sync();
   for (int64_t i = pc.a + threadIdx.x; i < pc.b; i += kTileThreads) {
     const int k = (int32_t)(ent[i] >> 32) >> 8;
     atomicAdd(&cnt[k / CT], 1u);
   }
-  __syncthreads();
+  block_sync();
   for (int t = threadIdx.x; t < ntc; t += kTileThreads)
     counts[(int64_t)blockIdx.x * ntc + t] = cnt[t];
 }
@@ -2052,7 +2052,7 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const HistChunk* 
   int64_t* cur = (int64_t*)smem;  // [ntc] next output position of each tile
   const HistChunk pc = pieces[blockIdx.x];
   for (int t = threadIdx.x; t < ntc; t += kTileThreads) cur[t] = base[(int64_t)blockIdx.x * ntc + t];
-  __syncthreads();
+  block_sync();
   for (int64_t i = pc.a + threadIdx.x; i < pc.b; i += kTileThreads) {
     const uint64_t e = ent[i];
     const int k = (int32_t)(e >> 32) >> 8;
@@ -2120,10 +2120,10 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
       s_a = pc.a;
       s_b = pc.b;
     }
-    __syncthreads();
+    block_sync();
     const int q = s_q;
     const int64_t pa = s_a, pb = s_b;
-    __syncthreads();
+    block_sync();
     if (q < 0) break;
     const ParentInfo pi = A.parents[q];
     const uint8_t* col = A.cols + (int64_t)pi.r * A.cols_rstride + (int64_t)pi.pos * A.npad;
@@ -2180,7 +2180,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         s_n[0][wave] = nl;
         s_n[1][wave] = nr;
       }
-      __syncthreads();
+      block_sync();
       if (tid == 0) {
         int tl = 0, tr = 0;
 #pragma unroll
@@ -2191,7 +2191,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         s_base[0] = tl ? atomicAdd(&cur[0], (unsigned long long)tl) : 0ull;
         s_base[1] = tr ? atomicAdd(&cur[1], (unsigned long long)(-(long long)tr)) - (unsigned long long)tr : 0ull;
       }
-      __syncthreads();
+      block_sync();
       unsigned long long bl = s_base[0], br = s_base[1];
       for (int w = 0; w < wave; w++) {
         bl += (unsigned long long)s_n[0][w];
@@ -2205,7 +2205,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs A) {
         bl += __popcll(ml[k]);
         br += __popcll(mr[k]);
       }
-      __syncthreads();  // s_n / s_base are rewritten by the next step
+      block_sync();  // s_n / s_base are rewritten by the next step
     }
   }
 }
@@ -2229,7 +2229,7 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ s
     if (row0 + r < N && cb < S) v = *(const uint4*)(src + (row0 + r) * S + cb);
     *(uint4*)&t[r][part * 16] = v;
   }
-  __syncthreads();
+  block_sync();
   const int cl = tid >> 2, rq = tid & 3;
   if (col0 + cl < C) {
     uint32_t w[4];
@@ -2378,7 +2378,7 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
       s_tot[tid] = t;
     }
   }
-  __syncthreads();
+  block_sync();
 
   double bgain = -INFINITY;
   int bfl = INT_MAX, bs = -1, bvalid = 0;
@@ -2509,7 +2509,7 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
   s_fl[tid] = bfl;
   s_s[tid] = bs;
   s_valid[tid] = bvalid;
-  __syncthreads();
+  block_sync();
   for (int o = 128; o > 0; o >>= 1) {
     if (tid < o) {
       const double g2 = s_gain[tid + o];
@@ -2521,7 +2521,7 @@ __global__ __launch_bounds__(256) void k_split(SplitArgs A) {
         s_valid[tid] = s_valid[tid + o];
       }
     }
-    __syncthreads();
+    block_sync();
   }
   int64_t* so = A.stats + (int64_t)slot * NS;  // so[k * plane + c]: total, left, right
   if (tid == 0) {
@@ -2585,7 +2585,7 @@ __global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
     for (int b = 0; b < NB; b++) t += (int64_t)hs[(int64_t)b * 3 + tid];
     s_tot[tid] = t;
   }
-  __syncthreads();
+  block_sync();
   const int64_t tc = s_tot[0], tsk = s_tot[1];
   const uint64_t tsq = A.node_sq[slot];
   const double is2 = A.inv_scale2;
@@ -2621,7 +2621,7 @@ __global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
   s_fl[tid] = ffl;
   s_s[tid] = fs;
   s_any[tid] = any;
-  __syncthreads();
+  block_sync();
   for (int o = 128; o > 0; o >>= 1) {
     if (tid < o) {
       const double g2 = s_g[tid + o];
@@ -2633,11 +2633,11 @@ __global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
       }
       s_any[tid] = min(s_any[tid], s_any[tid + o]);
     }
-    __syncthreads();
+    block_sync();
   }
   const double gb = s_g[0];
   const int bfl = s_fl[0], bs = s_s[0], first_fl = s_any[0];
-  __syncthreads();
+  block_sync();
   // pass 2: contenders within 2*delta of the best
   int cnt = 0;
   if (bfl != INT_MAX) {
@@ -2658,10 +2658,10 @@ __global__ __launch_bounds__(256) void k_split_screen(SplitArgs A) {
     }
   }
   s_cnt[tid] = cnt;
-  __syncthreads();
+  block_sync();
   for (int o = 128; o > 0; o >>= 1) {
     if (tid < o) s_cnt[tid] += s_cnt[tid + o];
-    __syncthreads();
+    block_sync();
   }
   if (tid == 0) {
     SplitOut o;
@@ -2787,7 +2787,7 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
           hs[((int64_t)t * Fmax + f0) * NB * hct + rem];
     }
   }
-  __syncthreads();
+  block_sync();
   for (int q = tid; q < g * NS; q += 256) {
     const int fl = q / NS, c = q - fl * NS;
     uint32_t* o = pre + (size_t)fl * FS + c;
@@ -2797,7 +2797,7 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
       o[(size_t)b * NSP] = acc;
     }
   }
-  __syncthreads();
+  block_sync();
 }
 
 __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
@@ -2818,7 +2818,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   // group 0 first: the node totals are feature 0's last prefix
   split_stage_prefix(hs, 0, min(G, Fr), NB, NS, A.Fmax, A.hct, pre);
   for (int c = tid; c < NS; c += 256) s_tot[c] = (int64_t)pre[(size_t)(NB - 1) * NSP + c];
-  __syncthreads();
+  block_sync();
   double ttot = 0.0;
   for (int c = 0; c < NS; c++) ttot += (double)s_tot[c];
   double imp = 0.0;
@@ -2845,7 +2845,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
     if (f0 > 0) {
       // per-wave maxima of the running best, written after the previous group
       const double* wm = s_wmax + ((grp - 1) & 1) * 4;
-      __syncthreads();  // previous group's prefix no longer read; wm visible
+      block_sync();  // previous group's prefix no longer read; wm visible
       thr = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
       split_stage_prefix(hs, f0, g, NB, NS, A.Fmax, A.hct, pre);
     }
@@ -2917,7 +2917,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   s_gain[tid] = bgain;
   s_key[tid] = bkey;
   s_valid[tid] = bvalid;
-  __syncthreads();
+  block_sync();
   for (int o = 128; o > 0; o >>= 1) {
     if (tid < o) {
       const double g2 = s_gain[tid + o];
@@ -2928,7 +2928,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
         s_valid[tid] = s_valid[tid + o];
       }
     }
-    __syncthreads();
+    block_sync();
   }
   const int key = s_key[0];
   const int bf = key == INT_MAX ? -1 : key / 65536, bsp = key == INT_MAX ? -1 : key % 65536;
@@ -2970,7 +2970,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
     so[A.plane + c] = l;
     so[2 * A.plane + c] = s_tot[c] - l;
   }
-  __syncthreads();
+  block_sync_mem();  // tid 0 reads the other threads' global stats words
   if (tid == 0 && bf >= 0) {  // the children's Gini.calculate, as the host's Calc would
     double imp2[2];
     for (int side = 0; side < 2; side++) {
@@ -3358,13 +3358,13 @@ __global__ __launch_bounds__(kPredThreads) void k_predict_tiled(PredictArgs A) {
   const unsigned char* r1p = rows + (tid + kPredThreads) * pitch;
   for (int c = 0; c < A.nchunks; c++) {
     const PredictChunk ch = A.chunks[c];
-    __syncthreads();  // previous chunk done (and the row tile written)
+    block_sync();  // previous chunk done (and the row tile written)
     const int nb = (int)(ch.n1 - ch.n0) * 8, lb = (int)(ch.l1 - ch.l0) * 8;
     for (int i = tid; i < (nb >> 3); i += kPredThreads)
       ((PNode*)chunk)[i] = A.nodes[ch.n0 + i];
     for (int i = tid; i < (lb >> 3); i += kPredThreads)
       ((double*)(chunk + nb))[i] = A.leaves[ch.l0 + i];
-    __syncthreads();
+    block_sync();
     for (int t = ch.t0; t < ch.t1; t++) {
       const PNode* tn = (const PNode*)chunk + (A.tree_node[t] - ch.n0);
       const double* tl = (const double*)(chunk + nb) + (A.tree_leaf[t] - ch.l0);
@@ -3600,7 +3600,7 @@ __global__ __launch_bounds__(64) void k_bt_hist(const uint32_t* __restrict__ row
   const int fl = blockIdx.y * FL + lane;
   const bool on = lane < FL && fl <= Fr;
   for (int k = lane; k < NB * 3 * FL; k += 64) acc[k] = 0.0;
-  __syncthreads();
+  block_sync();
   const int64_t a = seg[2 * q], b = seg[2 * q + 1];
   const bool total = fl == Fr;
   const bool gat = on && !total;  // lanes whose code decides the bin (the total lane: bin 0)
@@ -3672,7 +3672,7 @@ __global__ __launch_bounds__(64) void k_bt_hist(const uint32_t* __restrict__ row
       }
     }
   }
-  __syncthreads();
+  block_sync();
   if (on) {
     double* out = hist + ((int64_t)q * (Fr + 1) + fl) * NB * 3;
     const int nb = total ? 1 : NB;
@@ -3714,13 +3714,13 @@ __global__ __launch_bounds__(kBtPartT) void k_bt_partition(const uint32_t* __res
     return lt[bt_code(codes, code_bytes, (int64_t)r * S + p.g)] <= p.s;
   };
   if (tid == 0) s_tot = 0;
-  __syncthreads();
+  block_sync();
   int nl_mine = 0;  // this thread's left rows (pass 1)
   for (int64_t i = p.a + tid; i < p.b; i += kBtPartT) nl_mine += goes_left(in[i]) ? 1 : 0;
   // wave sum then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) nl_mine += __shfl_xor(nl_mine, o);
   if (lane == 0) atomicAdd(&s_tot, (unsigned long long)nl_mine);
-  __syncthreads();
+  block_sync();
   const int64_t nl = (int64_t)s_tot;
   int64_t lpos = p.a, rpos = p.a + nl;
   for (int64_t i0 = p.a; i0 < p.b; i0 += kBtPartT) {
@@ -3737,7 +3737,7 @@ __global__ __launch_bounds__(kBtPartT) void k_bt_partition(const uint32_t* __res
       s_l[wave] = __popcll(ml);
       s_r[wave] = __popcll(mr);
     }
-    __syncthreads();
+    block_sync();
     int bl = 0, br = 0, tl = 0, tr = 0;  // rows of the waves before this one; pass totals
 #pragma unroll
     for (int w = 0; w < W; w++) {
@@ -3754,7 +3754,7 @@ __global__ __launch_bounds__(kBtPartT) void k_bt_partition(const uint32_t* __res
     if (valid) out[left ? lpos + bl + rank_l : rpos + br + rank_r] = r;
     lpos += tl;
     rpos += tr;
-    __syncthreads();  // s_l / s_r are rewritten by the next pass
+    block_sync();  // s_l / s_r are rewritten by the next pass
   }
   if (tid == 0) nleft[blockIdx.x] = nl;
 }

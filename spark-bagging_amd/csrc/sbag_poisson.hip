@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kP4Streams* LANES) void k_poisson4(
     }
     st[624 + t] = 0u;
   }
-  __syncthreads();
+  block_sync();
   int64_t row = active ? part_off[p] : 0;
   const int64_t row_end = active ? part_off[p + 1] : 0;
   uint8_t* out = counts + (int64_t)r * N;

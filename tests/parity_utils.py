@@ -38,3 +38,41 @@ def assert_forest_equal(native, orf, rel_tol_pred=0.0):
     assert L == orf.nodes.shape[0]
     for t in range(L):
         assert_tree_equal(native, t, orf, t, rel_tol_pred)
+
+
+def fuzz_case(seed):
+    """One randomized parity case of scripts/fuzz_parity.py: (X, y, classification,
+    non-dyadic labels, partition offsets, fit params, feature kind)."""
+    rng = np.random.default_rng(seed)
+    N = int(np.exp(rng.uniform(np.log(2000), np.log(150_000))))
+    F = int(rng.choice([1, 3, 12, 40, 64, 65, 100, 140]))
+    cls = bool(rng.integers(0, 2))
+    kind = rng.choice(["mixed", "u8"])
+    if kind == "u8":  # 32-level integer columns: identity codes, the bench's layout
+        X = rng.integers(0, 32, size=(N, F)).astype(np.float64)
+    else:
+        X = np.empty((N, F))
+        for f in range(F):
+            levels = int(rng.choice([2, 3, 7, 31, 200, 5000]))
+            X[:, f] = np.round(rng.normal(size=N) * levels) / 8.0
+            X[rng.random(N) < 0.1, f] = 0.0
+    f64 = False
+    if cls:
+        C = int(rng.choice([2, 3, 5, 9, 17, 33, 64, 80]))
+        code = np.floor(np.abs(X[:, 0]) * 3 + np.abs(X[:, min(1, F - 1)])).astype(np.int64)
+        y = ((code + rng.integers(0, 4, N)) % C).astype(np.float64)
+    else:
+        f64 = bool(rng.random() < 0.35)
+        y = rng.integers(-400, 400, size=N) / 16.0 + X[:, 0] * 0.25
+        if f64:
+            y = y * 1.1 + 0.3
+    P = 1 if f64 else int(rng.integers(1, 7))
+    cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
+    part = [0] + [int(c) for c in cuts] + [N]
+    p = dict(L=int(rng.integers(1, 13)), replacement=bool(rng.integers(0, 2)),
+             ratio=float(rng.choice([1.0, 0.9, 0.63, 0.5])), depth=int(rng.integers(0, 15)),
+             bins=int(rng.choice([2, 5, 16, 32, 32, 64])), min_inst=int(rng.choice([1, 1, 3, 20])),
+             min_gain=float(rng.choice([0.0, 0.0, 0.001, 0.05])))
+    if not p["replacement"] and p["ratio"] == 1.0:
+        p["ratio"] = 0.7
+    return X, y, cls, f64, part, p, kind

@@ -158,3 +158,20 @@ def test_loading_a_malformed_model_directory_fails_cleanly(tmp_path):
     back = sb.BaggingRegressionModel.load(path)
     with pytest.raises(sb.IllegalArgumentException):
         back.native_forest()
+
+
+def test_kernel_barriers_wait_for_lds():
+    """Every workgroup barrier in the HIP sources goes through block_sync / block_sync_mem
+    (sbag_internal.h), which spell out the s_waitcnt: a bare __syncthreads() let a wave
+    cross the barrier with an LDS write in flight on gfx950 (k_split_gini, found by
+    scripts/fuzz_parity.py)."""
+    import glob
+    csrc = os.path.join(ROOT, "spark-bagging_amd", "csrc")
+    offenders = []
+    for path in sorted(glob.glob(os.path.join(csrc, "*.hip"))):
+        for n, line in enumerate(open(path), 1):
+            if re.search(r"\b__syncthreads\s*\(", line.split("//")[0]):
+                offenders.append(f"{os.path.basename(path)}:{n}")
+    assert not offenders, offenders
+    helpers = open(os.path.join(csrc, "sbag_internal.h")).read()
+    assert "__builtin_amdgcn_s_waitcnt(0xC07F);" in helpers

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle
-from parity_utils import assert_forest_equal, oracle_forest
+from parity_utils import assert_forest_equal, fuzz_case, oracle_forest
 
 import spark_bagging_amd as sb
 from spark_bagging_amd import _native as nat
@@ -81,3 +81,49 @@ def test_random_parity(ctx, seed):
     want = oracle.predict(orf, X, classification=cls)
     np.testing.assert_array_equal(nat.predict(ctx, forest, X, agg), want)
     np.testing.assert_array_equal(nat.predict_dataset(ctx, forest, ds, agg), want)
+
+
+def _fit_fuzz(ctx, seed):
+    X, y, cls, f64, part, p, kind = fuzz_case(seed)
+    sd = oracle.DEFAULT_SEED_CLASSIFIER if cls else oracle.DEFAULT_SEED_REGRESSOR
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        forest = nat.fit(ctx, ds, replacement=p["replacement"], sample_ratio=p["ratio"], seed=sd,
+                         learner_begin=0, learner_end=p["L"], partition_offsets=part,
+                         max_depth=p["depth"], max_bins=p["bins"],
+                         min_instances_per_node=p["min_inst"], min_info_gain=p["min_gain"],
+                         impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    finally:
+        ds.free()
+    counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, len(y))
+    subs = [oracle.subspace(p["ratio"], X.shape[1], sd + i) for i in range(p["L"])]
+    orf = oracle_forest(X, y, counts, subs, p["depth"], p["bins"], cls, p["min_inst"], p["min_gain"],
+                        part=part)
+    return forest, orf
+
+
+def test_split_gini_barrier_regression(ctx):
+    """scripts/fuzz_parity.py seed 50680 (62 057 rows, 63 classes, 5 bins, depth 14): with a
+    28-feature group, k_split_gini's wave maxima of the previous group were read across a
+    barrier the compiler had left without its LDS wait, so the screen threshold was stale and
+    different trees came out run to run.  Three fits, every tree bit-exact each time."""
+    for _ in range(3):
+        forest, orf = _fit_fuzz(ctx, 50680)
+        assert_forest_equal(forest, orf)
+        forest.free()
+
+
+# one passing draw per (labels, feature kind, P > 1) of the r03v fuzz pass (0 failures in
+# 2 245 draws, gpurun_out/r03v/fuzz.log): 64 / 80 classes, fp64 labels, u8 identity rows
+@pytest.mark.parametrize("seed", [60003, 60009, 60110, 60163, 60042, 60013, 60006, 60010,
+                                  60000, 60012, 60002, 60077])
+def test_fuzz_shapes_parity(ctx, seed):
+    """scripts/fuzz_parity.py draws (up to 150k rows, 140 features, 80 classes, depth 14,
+    several partitions, fp64 labels) against the oracle, node by node."""
+    X, y, cls, f64, part, p, kind = fuzz_case(seed)
+    forest, orf = _fit_fuzz(ctx, seed)
+    assert_forest_equal(forest, orf)
+    agg = nat.AGG_MODE if cls else nat.AGG_MEAN
+    np.testing.assert_array_equal(nat.predict(ctx, forest, X, agg),
+                                  oracle.predict(orf, X, classification=cls))
+    forest.free()
