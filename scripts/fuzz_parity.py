@@ -30,30 +30,40 @@ from parity_utils import assert_forest_equal, fuzz_case, oracle_forest  # noqa: 
 draw = fuzz_case  # tests/parity_utils.py
 
 
-def run(ctx, seed):
+def run(ctx, seed, extra=False):
     X, y, cls, f64, part, p, kind = draw(seed)
     sd = oracle.DEFAULT_SEED_CLASSIFIER if cls else oracle.DEFAULT_SEED_REGRESSOR
     N, F = X.shape
+    # --extra: a learner range that does not start at 0 and, half the time, a subspace
+    # ratio of its own (subspace_bug_compat off); its own stream, so the draws above keep
+    # their meaning (tests/test_gpu_random.py pins some)
+    lb, sub_ratio, compat = 0, p["ratio"], True
+    if extra:
+        rng2 = np.random.default_rng(seed + 10**7)
+        lb = int(rng2.choice([0, 1, 7, 129, 511]))
+        if rng2.random() < 0.5:
+            compat, sub_ratio = False, float(rng2.choice([1.0, 0.8, 0.3]))
     desc = (f"seed {seed} N {N} F {F} {kind} {'cls C=%d' % (int(y.max()) + 1) if cls else ('f64' if f64 else 'reg')} "
-            f"P {len(part) - 1} {p}")
+            f"P {len(part) - 1} lb {lb} sub {sub_ratio if not compat else 'H1'} {p}")
     ds = nat.DeviceDataset.from_numpy(X, y, ctx)
     try:
         forest = nat.fit(ctx, ds, replacement=p["replacement"], sample_ratio=p["ratio"], seed=sd,
-                         learner_begin=0, learner_end=p["L"], partition_offsets=part,
+                         learner_begin=lb, learner_end=lb + p["L"], partition_offsets=part,
+                         subspace_ratio=sub_ratio, subspace_bug_compat=compat,
                          max_depth=p["depth"], max_bins=p["bins"],
                          min_instances_per_node=p["min_inst"], min_info_gain=p["min_gain"],
                          impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
     except sb.SparkException as e:
         ds.free()
-        counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, N)
+        counts = oracle.bag(p["replacement"], p["ratio"], lb, lb + p["L"], sd, part, N)
         ok = e.code == nat.SBAG_EEMPTY and (counts.sum(axis=1) == 0).any()
         return ok, desc + f" -> {e}"
     except sb.IllegalArgumentException as e:
         ds.free()
-        ok = any(len(oracle.subspace(p["ratio"], F, sd + i)) == 0 for i in range(p["L"]))
+        ok = any(len(oracle.subspace(sub_ratio, F, sd + i)) == 0 for i in range(lb, lb + p["L"]))
         return ok, desc + f" -> {e}"
-    counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, N)
-    subs = [oracle.subspace(p["ratio"], F, sd + i) for i in range(p["L"])]
+    counts = oracle.bag(p["replacement"], p["ratio"], lb, lb + p["L"], sd, part, N)
+    subs = [oracle.subspace(sub_ratio, F, sd + i) for i in range(lb, lb + p["L"])]
     orf = oracle_forest(X, y, counts, subs, p["depth"], p["bins"], cls, p["min_inst"], p["min_gain"],
                         part=part)
     try:
@@ -62,6 +72,8 @@ def run(ctx, seed):
         want = oracle.predict(orf, X, classification=cls)
         got = nat.predict(ctx, forest, X, agg)
         np.testing.assert_array_equal(got, want)
+        if extra:  # rows already on the device: the binned transform
+            np.testing.assert_array_equal(nat.predict_dataset(ctx, forest, ds, agg), want)
     except AssertionError as e:
         return False, desc + " FAIL " + str(e)[:400]
     finally:
@@ -75,6 +87,8 @@ def main():
     ap.add_argument("--start", type=int, default=50_000)
     ap.add_argument("--minutes", type=float, default=5.0)
     ap.add_argument("--cases", type=int, default=10**9)
+    ap.add_argument("--extra", action="store_true",
+                    help="learner offsets, subspace ratios of their own, device transform")
     a = ap.parse_args()
     ctx = sb.default_context(0)
     t0 = time.time()
@@ -82,7 +96,7 @@ def main():
     seed = a.start
     while n < a.cases and time.time() - t0 < 60 * a.minutes:
         t1 = time.time()
-        ok, desc = run(ctx, seed)
+        ok, desc = run(ctx, seed, a.extra)
         n += 1
         fails += 0 if ok else 1
         print(("ok   " if ok else "FAIL ") + f"{time.time() - t1:6.1f}s " + desc, flush=True)
