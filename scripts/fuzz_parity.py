@@ -30,8 +30,42 @@ from parity_utils import assert_forest_equal, fuzz_case, oracle_forest  # noqa: 
 draw = fuzz_case  # tests/parity_utils.py
 
 
-def run(ctx, seed, extra=False):
-    X, y, cls, f64, part, p, kind = draw(seed)
+def draw_big(seed):
+    """--big: 1-3M rows and 16-32 learners, so the fit splits its learner range into two
+    halves on two streams and the histograms run at shard-like sizes."""
+    rng = np.random.default_rng(seed)
+    N = int(rng.integers(1 << 20, 3_000_000))
+    F = int(rng.choice([8, 20, 40, 100]))
+    cls = bool(rng.integers(0, 2))
+    kind = rng.choice(["mixed", "u8"])
+    if kind == "u8":
+        X = rng.integers(0, 32, size=(N, F)).astype(np.float64)
+    else:
+        X = np.round(rng.normal(size=(N, F)) * rng.choice([3, 31, 500], size=F)) / 8.0
+    f64 = False
+    if cls:
+        C = int(rng.choice([2, 5, 17, 64]))
+        code = np.floor(np.abs(X[:, 0]) * 3 + np.abs(X[:, min(1, F - 1)])).astype(np.int64)
+        y = ((code + rng.integers(0, 4, N)) % C).astype(np.float64)
+    else:
+        f64 = bool(rng.random() < 0.3)
+        y = rng.integers(-400, 400, size=N) / 16.0 + X[:, 0] * 0.25
+        if f64:
+            y = y * 1.1 + 0.3
+    P = 1 if f64 else int(rng.integers(1, 9))
+    cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
+    part = [0] + [int(c) for c in cuts] + [N]
+    p = dict(L=int(rng.choice([16, 24, 32])), replacement=bool(rng.integers(0, 2)),
+             ratio=float(rng.choice([1.0, 0.8, 0.5])), depth=int(rng.integers(3, 12)),
+             bins=int(rng.choice([16, 32, 64])), min_inst=int(rng.choice([1, 5])),
+             min_gain=float(rng.choice([0.0, 0.001])))
+    if not p["replacement"] and p["ratio"] == 1.0:
+        p["ratio"] = 0.7
+    return X, y, cls, f64, part, p, kind
+
+
+def run(ctx, seed, extra=False, big=False):
+    X, y, cls, f64, part, p, kind = (draw_big if big else draw)(seed)
     sd = oracle.DEFAULT_SEED_CLASSIFIER if cls else oracle.DEFAULT_SEED_REGRESSOR
     N, F = X.shape
     # --extra: a learner range that does not start at 0 and, half the time, a subspace
@@ -89,6 +123,7 @@ def main():
     ap.add_argument("--cases", type=int, default=10**9)
     ap.add_argument("--extra", action="store_true",
                     help="learner offsets, subspace ratios of their own, device transform")
+    ap.add_argument("--big", action="store_true", help="1-3M rows, 16-32 learners (draw_big)")
     a = ap.parse_args()
     ctx = sb.default_context(0)
     t0 = time.time()
@@ -96,7 +131,7 @@ def main():
     seed = a.start
     while n < a.cases and time.time() - t0 < 60 * a.minutes:
         t1 = time.time()
-        ok, desc = run(ctx, seed, a.extra)
+        ok, desc = run(ctx, seed, a.extra, a.big)
         n += 1
         fails += 0 if ok else 1
         print(("ok   " if ok else "FAIL ") + f"{time.time() - t1:6.1f}s " + desc, flush=True)
