@@ -116,6 +116,37 @@ def run(ctx, seed, extra=False, big=False):
     return True, desc
 
 
+def run_booster(ctx, seed):
+    """--booster: one GBM base learner (sbag_fit_booster, Spark's row-order fp64 sums) on a
+    draw's rows with real-valued labels, a bag and a subspace, against the oracle's tree."""
+    X, y, cls, f64, part, p, kind = draw(seed)
+    rng = np.random.default_rng(seed + 2 * 10**7)
+    N, F = X.shape
+    lab = rng.normal(size=N) * 3.3 + (X[:, 0] if F else 0.0) * 0.1
+    counts = oracle.bag(p["replacement"], p["ratio"], 5, 6, 77 + seed, part, N)[0]
+    sub = oracle.subspace(p["ratio"], F, 1234 + seed)
+    desc = f"booster seed {seed} N {N} F {F} {kind} P {len(part) - 1} {p}"
+    if counts.sum() == 0 or len(sub) == 0:
+        return True, desc + " (empty bag or subspace: skipped)"
+    ds = nat.DeviceDataset.from_numpy(X, np.zeros(N), ctx)
+    try:
+        f = nat.fit_booster(ctx, ds, lab, counts, sub, partition_offsets=part, max_depth=min(p["depth"], 10),
+                            max_bins=p["bins"], min_instances_per_node=p["min_inst"],
+                            min_info_gain=p["min_gain"])
+    finally:
+        ds.free()
+    orf = oracle.fit(X, lab, counts[None, :], [sub], max_depth=min(p["depth"], 10), max_bins=p["bins"],
+                     min_instances_per_node=p["min_inst"], min_info_gain=p["min_gain"], part=part)
+    try:
+        from parity_utils import assert_tree_equal
+        assert_tree_equal(f, 0, orf, 0)
+    except AssertionError as e:
+        return False, desc + " FAIL " + str(e)[:400]
+    finally:
+        f.free()
+    return True, desc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--start", type=int, default=50_000)
@@ -124,6 +155,7 @@ def main():
     ap.add_argument("--extra", action="store_true",
                     help="learner offsets, subspace ratios of their own, device transform")
     ap.add_argument("--big", action="store_true", help="1-3M rows, 16-32 learners (draw_big)")
+    ap.add_argument("--booster", action="store_true", help="GBM base learners (run_booster)")
     a = ap.parse_args()
     ctx = sb.default_context(0)
     t0 = time.time()
@@ -131,7 +163,7 @@ def main():
     seed = a.start
     while n < a.cases and time.time() - t0 < 60 * a.minutes:
         t1 = time.time()
-        ok, desc = run(ctx, seed, a.extra, a.big)
+        ok, desc = run_booster(ctx, seed) if a.booster else run(ctx, seed, a.extra, a.big)
         n += 1
         fails += 0 if ok else 1
         print(("ok   " if ok else "FAIL ") + f"{time.time() - t1:6.1f}s " + desc, flush=True)
