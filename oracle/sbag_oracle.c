@@ -282,9 +282,11 @@ static int cmp_double(const void* a, const void* b) {
    the split-finding sample with multiplicity (findSplitsBySorting drops zeros); n =
    metadata.numExamples; num_samples = (samplesFractionForFindSplits * numExamples).toInt,
    the expected sample size whose shortfall over nnz is the implied zero count. */
+/* thr holds cap values: a split-finding sample larger than num_samples can pass one more
+   target than numSplits (Spark then sets numSplits to the length it got); -1 past cap. */
 static int find_splits_values(double* vals /*nonzero values with multiplicity, sorted in place*/,
                               int64_t nnz, int64_t n, int64_t num_samples, int64_t max_bins,
-                              double* thr) {
+                              double* thr, int cap) {
   if (nnz == 0) return 0; /* featureSamples.isEmpty */
   const int64_t max_possible_bins = (max_bins < n) ? max_bins : n;
   const int64_t num_splits = max_possible_bins - 1;
@@ -331,6 +333,10 @@ static int find_splits_values(double* vals /*nonzero values with multiplicity, s
       const double pg = fabs((double)prev - target);
       const double cg = fabs((double)current - target);
       if (pg < cg) {
+        if (nt >= cap) {
+          free(vc);
+          return -1;
+        }
         thr[nt++] = (vc[i - 1].v + vc[i].v) / 2.0;
         target += stride;
       }
@@ -442,7 +448,7 @@ int or_find_splits(const double* X, int64_t N, int F, int feature, const uint8_t
       for (int c = 0; c < counts[r]; c++) vals[k++] = x;
   }
   *exact_out = or_split_sample_fraction(n, max_bins) >= 1.0;
-  int nt = find_splits_values(vals, nnz, n, n, max_bins, thr_out);
+  int nt = find_splits_values(vals, nnz, n, n, max_bins, thr_out, (int)max_bins);
   free(vals);
   return nt;
 }
@@ -706,10 +712,12 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
       if (cnt[r]) rows[k++] = r;
   }
   /* findSplits + TreePoint binning */
-  double* thr = (double*)malloc(sizeof(double) * (size_t)Fr * (size_t)p->max_bins);
+  const int tcap = p->max_bins + 64; /* thresholds per feature (find_splits_values) */
+  double* thr = (double*)malloc(sizeof(double) * (size_t)Fr * (size_t)tcap);
   int* nthr = (int*)malloc(sizeof(int) * (size_t)Fr);
   uint16_t* bins = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)nrows * (size_t)Fr);
   int all_exact = 1;
+  int too_many = 0;
   /* RandomForest.findSplits: the split-finding sample of the subbag */
   const double fraction = or_split_sample_fraction(n, p->max_bins);
   uint16_t* mult = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)N);
@@ -737,9 +745,14 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
       if (x != 0.0)
         for (int c = 0; c < mult[rows[k]]; c++) vals[q++] = x;
     }
-    nthr[fl] = find_splits_values(vals, nnz, n, num_samples, p->max_bins, thr + (int64_t)fl * p->max_bins);
+    nthr[fl] = find_splits_values(vals, nnz, n, num_samples, p->max_bins, thr + (int64_t)fl * tcap, tcap);
     free(vals);
-    const double* t = thr + (int64_t)fl * p->max_bins;
+    if (nthr[fl] < 0) { /* more thresholds than tcap: refuse rather than overflow */
+      nthr[fl] = 0;
+      too_many = 1;
+      continue;
+    }
+    const double* t = thr + (int64_t)fl * tcap;
     for (int64_t k = 0; k < nrows; k++) {
       const double x = xval(X, xkind, rows[k] * F + fg);
       int lo = 0, hi = nthr[fl]; /* #thresholds < x  == Arrays.binarySearch result */
@@ -758,7 +771,17 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
   tree.v[0].exists = 1;
   int64_t* node_of = (int64_t*)malloc(sizeof(int64_t) * (size_t)nrows);
   for (int64_t k = 0; k < nrows; k++) node_of[k] = 0;
-  const int nb = p->max_bins;
+  if (too_many) {
+    free(rows);
+    free(thr);
+    free(nthr);
+    free(bins);
+    free(mult);
+    return -6;
+  }
+  int nb = p->max_bins; /* bins per feature row: numSplits + 1, one more after a large sample */
+  for (int fl = 0; fl < Fr; fl++)
+    if (nthr[fl] + 1 > nb) nb = nthr[fl] + 1;
   int64_t first = 0, last = 0; /* this level's nodes: tree.v[first .. last] */
   for (int level = 0; level <= D && first <= last; level++) {
     int64_t nact = 0;
@@ -916,7 +939,7 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
           node->has_split = 1;
           node->split_f = best_f;
           node->split_bin = best_s;
-          node->threshold = thr[(int64_t)best_f * p->max_bins + best_s];
+          node->threshold = thr[(int64_t)best_f * tcap + best_s];
           const int child_leaf = (level + 1) == D;
           const int64_t ci = lnodes_push(&tree);
           lnodes_push(&tree);

@@ -24,44 +24,13 @@ import sbag_loader  # noqa: E402
 sb = sbag_loader.load()
 nat = sb._native
 import oracle  # noqa: E402
-from parity_utils import assert_forest_equal, fuzz_case, oracle_forest  # noqa: E402
+from parity_utils import assert_forest_equal, fuzz_case, fuzz_case_big, oracle_forest  # noqa: E402
 
 
 draw = fuzz_case  # tests/parity_utils.py
 
 
-def draw_big(seed):
-    """--big: 1-3M rows and 16-32 learners, so the fit splits its learner range into two
-    halves on two streams and the histograms run at shard-like sizes."""
-    rng = np.random.default_rng(seed)
-    N = int(rng.integers(1 << 20, 3_000_000))
-    F = int(rng.choice([8, 20, 40, 100]))
-    cls = bool(rng.integers(0, 2))
-    kind = rng.choice(["mixed", "u8"])
-    if kind == "u8":
-        X = rng.integers(0, 32, size=(N, F)).astype(np.float64)
-    else:
-        X = np.round(rng.normal(size=(N, F)) * rng.choice([3, 31, 500], size=F)) / 8.0
-    f64 = False
-    if cls:
-        C = int(rng.choice([2, 5, 17, 64]))
-        code = np.floor(np.abs(X[:, 0]) * 3 + np.abs(X[:, min(1, F - 1)])).astype(np.int64)
-        y = ((code + rng.integers(0, 4, N)) % C).astype(np.float64)
-    else:
-        f64 = bool(rng.random() < 0.3)
-        y = rng.integers(-400, 400, size=N) / 16.0 + X[:, 0] * 0.25
-        if f64:
-            y = y * 1.1 + 0.3
-    P = 1 if f64 else int(rng.integers(1, 9))
-    cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
-    part = [0] + [int(c) for c in cuts] + [N]
-    p = dict(L=int(rng.choice([16, 24, 32])), replacement=bool(rng.integers(0, 2)),
-             ratio=float(rng.choice([1.0, 0.8, 0.5])), depth=int(rng.integers(3, 12)),
-             bins=int(rng.choice([16, 32, 64])), min_inst=int(rng.choice([1, 5])),
-             min_gain=float(rng.choice([0.0, 0.001])))
-    if not p["replacement"] and p["ratio"] == 1.0:
-        p["ratio"] = 0.7
-    return X, y, cls, f64, part, p, kind
+draw_big = fuzz_case_big  # tests/parity_utils.py
 
 
 def run(ctx, seed, extra=False, big=False):

@@ -2587,6 +2587,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       NB = std::max(NB, t_nb[w]);
       identity = identity && t_id[w];
     }
+    // thresholds beyond maxBins - 1 are Spark's (a split-finding sample larger than
+    // numSamples passes one more target; RandomForest then sets numSplits to what it got):
+    // NB follows them, but bins are u8 codes
+    if (NB > 256)
+      return fail(SBAG_EUNSUPPORTED, "more than 256 bins in a feature (maxBins 256 and a "
+                                     "split-finding sample above numSamples)");
   }
   if (optimistic && identity) {
     NB = ncmax;  // the codes-as-bins root histogram already has this layout
@@ -4172,6 +4178,9 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
     nsplits[fl] = find_splits(ds->dict[g], vc.data() + vcoff[fl], ds->zero_code[g], n_items, nsamp,
                               tp.max_bins, thr[fl]);
     NB = std::max(NB, nsplits[fl] + 1);
+    if (NB > 256)  // u8 bin codes; Spark's count can pass maxBins after a large sample
+      return fail(SBAG_EUNSUPPORTED, "more than 256 bins in a feature (maxBins 256 and a "
+                                     "split-finding sample above numSamples)");
     // TreePoint.findBin: #thresholds < value
     for (size_t k = 0; k < ds->dict[g].size(); k++)
       lut[vcoff[fl] + (int64_t)k] = (uint8_t)(std::lower_bound(thr[fl].begin(), thr[fl].end(),

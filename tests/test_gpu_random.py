@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle
-from parity_utils import assert_forest_equal, fuzz_case, oracle_forest
+from parity_utils import assert_forest_equal, fuzz_case, fuzz_case_big, oracle_forest
 
 import spark_bagging_amd as sb
 from spark_bagging_amd import _native as nat
@@ -126,4 +126,31 @@ def test_fuzz_shapes_parity(ctx, seed):
     agg = nat.AGG_MODE if cls else nat.AGG_MEAN
     np.testing.assert_array_equal(nat.predict(ctx, forest, X, agg),
                                   oracle.predict(orf, X, classification=cls))
+    forest.free()
+
+
+def test_split_sample_one_more_threshold(ctx):
+    """scripts/fuzz_parity.py --big seed 90000 (2.87M rows, 32 learners, subspace ratio 0.3 of
+    its own, fp64 labels): a split-finding sample larger than numSamples passes one more
+    target than numSplits, so a feature gets maxBins thresholds (Spark keeps them and sets
+    numSplits to that length).  The oracle's fixed threshold buffer overflowed here; the
+    engine sizes its bins by the largest count.  Trees bit-exact, and one split uses bin 31."""
+    X, y, cls, f64, part, p, kind = fuzz_case_big(90000)
+    sd = oracle.DEFAULT_SEED_REGRESSOR
+    N, F = X.shape
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        forest = nat.fit(ctx, ds, replacement=p["replacement"], sample_ratio=p["ratio"], seed=sd,
+                         learner_begin=0, learner_end=p["L"], partition_offsets=part,
+                         subspace_ratio=0.3, subspace_bug_compat=False, max_depth=p["depth"],
+                         max_bins=p["bins"], min_instances_per_node=p["min_inst"],
+                         min_info_gain=p["min_gain"], impurity=nat.IMPURITY_VARIANCE)
+    finally:
+        ds.free()
+    counts = oracle.bag(p["replacement"], p["ratio"], 0, p["L"], sd, part, N)
+    subs = [oracle.subspace(0.3, F, sd + i) for i in range(p["L"])]
+    orf = oracle_forest(X, y, counts, subs, p["depth"], p["bins"], False, p["min_inst"],
+                        p["min_gain"], part=part)
+    assert max(int(orf.tree(t)[0]["split_bin"].max()) for t in range(p["L"])) == p["bins"] - 1
+    assert_forest_equal(forest, orf)
     forest.free()
