@@ -93,6 +93,10 @@ def hist_kernel_name(F, cls, N):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for --gpus > 1 (nccl = RCCL over xGMI; gloo "
+                         "stages the collectives through host memory, so N ranks can share one "
+                         "GPU: the multi-rank path rehearsed on a 1-GPU box)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
@@ -161,12 +165,20 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # ranks beyond the visible devices share them (gloo rehearsal of the multi-rank path on
+    # one GPU); with one rank per GPU this is LOCAL_RANK
+    dev = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(dev)
+    # host tensors for the timing collectives under gloo
+    tdev = "cuda" if args.backend == "nccl" else "cpu"
     sb = sbag_loader.load()
     nat = sb._native
-    ctx = nat.Context(local)
+    ctx = nat.Context(dev)
     N, F, L = args.rows, args.features, args.learners
     cls = args.classes > 0
     replication = None
@@ -184,12 +196,13 @@ def main():
         ds = D.replicate_dataset(ds0, dist, ctx)
         torch.cuda.synchronize()
         dist.barrier()
-        t_rep = torch.tensor([time.perf_counter() - t_r], dtype=torch.float64, device="cuda")
+        t_rep = torch.tensor([time.perf_counter() - t_r], dtype=torch.float64, device=tdev)
         dist.all_reduce(t_rep, op=dist.ReduceOp.MAX)
         replication = {"seconds": round(float(t_rep.item()), 4), "bytes": ds.codes_nbytes() + 8 * N,
                        "how": "rank 0 generates the synthetic dataset; ranks > 0 import its value "
-                              "codes, dictionaries and labels after RCCL broadcasts "
-                              "(distributed.replicate_dataset)"}
+                              "codes, dictionaries and labels after %s broadcasts "
+                              "(distributed.replicate_dataset)" % (
+                                  "RCCL" if args.backend == "nccl" else "gloo (host-staged)")}
     part = [int(round(i * N / args.partitions)) for i in range(args.partitions + 1)]
     lb = rank * L
 
@@ -215,7 +228,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -326,7 +339,8 @@ def main():
                                "binsToBestSplit, stable partition (DESIGN.md §4.7)"}
     out = {
         "metric": "estimator×rows trained/sec", "value": round(value, 1),
-        "unit": "estimator*rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "unit": "estimator*rows/s", "n_gpus": world, "backend": args.backend if world > 1 else None,
+        "devices_used": min(world, torch.cuda.device_count()), "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64",
         "data": "synthetic (device generator k_synth: splitmix64 codes mod 32, "

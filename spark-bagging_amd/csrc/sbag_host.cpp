@@ -344,6 +344,15 @@ struct sbag_dataset {
   int32_t cols_ncol = 0;
   uint32_t* d_planes = nullptr;
   int32_t planes_nsp = 0;
+  // every device buffer goes with the dataset, also when a constructor (create, import)
+  // returns early after some of them were allocated
+  ~sbag_dataset() {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (void* p : {(void*)d_codes, (void*)d_labk, (void*)d_y64, (void*)d_dict, (void*)d_dict_off,
+                    (void*)d_cols, (void*)d_planes})
+      if (p) (void)hipFree(p);
+  }
 };
 
 static int32_t row_stride(int32_t F) {
@@ -1220,14 +1229,7 @@ int sbag_dataset_free(sbag_dataset* ds) {
   CTX_LOCK(ds->ctx);
   (void)hipSetDevice(ds->ctx->device);
   (void)hipStreamSynchronize(ds->ctx->stream);
-  if (ds->d_codes) (void)hipFree(ds->d_codes);
-  if (ds->d_labk) (void)hipFree(ds->d_labk);
-  if (ds->d_y64) (void)hipFree(ds->d_y64);
-  if (ds->d_dict) (void)hipFree(ds->d_dict);
-  if (ds->d_dict_off) (void)hipFree(ds->d_dict_off);
-  if (ds->d_cols) (void)hipFree(ds->d_cols);
-  if (ds->d_planes) (void)hipFree(ds->d_planes);
-  delete ds;
+  delete ds;  // ~sbag_dataset frees the device buffers
   return SBAG_OK;
 }
 

@@ -14,6 +14,11 @@ namespace sbag {
 // the previous feature group: nondeterministic splits, found by scripts/fuzz_parity.py).
 // block_sync: s_waitcnt lgkmcnt(0) first; block_sync_mem: vmcnt(0) too, for global
 // memory written by one thread of the block and read by another after the barrier.
+// The immediates are the gfx9 s_waitcnt encoding (other generations lay the fields out
+// differently): the build refuses any other device target rather than drop the wait.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "sbag kernels are written for gfx9 (gfx950): block_sync's s_waitcnt encoding"
+#endif
 __device__ __forceinline__ void block_sync() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt 63 (no wait), expcnt 7, lgkmcnt 0
   __syncthreads();

@@ -163,12 +163,21 @@ def replicate_dataset(dataset, dist, ctx):
     for t in (codes, dvals, doff, y):
         dist.broadcast(t, 0)
     if rank == 0:
-        return dataset
+        out = dataset
+    else:
+        if on_dev:
+            torch.cuda.synchronize(dev)  # the broadcast has landed before the library reads it
+        out = nat.DeviceDataset.import_codes(ctx, (n, f, s, cb, dv), codes.data_ptr(), on_dev,
+                                             dvals[:dv].cpu().numpy(), doff.cpu().numpy(),
+                                             y.cpu().numpy())
+    # the staging tensors (a full copy of the codes: 25.6 GB for C4) go back to the device:
+    # the engine allocates with hipMalloc, which torch's caching allocator would otherwise
+    # keep from it
+    del codes, dvals, doff, y, lay
     if on_dev:
-        torch.cuda.synchronize(dev)  # the broadcast has landed before the library reads it
-    return nat.DeviceDataset.import_codes(ctx, (n, f, s, cb, dv), codes.data_ptr(), on_dev,
-                                          dvals[:dv].cpu().numpy(), doff.cpu().numpy(),
-                                          y.cpu().numpy())
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+    return out
 
 
 def fit_shard(estimator, frame, dist, devices=None):

@@ -162,3 +162,51 @@ def test_c5_shard(ctx):
                                   oracle.predict(orf, Xs, classification=True))
     forest.free()
     ds.free()
+
+
+def _full_shard(ctx, *, n, f, classes, replacement, ratio, seed, lb, le, depth, check):
+    """One GPU's whole learner shard of a multi-GPU config at its full size, fitted exactly as
+    bench.py --workload c4 / c5 times it.  The data are checked against the oracle's
+    generator on row slices (the full host copy would be 25.6 GB for C4); every tree
+    through the size-independent invariants, with its root count against its bag; the bags
+    of the `check` learners bit-exact against oracle.bag at full length."""
+    cls = classes > 0
+    ds = nat.DeviceDataset.synthetic(n, f, seed=DATA_SEED, num_classes=classes, ctx=ctx)
+    yall = ds.labels()
+    for r0 in (0, n // 3, n - 1000):
+        Xs, ys = oracle.synth(1000, f, DATA_SEED, classes, row_begin=r0, nthreads=1)
+        np.testing.assert_array_equal(ds.features(r0, r0 + 1000), Xs.astype(np.float64))
+        np.testing.assert_array_equal(yall[r0:r0 + 1000], ys)
+    del yall
+    part = _partitions(n)
+    forest = nat.fit(ctx, ds, replacement=replacement, sample_ratio=ratio, seed=seed,
+                     learner_begin=lb, learner_end=le, partition_offsets=part, max_depth=depth,
+                     max_bins=32, impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    assert len(forest) == le - lb
+    step = 8
+    for b0 in range(lb, le, step):
+        b1 = min(le, b0 + step)
+        counts = nat.sample(ctx, replacement, ratio, seed, b0, b1, n, part)
+        for i in range(b0, b1):
+            nodes, stats = forest.tree(i - lb)
+            check_tree_invariants(nodes, stats, cls, depth, int(counts[i - b0].sum(dtype=np.int64)))
+            if i in check:
+                want = oracle.bag(replacement, ratio, i, i + 1, seed, part, n)[0]
+                np.testing.assert_array_equal(counts[i - b0], want, err_msg=f"bag of learner {i}")
+        del counts
+    forest.free()
+    ds.free()
+
+
+def test_c4_full_shard(ctx):
+    """C4 (BASELINE configs[3]) at full size on one GPU: 100M rows x 256 features, rank 7's
+    learners [448, 512) of 512, P=128, depth 8 -- the shard bench.py --workload c4 times."""
+    _full_shard(ctx, n=100_000_000, f=256, classes=0, replacement=True, ratio=1.0, seed=SEED_REG,
+                lb=448, le=512, depth=8, check=(448, 511))
+
+
+def test_c5_full_shard(ctx):
+    """C5 (BASELINE configs[4]) at full size on one GPU: 50M rows x 100 features, 64 classes,
+    Bernoulli 0.5 without replacement, depth 12, rank 7's learners [112, 128) of 128."""
+    _full_shard(ctx, n=50_000_000, f=100, classes=64, replacement=False, ratio=0.5, seed=SEED_CLS,
+                lb=112, le=128, depth=12, check=(112, 127))
