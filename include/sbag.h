@@ -220,6 +220,8 @@ typedef struct {
   double hist_lds_atomics; /* LDS atomic wave-instructions issued by the hist launches   */
   double group_ms;         /* gini class tiles: entries regrouped by tile before the
                               histogram (k_tile_count / k_tile_scatter), not in hist_ms   */
+  double chain_ms;         /* fp64 labels: the chosen features' bins summed in Spark's row
+                              order (bucketing + routing + k_fb_chain)        */
 } sbag_timing;
 int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
 

@@ -7,8 +7,10 @@
 // bin) cell in row order, in fp64 (count += 1, sum += 1 * y, sumSq += 1 * y * y).  These
 // kernels reproduce those sums bit for bit:
 //
-//   k_chunk_inbag / k_chunk_scan / k_compact_ordered  the exploded bootstrap of each
-//                     replica: one entry per draw, in row order (a stable compaction)
+//   k_chunk_inbag / k_chunk_scan / k_compact_ordered  the bootstrap of each replica:
+//                     one entry (row, count, fixed-point label) per in-bag row, in row
+//                     order (a stable compaction); a row drawn c times adds its label c
+//                     times in a row
 //   k_f64_hist        one wave per (node, group of <= 64 features); lane = feature owns
 //                     that feature's NB cells in LDS and walks the node's entries in row
 //                     order, adding each row's label with LDS fp64 atomics (ds_add_f64):
@@ -66,10 +68,11 @@ constexpr int kChunkRows = 8192;
 }  // namespace
 
 // ---------------------------------------------------------------- ordered compaction
-// The fp64 path explodes the bootstrap (sql/bfunctions.scala:42-44: a row drawn c times is
-// c consecutive rows): every draw is its own entry (row | 1 << 32), in row order, so the
-// histogram walk adds one label per entry without a per-entry loop.
-// per (replica, 8192-row chunk): draws; per replica Σ count and max count
+// The fp64 path keeps every replica's in-bag rows in row order (Spark adds a node's rows to
+// its fp64 sums in that order): one entry row | (k << 8 | count) << 32 per in-bag row, k the
+// labels' fixed-point image for the integer screening histograms (a row drawn c times is c
+// consecutive rows in Spark, sql/bfunctions.scala:42-44: its label is added c times).
+// per (replica, 8192-row chunk): in-bag rows; per replica Σ count and max count
 __global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__ counts, int64_t N,
                                                      int R, int64_t chunks,
                                                      uint32_t* __restrict__ ncnt,
@@ -78,36 +81,39 @@ __global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__
   const int r = blockIdx.x % R;
   const int64_t chunk = blockIdx.x / R;
   const uint8_t* cr = counts + (int64_t)r * N;
-  unsigned int s = 0, m = 0;
+  unsigned int s = 0, m = 0, n = 0;
   for (int it = 0; it < kChunkRows / 256; it++) {
     const int64_t row = chunk * kChunkRows + it * 256 + threadIdx.x;
     if (row < N) {
       const unsigned int c = cr[row];
       s += c;
+      n += c ? 1u : 0u;
       m = max(m, c);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_down(s, o);
+    n += __shfl_down(n, o);
     m = max(m, (unsigned int)__shfl_down((int)m, o));
   }
-  __shared__ unsigned int s_s[4], s_m[4];
+  __shared__ unsigned int s_s[4], s_m[4], s_n[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
     s_s[wave] = s;
     s_m[wave] = m;
+    s_n[wave] = n;
   }
   block_sync();
   if (threadIdx.x == 0) {
     const unsigned int t = s_s[0] + s_s[1] + s_s[2] + s_s[3];  // <= 8192 * 255
-    ncnt[(int64_t)r * chunks + chunk] = t;
+    ncnt[(int64_t)r * chunks + chunk] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
     if (t) atomicAdd(&wsum[r], (unsigned long long)t);
     const unsigned int mm = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
     if (mm) atomicMax(&cmax[r], mm);
   }
 }
 
-// per replica: exclusive prefix of the chunks' draws; cursor[r] = the total
+// per replica: exclusive prefix of the chunks' entries; cursor[r] = the total
 __global__ __launch_bounds__(256) void k_chunk_scan(const uint32_t* __restrict__ ncnt, int64_t chunks,
                                                     unsigned long long* __restrict__ base,
                                                     unsigned long long* __restrict__ cursor) {
@@ -125,8 +131,9 @@ __global__ __launch_bounds__(256) void k_chunk_scan(const uint32_t* __restrict__
   if (threadIdx.x == 0) cursor[r] = carry;
 }
 
-// one entry (row | 1 << 32) per draw, in row order
-__global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restrict__ counts, int64_t N,
+// one entry per in-bag row, in row order
+__global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restrict__ counts,
+                                                         const int32_t* __restrict__ labk, int64_t N,
                                                          int R, int64_t chunks,
                                                          const unsigned long long* __restrict__ base,
                                                          uint64_t* __restrict__ ent, int64_t cap) {
@@ -143,14 +150,14 @@ __global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restri
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       c[j] = row0 + j < N ? cr[row0 + j] : 0u;
-      n += (int)c[j];
+      n += c[j] ? 1 : 0;
     }
     int tot;
     const int ex = block_excl_scan256(n, s_wave, &tot);
     unsigned long long pos = pos0 + (unsigned long long)ex;
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      for (uint32_t k = 0; k < c[j]; k++) er[pos++] = pack_entry((uint32_t)(row0 + j), 0, 1u);
+      if (c[j]) er[pos++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
     pos0 += (unsigned long long)tot;
   }
 }
@@ -162,13 +169,13 @@ void launch_chunk_draws(hipStream_t st, const uint8_t* counts, int64_t N, int R,
                      chunks, d_ncnt, d_wsum, d_cmax);
 }
 
-void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint64_t* ent,
-                            int64_t cap, const uint32_t* d_ncnt, unsigned long long* d_base,
-                            unsigned long long* d_cursor) {
+void launch_compact_ordered(hipStream_t st, const uint8_t* counts, const int32_t* labk, int64_t N,
+                            int R, uint64_t* ent, int64_t cap, const uint32_t* d_ncnt,
+                            unsigned long long* d_base, unsigned long long* d_cursor) {
   const int64_t chunks = compact_ordered_chunks(N);
   hipLaunchKernelGGL(k_chunk_scan, dim3(R), dim3(256), 0, st, d_ncnt, chunks, d_base, d_cursor);
-  hipLaunchKernelGGL(k_compact_ordered, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, R,
-                     chunks, d_base, ent, cap);
+  hipLaunchKernelGGL(k_compact_ordered, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, labk,
+                     N, R, chunks, d_base, ent, cap);
 }
 
 int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunkRows; }
@@ -181,7 +188,8 @@ int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunk
 // bin-0 cells (never read back).  A cell address is one 24-bit multiply-add, bin · M +
 // lane offset, M = 0 for the total and the idle lanes.
 //
-// The wave walks the node's entries (one per draw, compaction above) two batches of 64
+// The wave walks the node's entries (one per in-bag row, compaction above; a row drawn c
+// times adds its label c times in a row, its count c at once) two batches of 64
 // at a time: lane i holds entry i and its label, and the bins of the next batch are
 // gathered one per entry of the current one, right after that entry's atomics, so each
 // gather has ~63 entries of work to land in (the most the 6-bit vmcnt counter tracks).
@@ -192,7 +200,9 @@ int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunk
 // addresses, the LDS atomics and the next gather.  The node's last iteration runs whole:
 // entries past the end repeat the last entry with label y[N] = +0.0 (an exact no-op for
 // the sums, which start at +0.0 and so never become -0.0), and their count increments are
-// taken back from the last row's cells after the walk.
+// taken back from the last row's cells after the walk.  (This kernel is now the fallback of
+// the screened engine, sbag_f64s.hip: it histograms the nodes whose split the screen could
+// not decide, and every node under SBAG_F64_SCREEN=0.)
 //
 // Parts: at shallow levels (few nodes, few waves) a (node, group) is split over two
 // waves, one adding count and sum, the other sumSq: the two walks run in parallel and
@@ -203,22 +213,26 @@ typedef __attribute__((address_space(3))) double lds_double;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 template <int PART, int W>
-__device__ __forceinline__ void f64_add_entry(lds_char* L, double y, uint32_t bin, int j,
+__device__ __forceinline__ void f64_add_entry(lds_char* L, double y, uint32_t cnt, uint32_t bin, int j,
                                               uint32_t M1, uint32_t lo1, uint32_t M2, uint32_t lo2,
                                               bool act) {
   const uint64_t yb = (uint64_t)__double_as_longlong(y);
   const int ylo = __builtin_amdgcn_readlane((int)(uint32_t)yb, j);
   const int yhi = __builtin_amdgcn_readlane((int)(uint32_t)(yb >> 32), j);
+  // the row's draw count (wave-uniform): Spark adds its exploded copies one after another
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cnt, j);
   const double v = __longlong_as_double((long long)(((uint64_t)(uint32_t)yhi << 32) | (uint32_t)ylo));
   const double w = 1.0 * v;   // instanceWeight * label
   if (W < 64 && !act) return;  // lanes past W hold no cells
   lds_double* s = (lds_double*)(L + (__umul24(bin, M1) + lo1));
-  if (PART != 2) __hip_atomic_fetch_add(s, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (PART != 1)  // instanceWeight * label * label (its own array in part 2)
-    __hip_atomic_fetch_add(PART == 2 ? s : s + W, w * v, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (uint32_t k = 0; k < c; k++) {
+    if (PART != 2) __hip_atomic_fetch_add(s, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (PART != 1)  // instanceWeight * label * label (its own array in part 2)
+      __hip_atomic_fetch_add(PART == 2 ? s : s + W, w * v, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   if (PART != 2)
-    __hip_atomic_fetch_add((lds_u32*)(L + (__umul24(bin, M2) + lo2)), 1u, __ATOMIC_RELAXED,
+    __hip_atomic_fetch_add((lds_u32*)(L + (__umul24(bin, M2) + lo2)), c, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -264,9 +278,11 @@ __device__ __forceinline__ void f64_hist_body(const F64HistArgs& A, const F64Nod
     auto ld_y = [&](int64_t base, uint64_t e) -> double {
       return A.y[base + lane <= last ? (uint32_t)e : A.yzero];
     };
-    // even batches: eE, yE, bE; odd batches: eO, yO, bO -- each updated in place
+    auto cnt_of = [](uint64_t e) -> uint32_t { return (uint32_t)(e >> 32) & 0xffu; };
+    // even batches: eE, yE, cE, bE; odd batches: eO, yO, cO, bO -- each updated in place
     uint64_t eE = ld_entry(a), eO = ld_entry(a + kF64Batch);
     double yE = ld_y(a, eE), yO = ld_y(a + kF64Batch, eO);
+    uint32_t cE = cnt_of(eE), cO = cnt_of(eO);
     uint32_t bE[kF64Batch], bO[kF64Batch];
     // (the prologue's bins pass through an opaque xor, so the loop phi is not a widening
     // the compiler could fold to the top of the loop)
@@ -278,28 +294,32 @@ __device__ __forceinline__ void f64_hist_body(const F64HistArgs& A, const F64Nod
       eE = ld_entry(base + 2 * kF64Batch);
 #pragma unroll
       for (int j = 0; j < kF64Batch; j++) {
-        f64_add_entry<PART, W>(L, yE, bE[j], j, M1, lo1, M2, lo2, act);
+        f64_add_entry<PART, W>(L, yE, cE, bE[j], j, M1, lo1, M2, lo2, act);
         bO[j] = ld_bin(eO, j);
         __builtin_amdgcn_sched_barrier(0);  // keep each gather next to its entry
       }
       yE = ld_y(base + 2 * kF64Batch, eE);
+      cE = cnt_of(eE);
       // batch k + 1 (bO, yO): gather batch k + 2's bins, fetch batch k + 3's entries
       eO = ld_entry(base + 3 * kF64Batch);
 #pragma unroll
       for (int j = 0; j < kF64Batch; j++) {
-        f64_add_entry<PART, W>(L, yO, bO[j], j, M1, lo1, M2, lo2, act);
+        f64_add_entry<PART, W>(L, yO, cO, bO[j], j, M1, lo1, M2, lo2, act);
         bE[j] = ld_bin(eE, j);
         __builtin_amdgcn_sched_barrier(0);
       }
       yO = ld_y(base + 3 * kF64Batch, eO);
+      cO = cnt_of(eO);
       if (base + 2 * kF64Batch >= b) break;
     }
-    // the padding [b, base + 128) was counted in the last row's cells
+    // the padding [b, base + 128) repeated the last entry: its count went to the last
+    // row's cells once per padding entry (its sums added +0.0)
     const uint32_t pad = (uint32_t)(base + 2 * kF64Batch - b);
     if (PART != 2 && pad != 0u && act) {
-      const uint32_t bl = ld_row_bin((uint32_t)A.ent[last]);
-      __hip_atomic_fetch_sub((lds_u32*)(L + (__umul24(bl, M2) + lo2)), pad, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint64_t el = A.ent[last];
+      const uint32_t bl = ld_row_bin((uint32_t)el);
+      __hip_atomic_fetch_sub((lds_u32*)(L + (__umul24(bl, M2) + lo2)), pad * cnt_of(el),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   block_sync();

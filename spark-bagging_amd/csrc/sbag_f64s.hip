@@ -1,0 +1,490 @@
+// sbag_f64s.hip — the screened fp64 engine: bagging regression on arbitrary fp64 labels
+// without histogramming every feature in Spark's row order.
+//
+// Spark's DecisionTreeRegressor sums each (node, feature, bin) cell in fp64, row by row
+// (DTStatsAggregator.update; a row drawn c times is c consecutive rows,
+// sql/bfunctions.scala:42-44), so its gains depend on the summation order.  But only the
+// CHOSEN split's statistics reach the model (node impurity, gain, the children's
+// calculators); the other candidates matter only through the argmax.  So:
+//
+//   k_f64_screen   per node, every candidate's gain from the integer histograms of the
+//                  labels' fixed-point image k = round(y 2^s) (k_hist / k_hist_rl: exact
+//                  integer sums), with a rigorous bound on Spark's fp64 value: the
+//                  fixed-point error (|y - k 2^-s| <= eps), the summation error of the
+//                  row-order sums and Spark's rounding of the gain formula (host, dnode /
+//                  dpar).  The first max is Spark's when no other candidate's upper bound
+//                  reaches its lower bound and that lower bound is > 0 and >= minInfoGain;
+//                  otherwise the node is flagged and histogrammed exactly (k_f64_hist,
+//                  every feature in row order, then k_f64_split).
+//   k_fb_count / k_fb_scan / k_fb_scatter   for every decided node (and, at the root,
+//                  its first feature with splits, whose bins give Spark's parent stats):
+//                  a stable bucketing of the node's entries (row order) by the chosen
+//                  feature's bin into entK, fused with the stable two-way partition of
+//                  every split node into its children (left |= bin <= s), which keeps the
+//                  children's entries in row order for the next level
+//   k_fb_chain     one lane per (task, bin): the bucket's rows in row order, each label
+//                  added count times -- Spark's cell sums bit for bit
+//   k_fb_finish    binsToBestSplit over the chosen feature's exact bins (prefixes in bin
+//                  order, right = total - left, calculateImpurityStats with the node's
+//                  chained stats): the node's gain, impurity and children calculators
+//
+// Reference: ml/ensemble/ensembleParams.scala:113-115 (fitBaseLearner ->
+// DecisionTreeRegressor.train), ml/regression/BaggingRegressor.scala:146-150 (any Double
+// label); upstream RandomForest.findBestSplits / binsToBestSplit (Spark 2.4.3).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "sbag_internal.h"
+
+namespace sbag {
+
+namespace {
+constexpr double kU = 1.1102230246251565e-16;          // 2^-53, unit roundoff
+constexpr double kMinValueS = -1.7976931348623157e308;  // Double.MinValue
+
+__device__ __forceinline__ double var_imp(double count, double sum, double sumsq) {
+  if (count == 0) return 0.0;  // Variance.calculate
+  const double squared_loss = sumsq - (sum * sum) / count;
+  return squared_loss / count;
+}
+
+// block-wide exclusive scan of one int per thread (256 threads); block total in *total
+__device__ __forceinline__ int64_t scan256(int64_t v, int64_t* s_wave, int64_t* total) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int64_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  block_sync();
+  int64_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    if (w < wave) before += s_wave[w];
+    tot += s_wave[w];
+  }
+  block_sync();
+  *total = tot;
+  return before + incl - v;
+}
+}  // namespace
+
+// ---------------------------------------------------------------- screen
+// One candidate (lc, lsk) of a node (tc, tsk): the screened gain g = wL wR (muL - muR)^2
+// (the variance gain in exact arithmetic: Spark's sums of squares cancel) and a bound a on
+// |g - g*|, g* the exact-arithmetic gain of the true labels.  muL = lsk 2^-s / lc is within
+// eps of the true left mean; D = muL - muR within eD of the true difference, rounding
+// included; g = w D^2 within w ((|D| + eD)^2 - D^2) + 8u w (|D| + eD)^2.
+__device__ __forceinline__ void screen_cand(int64_t lc, int64_t lsk, int64_t tc, int64_t tsk, double n,
+                                            double is, double eps, double* g, double* a) {
+  const int64_t rc = tc - lc, rsk = tsk - lsk;
+  const double muL = (double)lsk * is / (double)lc;
+  const double muR = (double)rsk * is / (double)rc;
+  const double D = muL - muR;
+  const double w = ((double)lc / n) * ((double)rc / n);
+  *g = w * D * D;
+  const double eD = 2.0 * eps + 2.0 * kU * (fabs(muL) + fabs(muR) + fabs(D));
+  const double hiD = fabs(D) + eD;
+  *a = (w * (hiD * hiD - D * D) + 8.0 * kU * w * hiD * hiD) * 1.0001;
+}
+
+__global__ __launch_bounds__(256) void k_f64_screen(F64ScreenArgs A) {
+  const int slot = blockIdx.x, tid = threadIdx.x;
+  const int r = A.slot_r[slot];
+  const int Fr = A.Fr[r];
+  const int NB = A.NB;
+  const int64_t slot_words = (int64_t)A.Fmax * NB * 3;
+  __shared__ double s_g[256], s_a[256];
+  __shared__ int s_fl[256], s_s[256], s_cnt[256];
+  __shared__ int64_t s_tot[2];
+  const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
+  const uint64_t* hs = A.hist + (int64_t)slot * slot_words;
+  if (tid < 2) {  // the node's count and Σ c k (every feature's bins hold the same rows)
+    int64_t t = 0;
+    for (int b = 0; b < NB; b++) t += (int64_t)hs[(int64_t)b * 3 + tid];
+    s_tot[tid] = t;
+  }
+  block_sync();
+  const int64_t tc = s_tot[0], tsk = s_tot[1];
+  const double n = (double)tc, is = A.inv_scale, eps = A.eps;
+  // pass 1: first max of the screened gain (features in order, bins in order)
+  double fgb = -INFINITY, fab = 0.0;
+  int ffl = INT_MAX, fs = -1;
+  for (int fl = tid; fl < Fr; fl += 256) {
+    const int nsp = nb_r[fl] - 1;
+    const uint64_t* h = hs + (int64_t)fl * NB * 3;
+    int64_t lc = 0, lsk = 0;
+    for (int s = 0; s < nsp; s++) {
+      lc += (int64_t)h[s * 3];
+      lsk += (int64_t)h[s * 3 + 1];
+      if (lc < A.min_inst || tc - lc < A.min_inst) continue;  // invalid in Spark: MinValue
+      double g, a;
+      screen_cand(lc, lsk, tc, tsk, n, is, eps, &g, &a);
+      if (g > fgb) {
+        fgb = g;
+        fab = a;
+        ffl = fl;
+        fs = s;
+      }
+    }
+  }
+  s_g[tid] = fgb;
+  s_a[tid] = fab;
+  s_fl[tid] = ffl;
+  s_s[tid] = fs;
+  block_sync();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const double g2 = s_g[tid + o];
+      const int f2 = s_fl[tid + o];
+      if (g2 > s_g[tid] || (g2 == s_g[tid] && f2 < s_fl[tid])) {
+        s_g[tid] = g2;
+        s_a[tid] = s_a[tid + o];
+        s_fl[tid] = f2;
+        s_s[tid] = s_s[tid + o];
+      }
+    }
+    block_sync();
+  }
+  const double gb = s_g[0], ab = s_a[0];
+  const int bfl = s_fl[0], bs = s_s[0];
+  const double dn = A.dnode[slot], dp = A.dpar[slot];
+  block_sync();
+  // pass 2: candidates whose upper bound reaches the best's lower bound (the best too)
+  int cnt = 0;
+  if (bfl != INT_MAX) {
+    const double thr = gb - ab - 2.0 * dn;
+    for (int fl = tid; fl < Fr; fl += 256) {
+      const int nsp = nb_r[fl] - 1;
+      const uint64_t* h = hs + (int64_t)fl * NB * 3;
+      int64_t lc = 0, lsk = 0;
+      for (int s = 0; s < nsp; s++) {
+        lc += (int64_t)h[s * 3];
+        lsk += (int64_t)h[s * 3 + 1];
+        if (lc < A.min_inst || tc - lc < A.min_inst) continue;
+        double g, a;
+        screen_cand(lc, lsk, tc, tsk, n, is, eps, &g, &a);
+        if (!(g + a < thr)) cnt++;  // NaN counts as a contender
+      }
+    }
+  }
+  s_cnt[tid] = cnt;
+  block_sync();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) s_cnt[tid] += s_cnt[tid + o];
+    block_sync();
+  }
+  if (tid == 0) {
+    F64ScreenOut o{};
+    if (bfl == INT_MAX) {  // no count-valid candidate: decided exactly (leaf stats)
+      o.f = -1;
+      o.s = -1;
+      o.flag = 1;
+    } else {
+      // Spark's gain of the best lies in [gb - ab - dn - dp, ...]: a split (> 0) and
+      // valid (>= minInfoGain) for sure, and no other candidate can reach it
+      const double lo = gb - ab - dn - dp;
+      const bool certain = s_cnt[0] == 1 && lo > 0.0 && lo >= A.min_gain;
+      o.f = bfl;
+      o.s = bs;
+      o.flag = certain ? 0 : 1;
+      o.gain = gb;
+      o.margin = lo;
+    }
+    A.out[slot] = o;
+  }
+}
+
+void launch_f64_screen(hipStream_t st, const F64ScreenArgs& a, int M) {
+  hipLaunchKernelGGL(k_f64_screen, dim3(M), dim3(256), 0, st, a);
+}
+
+// ---------------------------------------------------------------- bucket + route
+__device__ __forceinline__ const uint8_t* task_col(const F64BucketArgs& A, const F64Task& t) {
+  return A.cols + (int64_t)t.r * A.cols_rstride + (int64_t)t.col * A.npad;
+}
+
+// per piece: entries per bin of the task's feature, entries going left (bin <= s)
+__global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
+  const F64TPiece pc = A.pieces[blockIdx.x];
+  const F64Task t = A.tasks[pc.task];
+  const int NB = A.NB, tid = threadIdx.x;
+  __shared__ uint32_t s_c[256];
+  __shared__ uint32_t s_l[4];
+  for (int b = tid; b < NB; b += 256) s_c[b] = 0u;
+  block_sync();
+  const uint8_t* col = task_col(A, t);
+  uint32_t nl = 0;
+  for (int64_t i = pc.a + tid; i < pc.b; i += 256) {
+    const uint32_t bin = col[(uint32_t)A.ent_in[i]];
+    atomicAdd(&s_c[bin], 1u);
+    nl += bin <= (uint32_t)t.s ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) nl += __shfl_down(nl, o);
+  if ((tid & 63) == 0) s_l[tid >> 6] = nl;
+  block_sync();
+  for (int b = tid; b < NB; b += 256) A.pcnt[(int64_t)blockIdx.x * NB + b] = s_c[b];
+  if (tid == 0) A.plcnt[blockIdx.x] = s_l[0] + s_l[1] + s_l[2] + s_l[3];
+}
+
+// per task: bucket bounds (bins in order, each bin's entries in row order), each piece's
+// first position per bin, left entries before each piece, the task's left total
+__global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
+  const int task = blockIdx.x, tid = threadIdx.x, NB = A.NB;
+  const F64Task t = A.tasks[task];
+  __shared__ int64_t s_start[257];
+  __shared__ int64_t s_wave[4];
+  if (t.kbase >= 0) {
+    int64_t tot = 0;
+    if (tid < NB)
+      for (int64_t p = t.piece0; p < t.piece1; p++) tot += A.pcnt[p * NB + tid];
+    int64_t all;
+    const int64_t ex = scan256(tid < NB ? tot : 0, s_wave, &all);
+    if (tid < NB) s_start[tid] = ex;
+    if (tid == 0) s_start[NB] = all;
+    block_sync();
+    int64_t* ko = A.kb_off + (int64_t)task * (NB + 1);
+    for (int b = tid; b <= NB; b += 256) ko[b] = t.kbase + s_start[b];
+    if (tid < NB) {
+      int64_t run = t.kbase + s_start[tid];
+      for (int64_t p = t.piece0; p < t.piece1; p++) {
+        A.pbase[p * NB + tid] = run;
+        run += A.pcnt[p * NB + tid];
+      }
+    }
+  }
+  if (t.part) {
+    int64_t carry = 0;
+    for (int64_t p0 = t.piece0; p0 < t.piece1; p0 += 256) {
+      const int64_t p = p0 + tid;
+      int64_t tot;
+      const int64_t ex = scan256(p < t.piece1 ? (int64_t)A.plcnt[p] : 0, s_wave, &tot);
+      if (p < t.piece1) A.plbase[p] = carry + ex;
+      carry += tot;
+    }
+    if (tid == 0) A.nleft[task] = carry;
+  }
+}
+
+// one wave per piece: every entry to its bucket (stable: rank among the round's entries of
+// the same bin, from ballots over the bin's bits) and, for split nodes, to its child
+// (left from the segment start, right after the left block, both in row order)
+__global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t pi = (int64_t)blockIdx.x * 4 + wv;
+  __shared__ int64_t s_base[4][256];
+  if (pi >= npieces) return;  // whole waves only; no block-wide barrier below
+  const F64TPiece pc = A.pieces[pi];
+  const F64Task t = A.tasks[pc.task];
+  const int NB = A.NB;
+  const bool chain = t.kbase >= 0;
+  int64_t* sb = s_base[wv];
+  if (chain)
+    for (int b = lane; b < NB; b += 64) sb[b] = A.pbase[pi * NB + b];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int64_t lrun = t.part ? A.plbase[pi] : 0;
+  const int64_t nl = t.part ? A.nleft[pc.task] : 0;
+  const uint8_t* col = task_col(A, t);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t i0 = pc.a; i0 < pc.b; i0 += 64) {
+    const int64_t i = i0 + lane;
+    const bool valid = i < pc.b;
+    const uint64_t e = valid ? A.ent_in[i] : 0ull;
+    const uint32_t bin = valid ? (uint32_t)col[(uint32_t)e] : 0u;
+    if (chain) {
+      uint64_t eq = __ballot(valid);
+      for (int k = 0; k < nbits; k++) {
+        const bool bit = (bin >> k) & 1u;
+        const uint64_t m = __ballot(bit);
+        eq &= bit ? m : ~m;
+      }
+      const int rank = __popcll(eq & lt), cnt = __popcll(eq);
+      const int64_t base = valid ? sb[bin] : 0;
+      if (valid) A.entK[base + rank] = e;
+      if (valid && rank == cnt - 1) sb[bin] = base + cnt;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (t.part) {
+      const bool left = valid && bin <= (uint32_t)t.s;
+      const uint64_t lm = __ballot(left);
+      const int64_t lr = __popcll(lm & lt);
+      if (valid) {
+        const int64_t pos = left ? t.a + lrun + lr : t.a + nl + (i - t.a - lrun - lr);
+        A.ent_out[pos] = e;
+      }
+      lrun += __popcll(lm);
+    }
+  }
+}
+
+// one lane per (task, bin): Spark's row-order fp64 sums of the bucket
+__global__ __launch_bounds__(256) void k_fb_chain(F64BucketArgs A, int nchain) {
+  const int NB = A.NB;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (int64_t)nchain * NB) return;
+  const int64_t task = g / NB;
+  const int b = (int)(g - task * NB);
+  const int64_t* ko = A.kb_off + task * (NB + 1);
+  const int64_t lo = ko[b], hi = ko[b + 1];
+  double s1 = 0.0, s2 = 0.0;
+  uint64_t cnt = 0;
+  int64_t i = lo;
+  constexpr int U = 8;
+  for (; i + U <= hi; i += U) {
+    uint64_t e[U];
+    double yv[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) e[j] = A.entK[i + j];
+#pragma unroll
+    for (int j = 0; j < U; j++) yv[j] = A.y[(uint32_t)e[j]];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+      const uint32_t c = (uint32_t)(e[j] >> 32) & 0xffu;
+      const double w = 1.0 * yv[j];   // instanceWeight * label
+      const double wy = w * yv[j];    // instanceWeight * label * label
+      for (uint32_t k = 0; k < c; k++) {
+        s1 += w;
+        s2 += wy;
+      }
+      cnt += c;
+    }
+  }
+  for (; i < hi; i++) {
+    const uint64_t e = A.entK[i];
+    const double yv = A.y[(uint32_t)e];
+    const uint32_t c = (uint32_t)(e >> 32) & 0xffu;
+    const double w = 1.0 * yv, wy = w * yv;
+    for (uint32_t k = 0; k < c; k++) {
+      s1 += w;
+      s2 += wy;
+    }
+    cnt += c;
+  }
+  double* o = A.chist + g * 3;
+  o[0] = (double)cnt;
+  o[1] = s1;
+  o[2] = s2;
+}
+
+void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain) {
+  if (npieces <= 0) return;
+  int nbits = 0;
+  while ((1 << nbits) < a.NB) nbits++;
+  hipLaunchKernelGGL(k_fb_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)a.ntasks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_fb_scatter, dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a, npieces,
+                     nbits);
+  const int64_t lanes = (int64_t)nchain * a.NB;
+  if (lanes > 0)
+    hipLaunchKernelGGL(k_fb_chain, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a, nchain);
+}
+
+// ---------------------------------------------------------------- finish
+// RandomForest.binsToBestSplit on the chosen feature's exact bins, in Spark's operation order
+// (as k_f64_split): the parent stats chained from the node (or, at the root, the first
+// feature with splits: its first candidate's left + right), the prefixes in bin order,
+// right = total - left, the first max over the feature's splits.
+__global__ __launch_bounds__(64) void k_fb_finish(F64FinishArgs A) {
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= A.n) return;
+  const F64FinishNode nd = A.nodes[q];
+  const int NB = A.NB;
+  double pc0 = nd.ch.calc[0], pc1 = nd.ch.calc[1], pc2 = nd.ch.calc[2], pimp = nd.ch.impurity;
+  if (!nd.ch.set) {
+    const double* fa = A.chist + (int64_t)nd.t0 * NB * 3;
+    double t0 = 0, t1 = 0, t2 = 0;
+    for (int s = 0; s <= nd.nsp0; s++) {
+      if (s == 0) {
+        t0 = fa[0];
+        t1 = fa[1];
+        t2 = fa[2];
+      } else {
+        t0 += fa[3 * s];
+        t1 += fa[3 * s + 1];
+        t2 += fa[3 * s + 2];
+      }
+    }
+    const double l0 = fa[0], l1 = fa[1], l2 = fa[2];
+    const double r0 = t0 - l0, r1 = t1 - l1, r2 = t2 - l2;
+    pc0 = l0 + r0;
+    pc1 = l1 + r1;
+    pc2 = l2 + r2;
+    pimp = var_imp(pc0, pc1, pc2);
+  }
+  const double* fa = A.chist + (int64_t)nd.t * NB * 3;
+  const int nsp = nd.nsp;
+  double t0 = fa[0], t1 = fa[1], t2 = fa[2];
+  for (int s = 1; s <= nsp; s++) {
+    t0 += fa[3 * s];
+    t1 += fa[3 * s + 1];
+    t2 += fa[3 * s + 2];
+  }
+  double c0 = 0, c1 = 0, c2 = 0, fg = 0.0, bl[3] = {0, 0, 0};
+  int fs = -1, fv = 0;
+  for (int s = 0; s < nsp; s++) {
+    if (s == 0) {
+      c0 = fa[0];
+      c1 = fa[1];
+      c2 = fa[2];
+    } else {
+      c0 += fa[3 * s];
+      c1 += fa[3 * s + 1];
+      c2 += fa[3 * s + 2];
+    }
+    const double r0 = t0 - c0, r1 = t1 - c1, r2 = t2 - c2;
+    const int64_t lc = (int64_t)c0, rc = (int64_t)r0;
+    double gain;
+    int valid;
+    if (lc < A.min_inst || rc < A.min_inst) {
+      gain = kMinValueS;
+      valid = 0;
+    } else {
+      const int64_t total = lc + rc;
+      const double li = var_imp(c0, c1, c2), ri = var_imp(r0, r1, r2);
+      const double lw = (double)lc / (double)total, rw = (double)rc / (double)total;
+      gain = pimp - lw * li - rw * ri;
+      valid = 1;
+      if (gain < A.min_gain) {
+        gain = kMinValueS;
+        valid = 0;
+      }
+    }
+    if (fs < 0 || gain > fg) {
+      fg = gain;
+      fs = s;
+      fv = valid;
+      bl[0] = c0;
+      bl[1] = c1;
+      bl[2] = c2;
+    }
+  }
+  F64SplitOut o{};
+  o.f = nd.f;
+  o.s = fs;
+  o.gain = fg;
+  o.impurity = pimp;
+  o.valid = fv;
+  o.calc[0] = pc0;
+  o.calc[1] = pc1;
+  o.calc[2] = pc2;
+  for (int k = 0; k < 3; k++) o.left[k] = bl[k];
+  o.right[0] = t0 - bl[0];
+  o.right[1] = t1 - bl[1];
+  o.right[2] = t2 - bl[2];
+  A.out[q] = o;
+}
+
+void launch_fb_finish(hipStream_t st, const F64FinishArgs& a) {
+  if (a.n <= 0) return;
+  hipLaunchKernelGGL(k_fb_finish, dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, st, a);
+}
+
+}  // namespace sbag

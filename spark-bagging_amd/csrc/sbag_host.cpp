@@ -333,6 +333,13 @@ struct sbag_dataset {
   int shift = 0;
   bool label_ok = false;                  // representable as |k| < 2^23
   int64_t kmin = 0, kmax = 0;
+  // labels that are not dyadic (fp64 path): the fixed-point image k = round(y 2^ashift),
+  // |k| <= 2^22, which the integer histograms screen splits with (|y - k 2^-ashift| <=
+  // 2^-ashift-1), and the labels' largest |y| and y*y (the screen's error bounds)
+  bool approx_ok = false;
+  int ashift = 0;
+  int64_t akmin = 0, akmax = 0;
+  double ymax_abs = 0.0, ymax_sq = 0.0;
   bool integral = false;                  // all labels integers >= 0 (classifiable)
   double* d_dict = nullptr;
   int64_t* d_dict_off = nullptr;
@@ -397,16 +404,46 @@ static void analyze_labels(sbag_dataset* ds) {
       ds->kmax = mx;
     }
   }
+  ds->approx_ok = false;
+  ds->ymax_abs = ds->ymax_sq = 0.0;
+  bool finite = true;
+  for (double v : ds->y) {
+    if (!std::isfinite(v)) {
+      finite = false;
+      break;
+    }
+    ds->ymax_abs = std::max(ds->ymax_abs, std::fabs(v));
+    ds->ymax_sq = std::max(ds->ymax_sq, v * v);
+  }
+  if (!ds->label_ok && finite && ds->ymax_abs > 0.0) {
+    // 2^e <= max|y| < 2^(e+1): max|y| 2^(21-e) < 2^22
+    ds->ashift = 21 - std::ilogb(ds->ymax_abs);
+    int64_t mn = 0, mx = 0;
+    for (double v : ds->y) {
+      const int64_t k = (int64_t)std::nearbyint(std::ldexp(v, ds->ashift));
+      mn = std::min(mn, k);
+      mx = std::max(mx, k);
+    }
+    ds->akmin = mn;
+    ds->akmax = mx;
+    ds->approx_ok = true;
+  }
 }
 
+// the labels' fixed point image on the device: exact (dyadic labels) or the screening
+// approximation of the fp64 path (zeros when neither applies)
 static int upload_labels(sbag_dataset* ds) {
-  sbag_ctx* c = ds->ctx;
   HIP_TRY(hipMalloc(&ds->d_labk, std::max<int64_t>(ds->N, 1) * 4));
-  if (!ds->label_ok) return SBAG_OK;
+  if (!ds->label_ok && !ds->approx_ok) {
+    HIP_TRY(hipMemset(ds->d_labk, 0, (size_t)std::max<int64_t>(ds->N, 1) * 4));
+    return SBAG_OK;
+  }
   std::vector<int32_t> k(ds->N);
-  for (int64_t i = 0; i < ds->N; i++) k[i] = (int32_t)std::ldexp(ds->y[i], ds->shift);
+  if (ds->label_ok)
+    for (int64_t i = 0; i < ds->N; i++) k[i] = (int32_t)std::ldexp(ds->y[i], ds->shift);
+  else
+    for (int64_t i = 0; i < ds->N; i++) k[i] = (int32_t)std::nearbyint(std::ldexp(ds->y[i], ds->ashift));
   HIP_TRY(hipMemcpy(ds->d_labk, k.data(), ds->N * 4, hipMemcpyHostToDevice));
-  (void)c;
   return SBAG_OK;
 }
 
@@ -678,7 +715,7 @@ struct EventTimer {
     }
   }
 };
-enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_FIX, T_GROUP, T_NCAT };
+enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_FIX, T_GROUP, T_CHAIN, T_NCAT };
 
 // ---------------------------------------------------------------- C ABI
 extern "C" {
@@ -1053,6 +1090,8 @@ int sbag_dataset_synthetic(sbag_ctx* c, int64_t N, int32_t F, uint64_t seed, int
     ds->y[i] = std::ldexp((double)k[i], -ds->shift);
     ds->kmin = std::min<int64_t>(ds->kmin, k[i]);
     ds->kmax = std::max<int64_t>(ds->kmax, k[i]);
+    ds->ymax_abs = std::max(ds->ymax_abs, std::fabs(ds->y[i]));
+    ds->ymax_sq = std::max(ds->ymax_sq, ds->y[i] * ds->y[i]);
   }
   ds->label_ok = true;
   ds->integral = ds->kmin >= 0 && num_classes > 0;
@@ -1093,7 +1132,6 @@ int sbag_dataset_set_labels(sbag_dataset* ds, const double* y) {
   if (ds->d_labk) HIP_TRY(hipFree(ds->d_labk));
   ds->d_labk = nullptr;
   TRY(upload_labels(ds));
-  if (!ds->label_ok) HIP_TRY(hipMemset(ds->d_labk, 0, (size_t)std::max<int64_t>(ds->N, 1) * 4));
   if (ds->d_y64) HIP_TRY(hipFree(ds->d_y64));
   ds->d_y64 = nullptr;
   return SBAG_OK;
@@ -1608,12 +1646,22 @@ BtRet bt_emit(const std::vector<BtNode>& nodes, int idx, HTree& t) {
 
 }  // namespace
 
-// fp64 labels: level-wise growth whose histograms are Spark's row-order fp64 sums
-// (sbag_f64.hip).  Every node is histogrammed from its own rows (the reference builds
-// both children's aggregates; a sibling by subtraction would round differently), split
-// search runs on the device in binsToBestSplit's order, and a stable partition keeps
-// each child's entries in row order for the next level.
-struct F64Grow {
+// fp64 labels (sbag_f64s.hip): level-wise growth whose node statistics are
+// Spark's row-order fp64 sums.  Every level:
+//   1. k_f64_screen picks each node's split from the integer histograms of the labels'
+//      fixed-point image (built like the dyadic engine's: smaller child + subtraction)
+//      when a rigorous bound proves it is binsToBestSplit's choice; other nodes are
+//      flagged and histogrammed exactly (k_f64_hist over every feature in row order, then
+//      k_f64_split);
+//   2. k_fb_* buckets every decided node's entries by the chosen feature's bin (at the root
+//      also by the first feature with splits, whose bins give Spark's parent stats), sums
+//      each bucket in row order, and routes every split node's entries stably into its
+//      children (their entries stay in row order);
+//   3. k_fb_finish evaluates the chosen feature exactly: gain, impurity, children stats.
+// Error bounds (host, per node): Spark's sums of n terms carry at most gamma_K sum|term|,
+// K = n + NB + 2 additions per term, gamma_K = K u / (1 - K u); a right child's stats
+// (total - left) carry the parent's total's error.  See DESIGN §4.7 for the derivation.
+struct F64sGrow {
   sbag_ctx* c;
   sbag_dataset* ds;
   const sbag_tree_params& tp;
@@ -1621,7 +1669,7 @@ struct F64Grow {
   int64_t N;
   int Fmax, NB, S;
   const std::vector<int32_t>& h_Fr;
-  const std::vector<std::vector<int32_t>>& sub;
+  const std::vector<int32_t>& h_nbins;
   const std::vector<std::vector<double>>& thr;  // [R * Fmax]
   const uint8_t* d_bins;
   int64_t bins_rstride;
@@ -1634,134 +1682,352 @@ struct F64Grow {
   uint64_t* entA;
   uint64_t* entB;
   int64_t cap;
-  const std::vector<unsigned long long>& inbag;
+  const std::vector<unsigned long long>& inbag;  // [4R]: entries, Σ count, max count, -
   EventTimer& tm;
-  int64_t hist_launches = 0;
-  double hist_entries = 0, hist_alg_bytes = 0;
+  void* hist_root;        // level-0 integer histograms, slot = replica
+  int64_t slot_words;     // Fmax * NB * 3
+  double inv_scale, eps;  // the labels' fixed-point image: k 2^-s, |y - k 2^-s| <= eps
+  // integer (count, Σ c k) histograms of node segments of `ent` into slots of `hist`
+  std::function<int(const std::vector<std::pair<int64_t, int64_t>>&, const std::vector<ParentInfo>&,
+                    const uint64_t*, void*)> int_hist;
+  // SURVEY §8d work bytes of a level's node segments
+  std::function<void(const std::vector<std::pair<int64_t, int64_t>>&, const std::vector<int>&)> add_work;
+  int64_t fallbacks = 0;
   int levels = 0;
 };
 
-static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
+static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   sbag_ctx* c = G.c;
   const int R = G.R, Fmax = G.Fmax, NB = G.NB, D = G.tp.max_depth;
-  // the labels on the device, once per dataset
+  const int64_t cap = G.cap;
+  // the labels on the device, once per dataset, published only when complete (+ one +0.0
+  // at index N: the label of k_f64_hist's padding entries)
   {
     std::lock_guard<std::mutex> lk(G.ds->layout_mu);
     if (!G.ds->d_y64) {
-      // + one +0.0 at index N: the label of the histogram walk's padding entries
-      HIP_TRY(hipMalloc(&G.ds->d_y64, (size_t)(G.N + 1) * 8));
-      HIP_TRY(hipMemcpy(G.ds->d_y64, G.ds->y.data(), (size_t)G.N * 8, hipMemcpyHostToDevice));
-      HIP_TRY(hipMemset(G.ds->d_y64 + G.N, 0, 8));
+      double* p = nullptr;
+      HIP_TRY(hipMalloc(&p, (size_t)(G.N + 1) * 8));
+      if (hipMemcpy(p, G.ds->y.data(), (size_t)G.N * 8, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemset(p + G.N, 0, 8) != hipSuccess) {
+        (void)hipFree(p);
+        return fail(SBAG_EDEVICE, "labels could not be copied to the device");
+      }
+      G.ds->d_y64 = p;
     }
   }
+  const double u = std::ldexp(1.0, -53);
+  const double M1 = G.ds->ymax_abs, M2 = G.ds->ymax_sq, Msq = std::max(M2, M1 * M1);
+  // gamma_K of a node of n draws (inf when K u >= 1: every screen then flags)
+  auto gam = [&](double n) {
+    const double k = (n + NB + 2.0) * u;
+    return k < 0.5 ? k / (1.0 - k) : INFINITY;
+  };
   struct LNode {
     int r, node;
     int64_t a, b;
+    double n, e1, e2;  // draws; error bounds of the node's calculator sums (sum, sumSq)
   };
   trees.assign(R, {});
   std::vector<LNode> cur;
   for (int r = 0; r < R; r++) {
     trees[r].push_back(BtNode{});
-    cur.push_back(LNode{r, 0, (int64_t)r * G.cap, (int64_t)r * G.cap + (int64_t)G.inbag[r]});
+    const double n = (double)G.inbag[R + r];
+    // root: Spark's parent stats l0 + (total - l0) of the first feature with splits
+    const double e = (2.0 * gam(n) + 4.0 * u) * 1.01 * n;
+    cur.push_back(LNode{r, 0, (int64_t)r * cap, (int64_t)r * cap + (int64_t)G.inbag[r], n, e * M1, e * M2});
   }
+  std::vector<int> f0(R, -1);  // first local feature with splits
+  for (int r = 0; r < R; r++)
+    for (int fl = 0; fl < G.h_Fr[r]; fl++)
+      if (G.h_nbins[(size_t)r * Fmax + fl] > 1) {
+        f0[r] = fl;
+        break;
+      }
+  // SBAG_F64_SCREEN=0: every node takes the exact path (the unscreened engine, for A/B and
+  // the parity tests)
+  const bool screen_on = !getenv("SBAG_F64_SCREEN") || atoi(getenv("SBAG_F64_SCREEN")) != 0;
+  void* hist_cur = G.hist_root;
+  std::string hist_cur_name = "histA", hist_nxt_name = "histB";
   uint64_t* ent_cur = G.entA;
   uint64_t* ent_nxt = G.entB;
   const size_t node_words = (size_t)(Fmax + 1) * NB * 3;
-  // nodes per histogram batch: the level's fp64 histograms within 4 GB
   const int64_t batch = std::max<int64_t>(1, ((int64_t)4 << 30) / (int64_t)(node_words * 8));
   for (int level = 0; level <= D && !cur.empty(); level++) {
     G.levels++;
     G.tm.level = level;
-    const int A = (int)cur.size();
-    // features per wave (SBAG_F64_FPW, default 64).  Narrower groups give the shallow
-    // levels more waves but multiply the LDS atomic instructions: FPW down to 8 at < 2048
-    // waves made the C3-shape fit 1.7x slower (gpurun_out/r03c).
-    const int fpw_env = getenv("SBAG_F64_FPW") ? atoi(getenv("SBAG_F64_FPW")) : 64;
-    const int FPW = std::max(1, std::min(f64_hist_width(NB), fpw_env));
-    const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
-    // levels with fewer waves than SIMDs split each (node, group) walk over two waves
-    // (count + sum, sumSq): the walk is the level's critical path there
-    const int split_below = getenv("SBAG_F64_SPLIT") ? atoi(getenv("SBAG_F64_SPLIT")) : 1024;
-    const int parts = (int64_t)A * ngroups < split_below ? 2 : 1;
-    std::vector<F64Node> hn(A);
-    std::vector<F64Chain> chain(A);
-    for (int q = 0; q < A; q++) {
-      hn[q] = F64Node{cur[q].a, cur[q].b, cur[q].r, 0};
-      const BtNode& n = trees[cur[q].r][cur[q].node];
-      F64Chain ch{};
-      if (level > 0) {
-        for (int i = 0; i < 3; i++) ch.calc[i] = n.calc[i];
-        ch.impurity = n.impurity;
-        ch.set = 1;
+    const int M = (int)cur.size();
+    // ---- 1. screen (level D only happens for maxDepth 0: the root's stats, exactly)
+    std::vector<F64ScreenOut> so(M);
+    for (auto& o : so) o.flag = 1;
+    if (screen_on && level < D) {
+      std::vector<int32_t> h_slot_r(M);
+      std::vector<double> hdn(M), hdp(M);
+      for (int i = 0; i < M; i++) {
+        h_slot_r[i] = cur[i].r;
+        const double n = cur[i].n, g = gam(n);
+        hdn[i] = (7.0 * g + 30.0 * u + 4.0 * (g + u) * (g + u) * n) * Msq * 1.01;
+        hdp[i] = (cur[i].e2 / n + cur[i].e1 * (2.0 * n * M1 + cur[i].e1) / (n * n) + 8.0 * u * Msq) * 1.01;
       }
-      chain[q] = ch;
-      G.hist_entries += (double)(cur[q].b - cur[q].a);
-      G.hist_alg_bytes += (double)(cur[q].b - cur[q].a) * (G.h_Fr[cur[q].r] + 8 + 8);
-    }
-    F64Node* d_nodes;
-    F64Chain* d_chain;
-    F64SplitOut* d_out;
-    double* d_hist;
-    TRY(ws_typed(c, "f64_nodes", (size_t)A, &d_nodes));
-    TRY(ws_typed(c, "f64_chain", (size_t)A, &d_chain));
-    TRY(ws_typed(c, "f64_sout", (size_t)A, &d_out));
-    TRY(ws_typed(c, "f64_hist", (size_t)std::min<int64_t>(A, batch) * node_words, &d_hist));
-    TRY(h2d(c, d_nodes, hn.data(), (size_t)A));
-    TRY(h2d(c, d_chain, chain.data(), (size_t)A));
-    for (int64_t q0 = 0; q0 < A; q0 += batch) {
-      const int nq = (int)std::min<int64_t>(batch, A - q0);
-      F64HistArgs ha{};
-      ha.ent = ent_cur;
-      ha.nodes = d_nodes + q0;
-      ha.y = G.ds->d_y64;
-      ha.bins = G.d_bins;
-      ha.bins_rstride = G.bins_rstride;
-      ha.S = G.S;
-      ha.Fmax = Fmax;
-      ha.pos = G.d_pos;
-      ha.Fr = G.d_Fr;
-      ha.NB = NB;
-      ha.FPW = FPW;
-      ha.parts = parts;
-      ha.bins_bytes = (double)G.N * G.S < 4294967295.0 ? (uint32_t)(G.N * G.S) : 0u;
-      ha.yzero = (uint32_t)G.N;
-      ha.hist = d_hist;
-      int h = G.tm.begin(T_HIST);
-      launch_f64_hist(c->stream, ha, nq, ngroups);
-      HIP_TRY(hipGetLastError());
-      G.tm.end(h);
-      G.hist_launches++;
-      F64SplitArgs sa{};
-      sa.hist = d_hist;
-      sa.nodes = d_nodes + q0;
-      sa.chain = d_chain + q0;
+      int32_t* d_slot_r;
+      double *d_dn, *d_dp;
+      F64ScreenOut* d_so;
+      TRY(ws_typed(c, "slot_r", (size_t)M, &d_slot_r));
+      TRY(ws_typed(c, "f64_dn", (size_t)M, &d_dn));
+      TRY(ws_typed(c, "f64_dp", (size_t)M, &d_dp));
+      TRY(ws_typed(c, "f64_so", (size_t)M, &d_so));
+      TRY(h2d(c, d_slot_r, h_slot_r.data(), (size_t)M));
+      TRY(h2d(c, d_dn, hdn.data(), (size_t)M));
+      TRY(h2d(c, d_dp, hdp.data(), (size_t)M));
+      F64ScreenArgs sa{};
+      sa.hist = (const uint64_t*)hist_cur;
+      sa.slot_r = d_slot_r;
       sa.Fr = G.d_Fr;
       sa.nbins = G.d_nbins;
       sa.Fmax = Fmax;
       sa.NB = NB;
       sa.min_inst = G.tp.min_instances_per_node;
       sa.min_gain = G.tp.min_info_gain;
-      sa.out = d_out + q0;
-      h = G.tm.begin(T_SPLIT);
-      launch_f64_split(c->stream, sa, nq);
+      sa.inv_scale = G.inv_scale;
+      sa.eps = G.eps;
+      sa.dnode = d_dn;
+      sa.dpar = d_dp;
+      sa.out = d_so;
+      int h = G.tm.begin(T_SPLIT);
+      launch_f64_screen(c->stream, sa, M);
       HIP_TRY(hipGetLastError());
       G.tm.end(h);
+      TRY(d2h(c, so.data(), d_so, (size_t)M));
     }
-    std::vector<F64SplitOut> so(A);
-    TRY(d2h(c, so.data(), d_out, (size_t)A));
-    // node updates (RandomForest.findBestSplits, host part)
-    struct Split {
-      int q, li;
+    // ---- exact fallback: flagged nodes, every feature summed in row order
+    std::vector<int> X, xi(M, -1);
+    for (int i = 0; i < M; i++)
+      if (so[i].flag) {
+        xi[i] = (int)X.size();
+        X.push_back(i);
+      }
+    G.fallbacks += (int64_t)X.size();
+    std::vector<F64SplitOut> xo(X.size());
+    if (!X.empty()) {
+      const int A = (int)X.size();
+      const int fpw_env = getenv("SBAG_F64_FPW") ? atoi(getenv("SBAG_F64_FPW")) : 64;
+      const int FPW = std::max(1, std::min(f64_hist_width(NB), fpw_env));
+      const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
+      const int split_below = getenv("SBAG_F64_SPLIT") ? atoi(getenv("SBAG_F64_SPLIT")) : 1024;
+      const int parts = (int64_t)A * ngroups < split_below ? 2 : 1;
+      std::vector<F64Node> hn(A);
+      std::vector<F64Chain> chain(A);
+      for (int k = 0; k < A; k++) {
+        const LNode& q = cur[X[k]];
+        hn[k] = F64Node{q.a, q.b, q.r, 0};
+        const BtNode& n = trees[q.r][q.node];
+        F64Chain ch{};
+        if (level > 0) {
+          for (int j = 0; j < 3; j++) ch.calc[j] = n.calc[j];
+          ch.impurity = n.impurity;
+          ch.set = 1;
+        }
+        chain[k] = ch;
+      }
+      F64Node* d_nodes;
+      F64Chain* d_chain;
+      F64SplitOut* d_out;
+      double* d_hist;
+      TRY(ws_typed(c, "f64_nodes", (size_t)A, &d_nodes));
+      TRY(ws_typed(c, "f64_chain", (size_t)A, &d_chain));
+      TRY(ws_typed(c, "f64_sout", (size_t)A, &d_out));
+      TRY(ws_typed(c, "f64_hist", (size_t)std::min<int64_t>(A, batch) * node_words, &d_hist));
+      TRY(h2d(c, d_nodes, hn.data(), (size_t)A));
+      TRY(h2d(c, d_chain, chain.data(), (size_t)A));
+      for (int64_t q0 = 0; q0 < A; q0 += batch) {
+        const int nq = (int)std::min<int64_t>(batch, A - q0);
+        F64HistArgs ha{};
+        ha.ent = ent_cur;
+        ha.nodes = d_nodes + q0;
+        ha.y = G.ds->d_y64;
+        ha.bins = G.d_bins;
+        ha.bins_rstride = G.bins_rstride;
+        ha.S = G.S;
+        ha.Fmax = Fmax;
+        ha.pos = G.d_pos;
+        ha.Fr = G.d_Fr;
+        ha.NB = NB;
+        ha.FPW = FPW;
+        ha.parts = parts;
+        ha.bins_bytes = (double)G.N * G.S < 4294967295.0 ? (uint32_t)(G.N * G.S) : 0u;
+        ha.yzero = (uint32_t)G.N;
+        ha.hist = d_hist;
+        int h = G.tm.begin(T_FIX);
+        launch_f64_hist(c->stream, ha, nq, ngroups);
+        HIP_TRY(hipGetLastError());
+        F64SplitArgs sa{};
+        sa.hist = d_hist;
+        sa.nodes = d_nodes + q0;
+        sa.chain = d_chain + q0;
+        sa.Fr = G.d_Fr;
+        sa.nbins = G.d_nbins;
+        sa.Fmax = Fmax;
+        sa.NB = NB;
+        sa.min_inst = G.tp.min_instances_per_node;
+        sa.min_gain = G.tp.min_info_gain;
+        sa.out = d_out + q0;
+        launch_f64_split(c->stream, sa, nq);
+        HIP_TRY(hipGetLastError());
+        G.tm.end(h);
+      }
+      TRY(d2h(c, xo.data(), d_out, (size_t)A));
+    }
+    // ---- 2. bucket + route tasks.  Pass 0: the decided nodes' chosen features (buckets and
+    // routing), then the flagged split nodes (routing only); pass 1 (root only): the first
+    // feature with splits where it is not the chosen one (buckets only)
+    std::vector<F64Task> tasks[2];
+    std::vector<F64FinishNode> fin;
+    std::vector<int> part_task(M, -1), fin_of(M, -1);
+    int64_t kb[2] = {0, 0};
+    auto add_task = [&](int pass, const LNode& q, int fl, int s, bool part, bool chain) {
+      F64Task t{};
+      t.a = q.a;
+      t.b = q.b;
+      t.kbase = chain ? kb[pass] : -1;
+      if (chain) kb[pass] += q.b - q.a;
+      t.r = q.r;
+      t.col = G.h_pos[(size_t)q.r * Fmax + fl];
+      t.s = s;
+      t.part = part ? 1 : 0;
+      tasks[pass].push_back(t);
+      return (int)tasks[pass].size() - 1;
     };
-    std::vector<Split> splits;
-    std::vector<F64PartNode> pn;
-    std::vector<F64PartPiece> pieces;
-    for (int q = 0; q < A; q++) {
-      const int r = cur[q].r;
-      const F64SplitOut& o = so[q];
+    for (int i = 0; i < M; i++) {
+      if (so[i].flag) continue;
+      const LNode& q = cur[i];
+      const int f = so[i].f, s = so[i].s;
+      F64FinishNode fn{};
+      // (children at maxDepth are leaves: nothing to route at the last split level)
+      fn.t = add_task(0, q, f, s, level + 1 < D, true);
+      part_task[i] = fn.t;
+      fn.f = f;
+      fn.s = s;
+      fn.nsp = G.h_nbins[(size_t)q.r * Fmax + f] - 1;
+      fn.t0 = -1;
+      if (level == 0) {
+        fn.ch.set = 0;
+        fn.nsp0 = G.h_nbins[(size_t)q.r * Fmax + f0[q.r]] - 1;
+        fn.t0 = f0[q.r] == f ? fn.t : -2 - add_task(1, q, f0[q.r], -1, false, true);  // pass 1: fixed below
+      } else {
+        const BtNode& n = trees[q.r][q.node];
+        for (int j = 0; j < 3; j++) fn.ch.calc[j] = n.calc[j];
+        fn.ch.impurity = n.impurity;
+        fn.ch.set = 1;
+      }
+      fin_of[i] = (int)fin.size();
+      fin.push_back(fn);
+    }
+    const int nchain0 = (int)tasks[0].size();
+    for (int k = 0; k < (int)X.size(); k++) {  // flagged split nodes: routing only
+      const int i = X[k];
+      const F64SplitOut& o = xo[k];
+      if (o.gain <= 0 || level == D || o.f < 0) continue;
+      const double li = bt_impurity(o.left), ri = bt_impurity(o.right);
+      const bool child_leaf = (level + 1) == D;
+      if ((child_leaf || li == 0.0) && (child_leaf || ri == 0.0)) continue;
+      part_task[i] = add_task(0, cur[i], o.f, o.s, true, false);
+    }
+    for (F64FinishNode& fn : fin)
+      if (fn.t0 <= -2) fn.t0 = nchain0 + (-2 - fn.t0);  // pass-1 chain sums follow pass 0's
+    const int nchain1 = (int)tasks[1].size();
+    std::vector<F64SplitOut> fo(fin.size());
+    std::vector<int64_t> nleft(tasks[0].size(), 0);
+    if (!tasks[0].empty()) {
+      double* d_chist;
+      TRY(ws_typed(c, "fb_chist", (size_t)std::max(1, nchain0 + nchain1) * NB * 3, &d_chist));
+      uint64_t* d_entK;
+      TRY(ws_typed(c, "fb_entK", (size_t)std::max<int64_t>(1, std::max(kb[0], kb[1])), &d_entK));
+      int h = G.tm.begin(T_CHAIN);
+      for (int pass = 0; pass < 2; pass++) {
+        std::vector<F64Task>& tk = tasks[pass];
+        if (tk.empty()) continue;
+        std::vector<F64TPiece> pcs;
+        for (size_t ti = 0; ti < tk.size(); ti++) {
+          tk[ti].piece0 = (int64_t)pcs.size();
+          for (int64_t x = tk[ti].a; x < tk[ti].b; x += kFbPiece)
+            pcs.push_back(F64TPiece{x, std::min(x + kFbPiece, tk[ti].b), (int32_t)ti, 0});
+          tk[ti].piece1 = (int64_t)pcs.size();
+        }
+        const int64_t np = (int64_t)pcs.size();
+        const int nt = (int)tk.size();
+        F64Task* d_tk;
+        F64TPiece* d_pc;
+        uint32_t *d_pcnt, *d_plcnt;
+        int64_t *d_pbase, *d_plbase, *d_nleft, *d_kboff;
+        TRY(ws_typed(c, "fb_tasks", (size_t)nt, &d_tk));
+        TRY(ws_typed(c, "fb_pieces", (size_t)std::max<int64_t>(np, 1), &d_pc));
+        TRY(ws_typed(c, "fb_pcnt", (size_t)std::max<int64_t>(np, 1) * NB, &d_pcnt));
+        TRY(ws_typed(c, "fb_plcnt", (size_t)std::max<int64_t>(np, 1), &d_plcnt));
+        TRY(ws_typed(c, "fb_pbase", (size_t)std::max<int64_t>(np, 1) * NB, &d_pbase));
+        TRY(ws_typed(c, "fb_plbase", (size_t)std::max<int64_t>(np, 1), &d_plbase));
+        TRY(ws_typed(c, "fb_nleft", (size_t)nt, &d_nleft));
+        TRY(ws_typed(c, "fb_kboff", (size_t)nt * (NB + 1), &d_kboff));
+        TRY(h2d(c, d_tk, tk.data(), (size_t)nt));
+        TRY(h2d(c, d_pc, pcs.data(), pcs.size()));
+        F64BucketArgs ba{};
+        ba.cols = G.d_cols;
+        ba.cols_rstride = G.cols_rstride;
+        ba.npad = G.npad;
+        ba.tasks = d_tk;
+        ba.pieces = d_pc;
+        ba.NB = NB;
+        ba.ntasks = nt;
+        ba.ent_in = ent_cur;
+        ba.ent_out = ent_nxt;
+        ba.entK = d_entK;
+        ba.pcnt = d_pcnt;
+        ba.plcnt = d_plcnt;
+        ba.pbase = d_pbase;
+        ba.plbase = d_plbase;
+        ba.nleft = d_nleft;
+        ba.kb_off = d_kboff;
+        ba.y = G.ds->d_y64;
+        ba.chist = d_chist + (pass == 0 ? 0 : (size_t)nchain0 * NB * 3);
+        launch_fb_route(c->stream, ba, np, pass == 0 ? nchain0 : nchain1);
+        HIP_TRY(hipGetLastError());
+        if (pass == 0) TRY(d2h(c, nleft.data(), d_nleft, nleft.size()));  // (pass 1 reuses the scratch)
+      }
+      G.tm.end(h);
+      if (!fin.empty()) {
+        F64FinishNode* d_fn;
+        F64SplitOut* d_fo;
+        TRY(ws_typed(c, "fb_fin", fin.size(), &d_fn));
+        TRY(ws_typed(c, "fb_fout", fin.size(), &d_fo));
+        TRY(h2d(c, d_fn, fin.data(), fin.size()));
+        F64FinishArgs fa{};
+        fa.chist = d_chist;
+        fa.nodes = d_fn;
+        fa.n = (int)fin.size();
+        fa.NB = NB;
+        fa.min_inst = G.tp.min_instances_per_node;
+        fa.min_gain = G.tp.min_info_gain;
+        fa.out = d_fo;
+        int hs = G.tm.begin(T_SPLIT);
+        launch_fb_finish(c->stream, fa);
+        HIP_TRY(hipGetLastError());
+        G.tm.end(hs);
+        TRY(d2h(c, fo.data(), d_fo, fo.size()));
+      }
+    }
+    // ---- 3. node updates (RandomForest.findBestSplits, host part), next level
+    std::vector<LNode> next;
+    std::vector<std::pair<int64_t, int64_t>> nseg, hseg;
+    std::vector<ParentInfo> hpar;
+    std::vector<int32_t> triples;
+    for (int i = 0; i < M; i++) {
+      const LNode& q = cur[i];
+      const bool decided = !so[i].flag;
+      const F64SplitOut& o = decided ? fo[fin_of[i]] : xo[xi[i]];
+      if (decided && (o.s != so[i].s || !o.valid || !(o.gain > 0.0) || o.gain < G.tp.min_info_gain))
+        return fail(SBAG_EDEVICE, "internal: the fp64 screen's split is not Spark's (bound violated)");
+      const int r = q.r;
       {
-        BtNode& n = trees[r][cur[q].node];
-        for (int i = 0; i < 3; i++) n.calc[i] = o.calc[i];
+        BtNode& n = trees[r][q.node];
+        for (int j = 0; j < 3; j++) n.calc[j] = o.calc[j];
         n.gain = o.gain;
         n.impurity = o.impurity;
         n.valid = o.f >= 0 && o.valid != 0;
@@ -1774,9 +2040,9 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
       }
       const bool child_leaf = (level + 1) == D;
       BtNode L, Rn;
-      for (int i = 0; i < 3; i++) {
-        L.calc[i] = o.left[i];
-        Rn.calc[i] = o.right[i];
+      for (int j = 0; j < 3; j++) {
+        L.calc[j] = o.left[j];
+        Rn.calc[j] = o.right[j];
       }
       // LearningNode(child, isLeaf, ImpurityStats.getEmptyImpurityStats(calculator))
       L.impurity = bt_impurity(L.calc);
@@ -1784,65 +2050,75 @@ static int grow_f64(F64Grow& G, std::vector<std::vector<BtNode>>& trees) {
       L.is_leaf = child_leaf || L.impurity == 0.0;
       Rn.is_leaf = child_leaf || Rn.impurity == 0.0;
       const int li = (int)trees[r].size();
-      trees[r][cur[q].node].left = li;
-      trees[r][cur[q].node].right = li + 1;
+      trees[r][q.node].left = li;
+      trees[r][q.node].right = li + 1;
       trees[r].push_back(L);
       trees[r].push_back(Rn);
       if (L.is_leaf && Rn.is_leaf) continue;  // nothing to route
-      F64PartNode p{};
-      p.a = cur[q].a;
-      p.b = cur[q].b;
-      p.piece0 = (int64_t)pieces.size();
-      for (int64_t x = p.a; x < p.b; x += kF64PartPiece)
-        pieces.push_back(F64PartPiece{x, std::min(x + kF64PartPiece, p.b), (int32_t)pn.size(), 0});
-      p.piece1 = (int64_t)pieces.size();
-      p.r = r;
-      p.col = G.h_pos[(size_t)r * Fmax + o.f];
-      p.s = o.s;
-      pn.push_back(p);
-      splits.push_back(Split{q, li});
+      const int t = part_task[i];
+      if (t < 0) return fail(SBAG_EDEVICE, "internal: split node without routing");
+      const int64_t m = q.a + nleft[t];
+      const double g = gam(q.n);
+      const double nl = L.calc[0], nr = Rn.calc[0];
+      const double el = g * nl * 1.01, er = 2.0 * (g + u) * (1.0 + g) * q.n * 1.01;
+      int sl = -1, sr = -1;
+      if (!L.is_leaf) {
+        sl = (int)next.size();
+        next.push_back(LNode{r, li, q.a, m, nl, el * M1, el * M2});
+        nseg.push_back({q.a, m});
+      }
+      if (!Rn.is_leaf) {
+        sr = (int)next.size();
+        next.push_back(LNode{r, li + 1, m, q.b, nr, er * M1, er * M2});
+        nseg.push_back({m, q.b});
+      }
+      // the smaller (or only) child is histogrammed, its sibling is parent - small
+      int hs = sl >= 0 ? sl : sr;
+      if (sl >= 0 && sr >= 0) {
+        hs = nl <= nr ? sl : sr;
+        triples.push_back(hs == sl ? sr : sl);
+        triples.push_back(i);
+        triples.push_back(hs);
+      }
+      hseg.push_back(nseg[hs]);
+      hpar.push_back(ParentInfo{r, -1, 0, 0, 0, hs, 0, 0});
     }
-    if (pn.empty()) break;
-    const int NP = (int)pn.size();
-    F64PartNode* d_pn;
-    F64PartPiece* d_pc;
-    int32_t* d_pleft;
-    int64_t *d_pbase, *d_nl;
-    TRY(ws_typed(c, "f64_pn", (size_t)NP, &d_pn));
-    TRY(ws_typed(c, "f64_pc", std::max<size_t>(pieces.size(), 1), &d_pc));
-    TRY(ws_typed(c, "f64_pleft", std::max<size_t>(pieces.size(), 1), &d_pleft));
-    TRY(ws_typed(c, "f64_pbase", std::max<size_t>(pieces.size(), 1), &d_pbase));
-    TRY(ws_typed(c, "f64_nl", (size_t)NP, &d_nl));
-    TRY(h2d(c, d_pn, pn.data(), (size_t)NP));
-    TRY(h2d(c, d_pc, pieces.data(), pieces.size()));
-    F64PartArgs pa{};
-    pa.cols = G.d_cols;
-    pa.cols_rstride = G.cols_rstride;
-    pa.npad = G.npad;
-    pa.nodes = d_pn;
-    pa.pieces = d_pc;
-    pa.ent_in = ent_cur;
-    pa.ent_out = ent_nxt;
-    pa.piece_left = d_pleft;
-    pa.piece_base = d_pbase;
-    pa.nleft = d_nl;
+    if (next.empty()) break;
+    const int Mn = (int)next.size();
     {
-      int h = G.tm.begin(T_PART);
-      launch_f64_partition(c->stream, pa, NP, (int64_t)pieces.size());
+      std::vector<int> seg_r(Mn);
+      for (int k = 0; k < Mn; k++) seg_r[k] = next[k].r;
+      G.add_work(nseg, seg_r);
+    }
+    void* hist_nxt;
+    TRY(ws_get(c, hist_nxt_name, (size_t)Mn * G.slot_words * 8, &hist_nxt));
+    {
+      std::vector<int32_t> zs;
+      for (const ParentInfo& p : hpar) zs.push_back(p.hist_slot);
+      const int64_t u32w = G.slot_words * 2;
+      if ((u32w & 3) == 0) {
+        int32_t* d_zs;
+        TRY(ws_typed(c, "zslots", zs.size(), &d_zs));
+        TRY(h2d(c, d_zs, zs.data(), zs.size()));
+        launch_zero_slots(c->stream, hist_nxt, d_zs, (int)zs.size(), u32w);
+        HIP_TRY(hipGetLastError());
+      } else {
+        HIP_TRY(hipMemsetAsync(hist_nxt, 0, (size_t)Mn * G.slot_words * 8, c->stream));
+      }
+    }
+    TRY(G.int_hist(hseg, hpar, ent_nxt, hist_nxt));
+    if (!triples.empty()) {
+      int32_t* d_tri;
+      TRY(ws_typed(c, "triples", triples.size(), &d_tri));
+      TRY(h2d(c, d_tri, triples.data(), triples.size()));
+      int h = G.tm.begin(T_SUB);
+      launch_subtract(c->stream, hist_nxt, hist_cur, d_tri, (int)triples.size() / 3, G.slot_words, false);
       HIP_TRY(hipGetLastError());
       G.tm.end(h);
     }
-    std::vector<int64_t> nl(NP);
-    TRY(d2h(c, nl.data(), d_nl, (size_t)NP));
-    std::vector<LNode> next;
-    for (int k = 0; k < NP; k++) {
-      const LNode& p = cur[splits[k].q];
-      const int li = splits[k].li;
-      const int64_t m = pn[k].a + nl[k];
-      if (!trees[p.r][li].is_leaf) next.push_back(LNode{p.r, li, pn[k].a, m});
-      if (!trees[p.r][li + 1].is_leaf) next.push_back(LNode{p.r, li + 1, m, pn[k].b});
-    }
     cur.swap(next);
+    std::swap(hist_cur_name, hist_nxt_name);
+    hist_cur = hist_nxt;
     std::swap(ent_cur, ent_nxt);
   }
   return SBAG_OK;
@@ -1864,14 +2140,20 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   if (tp.impurity != SBAG_IMPURITY_GINI && tp.impurity != SBAG_IMPURITY_VARIANCE)
     return fail(SBAG_EINVAL, "unknown impurity");
   // Regression labels that are not dyadic fixed point (|y * 2^s| < 2^23, s <= 40) take the
-  // row-order fp64 path (f64 mode, sbag_f64.hip): Spark's sums depend on their order
+  // fp64 path (f64 mode, sbag_f64s.hip / sbag_f64.hip): Spark's sums depend on their order
   // there. SBAG_F64=1 forces it on dyadic labels too (both paths then agree bit for bit).
   const bool force_f64 = getenv("SBAG_F64") && atoi(getenv("SBAG_F64")) != 0;
   const bool f64 = !gini && (!ds->label_ok || force_f64);
   if (f64) {
     for (double v : ds->y)
       if (!std::isfinite(v)) return fail(SBAG_EINVAL, "labels must be finite");
+    if (!ds->label_ok && !ds->approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
   }
+  // the labels' fixed-point image in the entries: exact for dyadic labels, else (f64 path)
+  // the screening approximation k = round(y 2^ashift)
+  const int lshift = ds->label_ok ? ds->shift : ds->ashift;
+  const int64_t lkmin = ds->label_ok ? ds->kmin : ds->akmin;
+  const int64_t lkmax = ds->label_ok ? ds->kmax : ds->akmax;
   if (gini && !ds->integral)
     return fail(SBAG_EINVAL, "Classifier was given dataset with invalid label: labels must be "
                              "integers in [0, 2^23)");
@@ -1932,36 +2214,26 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     TRY(run_sampler(c, &fp->sampler, poff, N, d_counts));
     tm.end(h);
   }
-  // ---- 2. in-bag entry lists (two ping-pong buffers per replica): capacity N, or for the
-  // fp64 path, which keeps one entry per draw, the largest replica's draws
+  // ---- 2. in-bag entry lists (two ping-pong buffers per replica, capacity N)
   unsigned long long* d_inbag;
   TRY(ws_typed(c, "inbag", (size_t)R * 4, &d_inbag));
   unsigned long long* d_wsum = d_inbag + R;
   unsigned int* d_cmax = (unsigned int*)(d_inbag + 2 * R);
   unsigned long long* d_sqsum = d_inbag + 3 * R;
   HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 32, c->stream));
-  int64_t cap = N;
-  uint32_t* d_ncnt = nullptr;
-  if (f64) {
-    int h = tm.begin(T_COMPACT);
-    TRY(ws_typed(c, "f64_ncnt", (size_t)R * compact_ordered_chunks(N), &d_ncnt));
-    launch_chunk_draws(c->stream, d_counts, N, R, d_ncnt, d_wsum, d_cmax);
-    HIP_TRY(hipGetLastError());
-    tm.end(h);
-    std::vector<unsigned long long> ws(R);
-    TRY(d2h(c, ws.data(), d_wsum, (size_t)R));
-    cap = 1;
-    for (unsigned long long w : ws) cap = std::max<int64_t>(cap, (int64_t)w);
-  }
+  const int64_t cap = N;
   uint64_t *entA, *entB;
   TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
   TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
   {
     int h = tm.begin(T_COMPACT);
-    if (f64) {  // row order inside every replica (the fp64 sums follow it)
+    if (f64) {  // row order inside every replica (Spark's fp64 sums follow it)
+      uint32_t* d_ncnt;
       unsigned long long* d_cbase;
+      TRY(ws_typed(c, "f64_ncnt", (size_t)R * compact_ordered_chunks(N), &d_ncnt));
       TRY(ws_typed(c, "f64_cbase", (size_t)R * compact_ordered_chunks(N), &d_cbase));
-      launch_compact_ordered(c->stream, d_counts, N, R, entA, cap, d_ncnt, d_cbase, d_inbag);
+      launch_chunk_draws(c->stream, d_counts, N, R, d_ncnt, d_wsum, d_cmax);
+      launch_compact_ordered(c->stream, d_counts, ds->d_labk, N, R, entA, cap, d_ncnt, d_cbase, d_inbag);
     } else {
       launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
                      d_sqsum);
@@ -1985,26 +2257,28 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       return fail(SBAG_EUNSUPPORTED, "class counts exceed 32 bits");
   }
   // ---- LDS packing: count field at bit cshift, flush_limit entries between flushes
-  const int64_t K0 = -ds->kmin;
-  const double kspan = (double)(ds->kmax - ds->kmin + 1);
-  const double kabs = (double)std::max(std::llabs(ds->kmin), std::llabs(ds->kmax));
+  const int64_t K0 = -lkmin;
+  const double kspan = (double)(lkmax - lkmin + 1);
+  const double kabs = (double)std::max(std::llabs(lkmin), std::llabs(lkmax));
   int64_t flush_limit = (int64_t)1 << 22;
   int cshift = 40;
   for (;; flush_limit /= 2) {
     if (flush_limit < 256)
       return fail(SBAG_EUNSUPPORTED, "label range too wide for the packed LDS histogram");
     const double wmax = (double)flush_limit * cmax;
-    if (gini || f64) {  // f64: only the u32 value-count histograms use the packing
+    if (gini) {
       if (wmax < 4294967295.0) break;
       continue;
     }
     cshift = (int)std::ceil(std::log2(wmax * kspan + 1.0));
     const int cbits = 64 - cshift;
-    if (cbits >= 1 && std::ldexp(1.0, cbits) > wmax && wmax * kabs * kabs < 1.8e19) break;
+    // (the sum-of-squares plane of the exact fallback needs wmax k^2 in 64 bits; the fp64
+    // path never builds it)
+    if (cbits >= 1 && std::ldexp(1.0, cbits) > wmax && (f64 || wmax * kabs * kabs < 1.8e19)) break;
   }
   // the row-lane histogram builds the word as (c << cshift) + c*(k + K0) with a 32-bit
   // low half: raise cshift to 32 when the count field keeps room for flush_limit * cmax
-  if (!gini && !f64 && cshift < 32 && (double)flush_limit * cmax < 4294967296.0) cshift = 32;
+  if (!gini && cshift < 32 && (double)flush_limit * cmax < 4294967296.0) cshift = 32;
   if (!gini && !f64 && (double)N * cmax * kabs * kabs >= std::ldexp(1.0, 53))
     return fail(SBAG_EUNSUPPORTED, "sum of squared labels would exceed 2^53 (not exact in fp64)");
 
@@ -2311,7 +2585,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   TRY(ws_typed(c, "pos", h_pos_codes.size(), &d_pos));
   TRY(h2d(c, d_pos, h_pos_codes.data(), h_pos_codes.size()));
   std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1), 0);
-  const bool optimistic = ds->code_bytes == 1 && ncmax <= tp.max_bins && !f64;
+  const bool optimistic = ds->code_bytes == 1 && ncmax <= tp.max_bins;
   // row-lane histogram: identity byte layout, packed variance words with cshift >= 32
   // (SBAG_HIST_RL: 0 = never, 1 = always 64-bit row addresses; tests pin both paths)
   const int rl_env = getenv("SBAG_HIST_RL") ? atoi(getenv("SBAG_HIST_RL")) : -1;
@@ -2777,51 +3051,6 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   TRY(h2d(c, d_nbins, h_nbins.data(), h_nbins.size()));
 
   hmark(12);
-  if (f64) {
-    F64Grow G{c, ds, tp, R, N, Fmax, NB, S, h_Fr, sub, thr, d_bins, bins_rstride, d_pos, d_Fr, d_nbins,
-              h_pos, d_cols, cols_rstride, npad, entA, entB, cap, inbag, tm};
-    std::vector<std::vector<BtNode>> ftrees;
-    TRY(grow_f64(G, ftrees));
-    HIP_TRY(hipEventRecord(ev_stop, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    forest->trees.resize(R);
-    for (int r = 0; r < R; r++) {
-      HTree& t = forest->trees[r];
-      t.sub = sub[r];
-      t.exact = exact[r];
-      t.ns = 3;
-      bt_emit(ftrees[r], 0, t);
-    }
-    forest->nclasses = 0;
-    double cats[T_NCAT] = {0};
-    std::vector<double> hist_each;
-    tm.collect(cats, &hist_each, T_HIST);
-    if (getenv("SBAG_LEVEL_TRACE")) {  // diagnostics: each fp64 histogram launch
-      size_t k = 0;
-      for (size_t i = 0; i < tm.ev.size(); i++)
-        if (tm.ev[i].first == T_HIST && k < hist_each.size())
-          fprintf(stderr, "[sbag] f64 level %d hist ms %.3f\n", tm.lv[i], hist_each[k++]);
-    }
-    float total_ms = 0;
-    (void)hipEventElapsedTime(&total_ms, ev_start, ev_stop);
-    (void)hipEventDestroy(ev_start);
-    (void)hipEventDestroy(ev_stop);
-    sbag_timing& T = forest->timing;
-    T.total_ms = total_ms;
-    T.sample_ms = cats[T_SAMPLE];
-    T.valuecount_ms = cats[T_VC];
-    T.bin_ms = cats[T_BIN];
-    T.compact_ms = cats[T_COMPACT];
-    T.hist_ms = cats[T_HIST];
-    T.split_ms = cats[T_SPLIT];
-    T.partition_ms = cats[T_PART];
-    T.hist_launches = G.hist_launches;
-    T.hist_entries = G.hist_entries;
-    T.hist_alg_bytes = G.hist_alg_bytes;
-    T.levels = G.levels;
-    *out = forest.release();
-    return SBAG_OK;
-  }
   // ---- 6. level-wise growth
   HistGeom g;
   if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode_for(h_pos, S)))
@@ -2855,6 +3084,76 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     std::vector<int> seg_r(R);
     for (int r = 0; r < R; r++) seg_r[r] = r;
     add_work(seg, seg_r);
+  }
+  if (f64) {
+    // the integer histograms of the labels' fixed-point image (exact when the labels are
+    // dyadic, SBAG_F64=1) screen the splits; Spark's row-order fp64 sums give the stats
+    F64sGrow G{c, ds, tp, R, N, Fmax, NB, S, h_Fr, h_nbins, thr, d_bins, bins_rstride, d_pos, d_Fr,
+               d_nbins, h_pos, d_cols, cols_rstride, npad, entA, entB, cap, inbag, tm, hist_cur,
+               slot_words, std::ldexp(1.0, -lshift),
+               ds->label_ok ? 0.0 : std::ldexp(1.0, -lshift - 1),
+               [&](const std::vector<std::pair<int64_t, int64_t>>& segs, const std::vector<ParentInfo>& par,
+                   const uint64_t* ent, void* hist) -> int {
+                 ha.ent_in = ent;
+                 ha.hist = hist;
+                 return launch(g, kHistVar, T_HIST, segs, par);
+               },
+               add_work};
+    std::vector<std::vector<BtNode>> ftrees;
+    TRY(grow_f64s(G, ftrees));
+    HIP_TRY(hipEventRecord(ev_stop, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    forest->trees.resize(R);
+    for (int r = 0; r < R; r++) {
+      HTree& t = forest->trees[r];
+      t.sub = sub[r];
+      t.exact = exact[r];
+      t.ns = 3;
+      bt_emit(ftrees[r], 0, t);
+    }
+    forest->nclasses = 0;
+    double cats[T_NCAT] = {0};
+    tm.collect(cats, nullptr, -1);
+    if (trace) {
+      std::map<int, std::array<double, T_NCAT>> per;
+      for (size_t i = 0; i < tm.ev.size(); i++) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, tm.ev[i].second.first, tm.ev[i].second.second);
+        auto it = per.find(tm.lv[i]);
+        if (it == per.end()) it = per.emplace(tm.lv[i], std::array<double, T_NCAT>{}).first;
+        it->second[tm.ev[i].first] += ms;
+      }
+      for (auto& kv : per)
+        fprintf(stderr, "[sbag] f64 level %d ms: hist %.2f screen+finish %.2f sub %.2f chain %.2f fix %.2f\n",
+                kv.first, kv.second[T_HIST], kv.second[T_SPLIT], kv.second[T_SUB], kv.second[T_CHAIN],
+                kv.second[T_FIX]);
+    }
+    float total_ms = 0;
+    (void)hipEventElapsedTime(&total_ms, ev_start, ev_stop);
+    (void)hipEventDestroy(ev_start);
+    (void)hipEventDestroy(ev_stop);
+    sbag_timing& T = forest->timing;
+    T.total_ms = total_ms;
+    T.sample_ms = cats[T_SAMPLE];
+    T.valuecount_ms = cats[T_VC];
+    T.bin_ms = cats[T_BIN];
+    T.compact_ms = cats[T_COMPACT];
+    T.hist_ms = cats[T_HIST];
+    T.split_ms = cats[T_SPLIT];
+    T.subtract_ms = cats[T_SUB];
+    T.partition_ms = cats[T_PART];
+    T.chain_ms = cats[T_CHAIN];
+    T.fix_ms = cats[T_FIX];
+    T.exact_fallbacks = G.fallbacks;
+    T.hist_launches = hist_launches;
+    T.hist_alg_bytes = hist_alg_bytes;
+    T.hist_entries = hist_entries;
+    T.hist_lds_atomics = hist_lds;
+    T.hist_work_bytes = hist_work;
+    T.hist_upper_bytes = hist_upper;
+    T.levels = G.levels;
+    *out = forest.release();
+    return SBAG_OK;
   }
   const double inv_scale = std::ldexp(1.0, -ds->shift), inv_scale2 = std::ldexp(1.0, -2 * ds->shift);
   uint64_t* ent_cur = entA;

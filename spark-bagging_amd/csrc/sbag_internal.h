@@ -361,14 +361,89 @@ struct F64PartArgs {
   int64_t* nleft;          // [nodes]
 };
 constexpr int64_t kF64PartPiece = 4096;
-// the exploded bootstrap: draws per (replica, chunk) and per replica (Σ, max), then one
-// entry per draw in row order
+// the stable bootstrap compaction of the fp64 path: in-bag rows per (replica, chunk) and
+// per replica (Σ count, max count), then one entry row | (k << 8 | count) << 32 per in-bag
+// row, in row order (k: the labels' fixed-point image, labk)
 void launch_chunk_draws(hipStream_t st, const uint8_t* counts, int64_t N, int R,
                         uint32_t* d_ncnt /*[R][chunks]*/, unsigned long long* d_wsum,
                         unsigned int* d_cmax);
-void launch_compact_ordered(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint64_t* ent,
-                            int64_t cap, const uint32_t* d_ncnt,
+void launch_compact_ordered(hipStream_t st, const uint8_t* counts, const int32_t* labk, int64_t N,
+                            int R, uint64_t* ent, int64_t cap, const uint32_t* d_ncnt,
                             unsigned long long* d_base /*[R][chunks]*/, unsigned long long* d_cursor);
+
+// ---- screened fp64 engine (sbag_f64s.hip): the split of a node is chosen from the integer
+// histograms of the labels' fixed-point image with a rigorous bound on Spark's fp64 gain
+// (k_f64_screen); only the chosen feature's bins are summed in Spark's row order
+// (k_fb_count / k_fb_scan / k_fb_scatter bucket each node's entries by that feature's
+// bin, stable, and route them to the children; k_fb_chain adds every bucket in row
+// order); k_fb_finish evaluates the chosen feature exactly as binsToBestSplit does.
+struct F64ScreenOut {
+  int32_t f, s;      // best local feature / split bin by the screen (-1: none)
+  int32_t flag;      // 1: undecided -> exact row-order histogram of every feature
+  int32_t pad;
+  double gain, margin;  // screened gain of the best candidate, its guaranteed lead
+};
+struct F64ScreenArgs {
+  const uint64_t* hist;     // [slot][Fmax][NB][3] integer (count, Σ c k, -)
+  const int32_t* slot_r;    // [M]
+  const int32_t* Fr;        // [R]
+  const int32_t* nbins;     // [R][Fmax]
+  int32_t Fmax, NB, min_inst, pad;
+  double min_gain;
+  double inv_scale;         // 2^-s: k 2^-s approximates y
+  double eps;               // max |y - k 2^-s| (2^-s-1)
+  const double* dnode;      // [M] bound on Spark's summation and rounding error of a
+                            //     candidate's child part (lw imp(L) + rw imp(R)) of the gain
+  const double* dpar;       // [M] bound on the error of the node's own impurity
+  F64ScreenOut* out;        // [M]
+};
+struct F64Task {            // one (node, feature) whose entries are bucketed / routed
+  int64_t a, b;             // entries [a, b) of ent_in (row order)
+  int64_t kbase;            // buckets at entK[kbase, kbase + b - a); -1: no buckets
+  int64_t piece0, piece1;   // its pieces
+  int32_t r, col, s, part;  // replica, column of the column-major bins, split bin, route?
+};
+struct F64TPiece {
+  int64_t a, b;
+  int32_t task, pad;
+};
+constexpr int64_t kFbPiece = 8192;
+struct F64BucketArgs {
+  const uint8_t* cols;      // [R?][C][npad]
+  int64_t cols_rstride, npad;
+  const F64Task* tasks;
+  const F64TPiece* pieces;
+  int32_t NB, ntasks;
+  const uint64_t* ent_in;
+  uint64_t* ent_out;        // children: left [a, a + nleft), right [a + nleft, b), row order
+  uint64_t* entK;           // buckets
+  uint32_t* pcnt;           // [piece][NB] entries per bin
+  uint32_t* plcnt;          // [piece] entries going left
+  int64_t* pbase;           // [piece][NB] bucket position of the piece's first entry per bin
+  int64_t* plbase;          // [piece] left entries of the task before the piece
+  int64_t* nleft;           // [task]
+  int64_t* kb_off;          // [task][NB + 1] bucket bounds in entK
+  const double* y;          // [N] labels
+  double* chist;            // [task][NB][3] count, sum, sumSq in Spark's row order
+};
+struct F64FinishNode {
+  int32_t t, t0;            // task of the chosen feature; task of the first feature with
+                            // splits (root: the parent stats), -1 when not needed
+  int32_t f, s;             // chosen local feature and split bin
+  int32_t nsp, nsp0;        // numSplits of f and of the first feature
+  int32_t pad[2];
+  F64Chain ch;
+};
+struct F64FinishArgs {
+  const double* chist;
+  const F64FinishNode* nodes;
+  int32_t n, NB, min_inst, pad;
+  double min_gain;
+  F64SplitOut* out;
+};
+void launch_f64_screen(hipStream_t st, const F64ScreenArgs& a, int M);
+void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain);
+void launch_fb_finish(hipStream_t st, const F64FinishArgs& a);
 int64_t compact_ordered_chunks(int64_t N);
 int f64_hist_width(int NB);
 size_t f64_hist_lds_bytes(int NB, int parts);

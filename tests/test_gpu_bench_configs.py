@@ -210,3 +210,33 @@ def test_c5_full_shard(ctx):
     Bernoulli 0.5 without replacement, depth 12, rank 7's learners [112, 128) of 128."""
     _full_shard(ctx, n=50_000_000, f=100, classes=64, replacement=False, ratio=0.5, seed=SEED_CLS,
                 lb=112, le=128, depth=12, check=(112, 127))
+
+
+def test_c3_nondyadic_as_benched(ctx):
+    """bench.py's nondyadic_labels line: C3 (10M x 100, P=128, 128 learners, depth 8) on the
+    real-valued labels 1.1 y + 0.3, through the screened fp64 engine.  Learners {0, 127}
+    bit-exact against the oracle's row-order fp64 fit; every tree's structure sound."""
+    n, L = 10_000_000, 128
+    ds, X, y = _dataset(ctx, n, 100, 0)
+    y2 = y * 1.1 + 0.3
+    ds.set_labels(y2)
+    part = _partitions(n)
+    forest = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                     learner_end=L, partition_offsets=part, max_depth=8, max_bins=32,
+                     impurity=nat.IMPURITY_VARIANCE)
+    assert len(forest) == L
+    t = forest.timing()
+    for i in range(L):
+        nodes, _ = forest.tree(i)
+        internal = nodes["left"] >= 0
+        assert (nodes["left"][internal] == np.nonzero(internal)[0] + 1).all()
+        assert (nodes["gain"][internal] > 0).all()
+    check = [0, 127]
+    ocounts = np.stack([oracle.bag(True, 1.0, i, i + 1, SEED_REG, part, n)[0] for i in check])
+    subs = [oracle.subspace(1.0, 100, SEED_REG + i) for i in check]
+    orf = oracle.fit(X, y2, ocounts, subs, max_depth=8, max_bins=32, nthreads=NTHREADS, part=part)
+    for k, i in enumerate(check):
+        assert_tree_equal(forest, i, orf, k)
+    print("c3 nondyadic: fit ms", t["total_ms"], "exact_fallbacks", t["exact_fallbacks"])
+    forest.free()
+    ds.free()

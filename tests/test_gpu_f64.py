@@ -155,3 +155,62 @@ def test_nonfinite_labels_rejected(ctx, cpusmall):
                     learner_end=2, max_depth=3, impurity=nat.IMPURITY_VARIANCE)
     finally:
         ds.free()
+
+
+def _fit(ctx, X, y, L, depth, part=None, **kw):
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        f = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                    learner_end=L, partition_offsets=part, max_depth=depth, max_bins=32,
+                    impurity=nat.IMPURITY_VARIANCE, **kw)
+    finally:
+        ds.free()
+    return f
+
+
+@pytest.mark.parametrize("case", ["cpusmall_pi", "cpusmall_sqrt", "ties", "tiny_spread"])
+def test_screened_engine_equals_unscreened(ctx, cpusmall, monkeypatch, case):
+    """The screened fp64 engine (sbag_f64s.hip: splits chosen from the integer histograms
+    of the labels' fixed-point image under a rigorous bound, only the chosen feature summed
+    in row order) gives the unscreened engine's trees (SBAG_F64_SCREEN=0: every feature of
+    every node in row order) byte for byte, including datasets built to defeat the screen:
+    duplicated columns (exact ties) and labels whose spread is a few ulps."""
+    X, y = cpusmall
+    if case == "cpusmall_pi":
+        y2 = y * np.pi
+    elif case == "cpusmall_sqrt":
+        y2 = np.sqrt(y + 0.5)
+    elif case == "ties":
+        X = np.concatenate([X, X[:, :4]], axis=1)  # every split of the first 4 columns ties
+        y2 = y / 3.0
+    else:
+        y2 = 1.0 + (y - y.mean()) * 1e-13  # gains at the rounding level: the screen must defer
+    a = _fit(ctx, X, y2, 6, 9)
+    ta = a.timing()
+    monkeypatch.setenv("SBAG_F64_SCREEN", "0")
+    b = _fit(ctx, X, y2, 6, 9)
+    tb = b.timing()
+    for t in range(6):
+        (na, sa), (nb, sb_) = a.tree(t), b.tree(t)
+        assert na.tobytes() == nb.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes()
+    assert tb["exact_fallbacks"] >= ta["exact_fallbacks"]
+    if case in ("cpusmall_pi", "cpusmall_sqrt"):
+        assert ta["exact_fallbacks"] < tb["exact_fallbacks"] / 2  # the screen decides most nodes
+    if case == "ties":
+        assert ta["exact_fallbacks"] > 0
+
+
+def test_c3_shape_nondyadic_screened(ctx):
+    """The bench's real-valued-label line at 1/10 of its rows: 1M x 100 synthetic u8 codes,
+    labels 1.1 y + 0.3, 16 learners, depth 8, P = 128 -- every tree bit-exact against the
+    oracle (row-order fp64 sums) and almost every node decided by the screen."""
+    N, F, L = 1_000_000, 100, 16
+    X, yk = oracle.synth(N, F, 20261015, 0)
+    y = yk * 1.1 + 0.3
+    part = [round(i * N / 128) for i in range(129)]
+    forest, orf = _fit_both(ctx, X.astype(np.float64), y, L, depth=8, part=part)
+    assert_forest_equal(forest, orf)
+    t = forest.timing()
+    nodes = sum(len(forest.tree(i)[0]) for i in range(L))
+    assert t["exact_fallbacks"] <= 0.02 * nodes, (t["exact_fallbacks"], nodes)
