@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <condition_variable>
 #include <functional>
@@ -1413,6 +1414,22 @@ static double bins_budget(sbag_ctx* c) {
 
 static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out);
 
+// Bins are u8 codes, so a feature may have at most 256 bins (255 thresholds).  Spark's
+// findSplitsForContinuousFeature can return maxBins thresholds when the split-finding sample
+// (subbags above max(maxBins^2, 10^4) rows) holds more nonzero values than numSamples; with
+// maxBins = 256 that is 257 bins.  Whether it happens depends on the sample (the seed), so
+// the combination that allows it -- maxBins 256, more than 65536 rows, a feature with more
+// than 255 distinct values -- is refused up front, for every seed.  (Below 65536 rows a
+// bag only reaches the sample when a with-replacement draw exceeds 65536 rows; the 257th
+// bin is then still refused when it occurs.)
+static int check_bins256(const sbag_tree_params& tp, int64_t rows, int max_distinct) {
+  if (tp.max_bins == 256 && rows > 65536 && max_distinct > 255)
+    return fail(SBAG_EUNSUPPORTED, "maxBins 256 on more than 65536 rows with a feature of more than 255 "
+                                   "distinct values: Spark's split-finding sample may return 256 "
+                                   "thresholds (257 bins) and bins are u8 codes; use maxBins <= 255");
+  return SBAG_OK;
+}
+
 // Learners are independent (seed + i per learner), so a range whose per-replica
 // bins do not fit is fitted as two halves and the trees concatenated in learner order.
 // sum of two forests' learner-ordered trees and timings (a then b)
@@ -2307,6 +2324,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   int ncmax = 0;
   if (!wide)
     for (int f = 0; f < F; f++) ncmax = std::max(ncmax, (int)ds->dict[f].size());
+  TRY(check_bins256(tp, N, wide ? INT_MAX : ncmax));
 
   // root "parents": one per replica, no routing, histogram slot = replica
   std::vector<ParentInfo> h_par(R);
@@ -4361,6 +4379,11 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
   const int64_t N = ds->N;
   const int F = ds->F;
   if (N >= ((int64_t)1 << 32)) return fail(SBAG_EUNSUPPORTED, "booster fit on 2^32 rows or more");
+  {
+    int maxd = 0;
+    for (const auto& d : ds->dict) maxd = std::max(maxd, (int)d.size());
+    TRY(check_bins256(tp, N, maxd));
+  }
   const int Fr = bp->subspace_len;
   if (Fr <= 0)
     return fail(SBAG_EINVAL, "requirement failed: VectorSlicer requires that at least one "

@@ -154,3 +154,26 @@ def test_split_sample_one_more_threshold(ctx):
     assert max(int(orf.tree(t)[0]["split_bin"].max()) for t in range(p["L"])) == p["bins"] - 1
     assert_forest_equal(forest, orf)
     forest.free()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_max_bins_256_refused_for_every_seed(ctx, seed):
+    """maxBins 256 on more than 65536 rows with a continuous feature can give a
+    feature 256 thresholds (257 bins, beyond u8 bin codes) depending on the split-finding
+    sample.  The engine refuses that combination up front for every seed, and fits the same
+    data at maxBins 255."""
+    rng = np.random.default_rng(5)
+    N = 70_000
+    X = np.round(rng.normal(size=(N, 3)), 4)
+    y = rng.normal(size=N)
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        with pytest.raises(nat.SparkException, match="maxBins 256"):
+            nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=seed, learner_begin=0,
+                    learner_end=2, max_depth=3, max_bins=256, impurity=nat.IMPURITY_VARIANCE)
+        f = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=seed, learner_begin=0,
+                    learner_end=2, max_depth=3, max_bins=255, impurity=nat.IMPURITY_VARIANCE)
+        assert len(f) == 2
+        f.free()
+    finally:
+        ds.free()
