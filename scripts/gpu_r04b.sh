@@ -2,7 +2,7 @@
 # Round 4: the screened fp64 engine -- parity first (small), then the C3-shape nondyadic
 # line, then the bench.
 set -u
-OUT=gpurun_out/r04b
+OUT=gpurun_out/${RUN:-r04b}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_f64.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_f64.log 2>&1 || { echo "f64 tests rc=$?"; tail -60 $OUT/gpu_f64.log; exit 1; }
 tail -3 $OUT/gpu_f64.log

@@ -18,12 +18,12 @@
 //                  every feature in row order, then k_f64_split).
 //   k_fb_count / k_fb_scan / k_fb_scatter   for every decided node (and, at the root,
 //                  its first feature with splits, whose bins give Spark's parent stats):
-//                  a stable bucketing of the node's entries (row order) by the chosen
-//                  feature's bin into entK, fused with the stable two-way partition of
+//                  a stable bucketing of the node's draws (row order) by the chosen
+//                  feature's bin, each draw's label written out, fused with the stable two-way partition of
 //                  every split node into its children (left |= bin <= s), which keeps the
 //                  children's entries in row order for the next level
-//   k_fb_chain     one lane per (task, bin): the bucket's rows in row order, each label
-//                  added count times -- Spark's cell sums bit for bit
+//   k_fb_chain     one lane per (task, bin): the bucket's draws in row order (a row drawn
+//                  c times is c consecutive labels) -- Spark's cell sums bit for bit
 //   k_fb_finish    binsToBestSplit over the chosen feature's exact bins (prefixes in bin
 //                  order, right = total - left, calculateImpurityStats with the node's
 //                  chained stats): the node's gain, impurity and children calculators
@@ -208,7 +208,11 @@ __device__ __forceinline__ const uint8_t* task_col(const F64BucketArgs& A, const
   return A.cols + (int64_t)t.r * A.cols_rstride + (int64_t)t.col * A.npad;
 }
 
-// per piece: entries per bin of the task's feature, entries going left (bin <= s)
+__device__ __forceinline__ uint32_t task_bin(const uint8_t* col, uint64_t e) {
+  return col ? (uint32_t)col[(uint32_t)e] : 0u;
+}
+
+// per piece: draws per bin of the task's feature, entries going left (bin <= s)
 __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   const F64TPiece pc = A.pieces[blockIdx.x];
   const F64Task t = A.tasks[pc.task];
@@ -217,11 +221,12 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   __shared__ uint32_t s_l[4];
   for (int b = tid; b < NB; b += 256) s_c[b] = 0u;
   block_sync();
-  const uint8_t* col = task_col(A, t);
+  const uint8_t* col = t.col >= 0 ? task_col(A, t) : nullptr;
   uint32_t nl = 0;
   for (int64_t i = pc.a + tid; i < pc.b; i += 256) {
-    const uint32_t bin = col[(uint32_t)A.ent_in[i]];
-    atomicAdd(&s_c[bin], 1u);
+    const uint64_t e = A.ent_in[i];
+    const uint32_t bin = task_bin(col, e);
+    atomicAdd(&s_c[bin], (uint32_t)(e >> 32) & 0xffu);
     nl += bin <= (uint32_t)t.s ? 1u : 0u;
   }
   for (int o = 32; o > 0; o >>= 1) nl += __shfl_down(nl, o);
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   if (tid == 0) A.plcnt[blockIdx.x] = s_l[0] + s_l[1] + s_l[2] + s_l[3];
 }
 
-// per task: bucket bounds (bins in order, each bin's entries in row order), each piece's
+// per task: bucket bounds (bins in order, each bin's draws in row order), each piece's
 // first position per bin, left entries before each piece, the task's left total
 __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
   const int task = blockIdx.x, tid = threadIdx.x, NB = A.NB;
@@ -270,10 +275,13 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
   }
 }
 
-// one wave per piece: every entry to its bucket (stable: rank among the round's entries of
-// the same bin, from ballots over the bin's bits) and, for split nodes, to its child
-// (left from the segment start, right after the left block, both in row order)
-__global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits) {
+// one wave per piece: every draw's label to its bucket (stable: a row's draws after the
+// draws of the round's earlier rows of the same bin -- their counts summed over the lanes
+// below with the same bin, from ballots over the bin's and the count's bits) and, for
+// split nodes, every entry to its child (left from the segment start, right after the left
+// block, both in row order)
+__global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits,
+                                                    int cbits) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t pi = (int64_t)blockIdx.x * 4 + wv;
   __shared__ int64_t s_base[4][256];
@@ -290,24 +298,33 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   int64_t lrun = t.part ? A.plbase[pi] : 0;
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
-  const uint8_t* col = task_col(A, t);
+  const uint8_t* col = t.col >= 0 ? task_col(A, t) : nullptr;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int64_t i0 = pc.a; i0 < pc.b; i0 += 64) {
     const int64_t i = i0 + lane;
     const bool valid = i < pc.b;
     const uint64_t e = valid ? A.ent_in[i] : 0ull;
-    const uint32_t bin = valid ? (uint32_t)col[(uint32_t)e] : 0u;
+    const uint32_t bin = valid ? task_bin(col, e) : 0u;
     if (chain) {
+      const uint32_t c = (uint32_t)(e >> 32) & 0xffu;  // 0 past the piece
+      const double y = valid ? A.y[(uint32_t)e] : 0.0;
       uint64_t eq = __ballot(valid);
       for (int k = 0; k < nbits; k++) {
         const bool bit = (bin >> k) & 1u;
         const uint64_t m = __ballot(bit);
         eq &= bit ? m : ~m;
       }
-      const int rank = __popcll(eq & lt), cnt = __popcll(eq);
+      // draws of the lanes below with this bin, and of all lanes with this bin
+      int64_t rank = 0, cnt = 0;
+      for (int k = 0; k < cbits; k++) {
+        const uint64_t m = __ballot((c >> k) & 1u) & eq;
+        rank += (int64_t)__popcll(m & lt) << k;
+        cnt += (int64_t)__popcll(m) << k;
+      }
       const int64_t base = valid ? sb[bin] : 0;
-      if (valid) A.entK[base + rank] = e;
-      if (valid && rank == cnt - 1) sb[bin] = base + cnt;
+      for (uint32_t k = 0; k < c; k++) A.bucket[base + rank + k] = y;
+      const bool last = valid && (eq & ~(lt | (1ull << lane))) == 0ull;  // highest lane of its bin
+      if (last) sb[bin] = base + cnt;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -325,66 +342,109 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   }
 }
 
-// one lane per (task, bin): Spark's row-order fp64 sums of the bucket
-__global__ __launch_bounds__(256) void k_fb_chain(F64BucketArgs A, int nchain) {
-  const int NB = A.NB;
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (int64_t)nchain * NB) return;
-  const int64_t task = g / NB;
-  const int b = (int)(g - task * NB);
-  const int64_t* ko = A.kb_off + task * (NB + 1);
-  const int64_t lo = ko[b], hi = ko[b + 1];
+// Spark's row-order fp64 sums of every bucket: one lane per (task, bin), 16 chains per
+// wave.  The chains' labels stream through LDS: the whole wave loads each chain's next
+// kChT labels with contiguous 512-byte loads (issued a stage ahead, while the current
+// stage is summed), then lane l < 16 adds its own slice in order (sum += y, sumSq += y*y:
+// instanceWeight 1.0 per draw, DTStatsAggregator.update).
+constexpr int kChC = 16;    // chains per wave
+constexpr int kChT = 128;   // labels per chain per stage
+constexpr int kChPitch = kChT + 1;
+__global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
+  __shared__ double s_y[kChC * kChPitch];
+  const int NB = A.NB, lane = threadIdx.x;
+  const int64_t nlanes = (int64_t)nchain * NB;
+  const int64_t g = (int64_t)blockIdx.x * kChC + lane;
+  int64_t lo = 0, hi = 0;
+  if (lane < kChC && g < nlanes) {
+    const int64_t task = g / NB;
+    const int b = (int)(g - task * NB);
+    const int64_t* ko = A.kb_off + task * (NB + 1);
+    lo = ko[b];
+    hi = ko[b + 1];
+  }
+  const int64_t len = hi - lo;
+  int64_t maxlen = len;
+  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
+  const double* bk = A.bucket;
+  auto rdl64 = [](int64_t x, int j) -> int64_t {  // lane j's value (j wave-uniform)
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), j);
+    return (int64_t)(((uint64_t)h << 32) | l);
+  };
+  // a stage: chain j's labels [off, off + kChT) -- loads u = 2j, 2j + 1, contiguous 512 B each
+  constexpr int kLd = kChC * kChT / 64;  // loads per stage (each lane: one double per load)
+  static_assert(kChT == 128, "two loads per chain slice");
+  double v[kLd];
+  auto load_stage = [&](int64_t off) {
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      const int j = u >> 1;                   // chain (wave-uniform)
+      const int x = (u & 1) * 64 + lane;      // position in its slice
+      const int64_t jlo = rdl64(lo, j), jlen = rdl64(len, j);
+      v[u] = off + x < jlen ? bk[jlo + off + x] : 0.0;
+    }
+  };
   double s1 = 0.0, s2 = 0.0;
-  uint64_t cnt = 0;
-  int64_t i = lo;
-  constexpr int U = 8;
-  for (; i + U <= hi; i += U) {
-    uint64_t e[U];
-    double yv[U];
+  load_stage(0);
+  for (int64_t off = 0; off < maxlen; off += kChT) {
 #pragma unroll
-    for (int j = 0; j < U; j++) e[j] = A.entK[i + j];
+    for (int u = 0; u < kLd; u++) {
+      const int e = u * 64 + lane;
+      s_y[(e / kChT) * kChPitch + (e % kChT)] = v[u];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (off + kChT < maxlen) load_stage(off + kChT);
+    const int n = (int)min((int64_t)kChT, max((int64_t)0, len - off));
+    if (lane < kChC) {
+      const double* sy = s_y + lane * kChPitch;
+      int x = 0;
+      for (; x + 8 <= n; x += 8) {  // 8 LDS reads in flight, then the adds in order
+        double yy[8];
 #pragma unroll
-    for (int j = 0; j < U; j++) yv[j] = A.y[(uint32_t)e[j]];
+        for (int k = 0; k < 8; k++) yy[k] = sy[x + k];
 #pragma unroll
-    for (int j = 0; j < U; j++) {
-      const uint32_t c = (uint32_t)(e[j] >> 32) & 0xffu;
-      const double w = 1.0 * yv[j];   // instanceWeight * label
-      const double wy = w * yv[j];    // instanceWeight * label * label
-      for (uint32_t k = 0; k < c; k++) {
-        s1 += w;
-        s2 += wy;
+        for (int k = 0; k < 8; k++) {
+          const double w = 1.0 * yy[k];  // instanceWeight * label
+          s1 += w;
+          s2 += w * yy[k];               // instanceWeight * label * label
+        }
       }
-      cnt += c;
+      for (; x < n; x++) {
+        const double y = sy[x];
+        const double w = 1.0 * y;
+        s1 += w;
+        s2 += w * y;
+      }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  for (; i < hi; i++) {
-    const uint64_t e = A.entK[i];
-    const double yv = A.y[(uint32_t)e];
-    const uint32_t c = (uint32_t)(e >> 32) & 0xffu;
-    const double w = 1.0 * yv, wy = w * yv;
-    for (uint32_t k = 0; k < c; k++) {
-      s1 += w;
-      s2 += wy;
-    }
-    cnt += c;
+  if (lane < kChC && g < nlanes) {
+    double* o = A.chist + g * 3;
+    o[0] = (double)len;  // one draw per label: count += 1.0 each
+    o[1] = s1;
+    o[2] = s2;
   }
-  double* o = A.chist + g * 3;
-  o[0] = (double)cnt;
-  o[1] = s1;
-  o[2] = s2;
 }
 
-void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain) {
-  if (npieces <= 0) return;
+void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain, int cbits) {
   int nbits = 0;
   while ((1 << nbits) < a.NB) nbits++;
-  hipLaunchKernelGGL(k_fb_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)a.ntasks), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_fb_scatter, dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a, npieces,
-                     nbits);
+  if (npieces > 0)
+    hipLaunchKernelGGL(k_fb_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
+  if (a.ntasks > 0)  // (tasks without pieces still get their bucket bounds)
+    hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)a.ntasks), dim3(256), 0, st, a);
+  if (npieces > 0)
+    hipLaunchKernelGGL(k_fb_scatter, dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
+                       npieces, nbits, cbits);
   const int64_t lanes = (int64_t)nchain * a.NB;
   if (lanes > 0)
-    hipLaunchKernelGGL(k_fb_chain, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, a, nchain);
+    hipLaunchKernelGGL(k_fb_chain, dim3((unsigned)((lanes + kChC - 1) / kChC)), dim3(64), 0, st, a,
+                       nchain);
 }
 
 // ---------------------------------------------------------------- finish

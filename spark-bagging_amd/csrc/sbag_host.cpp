@@ -1703,6 +1703,7 @@ struct F64sGrow {
   EventTimer& tm;
   void* hist_root;        // level-0 integer histograms, slot = replica
   int64_t slot_words;     // Fmax * NB * 3
+  unsigned int cmax;      // largest draw count of a row
   double inv_scale, eps;  // the labels' fixed-point image: k 2^-s, |y - k 2^-s| <= eps
   // integer (count, Σ c k) histograms of node segments of `ent` into slots of `hist`
   std::function<int(const std::vector<std::pair<int64_t, int64_t>>&, const std::vector<ParentInfo>&,
@@ -1815,7 +1816,69 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       G.tm.end(h);
       TRY(d2h(c, so.data(), d_so, (size_t)M));
     }
-    // ---- exact fallback: flagged nodes, every feature summed in row order
+    // Buckets + routing of a task list (launch_fb_route): the chain sums of its first
+    // `nchain` tasks land at chist (task-major [NB][3]); nleft (optional) gets the left
+    // entries of every routing task.  Bucket space: the chain tasks' draws.
+    int cbits = 0;
+    while ((1u << cbits) <= G.cmax) cbits++;
+    auto run_tasks = [&](std::vector<F64Task>& tk, int nchain, int64_t nlabels, double* chist,
+                         std::vector<int64_t>* nleft_out) -> int {
+      if (tk.empty()) return SBAG_OK;
+      std::vector<F64TPiece> pcs;
+      for (size_t ti = 0; ti < tk.size(); ti++) {
+        tk[ti].piece0 = (int64_t)pcs.size();
+        for (int64_t x = tk[ti].a; x < tk[ti].b; x += kFbPiece)
+          pcs.push_back(F64TPiece{x, std::min(x + kFbPiece, tk[ti].b), (int32_t)ti, 0});
+        tk[ti].piece1 = (int64_t)pcs.size();
+      }
+      const int64_t np = (int64_t)pcs.size();
+      const int nt = (int)tk.size();
+      F64Task* d_tk;
+      F64TPiece* d_pc;
+      uint32_t *d_pcnt, *d_plcnt;
+      int64_t *d_pbase, *d_plbase, *d_nleft, *d_kboff;
+      double* d_bucket;
+      TRY(ws_typed(c, "fb_tasks", (size_t)nt, &d_tk));
+      TRY(ws_typed(c, "fb_pieces", (size_t)std::max<int64_t>(np, 1), &d_pc));
+      TRY(ws_typed(c, "fb_pcnt", (size_t)std::max<int64_t>(np, 1) * NB, &d_pcnt));
+      TRY(ws_typed(c, "fb_plcnt", (size_t)std::max<int64_t>(np, 1), &d_plcnt));
+      TRY(ws_typed(c, "fb_pbase", (size_t)std::max<int64_t>(np, 1) * NB, &d_pbase));
+      TRY(ws_typed(c, "fb_plbase", (size_t)std::max<int64_t>(np, 1), &d_plbase));
+      TRY(ws_typed(c, "fb_nleft", (size_t)nt, &d_nleft));
+      TRY(ws_typed(c, "fb_kboff", (size_t)nt * (NB + 1), &d_kboff));
+      TRY(ws_typed(c, "fb_bucket", (size_t)std::max<int64_t>(1, nlabels), &d_bucket));
+      TRY(h2d(c, d_tk, tk.data(), (size_t)nt));
+      TRY(h2d(c, d_pc, pcs.data(), pcs.size()));
+      F64BucketArgs ba{};
+      ba.cols = G.d_cols;
+      ba.cols_rstride = G.cols_rstride;
+      ba.npad = G.npad;
+      ba.tasks = d_tk;
+      ba.pieces = d_pc;
+      ba.NB = NB;
+      ba.ntasks = nt;
+      ba.ent_in = ent_cur;
+      ba.ent_out = ent_nxt;
+      ba.bucket = d_bucket;
+      ba.pcnt = d_pcnt;
+      ba.plcnt = d_plcnt;
+      ba.pbase = d_pbase;
+      ba.plbase = d_plbase;
+      ba.nleft = d_nleft;
+      ba.kb_off = d_kboff;
+      ba.y = G.ds->d_y64;
+      ba.chist = chist;
+      launch_fb_route(c->stream, ba, np, nchain, cbits);
+      HIP_TRY(hipGetLastError());
+      if (nleft_out) {
+        nleft_out->assign(tk.size(), 0);
+        TRY(d2h(c, nleft_out->data(), d_nleft, tk.size()));
+      }
+      return SBAG_OK;
+    };
+    // ---- exact fallback: flagged nodes, every feature's bins in Spark's row order (one
+    // bucketing + chain task per (node, feature); the node total too when the replica has
+    // no feature with splits), then k_f64_split over them, in batches of bounded bucket space
     std::vector<int> X, xi(M, -1);
     for (int i = 0; i < M; i++)
       if (so[i].flag) {
@@ -1824,17 +1887,24 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       }
     G.fallbacks += (int64_t)X.size();
     std::vector<F64SplitOut> xo(X.size());
-    if (!X.empty()) {
-      const int A = (int)X.size();
-      const int fpw_env = getenv("SBAG_F64_FPW") ? atoi(getenv("SBAG_F64_FPW")) : 64;
-      const int FPW = std::max(1, std::min(f64_hist_width(NB), fpw_env));
-      const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
-      const int split_below = getenv("SBAG_F64_SPLIT") ? atoi(getenv("SBAG_F64_SPLIT")) : 1024;
-      const int parts = (int64_t)A * ngroups < split_below ? 2 : 1;
+    static const bool walk_fallback = getenv("SBAG_F64_FALLBACK") && !strcmp(getenv("SBAG_F64_FALLBACK"), "hist");
+    for (size_t k0 = 0; k0 < X.size();) {
+      // a batch: nodes while their feature tasks' draws fit the budget (one node at least)
+      const double budget = (double)((int64_t)1 << 29);  // labels (4 GB)
+      size_t k1 = k0;
+      double used = 0;
+      while (k1 < X.size()) {
+        const LNode& q = cur[X[k1]];
+        const double need = q.n * (G.h_Fr[q.r] + 1);
+        if (k1 > k0 && used + need > budget) break;
+        used += need;
+        k1++;
+      }
+      const int A = (int)(k1 - k0);
       std::vector<F64Node> hn(A);
       std::vector<F64Chain> chain(A);
       for (int k = 0; k < A; k++) {
-        const LNode& q = cur[X[k]];
+        const LNode& q = cur[X[k0 + k]];
         hn[k] = F64Node{q.a, q.b, q.r, 0};
         const BtNode& n = trees[q.r][q.node];
         F64Chain ch{};
@@ -1852,14 +1922,18 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       TRY(ws_typed(c, "f64_nodes", (size_t)A, &d_nodes));
       TRY(ws_typed(c, "f64_chain", (size_t)A, &d_chain));
       TRY(ws_typed(c, "f64_sout", (size_t)A, &d_out));
-      TRY(ws_typed(c, "f64_hist", (size_t)std::min<int64_t>(A, batch) * node_words, &d_hist));
+      TRY(ws_typed(c, "f64_hist", (size_t)A * node_words, &d_hist));
       TRY(h2d(c, d_nodes, hn.data(), (size_t)A));
       TRY(h2d(c, d_chain, chain.data(), (size_t)A));
-      for (int64_t q0 = 0; q0 < A; q0 += batch) {
-        const int nq = (int)std::min<int64_t>(batch, A - q0);
+      int h = G.tm.begin(T_FIX);
+      if (walk_fallback) {  // SBAG_F64_FALLBACK=hist: the row-order walk of every feature
+        const int fpw_env = getenv("SBAG_F64_FPW") ? atoi(getenv("SBAG_F64_FPW")) : 64;
+        const int FPW = std::max(1, std::min(f64_hist_width(NB), fpw_env));
+        const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
+        const int parts = (int64_t)A * ngroups < 1024 ? 2 : 1;
         F64HistArgs ha{};
         ha.ent = ent_cur;
-        ha.nodes = d_nodes + q0;
+        ha.nodes = d_nodes;
         ha.y = G.ds->d_y64;
         ha.bins = G.d_bins;
         ha.bins_rstride = G.bins_rstride;
@@ -1873,25 +1947,63 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
         ha.bins_bytes = (double)G.N * G.S < 4294967295.0 ? (uint32_t)(G.N * G.S) : 0u;
         ha.yzero = (uint32_t)G.N;
         ha.hist = d_hist;
-        int h = G.tm.begin(T_FIX);
-        launch_f64_hist(c->stream, ha, nq, ngroups);
+        launch_f64_hist(c->stream, ha, A, ngroups);
         HIP_TRY(hipGetLastError());
-        F64SplitArgs sa{};
-        sa.hist = d_hist;
-        sa.nodes = d_nodes + q0;
-        sa.chain = d_chain + q0;
-        sa.Fr = G.d_Fr;
-        sa.nbins = G.d_nbins;
-        sa.Fmax = Fmax;
-        sa.NB = NB;
-        sa.min_inst = G.tp.min_instances_per_node;
-        sa.min_gain = G.tp.min_info_gain;
-        sa.out = d_out + q0;
-        launch_f64_split(c->stream, sa, nq);
-        HIP_TRY(hipGetLastError());
-        G.tm.end(h);
+      } else {
+        // tasks [k][Fmax + 1] (the chain sums land in k_f64_split's [node][Fmax + 1][NB][3]
+        // layout), run in chunks of consecutive tasks whose labels fit the budget
+        std::vector<F64Task> ft;
+        std::vector<int64_t> fdraws;
+        ft.reserve((size_t)A * (Fmax + 1));
+        for (int k = 0; k < A; k++) {
+          const LNode& q = cur[X[k0 + k]];
+          for (int fl = 0; fl <= Fmax; fl++) {
+            F64Task t{};
+            t.r = q.r;
+            t.s = -1;
+            t.part = 0;
+            const bool real = fl < G.h_Fr[q.r] || (fl == G.h_Fr[q.r] && f0[q.r] < 0);
+            if (real) {
+              t.a = q.a;
+              t.b = q.b;
+              t.col = fl < G.h_Fr[q.r] ? G.h_pos[(size_t)q.r * Fmax + fl] : -1;
+            } else {
+              t.a = t.b = q.a;  // empty: zero sums (never read by k_f64_split)
+              t.col = -1;
+            }
+            ft.push_back(t);
+            fdraws.push_back(real ? (int64_t)q.n : 0);
+          }
+        }
+        for (size_t t0 = 0; t0 < ft.size();) {
+          size_t t1 = t0;
+          int64_t kbc = 0;
+          while (t1 < ft.size() && (t1 == t0 || (double)(kbc + fdraws[t1]) <= budget)) {
+            ft[t1].kbase = kbc;
+            kbc += fdraws[t1];
+            t1++;
+          }
+          std::vector<F64Task> sub(ft.begin() + t0, ft.begin() + t1);
+          TRY(run_tasks(sub, (int)sub.size(), kbc, d_hist + t0 * (size_t)NB * 3, nullptr));
+          t0 = t1;
+        }
       }
-      TRY(d2h(c, xo.data(), d_out, (size_t)A));
+      F64SplitArgs sa{};
+      sa.hist = d_hist;
+      sa.nodes = d_nodes;
+      sa.chain = d_chain;
+      sa.Fr = G.d_Fr;
+      sa.nbins = G.d_nbins;
+      sa.Fmax = Fmax;
+      sa.NB = NB;
+      sa.min_inst = G.tp.min_instances_per_node;
+      sa.min_gain = G.tp.min_info_gain;
+      sa.out = d_out;
+      launch_f64_split(c->stream, sa, A);
+      HIP_TRY(hipGetLastError());
+      G.tm.end(h);
+      TRY(d2h(c, xo.data() + k0, d_out, (size_t)A));
+      k0 = k1;
     }
     // ---- 2. bucket + route tasks.  Pass 0: the decided nodes' chosen features (buckets and
     // routing), then the flagged split nodes (routing only); pass 1 (root only): the first
@@ -1905,7 +2017,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       t.a = q.a;
       t.b = q.b;
       t.kbase = chain ? kb[pass] : -1;
-      if (chain) kb[pass] += q.b - q.a;
+      if (chain) kb[pass] += (int64_t)q.n;  // one label per draw
       t.r = q.r;
       t.col = G.h_pos[(size_t)q.r * Fmax + fl];
       t.s = s;
@@ -1952,62 +2064,13 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       if (fn.t0 <= -2) fn.t0 = nchain0 + (-2 - fn.t0);  // pass-1 chain sums follow pass 0's
     const int nchain1 = (int)tasks[1].size();
     std::vector<F64SplitOut> fo(fin.size());
-    std::vector<int64_t> nleft(tasks[0].size(), 0);
+    std::vector<int64_t> nleft;
     if (!tasks[0].empty()) {
       double* d_chist;
       TRY(ws_typed(c, "fb_chist", (size_t)std::max(1, nchain0 + nchain1) * NB * 3, &d_chist));
-      uint64_t* d_entK;
-      TRY(ws_typed(c, "fb_entK", (size_t)std::max<int64_t>(1, std::max(kb[0], kb[1])), &d_entK));
       int h = G.tm.begin(T_CHAIN);
-      for (int pass = 0; pass < 2; pass++) {
-        std::vector<F64Task>& tk = tasks[pass];
-        if (tk.empty()) continue;
-        std::vector<F64TPiece> pcs;
-        for (size_t ti = 0; ti < tk.size(); ti++) {
-          tk[ti].piece0 = (int64_t)pcs.size();
-          for (int64_t x = tk[ti].a; x < tk[ti].b; x += kFbPiece)
-            pcs.push_back(F64TPiece{x, std::min(x + kFbPiece, tk[ti].b), (int32_t)ti, 0});
-          tk[ti].piece1 = (int64_t)pcs.size();
-        }
-        const int64_t np = (int64_t)pcs.size();
-        const int nt = (int)tk.size();
-        F64Task* d_tk;
-        F64TPiece* d_pc;
-        uint32_t *d_pcnt, *d_plcnt;
-        int64_t *d_pbase, *d_plbase, *d_nleft, *d_kboff;
-        TRY(ws_typed(c, "fb_tasks", (size_t)nt, &d_tk));
-        TRY(ws_typed(c, "fb_pieces", (size_t)std::max<int64_t>(np, 1), &d_pc));
-        TRY(ws_typed(c, "fb_pcnt", (size_t)std::max<int64_t>(np, 1) * NB, &d_pcnt));
-        TRY(ws_typed(c, "fb_plcnt", (size_t)std::max<int64_t>(np, 1), &d_plcnt));
-        TRY(ws_typed(c, "fb_pbase", (size_t)std::max<int64_t>(np, 1) * NB, &d_pbase));
-        TRY(ws_typed(c, "fb_plbase", (size_t)std::max<int64_t>(np, 1), &d_plbase));
-        TRY(ws_typed(c, "fb_nleft", (size_t)nt, &d_nleft));
-        TRY(ws_typed(c, "fb_kboff", (size_t)nt * (NB + 1), &d_kboff));
-        TRY(h2d(c, d_tk, tk.data(), (size_t)nt));
-        TRY(h2d(c, d_pc, pcs.data(), pcs.size()));
-        F64BucketArgs ba{};
-        ba.cols = G.d_cols;
-        ba.cols_rstride = G.cols_rstride;
-        ba.npad = G.npad;
-        ba.tasks = d_tk;
-        ba.pieces = d_pc;
-        ba.NB = NB;
-        ba.ntasks = nt;
-        ba.ent_in = ent_cur;
-        ba.ent_out = ent_nxt;
-        ba.entK = d_entK;
-        ba.pcnt = d_pcnt;
-        ba.plcnt = d_plcnt;
-        ba.pbase = d_pbase;
-        ba.plbase = d_plbase;
-        ba.nleft = d_nleft;
-        ba.kb_off = d_kboff;
-        ba.y = G.ds->d_y64;
-        ba.chist = d_chist + (pass == 0 ? 0 : (size_t)nchain0 * NB * 3);
-        launch_fb_route(c->stream, ba, np, pass == 0 ? nchain0 : nchain1);
-        HIP_TRY(hipGetLastError());
-        if (pass == 0) TRY(d2h(c, nleft.data(), d_nleft, nleft.size()));  // (pass 1 reuses the scratch)
-      }
+      TRY(run_tasks(tasks[0], nchain0, kb[0], d_chist, &nleft));
+      TRY(run_tasks(tasks[1], nchain1, kb[1], d_chist + (size_t)nchain0 * NB * 3, nullptr));
       G.tm.end(h);
       if (!fin.empty()) {
         F64FinishNode* d_fn;
@@ -3108,7 +3171,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     // dyadic, SBAG_F64=1) screen the splits; Spark's row-order fp64 sums give the stats
     F64sGrow G{c, ds, tp, R, N, Fmax, NB, S, h_Fr, h_nbins, thr, d_bins, bins_rstride, d_pos, d_Fr,
                d_nbins, h_pos, d_cols, cols_rstride, npad, entA, entB, cap, inbag, tm, hist_cur,
-               slot_words, std::ldexp(1.0, -lshift),
+               slot_words, cmax, std::ldexp(1.0, -lshift),
                ds->label_ok ? 0.0 : std::ldexp(1.0, -lshift - 1),
                [&](const std::vector<std::pair<int64_t, int64_t>>& segs, const std::vector<ParentInfo>& par,
                    const uint64_t* ent, void* hist) -> int {
