@@ -319,6 +319,25 @@ static int ensure_jump(sbag_ctx* c) {
 }
 
 // ---------------------------------------------------------------- dataset
+// A label column and its device images: the dataset's own, or (sbag_fit_booster) the
+// pseudo-residuals of one boosting iteration over the same rows
+struct LabelSet {
+  std::vector<double> y;
+  int32_t* d_labk = nullptr;              // labels as fixed point k = y * 2^shift
+  double* d_y64 = nullptr;                // fp64 labels on the device (f64 fits; built lazily)
+  int shift = 0;
+  bool label_ok = false;                  // representable as |k| < 2^23
+  int64_t kmin = 0, kmax = 0;
+  bool integral = false;                  // all labels integers >= 0 (classifiable)
+  // labels that are not dyadic (fp64 path): the fixed-point image k = round(y 2^ashift),
+  // |k| <= 2^22, which the integer histograms screen splits with (|y - k 2^-ashift| <=
+  // 2^-ashift-1), and the labels' largest |y| and y*y (the screen's error bounds)
+  bool approx_ok = false;
+  int ashift = 0;
+  int64_t akmin = 0, akmax = 0;
+  double ymax_abs = 0.0, ymax_sq = 0.0;
+};
+
 struct sbag_dataset {
   sbag_ctx* ctx = nullptr;
   int64_t N = 0;
@@ -328,20 +347,7 @@ struct sbag_dataset {
   std::vector<uint32_t> h_codes;          // wide datasets: the codes on the host too [N][S]
   std::vector<std::vector<double>> dict;  // sorted distinct values per feature (-0.0 == 0.0)
   std::vector<int32_t> zero_code;         // code of 0.0, -1 when absent
-  std::vector<double> y;
-  int32_t* d_labk = nullptr;              // labels as fixed point k = y * 2^shift
-  double* d_y64 = nullptr;                // fp64 labels on the device (f64 fits; built lazily)
-  int shift = 0;
-  bool label_ok = false;                  // representable as |k| < 2^23
-  int64_t kmin = 0, kmax = 0;
-  // labels that are not dyadic (fp64 path): the fixed-point image k = round(y 2^ashift),
-  // |k| <= 2^22, which the integer histograms screen splits with (|y - k 2^-ashift| <=
-  // 2^-ashift-1), and the labels' largest |y| and y*y (the screen's error bounds)
-  bool approx_ok = false;
-  int ashift = 0;
-  int64_t akmin = 0, akmax = 0;
-  double ymax_abs = 0.0, ymax_sq = 0.0;
-  bool integral = false;                  // all labels integers >= 0 (classifiable)
+  LabelSet lab;                           // the label column (owns its device images)
   double* d_dict = nullptr;
   int64_t* d_dict_off = nullptr;
   // Layouts derived from the codes alone, for fits whose bins are the codes: the
@@ -357,7 +363,7 @@ struct sbag_dataset {
   ~sbag_dataset() {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    for (void* p : {(void*)d_codes, (void*)d_labk, (void*)d_y64, (void*)d_dict, (void*)d_dict_off,
+    for (void* p : {(void*)d_codes, (void*)lab.d_labk, (void*)lab.d_y64, (void*)d_dict, (void*)d_dict_off,
                     (void*)d_cols, (void*)d_planes})
       if (p) (void)hipFree(p);
   }
@@ -368,19 +374,19 @@ static int32_t row_stride(int32_t F) {
   return (F + 127) / 128 * 128;
 }
 
-static void analyze_labels(sbag_dataset* ds) {
-  ds->label_ok = false;
-  ds->integral = true;
-  for (double v : ds->y)
+static void analyze_labels(LabelSet& L) {
+  L.label_ok = false;
+  L.integral = true;
+  for (double v : L.y)
     if (!(v >= 0 && v == std::floor(v) && v < 8388608.0)) {
-      ds->integral = false;
+      L.integral = false;
       break;
     }
-  for (int s = 0; s <= 40 && !ds->label_ok; s++) {
+  for (int s = 0; s <= 40 && !L.label_ok; s++) {
     bool ok = true;
     int64_t mn = 0, mx = 0;
     bool first = true;
-    for (double v : ds->y) {
+    for (double v : L.y) {
       if (!std::isfinite(v)) {
         ok = false;
         break;
@@ -399,53 +405,59 @@ static void analyze_labels(sbag_dataset* ds) {
       mx = std::max(mx, ki);
     }
     if (ok) {
-      ds->label_ok = true;
-      ds->shift = s;
-      ds->kmin = mn;
-      ds->kmax = mx;
+      L.label_ok = true;
+      L.shift = s;
+      L.kmin = mn;
+      L.kmax = mx;
     }
   }
-  ds->approx_ok = false;
-  ds->ymax_abs = ds->ymax_sq = 0.0;
+  L.approx_ok = false;
+  L.ymax_abs = L.ymax_sq = 0.0;
   bool finite = true;
-  for (double v : ds->y) {
+  for (double v : L.y) {
     if (!std::isfinite(v)) {
       finite = false;
       break;
     }
-    ds->ymax_abs = std::max(ds->ymax_abs, std::fabs(v));
-    ds->ymax_sq = std::max(ds->ymax_sq, v * v);
+    L.ymax_abs = std::max(L.ymax_abs, std::fabs(v));
+    L.ymax_sq = std::max(L.ymax_sq, v * v);
   }
-  if (!ds->label_ok && finite && ds->ymax_abs > 0.0) {
+  if (!L.label_ok && finite && L.ymax_abs > 0.0) {
     // 2^e <= max|y| < 2^(e+1): max|y| 2^(21-e) < 2^22
-    ds->ashift = 21 - std::ilogb(ds->ymax_abs);
+    L.ashift = 21 - std::ilogb(L.ymax_abs);
     int64_t mn = 0, mx = 0;
-    for (double v : ds->y) {
-      const int64_t k = (int64_t)std::nearbyint(std::ldexp(v, ds->ashift));
+    for (double v : L.y) {
+      const int64_t k = (int64_t)std::nearbyint(std::ldexp(v, L.ashift));
       mn = std::min(mn, k);
       mx = std::max(mx, k);
     }
-    ds->akmin = mn;
-    ds->akmax = mx;
-    ds->approx_ok = true;
+    L.akmin = mn;
+    L.akmax = mx;
+    L.approx_ok = true;
   }
 }
+static void analyze_labels(sbag_dataset* ds) { analyze_labels(ds->lab); }
 
-// the labels' fixed point image on the device: exact (dyadic labels) or the screening
-// approximation of the fp64 path (zeros when neither applies)
-static int upload_labels(sbag_dataset* ds) {
-  HIP_TRY(hipMalloc(&ds->d_labk, std::max<int64_t>(ds->N, 1) * 4));
-  if (!ds->label_ok && !ds->approx_ok) {
-    HIP_TRY(hipMemset(ds->d_labk, 0, (size_t)std::max<int64_t>(ds->N, 1) * 4));
+// the labels' fixed point image (exact for dyadic labels, else the screening approximation
+// of the fp64 path, else zeros) into dst [N] on the device
+static int labk_image(const LabelSet& L, int32_t* dst) {
+  const int64_t N = (int64_t)L.y.size();
+  if (!L.label_ok && !L.approx_ok) {
+    HIP_TRY(hipMemset(dst, 0, (size_t)std::max<int64_t>(N, 1) * 4));
     return SBAG_OK;
   }
-  std::vector<int32_t> k(ds->N);
-  if (ds->label_ok)
-    for (int64_t i = 0; i < ds->N; i++) k[i] = (int32_t)std::ldexp(ds->y[i], ds->shift);
+  std::vector<int32_t> k(N);
+  if (L.label_ok)
+    for (int64_t i = 0; i < N; i++) k[i] = (int32_t)std::ldexp(L.y[i], L.shift);
   else
-    for (int64_t i = 0; i < ds->N; i++) k[i] = (int32_t)std::nearbyint(std::ldexp(ds->y[i], ds->ashift));
-  HIP_TRY(hipMemcpy(ds->d_labk, k.data(), ds->N * 4, hipMemcpyHostToDevice));
+    for (int64_t i = 0; i < N; i++) k[i] = (int32_t)std::nearbyint(std::ldexp(L.y[i], L.ashift));
+  HIP_TRY(hipMemcpy(dst, k.data(), (size_t)N * 4, hipMemcpyHostToDevice));
   return SBAG_OK;
+}
+
+static int upload_labels(sbag_dataset* ds) {
+  HIP_TRY(hipMalloc(&ds->lab.d_labk, std::max<int64_t>(ds->N, 1) * 4));
+  return labk_image(ds->lab, ds->lab.d_labk);
 }
 
 static int upload_dict(sbag_dataset* ds) {
@@ -1013,7 +1025,7 @@ static int build_dataset(sbag_ctx* c, int64_t N, int32_t F, const DsSource& src,
                       hipMemcpyHostToDevice));
     if (cb == 4) std::memcpy((uint8_t*)ds->h_codes.data() + (size_t)r0 * row_bytes, buf.data(), (size_t)n * row_bytes);
   }
-  ds->y.assign(y, y + N);
+  ds->lab.y.assign(y, y + N);
   analyze_labels(ds.get());
   TRY(upload_labels(ds.get()));
   TRY(upload_dict(ds.get()));
@@ -1079,27 +1091,27 @@ int sbag_dataset_synthetic(sbag_ctx* c, int64_t N, int32_t F, uint64_t seed, int
   ds->zero_code.assign(F, 0);
   HIP_TRY(hipMalloc(&ds->d_codes, (size_t)N * ds->S + 256));
   HIP_TRY(hipMemset((uint8_t*)ds->d_codes + (size_t)N * ds->S, 0, 256));
-  HIP_TRY(hipMalloc(&ds->d_labk, (size_t)N * 4));
-  launch_synth(c->stream, (uint8_t*)ds->d_codes, ds->S, N, F, seed, num_classes, ds->d_labk);
+  HIP_TRY(hipMalloc(&ds->lab.d_labk, (size_t)N * 4));
+  launch_synth(c->stream, (uint8_t*)ds->d_codes, ds->S, N, F, seed, num_classes, ds->lab.d_labk);
   HIP_TRY(hipGetLastError());
   std::vector<int32_t> k(N);
-  TRY(d2h(c, k.data(), ds->d_labk, (size_t)N));
-  ds->shift = num_classes ? 0 : 6;
-  ds->y.resize(N);
-  ds->kmin = ds->kmax = k[0];
+  TRY(d2h(c, k.data(), ds->lab.d_labk, (size_t)N));
+  ds->lab.shift = num_classes ? 0 : 6;
+  ds->lab.y.resize(N);
+  ds->lab.kmin = ds->lab.kmax = k[0];
   for (int64_t i = 0; i < N; i++) {
-    ds->y[i] = std::ldexp((double)k[i], -ds->shift);
-    ds->kmin = std::min<int64_t>(ds->kmin, k[i]);
-    ds->kmax = std::max<int64_t>(ds->kmax, k[i]);
-    ds->ymax_abs = std::max(ds->ymax_abs, std::fabs(ds->y[i]));
-    ds->ymax_sq = std::max(ds->ymax_sq, ds->y[i] * ds->y[i]);
+    ds->lab.y[i] = std::ldexp((double)k[i], -ds->lab.shift);
+    ds->lab.kmin = std::min<int64_t>(ds->lab.kmin, k[i]);
+    ds->lab.kmax = std::max<int64_t>(ds->lab.kmax, k[i]);
+    ds->lab.ymax_abs = std::max(ds->lab.ymax_abs, std::fabs(ds->lab.y[i]));
+    ds->lab.ymax_sq = std::max(ds->lab.ymax_sq, ds->lab.y[i] * ds->lab.y[i]);
   }
-  ds->label_ok = true;
-  ds->integral = ds->kmin >= 0 && num_classes > 0;
+  ds->lab.label_ok = true;
+  ds->lab.integral = ds->lab.kmin >= 0 && num_classes > 0;
   if (num_classes == 0) {
-    ds->integral = true;
-    for (int64_t i = 0; i < N && ds->integral; i++)
-      if (ds->y[i] < 0 || ds->y[i] != std::floor(ds->y[i])) ds->integral = false;
+    ds->lab.integral = true;
+    for (int64_t i = 0; i < N && ds->lab.integral; i++)
+      if (ds->lab.y[i] < 0 || ds->lab.y[i] != std::floor(ds->lab.y[i])) ds->lab.integral = false;
   }
   TRY(upload_dict(ds.get()));
   *out = ds.release();
@@ -1115,7 +1127,7 @@ int sbag_dataset_info(const sbag_dataset* ds, int64_t* N, int32_t* F) {
 
 int sbag_dataset_labels(const sbag_dataset* ds, double* y) {
   if (!ds || !y) return fail(SBAG_EINVAL, "bad arguments");
-  std::copy(ds->y.begin(), ds->y.end(), y);
+  std::copy(ds->lab.y.begin(), ds->lab.y.end(), y);
   return SBAG_OK;
 }
 
@@ -1128,13 +1140,13 @@ int sbag_dataset_set_labels(sbag_dataset* ds, const double* y) {
   HIP_TRY(hipSetDevice(c->device));
   std::lock_guard<std::mutex> lk(ds->layout_mu);
   HIP_TRY(hipStreamSynchronize(c->stream));  // no fit of this context still reads the labels
-  ds->y.assign(y, y + ds->N);
+  ds->lab.y.assign(y, y + ds->N);
   analyze_labels(ds);
-  if (ds->d_labk) HIP_TRY(hipFree(ds->d_labk));
-  ds->d_labk = nullptr;
+  if (ds->lab.d_labk) HIP_TRY(hipFree(ds->lab.d_labk));
+  ds->lab.d_labk = nullptr;
   TRY(upload_labels(ds));
-  if (ds->d_y64) HIP_TRY(hipFree(ds->d_y64));
-  ds->d_y64 = nullptr;
+  if (ds->lab.d_y64) HIP_TRY(hipFree(ds->lab.d_y64));
+  ds->lab.d_y64 = nullptr;
   return SBAG_OK;
 }
 
@@ -1179,7 +1191,7 @@ int sbag_dataset_export(const sbag_dataset* ds, void* codes, int32_t codes_on_de
       o += (int64_t)d.size();
     }
   }
-  if (y) std::copy(ds->y.begin(), ds->y.end(), y);
+  if (y) std::copy(ds->lab.y.begin(), ds->lab.y.end(), y);
   return SBAG_OK;
 }
 
@@ -1237,7 +1249,7 @@ int sbag_dataset_import(sbag_ctx* c, int64_t N, int32_t F, int32_t S, int32_t cb
     ds->h_codes.resize((size_t)N * S);
     HIP_TRY(hipMemcpy(ds->h_codes.data(), ds->d_codes, bytes, hipMemcpyDeviceToHost));
   }
-  ds->y.assign(y, y + N);
+  ds->lab.y.assign(y, y + N);
   analyze_labels(ds.get());
   TRY(upload_labels(ds.get()));
   *out = ds.release();
@@ -1412,7 +1424,15 @@ static double bins_budget(sbag_ctx* c) {
   return 0.4 * (double)tot / std::max(1, c->concurrent_parts);
 }
 
-static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out);
+// sbag_fit_booster's base-learner fit: one learner whose bag, subspace and labels are given
+// (GBM*.train: the iteration's bag column, its subspace, the pseudo-residuals)
+struct FitExt {
+  const uint8_t* counts;  // host [N]
+  std::vector<int32_t> sub;
+  const LabelSet* lab;    // labels with their device images
+};
+static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out,
+                     const FitExt* ext = nullptr);
 
 // Bins are u8 codes, so a feature may have at most 256 bins (255 thresholds).  Spark's
 // findSplitsForContinuousFeature can return maxBins thresholds when the split-finding sample
@@ -1681,6 +1701,7 @@ BtRet bt_emit(const std::vector<BtNode>& nodes, int idx, HTree& t) {
 struct F64sGrow {
   sbag_ctx* c;
   sbag_dataset* ds;
+  const LabelSet& lab;    // the fit's labels (the dataset's, or a booster's residuals)
   const sbag_tree_params& tp;
   int R;
   int64_t N;
@@ -1718,23 +1739,28 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   sbag_ctx* c = G.c;
   const int R = G.R, Fmax = G.Fmax, NB = G.NB, D = G.tp.max_depth;
   const int64_t cap = G.cap;
-  // the labels on the device, once per dataset, published only when complete (+ one +0.0
-  // at index N: the label of k_f64_hist's padding entries)
-  {
+  // the labels on the device, once per label set, published only when complete (+ one
+  // +0.0 at index N: the label of k_f64_hist's padding entries)
+  double* d_y64 = nullptr;
+  if (&G.lab != &G.ds->lab) {  // a booster's residuals: uploaded by sbag_fit_booster
+    d_y64 = G.lab.d_y64;
+    if (!d_y64) return fail(SBAG_EDEVICE, "internal: booster labels not on the device");
+  } else {
     std::lock_guard<std::mutex> lk(G.ds->layout_mu);
-    if (!G.ds->d_y64) {
+    if (!G.ds->lab.d_y64) {
       double* p = nullptr;
       HIP_TRY(hipMalloc(&p, (size_t)(G.N + 1) * 8));
-      if (hipMemcpy(p, G.ds->y.data(), (size_t)G.N * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      if (hipMemcpy(p, G.ds->lab.y.data(), (size_t)G.N * 8, hipMemcpyHostToDevice) != hipSuccess ||
           hipMemset(p + G.N, 0, 8) != hipSuccess) {
         (void)hipFree(p);
         return fail(SBAG_EDEVICE, "labels could not be copied to the device");
       }
-      G.ds->d_y64 = p;
+      G.ds->lab.d_y64 = p;
     }
+    d_y64 = G.ds->lab.d_y64;
   }
   const double u = std::ldexp(1.0, -53);
-  const double M1 = G.ds->ymax_abs, M2 = G.ds->ymax_sq, Msq = std::max(M2, M1 * M1);
+  const double M1 = G.lab.ymax_abs, M2 = G.lab.ymax_sq, Msq = std::max(M2, M1 * M1);
   // gamma_K of a node of n draws (inf when K u >= 1: every screen then flags)
   auto gam = [&](double n) {
     const double k = (n + NB + 2.0) * u;
@@ -1866,7 +1892,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.plbase = d_plbase;
       ba.nleft = d_nleft;
       ba.kb_off = d_kboff;
-      ba.y = G.ds->d_y64;
+      ba.y = d_y64;
       ba.chist = chist;
       launch_fb_route(c->stream, ba, np, nchain, cbits);
       HIP_TRY(hipGetLastError());
@@ -1934,7 +1960,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
         F64HistArgs ha{};
         ha.ent = ent_cur;
         ha.nodes = d_nodes;
-        ha.y = G.ds->d_y64;
+        ha.y = d_y64;
         ha.bins = G.d_bins;
         ha.bins_rstride = G.bins_rstride;
         ha.S = G.S;
@@ -2204,7 +2230,9 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   return SBAG_OK;
 }
 
-static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
+static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out,
+                     const FitExt* ext) {
+  const LabelSet& lab = ext ? *ext->lab : ds->lab;
   const sbag_tree_params& tp = fp->tree;
   TRY(check_sampler(&fp->sampler));
   if (tp.max_depth < 0 || tp.max_depth > 30)
@@ -2223,18 +2251,18 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   // fp64 path (f64 mode, sbag_f64s.hip / sbag_f64.hip): Spark's sums depend on their order
   // there. SBAG_F64=1 forces it on dyadic labels too (both paths then agree bit for bit).
   const bool force_f64 = getenv("SBAG_F64") && atoi(getenv("SBAG_F64")) != 0;
-  const bool f64 = !gini && (!ds->label_ok || force_f64);
+  const bool f64 = !gini && (!lab.label_ok || force_f64);
   if (f64) {
-    for (double v : ds->y)
+    for (double v : lab.y)
       if (!std::isfinite(v)) return fail(SBAG_EINVAL, "labels must be finite");
-    if (!ds->label_ok && !ds->approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
+    if (!lab.label_ok && !lab.approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
   }
   // the labels' fixed-point image in the entries: exact for dyadic labels, else (f64 path)
   // the screening approximation k = round(y 2^ashift)
-  const int lshift = ds->label_ok ? ds->shift : ds->ashift;
-  const int64_t lkmin = ds->label_ok ? ds->kmin : ds->akmin;
-  const int64_t lkmax = ds->label_ok ? ds->kmax : ds->akmax;
-  if (gini && !ds->integral)
+  const int lshift = lab.label_ok ? lab.shift : lab.ashift;
+  const int64_t lkmin = lab.label_ok ? lab.kmin : lab.akmin;
+  const int64_t lkmax = lab.label_ok ? lab.kmax : lab.akmax;
+  if (gini && !lab.integral)
     return fail(SBAG_EINVAL, "Classifier was given dataset with invalid label: labels must be "
                              "integers in [0, 2^23)");
   HIP_TRY(hipSetDevice(c->device));
@@ -2254,6 +2282,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   std::vector<std::vector<int32_t>> sub(R);
   int Fmax = 0;
   for (int r = 0; r < R; r++) {
+    if (ext) {  // the booster's subspace (R = 1)
+      sub[r] = ext->sub;
+      Fmax = std::max(Fmax, (int)ext->sub.size());
+      continue;
+    }
     std::vector<int32_t> idx(F);
     int n = 0;
     TRY(sbag_subspace(sratio, F, (int64_t)((uint64_t)fp->sampler.seed + (uint64_t)(int64_t)(lb + r)),
@@ -2291,7 +2324,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   TRY(ws_typed(c, "counts", (size_t)R * N, &d_counts));
   {
     int h = tm.begin(T_SAMPLE);
-    TRY(run_sampler(c, &fp->sampler, poff, N, d_counts));
+    if (ext)  // the booster's bag column
+      TRY(h2d(c, d_counts, ext->counts, (size_t)N));
+    else
+      TRY(run_sampler(c, &fp->sampler, poff, N, d_counts));
     tm.end(h);
   }
   // ---- 2. in-bag entry lists (two ping-pong buffers per replica, capacity N)
@@ -2313,9 +2349,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       TRY(ws_typed(c, "f64_ncnt", (size_t)R * compact_ordered_chunks(N), &d_ncnt));
       TRY(ws_typed(c, "f64_cbase", (size_t)R * compact_ordered_chunks(N), &d_cbase));
       launch_chunk_draws(c->stream, d_counts, N, R, d_ncnt, d_wsum, d_cmax);
-      launch_compact_ordered(c->stream, d_counts, ds->d_labk, N, R, entA, cap, d_ncnt, d_cbase, d_inbag);
+      launch_compact_ordered(c->stream, d_counts, lab.d_labk, N, R, entA, cap, d_ncnt, d_cbase, d_inbag);
     } else {
-      launch_compact(c->stream, d_counts, N, R, ds->d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
+      launch_compact(c->stream, d_counts, N, R, lab.d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
                      d_sqsum);
     }
     HIP_TRY(hipGetLastError());
@@ -2396,7 +2432,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     h_par[r] = ParentInfo{r, -1, 0, 0, 0, r, 0, 0};
     seg[r] = {(int64_t)r * cap, (int64_t)r * cap + (int64_t)inbag[r]};
   }
-  const int NS = gini ? (int)ds->kmax + 1 : 3;
+  const int NS = gini ? (int)lab.kmax + 1 : 3;
   if (NS > kMaxHostNS) return fail(SBAG_EUNSUPPORTED, "more than 4095 classes");
   const size_t word_bytes = gini ? 4 : 8;
   HistWork work;
@@ -3169,10 +3205,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   if (f64) {
     // the integer histograms of the labels' fixed-point image (exact when the labels are
     // dyadic, SBAG_F64=1) screen the splits; Spark's row-order fp64 sums give the stats
-    F64sGrow G{c, ds, tp, R, N, Fmax, NB, S, h_Fr, h_nbins, thr, d_bins, bins_rstride, d_pos, d_Fr,
+    F64sGrow G{c, ds, lab, tp, R, N, Fmax, NB, S, h_Fr, h_nbins, thr, d_bins, bins_rstride, d_pos, d_Fr,
                d_nbins, h_pos, d_cols, cols_rstride, npad, entA, entB, cap, inbag, tm, hist_cur,
                slot_words, cmax, std::ldexp(1.0, -lshift),
-               ds->label_ok ? 0.0 : std::ldexp(1.0, -lshift - 1),
+               lab.label_ok ? 0.0 : std::ldexp(1.0, -lshift - 1),
                [&](const std::vector<std::pair<int64_t, int64_t>>& segs, const std::vector<ParentInfo>& par,
                    const uint64_t* ent, void* hist) -> int {
                  ha.ent_in = ent;
@@ -3236,7 +3272,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     *out = forest.release();
     return SBAG_OK;
   }
-  const double inv_scale = std::ldexp(1.0, -ds->shift), inv_scale2 = std::ldexp(1.0, -2 * ds->shift);
+  const double inv_scale = std::ldexp(1.0, -lab.shift), inv_scale2 = std::ldexp(1.0, -2 * lab.shift);
   uint64_t* ent_cur = entA;
   uint64_t* ent_nxt = entB;
   // Tile-resident gini entries (C5's class tiles): the root's class-tile grouping is kept
@@ -3404,7 +3440,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         if (level == 0) {
           const int64_t* tot = &sst[(size_t)i * NS];
           n.stats.assign(tot, tot + NS);
-          n.impurity = Calc{n.stats.data(), NS, gini, ds->shift}.impurity();
+          n.impurity = Calc{n.stats.data(), NS, gini, lab.shift}.impurity();
         }
         for (int k = 0; k < NS; k++) rig[k] = n.stats[k] - lef[k];
         const SplitOut& so = sout[i];
@@ -3432,8 +3468,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
           L.impurity = sout[i].imp_l;
           Rn.impurity = sout[i].imp_r;
         } else {
-          L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
-          Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
+          L.impurity = Calc{L.stats.data(), NS, gini, lab.shift}.impurity();
+          Rn.impurity = Calc{Rn.stats.data(), NS, gini, lab.shift}.impurity();
         }
         wl = wl && L.impurity != 0.0;
         wr = wr && Rn.impurity != 0.0;
@@ -3638,8 +3674,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         } else {
           L.stats[2] = (int64_t)sql[q];
           Rn.stats[2] = (int64_t)(psq - sql[q]);
-          L.impurity = Calc{L.stats.data(), NS, gini, ds->shift}.impurity();
-          Rn.impurity = Calc{Rn.stats.data(), NS, gini, ds->shift}.impurity();
+          L.impurity = Calc{L.stats.data(), NS, gini, lab.shift}.impurity();
+          Rn.impurity = Calc{Rn.stats.data(), NS, gini, lab.shift}.impurity();
           // Spark's gain of the chosen split (calculateImpurityStats, operation order)
           HNode& n = trees[sp.r][sp.ni];
           const double lc = (double)L.stats[0], rc = (double)Rn.stats[0];
@@ -3691,8 +3727,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       }
       int hs = -1;
       if (wl && wr) {
-        const bool small_left = Calc{L.stats.data(), NS, gini, ds->shift}.count() <=
-                                Calc{Rn.stats.data(), NS, gini, ds->shift}.count();
+        const bool small_left = Calc{L.stats.data(), NS, gini, lab.shift}.count() <=
+                                Calc{Rn.stats.data(), NS, gini, lab.shift}.count();
         hs = small_left ? sl : sr;
         triples.push_back(small_left ? sr : sl);  // dst (larger child)
         triples.push_back(sp.slot);               // parent slot (current level)
@@ -3791,12 +3827,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         t.sub = sub[r];
         t.exact = exact[r];
         t.ns = ns_of[r];
-        emit(trees[r], 0, t, NS, gini, ds->shift, ns_of[r]);
+        emit(trees[r], 0, t, NS, gini, lab.shift, ns_of[r]);
       }
     };
     c->pool.run(nth, work);
   }
-  forest->nclasses = gini ? std::max(nclasses, (int)ds->kmax + 1) : 0;
+  forest->nclasses = gini ? std::max(nclasses, (int)lab.kmax + 1) : 0;
   double cats[T_NCAT] = {0};
   tm.collect(cats, nullptr, -1);
   if (trace) {
@@ -4437,8 +4473,6 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
   if (tp.min_instances_per_node < 1)
     return fail(SBAG_EINVAL, "minInstancesPerNode given invalid value (must be >= 1)");
   if (!(tp.min_info_gain >= 0.0)) return fail(SBAG_EINVAL, "minInfoGain given invalid value");
-  if (ds->code_bytes == 4)
-    return fail(SBAG_EUNSUPPORTED, "booster fit on features with more than 65536 distinct values");
   const int64_t N = ds->N;
   const int F = ds->F;
   if (N >= ((int64_t)1 << 32)) return fail(SBAG_EUNSUPPORTED, "booster fit on 2^32 rows or more");
@@ -4461,6 +4495,49 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
   std::vector<int64_t> poff;
   TRY(check_partitions(bp->num_partitions, bp->partition_offsets, N, poff));
   HIP_TRY(hipSetDevice(c->device));
+  static const bool bt_engine = getenv("SBAG_BOOSTER_ENGINE") && !strcmp(getenv("SBAG_BOOSTER_ENGINE"), "bt");
+  if (!bt_engine) {
+    // the bagging engine with one learner (fit_range): the iteration's bag column and
+    // subspace, its residuals as labels -- screened fp64 splits and row-order sums
+    // (sbag_f64s.hip) for real-valued residuals, the integer engine for dyadic ones
+    {
+      int64_t n_items = 0;
+      for (int64_t r = 0; r < N; r++) n_items += bp->counts[r];
+      if (n_items == 0)
+        return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
+                                 "empty one.");
+    }
+    LabelSet lab;
+    lab.y.assign(labels, labels + N);
+    analyze_labels(lab);
+    TRY(ws_typed(c, "bt_labk", (size_t)N, &lab.d_labk));
+    TRY(labk_image(lab, lab.d_labk));
+    TRY(ws_typed(c, "bt_y64", (size_t)N + 1, &lab.d_y64));
+    TRY(h2d(c, lab.d_y64, labels, (size_t)N));
+    HIP_TRY(hipMemsetAsync(lab.d_y64 + N, 0, 8, c->stream));
+    FitExt ext{bp->counts, sub, &lab};
+    sbag_fit_params fp{};
+    fp.sampler.replacement = 1;
+    fp.sampler.sample_ratio = 1.0;
+    fp.sampler.seed = 0;
+    fp.sampler.learner_begin = 0;
+    fp.sampler.learner_end = 1;
+    fp.subspace_ratio = 1.0;
+    fp.subspace_bug_compat = 0;
+    fp.num_partitions = bp->num_partitions;
+    fp.partition_offsets = bp->partition_offsets;
+    fp.tree = tp;
+    sbag_forest* f = nullptr;
+    const int rc = fit_range(c, const_cast<sbag_dataset*>(ds), &fp, &f, &ext);
+    if (rc == kSplitRange) return fail(SBAG_EUNSUPPORTED, "the booster's bins exceed the device budget");
+    TRY(rc);
+    *out = f;
+    return SBAG_OK;
+  }
+  // SBAG_BOOSTER_ENGINE=bt: the round-3 booster engine (one lane per (node, feature) walking
+  // the node's rows in order), kept for A/B
+  if (ds->code_bytes == 4)
+    return fail(SBAG_EUNSUPPORTED, "booster fit on features with more than 65536 distinct values");
   const int D = tp.max_depth;
   // in-bag rows in row order; numExamples of the subbag = sum of the counts
   std::vector<uint32_t> rows;
