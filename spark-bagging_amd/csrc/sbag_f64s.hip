@@ -212,7 +212,8 @@ __device__ __forceinline__ uint32_t task_bin(const uint8_t* col, uint64_t e) {
   return col ? (uint32_t)col[(uint32_t)e] : 0u;
 }
 
-// per piece: draws per bin of the task's feature, entries going left (bin <= s)
+// per piece: draws per bin of the task's feature, entries going left (bin <= s).  Each
+// thread takes 4 entries per step, their loads and gathers issued before the atomics.
 __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   const F64TPiece pc = A.pieces[blockIdx.x];
   const F64Task t = A.tasks[pc.task];
@@ -223,11 +224,25 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   block_sync();
   const uint8_t* col = t.col >= 0 ? task_col(A, t) : nullptr;
   uint32_t nl = 0;
-  for (int64_t i = pc.a + tid; i < pc.b; i += 256) {
-    const uint64_t e = A.ent_in[i];
-    const uint32_t bin = task_bin(col, e);
-    atomicAdd(&s_c[bin], (uint32_t)(e >> 32) & 0xffu);
-    nl += bin <= (uint32_t)t.s ? 1u : 0u;
+  constexpr int U = 4;
+  for (int64_t i0 = pc.a; i0 < pc.b; i0 += 256 * U) {
+    uint64_t e[U];
+    uint32_t bin[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + u * 256 + tid;
+      e[u] = i < pc.b ? A.ent_in[i] : 0ull;  // count 0 past the piece
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) bin[u] = task_bin(col, e[u]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t c = (uint32_t)(e[u] >> 32) & 0xffu;
+      if (c) {
+        atomicAdd(&s_c[bin[u]], c);
+        nl += bin[u] <= (uint32_t)t.s ? 1u : 0u;
+      }
+    }
   }
   for (int o = 32; o > 0; o >>= 1) nl += __shfl_down(nl, o);
   if ((tid & 63) == 0) s_l[tid >> 6] = nl;
@@ -279,7 +294,9 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
 // draws of the round's earlier rows of the same bin -- their counts summed over the lanes
 // below with the same bin, from ballots over the bin's and the count's bits) and, for
 // split nodes, every entry to its child (left from the segment start, right after the left
-// block, both in row order)
+// block, both in row order).  Software-pipelined: a round's entries are loaded two rounds
+// ahead and their bin and label gathered one round ahead, so the gathers' latency overlaps
+// the previous round's ballots and stores.
 __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits,
                                                     int cbits) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -300,14 +317,24 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
   const uint8_t* col = t.col >= 0 ? task_col(A, t) : nullptr;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  auto ld_e = [&](int64_t i0) -> uint64_t {
+    const int64_t i = i0 + lane;
+    return i < pc.b ? A.ent_in[i] : 0ull;
+  };
+  // round k: (e0, bin0, y0); round k + 1: e1 (its bin and label are gathered during round k)
+  uint64_t e0 = ld_e(pc.a), e1 = ld_e(pc.a + 64);
+  uint32_t bin0 = task_bin(col, e0);
+  double y0 = chain ? A.y[(uint32_t)e0] : 0.0;
   for (int64_t i0 = pc.a; i0 < pc.b; i0 += 64) {
+    const uint64_t e2 = ld_e(i0 + 128);
+    const uint32_t bin1 = task_bin(col, e1);
+    const double y1 = chain ? A.y[(uint32_t)e1] : 0.0;
     const int64_t i = i0 + lane;
     const bool valid = i < pc.b;
-    const uint64_t e = valid ? A.ent_in[i] : 0ull;
-    const uint32_t bin = valid ? task_bin(col, e) : 0u;
+    const uint64_t e = e0;
+    const uint32_t bin = valid ? bin0 : 0u;
     if (chain) {
       const uint32_t c = (uint32_t)(e >> 32) & 0xffu;  // 0 past the piece
-      const double y = valid ? A.y[(uint32_t)e] : 0.0;
       uint64_t eq = __ballot(valid);
       for (int k = 0; k < nbits; k++) {
         const bool bit = (bin >> k) & 1u;
@@ -322,7 +349,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
         cnt += (int64_t)__popcll(m) << k;
       }
       const int64_t base = valid ? sb[bin] : 0;
-      for (uint32_t k = 0; k < c; k++) A.bucket[base + rank + k] = y;
+      for (uint32_t k = 0; k < c; k++) A.bucket[base + rank + k] = y0;
       const bool last = valid && (eq & ~(lt | (1ull << lane))) == 0ull;  // highest lane of its bin
       if (last) sb[bin] = base + cnt;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -339,6 +366,10 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
       }
       lrun += __popcll(lm);
     }
+    e0 = e1;
+    bin0 = bin1;
+    y0 = y1;
+    e1 = e2;
   }
 }
 
