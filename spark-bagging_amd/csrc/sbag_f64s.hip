@@ -18,12 +18,13 @@
 //                  every feature in row order, then k_f64_split).
 //   k_fb_count / k_fb_scan / k_fb_scatter   for every decided node (and, at the root,
 //                  its first feature with splits, whose bins give Spark's parent stats):
-//                  a stable bucketing of the node's draws (row order) by the chosen
-//                  feature's bin, each draw's label written out, fused with the stable two-way partition of
+//                  a stable bucketing of the node's entries (row order) by the chosen
+//                  feature's bin, fused with the stable two-way partition of
 //                  every split node into its children (left |= bin <= s), which keeps the
 //                  children's entries in row order for the next level
-//   k_fb_chain     one lane per (task, bin): the bucket's draws in row order (a row drawn
-//                  c times is c consecutive labels) -- Spark's cell sums bit for bit
+//   k_fb_chain     one lane per (task, bin): the bucket's rows in row order, each label
+//                  added count times (a row drawn c times is c consecutive rows) --
+//                  Spark's cell sums bit for bit
 //   k_fb_finish    binsToBestSplit over the chosen feature's exact bins (prefixes in bin
 //                  order, right = total - left, calculateImpurityStats with the node's
 //                  chained stats): the node's gain, impurity and children calculators
@@ -212,8 +213,31 @@ __device__ __forceinline__ uint32_t task_bin(const uint8_t* col, uint64_t e) {
   return col ? (uint32_t)col[(uint32_t)e] : 0u;
 }
 
-// per piece: draws per bin of the task's feature, entries going left (bin <= s).  Each
-// thread takes 4 entries per step, their loads and gathers issued before the atomics.
+// Buffer resources make every lane's gather and store the same instruction whatever its
+// entry: an offset past the resource's size reads 0 and drops a store.  (Exec-masked
+// branches around memory operations leave the compiler's vmcnt counting uncertain on the
+// merged path, and it then waits for every outstanding load and store.)
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(uint32_t)bytes, 0x00020000);
+}
+// the task's bin column (rows < 2^32 bytes); the node-total task (col < 0): size 0, bin 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t task_col_rsrc(const F64BucketArgs& A, const F64Task& t) {
+  return t.col >= 0 ? rsrc_of(task_col(A, t), (uint64_t)A.npad) : rsrc_of(A.cols, 0);
+}
+__device__ __forceinline__ uint32_t rbin(__amdgpu_buffer_rsrc_t rc, uint64_t e) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rc, (int)(uint32_t)e, 0, 0);
+}
+__device__ __forceinline__ void rstore64(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t v) {
+  v2u32 w;
+  w.x = (uint32_t)v;
+  w.y = (uint32_t)(v >> 32);
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, (int)off, 0, 0);
+}
+
+// per piece: entries per bin of the task's feature, entries going left (bin <= s).  Each
+// thread takes 4 entries per step, their loads (clamped indices: no branches, so the
+// gathers are issued back to back) and gathers before the atomics.
 __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   const F64TPiece pc = A.pieces[blockIdx.x];
   const F64Task t = A.tasks[pc.task];
@@ -222,27 +246,23 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   __shared__ uint32_t s_l[4];
   for (int b = tid; b < NB; b += 256) s_c[b] = 0u;
   block_sync();
-  const uint8_t* col = t.col >= 0 ? task_col(A, t) : nullptr;
+  const __amdgpu_buffer_rsrc_t rc = task_col_rsrc(A, t);
   uint32_t nl = 0;
   constexpr int U = 4;
+  const int64_t last = pc.b - 1;
   for (int64_t i0 = pc.a; i0 < pc.b; i0 += 256 * U) {
     uint64_t e[U];
     uint32_t bin[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int64_t i = i0 + u * 256 + tid;
-      e[u] = i < pc.b ? A.ent_in[i] : 0ull;  // count 0 past the piece
-    }
+    for (int u = 0; u < U; u++) e[u] = A.ent_in[min(i0 + u * 256 + tid, last)];
 #pragma unroll
-    for (int u = 0; u < U; u++) bin[u] = task_bin(col, e[u]);
+    for (int u = 0; u < U; u++) bin[u] = rbin(rc, e[u]);
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t c = (uint32_t)(e[u] >> 32) & 0xffu;
-      if (c) {
-        atomicAdd(&s_c[bin[u]], c);
+    for (int u = 0; u < U; u++)
+      if (i0 + u * 256 + tid < pc.b) {
+        atomicAdd(&s_c[bin[u]], 1u);
         nl += bin[u] <= (uint32_t)t.s ? 1u : 0u;
       }
-    }
   }
   for (int o = 32; o > 0; o >>= 1) nl += __shfl_down(nl, o);
   if ((tid & 63) == 0) s_l[tid >> 6] = nl;
@@ -251,7 +271,7 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   if (tid == 0) A.plcnt[blockIdx.x] = s_l[0] + s_l[1] + s_l[2] + s_l[3];
 }
 
-// per task: bucket bounds (bins in order, each bin's draws in row order), each piece's
+// per task: bucket bounds (bins in order, each bin's entries in row order), each piece's
 // first position per bin, left entries before each piece, the task's left total
 __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
   const int task = blockIdx.x, tid = threadIdx.x, NB = A.NB;
@@ -290,16 +310,18 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
   }
 }
 
-// one wave per piece: every draw's label to its bucket (stable: a row's draws after the
-// draws of the round's earlier rows of the same bin -- their counts summed over the lanes
-// below with the same bin, from ballots over the bin's and the count's bits) and, for
-// split nodes, every entry to its child (left from the segment start, right after the left
-// block, both in row order).  Software-pipelined: a round's entries are loaded two rounds
-// ahead and their bin and label gathered one round ahead, so the gathers' latency overlaps
-// the previous round's ballots and stores.
-__global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits,
-                                                    int cbits) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// one wave per piece: every entry to its bucket (stable: its rank among the round's
+// entries of the same bin, from ballots over the bin's bits) and, for split nodes, to its
+// child (left from the segment start, right after the left block, both in row order).
+// Every lane issues the same memory operations each round (loads at clamped indices, one
+// bucket store, one child store, buffer operations whose out-of-range offsets are dropped),
+// so the compiler's vmcnt waits stay counted.  (The wave's LDS operations on sb execute in
+// order, and the compiler keeps a store to sb[x] before a later load of sb[y] it cannot
+// prove distinct: no fence, which would drain the vector memory counter too.)
+__global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits) {
+  // (the wave index in an SGPR: the piece, its task and the buffer resources built from them
+  // are then wave-uniform, with no per-lane waterfall loop around the buffer operations)
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t pi = (int64_t)blockIdx.x * 4 + wv;
   __shared__ int64_t s_base[4][256];
   if (pi >= npieces) return;  // whole waves only; no block-wide barrier below
@@ -308,81 +330,69 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const int NB = A.NB;
   const bool chain = t.kbase >= 0;
   int64_t* sb = s_base[wv];
-  if (chain)
-    for (int b = lane; b < NB; b += 64) sb[b] = A.pbase[pi * NB + b];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int b = lane; b < NB; b += 64) sb[b] = chain ? A.pbase[pi * NB + b] : 0;
   int64_t lrun = t.part ? A.plbase[pi] : 0;
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
-  const uint8_t* col = t.col >= 0 ? task_col(A, t) : nullptr;
+  const __amdgpu_buffer_rsrc_t rc = task_col_rsrc(A, t);
+  // the task's buckets and its children's segment (each < 4 GB: a node's entries)
+  const __amdgpu_buffer_rsrc_t rk = rsrc_of(A.bucket + (chain ? t.kbase : 0), chain ? (uint64_t)(t.b - t.a) * 8 : 0);
+  const __amdgpu_buffer_rsrc_t ro = rsrc_of(A.ent_out + t.a, t.part ? (uint64_t)(t.b - t.a) * 8 : 0);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  auto ld_e = [&](int64_t i0) -> uint64_t {
-    const int64_t i = i0 + lane;
-    return i < pc.b ? A.ent_in[i] : 0ull;
-  };
-  // round k: (e0, bin0, y0); round k + 1: e1 (its bin and label are gathered during round k)
-  uint64_t e0 = ld_e(pc.a), e1 = ld_e(pc.a + 64);
-  uint32_t bin0 = task_bin(col, e0);
-  double y0 = chain ? A.y[(uint32_t)e0] : 0.0;
-  for (int64_t i0 = pc.a; i0 < pc.b; i0 += 64) {
-    const uint64_t e2 = ld_e(i0 + 128);
-    const uint32_t bin1 = task_bin(col, e1);
-    const double y1 = chain ? A.y[(uint32_t)e1] : 0.0;
-    const int64_t i = i0 + lane;
-    const bool valid = i < pc.b;
-    const uint64_t e = e0;
-    const uint32_t bin = valid ? bin0 : 0u;
-    if (chain) {
-      const uint32_t c = (uint32_t)(e >> 32) & 0xffu;  // 0 past the piece
+  const int64_t last = pc.b - 1;
+  // kScU rounds of 64 entries per step: all their entry loads, then all their bin
+  // gathers, then the rounds' ballots and stores -- one memory latency per step, not per
+  // round (vmcnt counts stores and loads in order on gfx9, so loads carried across steps
+  // would wait for the stores issued after them anyway)
+  constexpr int kScU = 8;
+  for (int64_t i0 = pc.a; i0 < pc.b; i0 += 64 * kScU) {
+    uint64_t ev[kScU];
+    uint32_t bv[kScU];
+#pragma unroll
+    for (int u = 0; u < kScU; u++) ev[u] = A.ent_in[min(i0 + 64 * u + lane, last)];
+#pragma unroll
+    for (int u = 0; u < kScU; u++) bv[u] = rbin(rc, ev[u]);
+#pragma unroll
+    for (int u = 0; u < kScU; u++) {
+      const int64_t i = i0 + 64 * u + lane;
+      const bool valid = i < pc.b;
+      const uint64_t e = ev[u];
+      const uint32_t bin = valid ? bv[u] : 0u;
+      // both stores every round, whatever the task does (a task without buckets or
+      // without children has a zero-size resource: the store is dropped) -- no branch
       uint64_t eq = __ballot(valid);
       for (int k = 0; k < nbits; k++) {
         const bool bit = (bin >> k) & 1u;
         const uint64_t m = __ballot(bit);
         eq &= bit ? m : ~m;
       }
-      // draws of the lanes below with this bin, and of all lanes with this bin
-      int64_t rank = 0, cnt = 0;
-      for (int k = 0; k < cbits; k++) {
-        const uint64_t m = __ballot((c >> k) & 1u) & eq;
-        rank += (int64_t)__popcll(m & lt) << k;
-        cnt += (int64_t)__popcll(m) << k;
-      }
-      const int64_t base = valid ? sb[bin] : 0;
-      for (uint32_t k = 0; k < c; k++) A.bucket[base + rank + k] = y0;
-      const bool last = valid && (eq & ~(lt | (1ull << lane))) == 0ull;  // highest lane of its bin
-      if (last) sb[bin] = base + cnt;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (t.part) {
+      const int rank = __popcll(eq & lt), cnt = __popcll(eq);
+      const int64_t base = sb[bin];
+      // (positions relative to the task's buckets; invalid lanes store past the end: dropped)
+      rstore64(rk, valid ? (uint32_t)(base - t.kbase + rank) * 8u : 0xFFFFFFF0u, e);
+      if (valid && rank == cnt - 1) sb[bin] = base + cnt;
       const bool left = valid && bin <= (uint32_t)t.s;
       const uint64_t lm = __ballot(left);
       const int64_t lr = __popcll(lm & lt);
-      if (valid) {
-        const int64_t pos = left ? t.a + lrun + lr : t.a + nl + (i - t.a - lrun - lr);
-        A.ent_out[pos] = e;
-      }
+      const int64_t pos = left ? lrun + lr : nl + (i - t.a - lrun - lr);  // within the segment
+      rstore64(ro, valid ? (uint32_t)pos * 8u : 0xFFFFFFF0u, e);
       lrun += __popcll(lm);
     }
-    e0 = e1;
-    bin0 = bin1;
-    y0 = y1;
-    e1 = e2;
   }
 }
 
 // Spark's row-order fp64 sums of every bucket: one lane per (task, bin), 16 chains per
-// wave.  The chains' labels stream through LDS: the whole wave loads each chain's next
-// kChT labels with contiguous 512-byte loads (issued a stage ahead, while the current
-// stage is summed), then lane l < 16 adds its own slice in order (sum += y, sumSq += y*y:
-// instanceWeight 1.0 per draw, DTStatsAggregator.update).
+// wave.  The chains' entries stream through LDS: the whole wave loads each chain's next
+// kChT entries with contiguous 512-byte loads two stages ahead, gathers their labels one
+// stage ahead (independent loads, every lane the same count: the waits stay counted), and
+// writes labels and draw counts to LDS; then lane l < 16 adds its own slice in order, each
+// label count times (sum += y, sumSq += y*y: instanceWeight 1.0 per draw,
+// DTStatsAggregator.update; a row drawn c times is c consecutive rows).
 constexpr int kChC = 16;    // chains per wave
-constexpr int kChT = 128;   // labels per chain per stage
+constexpr int kChT = 64;    // entries per chain per stage
 constexpr int kChPitch = kChT + 1;
 __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
   __shared__ double s_y[kChC * kChPitch];
+  __shared__ uint8_t s_c[kChC * kChPitch];
   const int NB = A.NB, lane = threadIdx.x;
   const int64_t nlanes = (int64_t)nchain * NB;
   const int64_t g = (int64_t)blockIdx.x * kChC + lane;
@@ -397,72 +407,88 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
   const int64_t len = hi - lo;
   int64_t maxlen = len;
   for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
-  const double* bk = A.bucket;
+  const uint64_t* bk = A.bucket;
   auto rdl64 = [](int64_t x, int j) -> int64_t {  // lane j's value (j wave-uniform)
     const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j);
     const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), j);
     return (int64_t)(((uint64_t)h << 32) | l);
   };
-  // a stage: chain j's labels [off, off + kChT) -- loads u = 2j, 2j + 1, contiguous 512 B each
-  constexpr int kLd = kChC * kChT / 64;  // loads per stage (each lane: one double per load)
-  static_assert(kChT == 128, "two loads per chain slice");
-  double v[kLd];
-  auto load_stage = [&](int64_t off) {
+  // a stage: chain j's entries [off, off + kChT) -- loads u = kPer j ... kPer j + kPer - 1,
+  // 512 B each; lanes past a chain's end load its first entry again (a valid row) and store
+  // count 0
+  constexpr int kPer = kChT / 64;
+  constexpr int kLd = kChC * kPer;
+  static_assert(kChT % 64 == 0, "whole 64-entry loads per chain slice");
+  int64_t jlo[kChC], jlen[kChC];
+#pragma unroll
+  for (int j = 0; j < kChC; j++) {
+    jlo[j] = rdl64(lo, j);
+    jlen[j] = rdl64(len, j);
+  }
+  auto load_entries = [&](int64_t off, uint64_t (&ev)[kLd]) {
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
-      const int j = u >> 1;                   // chain (wave-uniform)
-      const int x = (u & 1) * 64 + lane;      // position in its slice
-      const int64_t jlo = rdl64(lo, j), jlen = rdl64(len, j);
-      v[u] = off + x < jlen ? bk[jlo + off + x] : 0.0;
+      const int j = u / kPer;
+      const int64_t x = off + (u % kPer) * 64 + lane;
+      ev[u] = bk[jlen[j] > 0 ? jlo[j] + (x < jlen[j] ? x : 0) : 0];  // (empty chains: entry 0)
     }
   };
+  auto gather = [&](const uint64_t (&ev)[kLd], double (&yv)[kLd]) {
+#pragma unroll
+    for (int u = 0; u < kLd; u++) yv[u] = A.y[(uint32_t)ev[u]];
+  };
+  uint64_t eA[kLd], eB[kLd];
+  double yv[kLd];
+  if (maxlen > 0) {
+    load_entries(0, eA);
+    load_entries(kChT, eB);
+    gather(eA, yv);
+  }
   double s1 = 0.0, s2 = 0.0;
-  load_stage(0);
+  uint64_t cnt = 0;
   for (int64_t off = 0; off < maxlen; off += kChT) {
+    // stage `off` to LDS (entries eA, labels yv)
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
-      const int e = u * 64 + lane;
-      s_y[(e / kChT) * kChPitch + (e % kChT)] = v[u];
+      const int j = u / kPer;
+      const int x = (u % kPer) * 64 + lane;
+      const bool in = off + x < jlen[j];
+      s_y[j * kChPitch + x] = yv[u];
+      s_c[j * kChPitch + x] = in ? (uint8_t)((eA[u] >> 32) & 0xffu) : (uint8_t)0;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (off + kChT < maxlen) load_stage(off + kChT);
+    // the stage after next: entries; the next stage: labels
+#pragma unroll
+    for (int u = 0; u < kLd; u++) eA[u] = eB[u];
+    if (off + kChT < maxlen) {
+      load_entries(off + 2 * kChT, eB);
+      gather(eA, yv);
+    }
     const int n = (int)min((int64_t)kChT, max((int64_t)0, len - off));
     if (lane < kChC) {
       const double* sy = s_y + lane * kChPitch;
-      int x = 0;
-      for (; x + 8 <= n; x += 8) {  // 8 LDS reads in flight, then the adds in order
-        double yy[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) yy[k] = sy[x + k];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const double w = 1.0 * yy[k];  // instanceWeight * label
-          s1 += w;
-          s2 += w * yy[k];               // instanceWeight * label * label
-        }
-      }
-      for (; x < n; x++) {
+      const uint8_t* sc = s_c + lane * kChPitch;
+      for (int x = 0; x < n; x++) {
         const double y = sy[x];
-        const double w = 1.0 * y;
-        s1 += w;
-        s2 += w * y;
+        const uint32_t c = sc[x];
+        const double w = 1.0 * y;    // instanceWeight * label
+        const double wy = w * y;     // instanceWeight * label * label
+        for (uint32_t k = 0; k < c; k++) {
+          s1 += w;
+          s2 += wy;
+        }
+        cnt += c;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (lane < kChC && g < nlanes) {
     double* o = A.chist + g * 3;
-    o[0] = (double)len;  // one draw per label: count += 1.0 each
+    o[0] = (double)cnt;  // count += 1.0 per draw
     o[1] = s1;
     o[2] = s2;
   }
 }
 
-void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain, int cbits) {
+void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain) {
   int nbits = 0;
   while ((1 << nbits) < a.NB) nbits++;
   if (npieces > 0)
@@ -471,7 +497,7 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
     hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)a.ntasks), dim3(256), 0, st, a);
   if (npieces > 0)
     hipLaunchKernelGGL(k_fb_scatter, dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
-                       npieces, nbits, cbits);
+                       npieces, nbits);
   const int64_t lanes = (int64_t)nchain * a.NB;
   if (lanes > 0)
     hipLaunchKernelGGL(k_fb_chain, dim3((unsigned)((lanes + kChC - 1) / kChC)), dim3(64), 0, st, a,

@@ -1844,9 +1844,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     }
     // Buckets + routing of a task list (launch_fb_route): the chain sums of its first
     // `nchain` tasks land at chist (task-major [NB][3]); nleft (optional) gets the left
-    // entries of every routing task.  Bucket space: the chain tasks' draws.
-    int cbits = 0;
-    while ((1u << cbits) <= G.cmax) cbits++;
+    // entries of every routing task.  Bucket space: the chain tasks' entries.
     auto run_tasks = [&](std::vector<F64Task>& tk, int nchain, int64_t nlabels, double* chist,
                          std::vector<int64_t>* nleft_out) -> int {
       if (tk.empty()) return SBAG_OK;
@@ -1863,7 +1861,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       F64TPiece* d_pc;
       uint32_t *d_pcnt, *d_plcnt;
       int64_t *d_pbase, *d_plbase, *d_nleft, *d_kboff;
-      double* d_bucket;
+      uint64_t* d_bucket;
       TRY(ws_typed(c, "fb_tasks", (size_t)nt, &d_tk));
       TRY(ws_typed(c, "fb_pieces", (size_t)std::max<int64_t>(np, 1), &d_pc));
       TRY(ws_typed(c, "fb_pcnt", (size_t)std::max<int64_t>(np, 1) * NB, &d_pcnt));
@@ -1894,7 +1892,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.kb_off = d_kboff;
       ba.y = d_y64;
       ba.chist = chist;
-      launch_fb_route(c->stream, ba, np, nchain, cbits);
+      launch_fb_route(c->stream, ba, np, nchain);
       HIP_TRY(hipGetLastError());
       if (nleft_out) {
         nleft_out->assign(tk.size(), 0);
@@ -1916,12 +1914,12 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     static const bool walk_fallback = getenv("SBAG_F64_FALLBACK") && !strcmp(getenv("SBAG_F64_FALLBACK"), "hist");
     for (size_t k0 = 0; k0 < X.size();) {
       // a batch: nodes while their feature tasks' draws fit the budget (one node at least)
-      const double budget = (double)((int64_t)1 << 29);  // labels (4 GB)
+      const double budget = (double)((int64_t)1 << 29);  // bucket entries (4 GB)
       size_t k1 = k0;
       double used = 0;
       while (k1 < X.size()) {
         const LNode& q = cur[X[k1]];
-        const double need = q.n * (G.h_Fr[q.r] + 1);
+        const double need = (double)(q.b - q.a) * (G.h_Fr[q.r] + 1);
         if (k1 > k0 && used + need > budget) break;
         used += need;
         k1++;
@@ -1998,7 +1996,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
               t.col = -1;
             }
             ft.push_back(t);
-            fdraws.push_back(real ? (int64_t)q.n : 0);
+            fdraws.push_back(real ? q.b - q.a : 0);
           }
         }
         for (size_t t0 = 0; t0 < ft.size();) {
@@ -2043,7 +2041,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       t.a = q.a;
       t.b = q.b;
       t.kbase = chain ? kb[pass] : -1;
-      if (chain) kb[pass] += (int64_t)q.n;  // one label per draw
+      if (chain) kb[pass] += q.b - q.a;  // one bucket entry per in-bag row
       t.r = q.r;
       t.col = G.h_pos[(size_t)q.r * Fmax + fl];
       t.s = s;

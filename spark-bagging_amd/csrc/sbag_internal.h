@@ -399,7 +399,7 @@ struct F64ScreenArgs {
 };
 struct F64Task {            // one (node, feature) whose entries are bucketed / routed
   int64_t a, b;             // entries [a, b) of ent_in (row order)
-  int64_t kbase;            // buckets at bucket[kbase, kbase + draws); -1: no buckets
+  int64_t kbase;            // buckets at bucket[kbase, kbase + b - a); -1: no buckets
   int64_t piece0, piece1;   // its pieces
   int32_t r, col, s, part;  // replica, column of the column-major bins (-1: every entry in
                             // bin 0, the node total), split bin, route?
@@ -417,10 +417,10 @@ struct F64BucketArgs {
   int32_t NB, ntasks;
   const uint64_t* ent_in;
   uint64_t* ent_out;        // children: left [a, a + nleft), right [a + nleft, b), row order
-  double* bucket;           // the buckets: each draw's label (a row drawn c times c times)
-  uint32_t* pcnt;           // [piece][NB] draws per bin
+  uint64_t* bucket;         // the buckets: the node's entries grouped by bin, row order kept
+  uint32_t* pcnt;           // [piece][NB] entries per bin
   uint32_t* plcnt;          // [piece] entries going left
-  int64_t* pbase;           // [piece][NB] bucket position of the piece's first draw per bin
+  int64_t* pbase;           // [piece][NB] bucket position of the piece's first entry per bin
   int64_t* plbase;          // [piece] left entries of the task before the piece
   int64_t* nleft;           // [task]
   int64_t* kb_off;          // [task][NB + 1] bucket bounds in entK
@@ -443,7 +443,7 @@ struct F64FinishArgs {
   F64SplitOut* out;
 };
 void launch_f64_screen(hipStream_t st, const F64ScreenArgs& a, int M);
-void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain, int cbits);
+void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain);
 void launch_fb_finish(hipStream_t st, const F64FinishArgs& a);
 int64_t compact_ordered_chunks(int64_t N);
 int f64_hist_width(int NB);
