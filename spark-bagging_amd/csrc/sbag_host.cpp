@@ -2861,8 +2861,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       HIP_TRY(hipMemsetAsync(d_snr, 0, reps.size() * 4, c->stream));
       uint16_t* d_gsums;
       TRY(ws_typed(c, "ss_gsums", (size_t)split_sample_groups((int64_t)R * N), &d_gsums));
+      bool gap_all = true;  // every sampled replica's fraction <= 0.4: GapSampling
+      for (size_t k = 0; k < reps.size(); k++) gap_all = gap_all && fl2[2 * k] <= 0.4;
       launch_split_sample(c->stream, d_counts, N, R, d_spoff, P, d_reps, (int)reps.size(), d_pst,
-                          d_frac, d_gsums, d_srows, cap, d_snr);
+                          d_frac, d_gsums, d_srows, cap, d_snr, gap_all);
       HIP_TRY(hipGetLastError());
       if (!wide)
         launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, (int)reps.size(), ds->d_codes,
@@ -4614,7 +4616,7 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
     TRY(ws_typed(c, "ss_gsums", (size_t)split_sample_groups(N), &d_gsums));
     HIP_TRY(hipMemsetAsync(d_snr, 0, 4, c->stream));
     launch_split_sample(c->stream, d_cnt, N, 1, d_spoff, P, d_reps, 1, d_pst, d_frac, d_gsums,
-                        d_srows, cap, d_snr);
+                        d_srows, cap, d_snr, frac <= 0.4);
     HIP_TRY(hipGetLastError());
     launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, 1, ds->d_codes, ds->code_bytes,
                            ds->S, d_sub, d_Fr, Fr, d_vcoff, d_vc,

@@ -219,7 +219,8 @@ void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, int64
                          const uint64_t* d_part_state,
                          const double* d_frac /*[nrep][2]: fraction, log1p(-fraction)*/,
                          uint16_t* d_gsums /*[split_sample_groups(R * N)]*/,
-                         uint32_t* d_rows /*[nrep][cap]*/, int64_t cap, uint32_t* d_nrows);
+                         uint32_t* d_rows /*[nrep][cap]*/, int64_t cap, uint32_t* d_nrows,
+                         bool gap_sampling /* every replica's fraction <= 0.4 */);
 void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                             const uint32_t* d_nrows, const int32_t* d_reps, int nrep,
                             const void* codes, int code_bytes, int32_t S, const int32_t* d_sub,

@@ -978,6 +978,129 @@ __global__ __launch_bounds__(64) void k_split_sample(
   flush();
 }
 
+// Few partitions (P < 64: a GBM booster's single partition, or any fit on one partition):
+// k_split_sample's lanes are partitions, so one lane would walk the whole subbag with a
+// dependent load per taken item.  Here a wave takes one (replica, partition): GapSampling's
+// gaps depend only on its XORShift stream, so every lane steps the stream to its own draw of
+// a block of 64 (the stream is sequential: each lane runs the 64 steps, keeps the one it
+// owns), the gaps' prefix gives the block's 64 taken item positions, and the wave streams the
+// partition's count bytes (1024 rows per chunk, one chunk ahead) and resolves the positions
+// that fall in each chunk to their rows.  The same items as the one-lane walk, in the same
+// order: the row list is identical.
+__global__ __launch_bounds__(64) void k_split_sample_gap(
+    const uint8_t* __restrict__ counts, int64_t N, const int64_t* __restrict__ part_off, int P,
+    const int32_t* __restrict__ reps, const uint64_t* __restrict__ part_state,
+    const double* __restrict__ frac, uint32_t* __restrict__ rows_out, int64_t cap,
+    uint32_t* __restrict__ nrows) {
+  __shared__ int64_t s_t[64];
+  __shared__ uint32_t s_rows[64];
+  const int ri = blockIdx.y, p = blockIdx.x, lane = threadIdx.x;
+  const int r = reps[ri];
+  const double lnq = frac[2 * ri + 1];
+  uint64_t st = part_state[p];
+  const uint8_t* cr = counts + (int64_t)r * N;
+  const int64_t r0 = part_off[p], r1 = part_off[p + 1];
+  uint32_t* out = rows_out + (int64_t)ri * cap;
+  // the current chunk: rows [c0, c0 + 1024), lane l's 16 rows [c0 + 16 l, c0 + 16 l + 16)
+  auto load16 = [&](int64_t c0, uint32_t (&w)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int64_t row = c0 + 16 * lane + k;
+      w[k] = row < r1 ? (uint32_t)cr[row] : 0u;
+    }
+  };
+  int64_t c0 = r0;
+  uint32_t cw[16], nw[16];
+  load16(c0, cw);
+  load16(c0 + 1024, nw);
+  // items before the chunk, and this lane's item range inside it
+  int64_t ib = 0;
+  uint32_t lsum = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) lsum += cw[k];
+  uint32_t incl = lsum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  uint32_t ctot = __shfl(incl, 63);
+  int64_t next = 0;  // item index of the next draw's gap origin
+  bool done = r0 >= r1;
+  while (!done) {
+    // 64 gaps: lane j keeps draw j of the block (every lane steps the shared stream)
+    double myu = 0.0;
+    for (int j = 0; j < 64; j++) {
+      st = xs_step_s(st);
+      const int64_t a = (int64_t)(st & ((1ull << 26) - 1));
+      st = xs_step_s(st);
+      const int64_t b = (int64_t)(st & ((1ull << 27) - 1));
+      const double u = (double)((a << 27) + b) * 0x1.0p-53;
+      if (j == lane) myu = u;
+    }
+    // countForDropping = (log(u) / lnq).toInt (a JVM cast saturates)
+    const double q = log(fmax(myu, 5e-11)) / lnq;
+    const int64_t g = (int64_t)(q >= 2147483647.0 ? 2147483647.0 : q);
+    // taken item = previous + 1 + gap (the first: gap): an inclusive scan of gap + 1
+    int64_t d = g + 1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = __shfl_up(d, o);
+      if (lane >= o) d += u;
+    }
+    const int64_t tgt = next + d - 1;
+    s_t[lane] = tgt;
+    next = next + __shfl(d, 63);
+    int nfound = 0;
+    // resolve the block's targets against the streamed chunks
+    for (int j = 0; j < 64;) {
+      const int64_t t = s_t[j];  // (LDS, same wave: in order)
+      if (t >= ib + (int64_t)ctot) {  // past this chunk: the next one
+        if (c0 + 1024 >= r1) {
+          done = true;
+          break;
+        }
+        ib += ctot;
+        c0 += 1024;
+#pragma unroll
+        for (int k = 0; k < 16; k++) cw[k] = nw[k];
+        load16(c0 + 1024, nw);
+        lsum = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) lsum += cw[k];
+        incl = lsum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(incl, o);
+          if (lane >= o) incl += u;
+        }
+        ctot = __shfl(incl, 63);
+        continue;
+      }
+      // the lane whose rows hold item t, then the row among its 16
+      const int64_t o = t - ib;
+      const bool mine = o >= (int64_t)(incl - lsum) && o < (int64_t)incl;
+      const uint64_t m = __ballot(mine);
+      const int owner = __ffsll((unsigned long long)m) - 1;
+      if (lane == owner) {
+        uint32_t acc = incl - lsum;
+        int k = 0;
+        while (k < 15 && (int64_t)(acc + cw[k]) <= o) acc += cw[k++];
+        s_rows[nfound] = (uint32_t)(c0 + 16 * lane + k);
+      }
+      nfound++;
+      j++;
+    }
+    // append the block's rows (one atomic per block)
+    if (nfound > 0) {
+      uint32_t k0 = 0;
+      if (lane == 0) k0 = atomicAdd(&nrows[ri], (uint32_t)nfound);
+      k0 = (uint32_t)__shfl((int)k0, 0);
+      if (lane < nfound && (int64_t)k0 + lane < cap) out[k0 + lane] = s_rows[lane];
+    }
+  }
+}
+
 // Phase 2, grid (sample chunks of kSvcRows, replicas): each sampled row adds its value codes
 // to the replica's counts, in LDS when they fit (`lds_words`), flushed once.
 constexpr int kSvcRows = 1024;  // sampled rows per k_split_sample_vc workgroup
@@ -1052,8 +1175,16 @@ __global__ __launch_bounds__(256) void k_group_sums(const uint8_t* __restrict__ 
 void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, int64_t R,
                          const int64_t* d_part_off, int P, const int32_t* d_reps, int nrep,
                          const uint64_t* d_part_state, const double* d_frac, uint16_t* d_gsums,
-                         uint32_t* d_rows, int64_t cap, uint32_t* d_nrows) {
+                         uint32_t* d_rows, int64_t cap, uint32_t* d_nrows, bool gap_sampling) {
   if (nrep == 0 || P == 0) return;
+  // few partitions and GapSampling (every fraction <= 0.4): a wave per (replica, partition);
+  // else k_split_sample's lanes walk the partitions (SBAG_SPLIT_SAMPLE_LANES=1 forces them)
+  static const bool lanes_env = getenv("SBAG_SPLIT_SAMPLE_LANES") && atoi(getenv("SBAG_SPLIT_SAMPLE_LANES"));
+  if (P < 64 && gap_sampling && !lanes_env) {
+    hipLaunchKernelGGL(k_split_sample_gap, dim3((unsigned)P, (unsigned)nrep), dim3(64), 0, st, counts,
+                       N, d_part_off, P, d_reps, d_part_state, d_frac, d_rows, cap, d_nrows);
+    return;
+  }
   const int64_t ng = split_sample_groups(R * N);
   hipLaunchKernelGGL(k_group_sums, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, st, counts,
                      R * N, d_gsums, ng);
