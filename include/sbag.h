@@ -222,6 +222,9 @@ typedef struct {
                               histogram (k_tile_count / k_tile_scatter), not in hist_ms   */
   double chain_ms;         /* fp64 labels: the chosen features' bins summed in Spark's row
                               order (bucketing + routing + k_fb_chain)        */
+  double root_ms;          /* root histogram as an int8 MFMA contraction (k_hist_mfma);
+                              0 when the root went through k_hist_rl (then in hist_ms)     */
+  double root_mfma_ops;    /* its int8 operations (2 x 32^3 per MFMA)                      */
 } sbag_timing;
 int sbag_forest_timing(const sbag_forest* f, sbag_timing* out);
 

@@ -86,7 +86,8 @@ class Timing(ctypes.Structure):
         ("levels", ctypes.c_int64), ("partition_ms", ctypes.c_double),
         ("hist_work_bytes", ctypes.c_double), ("fix_ms", ctypes.c_double),
         ("exact_fallbacks", ctypes.c_int64), ("hist_lds_atomics", ctypes.c_double),
-        ("group_ms", ctypes.c_double), ("chain_ms", ctypes.c_double)]
+        ("group_ms", ctypes.c_double), ("chain_ms", ctypes.c_double),
+        ("root_ms", ctypes.c_double), ("root_mfma_ops", ctypes.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

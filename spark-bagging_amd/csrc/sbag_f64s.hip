@@ -334,12 +334,16 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   int64_t lrun = t.part ? A.plbase[pi] : 0;
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
   const __amdgpu_buffer_rsrc_t rc = task_col_rsrc(A, t);
-  // the task's buckets and its children's segment (each < 4 GB: a node's entries)
-  const __amdgpu_buffer_rsrc_t rk = rsrc_of(A.bucket + (chain ? t.kbase : 0), chain ? (uint64_t)(t.b - t.a) * 8 : 0);
+  // the task's buckets (labels and counts) and its children's segment (each < 4 GB: a
+  // node's entries); the labels (rows < 2^29)
+  const uint64_t nk = chain ? (uint64_t)(t.b - t.a) : 0;
+  const __amdgpu_buffer_rsrc_t rk = rsrc_of(A.bky + (chain ? t.kbase : 0), nk * 8);
+  const __amdgpu_buffer_rsrc_t rkc = rsrc_of(A.bkc + (chain ? t.kbase : 0), nk);
   const __amdgpu_buffer_rsrc_t ro = rsrc_of(A.ent_out + t.a, t.part ? (uint64_t)(t.b - t.a) * 8 : 0);
+  const __amdgpu_buffer_rsrc_t ry = rsrc_of(A.y, chain ? 0xFFFFFFFFull : 0);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t last = pc.b - 1;
-  // kScU rounds of 64 entries per step: all their entry loads, then all their bin
+  // kScU rounds of 64 entries per step: all their entry loads, then all their bin and label
   // gathers, then the rounds' ballots and stores -- one memory latency per step, not per
   // round (vmcnt counts stores and loads in order on gfx9, so loads carried across steps
   // would wait for the stores issued after them anyway)
@@ -347,18 +351,22 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   for (int64_t i0 = pc.a; i0 < pc.b; i0 += 64 * kScU) {
     uint64_t ev[kScU];
     uint32_t bv[kScU];
+    v2u32 yv[kScU];
 #pragma unroll
     for (int u = 0; u < kScU; u++) ev[u] = A.ent_in[min(i0 + 64 * u + lane, last)];
 #pragma unroll
-    for (int u = 0; u < kScU; u++) bv[u] = rbin(rc, ev[u]);
+    for (int u = 0; u < kScU; u++) {
+      bv[u] = rbin(rc, ev[u]);
+      yv[u] = __builtin_amdgcn_raw_buffer_load_b64(ry, (int)((uint32_t)ev[u] * 8u), 0, 0);
+    }
 #pragma unroll
     for (int u = 0; u < kScU; u++) {
       const int64_t i = i0 + 64 * u + lane;
       const bool valid = i < pc.b;
       const uint64_t e = ev[u];
       const uint32_t bin = valid ? bv[u] : 0u;
-      // both stores every round, whatever the task does (a task without buckets or
-      // without children has a zero-size resource: the store is dropped) -- no branch
+      // every store every round, whatever the task does (a task without buckets or
+      // without children has zero-size resources: the stores are dropped) -- no branch
       uint64_t eq = __ballot(valid);
       for (int k = 0; k < nbits; k++) {
         const bool bit = (bin >> k) & 1u;
@@ -368,7 +376,9 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
       const int rank = __popcll(eq & lt), cnt = __popcll(eq);
       const int64_t base = sb[bin];
       // (positions relative to the task's buckets; invalid lanes store past the end: dropped)
-      rstore64(rk, valid ? (uint32_t)(base - t.kbase + rank) * 8u : 0xFFFFFFF0u, e);
+      const uint32_t kp = valid ? (uint32_t)(base - t.kbase + rank) : 0x1FFFFFFEu;
+      __builtin_amdgcn_raw_buffer_store_b64(yv[u], rk, (int)(kp * 8u), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(e >> 32), rkc, (int)kp, 0, 0);
       if (valid && rank == cnt - 1) sb[bin] = base + cnt;
       const bool left = valid && bin <= (uint32_t)t.s;
       const uint64_t lm = __ballot(left);
@@ -381,12 +391,11 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
 }
 
 // Spark's row-order fp64 sums of every bucket: one lane per (task, bin), 16 chains per
-// wave.  The chains' entries stream through LDS: the whole wave loads each chain's next
-// kChT entries with contiguous 512-byte loads two stages ahead, gathers their labels one
-// stage ahead (independent loads, every lane the same count: the waits stay counted), and
-// writes labels and draw counts to LDS; then lane l < 16 adds its own slice in order, each
-// label count times (sum += y, sumSq += y*y: instanceWeight 1.0 per draw,
-// DTStatsAggregator.update; a row drawn c times is c consecutive rows).
+// wave.  The chains' labels and counts stream through LDS: the whole wave loads each
+// chain's next kChT labels and counts with contiguous loads two stages ahead and writes
+// them to LDS; then lane l < 16 adds its own slice in order, each label count times
+// (sum += y, sumSq += y*y: instanceWeight 1.0 per draw, DTStatsAggregator.update; a row
+// drawn c times is c consecutive rows).
 constexpr int kChC = 16;    // chains per wave
 constexpr int kChT = 64;    // entries per chain per stage
 constexpr int kChPitch = kChT + 1;
@@ -407,15 +416,13 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
   const int64_t len = hi - lo;
   int64_t maxlen = len;
   for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
-  const uint64_t* bk = A.bucket;
   auto rdl64 = [](int64_t x, int j) -> int64_t {  // lane j's value (j wave-uniform)
     const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j);
     const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), j);
     return (int64_t)(((uint64_t)h << 32) | l);
   };
   // a stage: chain j's entries [off, off + kChT) -- loads u = kPer j ... kPer j + kPer - 1,
-  // 512 B each; lanes past a chain's end load its first entry again (a valid row) and store
-  // count 0
+  // 64 entries each; lanes past a chain's end load its first entry again and store count 0
   constexpr int kPer = kChT / 64;
   constexpr int kLd = kChC * kPer;
   static_assert(kChT % 64 == 0, "whole 64-entry loads per chain slice");
@@ -425,59 +432,64 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
     jlo[j] = rdl64(lo, j);
     jlen[j] = rdl64(len, j);
   }
-  auto load_entries = [&](int64_t off, uint64_t (&ev)[kLd]) {
+  auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&cv)[kLd]) {
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
       const int j = u / kPer;
       const int64_t x = off + (u % kPer) * 64 + lane;
-      ev[u] = bk[jlen[j] > 0 ? jlo[j] + (x < jlen[j] ? x : 0) : 0];  // (empty chains: entry 0)
+      const int64_t at = jlen[j] > 0 ? jlo[j] + (x < jlen[j] ? x : 0) : 0;  // (empty: entry 0)
+      yv[u] = A.bky[at];
+      cv[u] = x < jlen[j] ? (uint32_t)A.bkc[at] : 0u;
     }
   };
-  auto gather = [&](const uint64_t (&ev)[kLd], double (&yv)[kLd]) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) yv[u] = A.y[(uint32_t)ev[u]];
-  };
-  uint64_t eA[kLd], eB[kLd];
-  double yv[kLd];
+  double yA[kLd], yB[kLd];
+  uint32_t cA[kLd], cB[kLd];
   if (maxlen > 0) {
-    load_entries(0, eA);
-    load_entries(kChT, eB);
-    gather(eA, yv);
+    load(0, yA, cA);
+    load(kChT, yB, cB);
   }
   double s1 = 0.0, s2 = 0.0;
   uint64_t cnt = 0;
   for (int64_t off = 0; off < maxlen; off += kChT) {
-    // stage `off` to LDS (entries eA, labels yv)
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
       const int j = u / kPer;
       const int x = (u % kPer) * 64 + lane;
-      const bool in = off + x < jlen[j];
-      s_y[j * kChPitch + x] = yv[u];
-      s_c[j * kChPitch + x] = in ? (uint8_t)((eA[u] >> 32) & 0xffu) : (uint8_t)0;
+      s_y[j * kChPitch + x] = yA[u];
+      s_c[j * kChPitch + x] = (uint8_t)cA[u];
     }
-    // the stage after next: entries; the next stage: labels
 #pragma unroll
-    for (int u = 0; u < kLd; u++) eA[u] = eB[u];
-    if (off + kChT < maxlen) {
-      load_entries(off + 2 * kChT, eB);
-      gather(eA, yv);
+    for (int u = 0; u < kLd; u++) {
+      yA[u] = yB[u];
+      cA[u] = cB[u];
     }
+    if (off + 2 * kChT < maxlen) load(off + 2 * kChT, yB, cB);
     const int n = (int)min((int64_t)kChT, max((int64_t)0, len - off));
     if (lane < kChC) {
       const double* sy = s_y + lane * kChPitch;
       const uint8_t* sc = s_c + lane * kChPitch;
-      for (int x = 0; x < n; x++) {
-        const double y = sy[x];
-        const uint32_t c = sc[x];
-        const double w = 1.0 * y;    // instanceWeight * label
-        const double wy = w * y;     // instanceWeight * label * label
-        for (uint32_t k = 0; k < c; k++) {
+      // (4 entries' LDS reads ahead of their adds; every bucket entry is drawn, c >= 1)
+      auto add = [&](double y, uint32_t c) {
+        const double w = 1.0 * y;  // instanceWeight * label
+        const double wy = w * y;   // instanceWeight * label * label
+        s1 += w;
+        s2 += wy;
+        for (uint32_t k = 1; k < c; k++) {
           s1 += w;
           s2 += wy;
         }
         cnt += c;
+      };
+      int x = 0;
+      for (; x + 4 <= n; x += 4) {
+        const double y0 = sy[x], y1 = sy[x + 1], y2 = sy[x + 2], y3 = sy[x + 3];
+        const uint32_t c0 = sc[x], c1 = sc[x + 1], c2 = sc[x + 2], c3 = sc[x + 3];
+        add(y0, c0);
+        add(y1, c1);
+        add(y2, c2);
+        add(y3, c3);
       }
+      for (; x < n; x++) add(sy[x], sc[x]);
     }
   }
   if (lane < kChC && g < nlanes) {

@@ -358,6 +358,7 @@ struct sbag_dataset {
   int32_t cols_ncol = 0;
   uint32_t* d_planes = nullptr;
   int32_t planes_nsp = 0;
+  bool planes_done = false;  // the planes were built (or found not to fit) by a fit
   // every device buffer goes with the dataset, also when a constructor (create, import)
   // returns early after some of them were allocated
   ~sbag_dataset() {
@@ -728,7 +729,7 @@ struct EventTimer {
     }
   }
 };
-enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_FIX, T_GROUP, T_CHAIN, T_NCAT };
+enum { T_SAMPLE, T_VC, T_BIN, T_COMPACT, T_HIST, T_SPLIT, T_SUB, T_PART, T_FIX, T_GROUP, T_CHAIN, T_ROOT, T_NCAT };
 
 // ---------------------------------------------------------------- C ABI
 extern "C" {
@@ -1861,7 +1862,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       F64TPiece* d_pc;
       uint32_t *d_pcnt, *d_plcnt;
       int64_t *d_pbase, *d_plbase, *d_nleft, *d_kboff;
-      uint64_t* d_bucket;
+      double* d_bky;
+      uint8_t* d_bkc;
       TRY(ws_typed(c, "fb_tasks", (size_t)nt, &d_tk));
       TRY(ws_typed(c, "fb_pieces", (size_t)std::max<int64_t>(np, 1), &d_pc));
       TRY(ws_typed(c, "fb_pcnt", (size_t)std::max<int64_t>(np, 1) * NB, &d_pcnt));
@@ -1870,7 +1872,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       TRY(ws_typed(c, "fb_plbase", (size_t)std::max<int64_t>(np, 1), &d_plbase));
       TRY(ws_typed(c, "fb_nleft", (size_t)nt, &d_nleft));
       TRY(ws_typed(c, "fb_kboff", (size_t)nt * (NB + 1), &d_kboff));
-      TRY(ws_typed(c, "fb_bucket", (size_t)std::max<int64_t>(1, nlabels), &d_bucket));
+      TRY(ws_typed(c, "fb_bky", (size_t)std::max<int64_t>(1, nlabels), &d_bky));
+      TRY(ws_typed(c, "fb_bkc", (size_t)std::max<int64_t>(1, nlabels), &d_bkc));
       TRY(h2d(c, d_tk, tk.data(), (size_t)nt));
       TRY(h2d(c, d_pc, pcs.data(), pcs.size()));
       F64BucketArgs ba{};
@@ -1883,7 +1886,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.ntasks = nt;
       ba.ent_in = ent_cur;
       ba.ent_out = ent_nxt;
-      ba.bucket = d_bucket;
+      ba.bky = d_bky;
+      ba.bkc = d_bkc;
       ba.pcnt = d_pcnt;
       ba.plcnt = d_plcnt;
       ba.pbase = d_pbase;
@@ -2254,6 +2258,9 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     for (double v : lab.y)
       if (!std::isfinite(v)) return fail(SBAG_EINVAL, "labels must be finite");
     if (!lab.label_ok && !lab.approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
+    // (the bucketing kernels address the labels with 32-bit byte offsets)
+    if (ds->N >= ((int64_t)1 << 29))
+      return fail(SBAG_EUNSUPPORTED, "fp64 (non-dyadic) labels: at most 2^29 - 1 rows per dataset");
   }
   // the labels' fixed-point image in the entries: exact for dyadic labels, else (f64 path)
   // the screening approximation k = round(y 2^ashift)
@@ -2471,6 +2478,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     for (int r = 0; r < R; r++) hist_work += act[r] ? 3.0 * N : 0.0;
   };
   int64_t hist_launches = 0;
+  double root_mfma_ops = 0;  // int8 MFMA operations of the root histogram (0: k_hist_rl)
   static const bool trace = getenv("SBAG_LEVEL_TRACE") != nullptr;
   int trace_level = -1;
   static const bool group_off = getenv("SBAG_NO_TILE_GROUPING") != nullptr;
@@ -2686,6 +2694,21 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     return SBAG_OK;
   };
 
+  // the column-major copy of the codes [F][npad] (the bins when they are the codes), once
+  // per dataset (part of ingest: kept with it)
+  auto ensure_cols = [&]() -> int {
+    std::lock_guard<std::mutex> lk(ds->layout_mu);
+    if (!ds->d_cols) {
+      const int64_t np = (N + 63) / 64 * 64;
+      HIP_TRY(hipMalloc(&ds->d_cols, (size_t)ds->F * np));
+      launch_transpose(c->stream, (const uint8_t*)ds->d_codes, N, ds->S, ds->F, ds->d_cols, np, 1, 0, 0);
+      HIP_TRY(hipGetLastError());
+      ds->cols_ncol = ds->F;
+      // other contexts (the learner-part twins) read it without this stream's order
+      HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return SBAG_OK;
+  };
   // ---- 3. value counts -> thresholds.  Optimistic path: when every feature has
   // at most maxBins distinct values, histogram the root over the value codes
   // directly; its count stats ARE the value counts, and if every replica's
@@ -2728,7 +2751,54 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     ha.NB = ncmax;
     ha.NS = NS;
     ha.count_only = 0;
-    TRY(launch(g0, gini ? kHistGini : kHistVar, T_HIST, seg, h_par));
+    // Variance with every replica on every feature of <= 32 codes, counts <= 127: the root
+    // histogram as an int8 MFMA contraction (sbag_mfma.hip; SBAG_ROOT_MFMA=0: k_hist_rl)
+    const int mfma_env = getenv("SBAG_ROOT_MFMA") ? atoi(getenv("SBAG_ROOT_MFMA")) : 1;
+    bool mfma_root = !gini && mfma_env != 0 && ncmax <= 32 && N % 16 == 0 && cmax <= 127 &&
+                     Fmax == F && !getenv("SBAG_NO_LAYOUT_CACHE");
+    for (int r = 0; r < R && mfma_root; r++) {
+      if (h_Fr[r] != F) mfma_root = false;
+      for (int fl = 0; fl < h_Fr[r] && mfma_root; fl++)
+        if (h_pos_codes[(size_t)r * Fmax + fl] != fl) mfma_root = false;
+    }
+    // 7-bit digit planes of k + K0 (the sums) and, for exact labels, of k^2 (the squares)
+    auto digits7 = [](uint64_t v) {
+      int d = 1;
+      while (d < 10 && (v >> (7 * d)) != 0) d++;
+      return d;
+    };
+    const uint64_t kspan_u = (uint64_t)(lkmax - lkmin);
+    const uint64_t kabs_u = (uint64_t)std::max(std::llabs(lkmin), std::llabs(lkmax));
+    const int nd1 = digits7(kspan_u), nd2 = f64 ? 0 : digits7(kabs_u * kabs_u);
+    if (nd1 + nd2 > 6) mfma_root = false;
+    if (mfma_root) {
+      TRY(ensure_cols());
+      uint8_t* d_dig;
+      TRY(ws_typed(c, "mfma_digits", (size_t)(nd1 + nd2) * N, &d_dig));
+      int h = tm.begin(T_ROOT);
+      launch_label_digits(c->stream, lab.d_labk, N, (int32_t)K0, nd1, nd2, d_dig);
+      MfmaHistArgs ma{};
+      ma.counts = d_counts;
+      ma.cols = ds->d_cols;
+      ma.digits = d_dig;
+      ma.N = N;
+      ma.npad = (N + 63) / 64 * 64;
+      ma.R = R;
+      ma.F = F;
+      ma.Fmax = Fmax;
+      ma.NB = ncmax;
+      ma.ND1 = nd1;
+      ma.ND = nd1 + nd2;
+      ma.K0 = (int32_t)K0;
+      ma.hist = (unsigned long long*)hist_cur;
+      if (!launch_hist_mfma(c->stream, ma)) return fail(SBAG_EDEVICE, "internal: MFMA root histogram geometry");
+      HIP_TRY(hipGetLastError());
+      tm.end(h);
+      root_mfma_ops += 2.0 * 32.0 * 32.0 * 32.0 * (double)((N + 31) / 32) * F *
+                       (double)(((R + 31) / 32)) * (1 + nd1 + nd2);
+    } else {
+      TRY(launch(g0, gini ? kHistGini : kHistVar, T_HIST, seg, h_par));
+    }
     const int64_t words = (int64_t)R * Fmax * ncmax * NS;
     std::vector<uint8_t> tmp((size_t)words * word_bytes);
     TRY(d2h(c, tmp.data(), (const uint8_t*)hist_cur, tmp.size()));
@@ -3124,21 +3194,19 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     };
     if (identity && !getenv("SBAG_NO_LAYOUT_CACHE")) {
       // the codes are the bins: every column of every feature, once per dataset
+      TRY(ensure_cols());
       std::lock_guard<std::mutex> lk(ds->layout_mu);
-      if (!ds->d_cols) {
-        const int nc = ds->F;
-        HIP_TRY(hipMalloc(&ds->d_cols, (size_t)nc * npad));
-        launch_transpose(c->stream, d_bins, N, S, nc, ds->d_cols, npad, 1, 0, 0);
-        HIP_TRY(hipGetLastError());
-        ds->cols_ncol = nc;
+      if (!ds->planes_done) {
+        ds->planes_done = true;
+        const int nc = ds->cols_ncol;
         if (planes_fit(nc, plane_nsp)) {
           HIP_TRY(hipMalloc(&ds->d_planes, (size_t)nc * plane_nsp * plane_nw32 * 4));
           launch_planes(c->stream, ds->d_cols, npad, nc, plane_nsp, plane_nw32, ds->d_planes);
           HIP_TRY(hipGetLastError());
           ds->planes_nsp = plane_nsp;
+          // other contexts (the learner-part twins) read them without this stream's order
+          HIP_TRY(hipStreamSynchronize(c->stream));
         }
-        // other contexts (the learner-part twins) read them without this stream's order
-        HIP_TRY(hipStreamSynchronize(c->stream));
       }
       d_cols = ds->d_cols;
       if (ds->d_planes && ds->planes_nsp >= plane_nsp) {
@@ -3260,6 +3328,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     T.subtract_ms = cats[T_SUB];
     T.partition_ms = cats[T_PART];
     T.chain_ms = cats[T_CHAIN];
+    T.root_ms = cats[T_ROOT];
+    T.root_mfma_ops = root_mfma_ops;
     T.fix_ms = cats[T_FIX];
     T.exact_fallbacks = G.fallbacks;
     T.hist_launches = hist_launches;
@@ -3869,6 +3939,8 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   T.hist_work_bytes = hist_work;
   T.fix_ms = cats[T_FIX];
   T.group_ms = cats[T_GROUP];
+  T.root_ms = cats[T_ROOT];
+  T.root_mfma_ops = root_mfma_ops;
   T.exact_fallbacks = fallbacks;
   T.hist_launches = hist_launches;
   T.hist_alg_bytes = hist_alg_bytes;

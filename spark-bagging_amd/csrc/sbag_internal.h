@@ -418,7 +418,8 @@ struct F64BucketArgs {
   int32_t NB, ntasks;
   const uint64_t* ent_in;
   uint64_t* ent_out;        // children: left [a, a + nleft), right [a + nleft, b), row order
-  uint64_t* bucket;         // the buckets: the node's entries grouped by bin, row order kept
+  double* bky;              // the buckets: the node's entries' labels grouped by bin, row
+  uint8_t* bkc;             //   order kept, and their draw counts
   uint32_t* pcnt;           // [piece][NB] entries per bin
   uint32_t* plcnt;          // [piece] entries going left
   int64_t* pbase;           // [piece][NB] bucket position of the piece's first entry per bin
@@ -443,6 +444,18 @@ struct F64FinishArgs {
   double min_gain;
   F64SplitOut* out;
 };
+// sbag_mfma.hip: the root histogram of shared identity bins as an int8 MFMA contraction
+struct MfmaHistArgs {
+  const uint8_t* counts;  // [R][N], every count <= 127
+  const uint8_t* cols;    // [F][npad] column-major bin codes
+  const uint8_t* digits;  // [ND][N] 7-bit digits: planes [0, ND1) of k + K0, then of k^2
+  int64_t N, npad;
+  int32_t R, F, Fmax, NB, ND1, ND, K0;
+  unsigned long long* hist;  // [R][Fmax][NB][3] words: += count, += sum c k, (ND > ND1) += sum c k^2
+};
+bool launch_hist_mfma(hipStream_t st, const MfmaHistArgs& a);
+void launch_label_digits(hipStream_t st, const int32_t* labk, int64_t N, int32_t K0, int nd1, int nd2,
+                         uint8_t* digits);
 void launch_f64_screen(hipStream_t st, const F64ScreenArgs& a, int M);
 void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain);
 void launch_fb_finish(hipStream_t st, const F64FinishArgs& a);
