@@ -31,6 +31,7 @@ t0 = time.perf_counter()
 f = fit()
 dt = time.perf_counter() - t0
 print(json.dumps({"rows": N, "learners": L, "fit_ms": round(1000 * dt, 1),
+                  "exact_fallbacks": f.timing()["exact_fallbacks"],
                   "breakdown": {k: round(v, 2) for k, v in f.timing().items() if k.endswith("_ms")}}))
 f.free()
 ds.free()

@@ -1904,27 +1904,54 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       }
       return SBAG_OK;
     };
-    // ---- exact fallback: flagged nodes, every feature's bins in Spark's row order (one
-    // bucketing + chain task per (node, feature); the node total too when the replica has
-    // no feature with splits), then k_f64_split over them, in batches of bounded bucket space
+    // ---- exact fallback: flagged nodes, every feature's bins in Spark's row order, then
+    // k_f64_split over them.  Nodes up to walk_max entries: k_f64_hist (one wave per (node,
+    // feature group) walks the node's entries in order -- latency-bound per node, but the
+    // nodes run side by side); bigger ones: one bucketing + chain task per (node, feature)
+    // (the node total too when the replica has no feature with splits), throughput-bound,
+    // in batches of bounded bucket space.  (C3 shape, 1.1 y + 0.3, serialized: 93 flagged
+    // nodes of 8k-800k entries per fit; all walked 120 ms -- ~77 ns per entry of the largest
+    // node of a batch -- all chained 53 ms.)
+    // (read per level: the tests switch them between fits)
+    const bool walk_all = getenv("SBAG_F64_FALLBACK") && !strcmp(getenv("SBAG_F64_FALLBACK"), "hist");
+    const bool chain_all = getenv("SBAG_F64_FALLBACK") && !strcmp(getenv("SBAG_F64_FALLBACK"), "chain");
+    const int64_t walk_max =
+        getenv("SBAG_F64_WALK_MAX") ? atoll(getenv("SBAG_F64_WALK_MAX")) : (int64_t)8192;
+    auto walked = [&](int i) {
+      return walk_all || (!chain_all && cur[i].b - cur[i].a <= walk_max);
+    };
     std::vector<int> X, xi(M, -1);
-    for (int i = 0; i < M; i++)
-      if (so[i].flag) {
-        xi[i] = (int)X.size();
-        X.push_back(i);
-      }
+    for (int pass = 0; pass < 2; pass++)  // walked nodes first
+      for (int i = 0; i < M; i++)
+        if (so[i].flag && walked(i) == (pass == 0)) {
+          xi[i] = (int)X.size();
+          X.push_back(i);
+        }
+    size_t nwalk = 0;
+    while (nwalk < X.size() && walked(X[nwalk])) nwalk++;
     G.fallbacks += (int64_t)X.size();
+    if (getenv("SBAG_LEVEL_TRACE")) {
+      int64_t nof = 0, big = 0, ent = 0;
+      for (int i : X) {
+        nof += so[i].f < 0 ? 1 : 0;
+        big = std::max<int64_t>(big, cur[i].b - cur[i].a);
+        ent += cur[i].b - cur[i].a;
+      }
+      fprintf(stderr, "[sbag] f64 level %d nodes %d flagged %zu (no candidate %lld, walked %zu) entries %lld largest %lld\n",
+              level, M, X.size(), (long long)nof, nwalk, (long long)ent, (long long)big);
+    }
     std::vector<F64SplitOut> xo(X.size());
-    static const bool walk_fallback = getenv("SBAG_F64_FALLBACK") && !strcmp(getenv("SBAG_F64_FALLBACK"), "hist");
     for (size_t k0 = 0; k0 < X.size();) {
-      // a batch: nodes while their feature tasks' draws fit the budget (one node at least)
+      // a batch: walked nodes (up to 4096), or chained nodes while their feature tasks'
+      // draws fit the budget (one node at least)
+      const bool walk_fallback = k0 < nwalk;
       const double budget = (double)((int64_t)1 << 29);  // bucket entries (4 GB)
       size_t k1 = k0;
       double used = 0;
-      while (k1 < X.size()) {
+      while (k1 < X.size() && (k1 < nwalk) == walk_fallback) {
         const LNode& q = cur[X[k1]];
-        const double need = (double)(q.b - q.a) * (G.h_Fr[q.r] + 1);
-        if (k1 > k0 && used + need > budget) break;
+        const double need = walk_fallback ? 1.0 : (double)(q.b - q.a) * (G.h_Fr[q.r] + 1);
+        if (k1 > k0 && used + need > (walk_fallback ? 4096.0 : budget)) break;
         used += need;
         k1++;
       }
@@ -1954,7 +1981,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       TRY(h2d(c, d_nodes, hn.data(), (size_t)A));
       TRY(h2d(c, d_chain, chain.data(), (size_t)A));
       int h = G.tm.begin(T_FIX);
-      if (walk_fallback) {  // SBAG_F64_FALLBACK=hist: the row-order walk of every feature
+      if (walk_fallback) {  // the row-order walk of every feature
         const int fpw_env = getenv("SBAG_F64_FPW") ? atoi(getenv("SBAG_F64_FPW")) : 64;
         const int FPW = std::max(1, std::min(f64_hist_width(NB), fpw_env));
         const int ngroups = (Fmax + 1 + FPW - 1) / FPW;
@@ -2761,15 +2788,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       for (int fl = 0; fl < h_Fr[r] && mfma_root; fl++)
         if (h_pos_codes[(size_t)r * Fmax + fl] != fl) mfma_root = false;
     }
-    // 7-bit digit planes of k + K0 (the sums) and, for exact labels, of k^2 (the squares)
-    auto digits7 = [](uint64_t v) {
-      int d = 1;
-      while (d < 10 && (v >> (7 * d)) != 0) d++;
-      return d;
-    };
-    const uint64_t kspan_u = (uint64_t)(lkmax - lkmin);
-    const uint64_t kabs_u = (uint64_t)std::max(std::llabs(lkmin), std::llabs(lkmax));
-    const int nd1 = digits7(kspan_u), nd2 = f64 ? 0 : digits7(kabs_u * kabs_u);
+    // 7-bit digit planes of k + K0 (< 2^24: at most 4).  The root needs no squares plane
+    // (words [.][2]): the screen decides from (count, Σck), and the exact path's Σck² comes
+    // from k_compact / k_partition reductions and kHistSq launches
+    int nd1 = 1;
+    while (nd1 < 10 && ((uint64_t)(lkmax - lkmin) >> (7 * nd1)) != 0) nd1++;
+    const int nd2 = 0;
     if (nd1 + nd2 > 6) mfma_root = false;
     if (mfma_root) {
       TRY(ensure_cols());

@@ -190,14 +190,17 @@ def test_screened_engine_equals_unscreened(ctx, cpusmall, monkeypatch, case):
     monkeypatch.setenv("SBAG_F64_SCREEN", "0")
     b = _fit(ctx, X, y2, 6, 9)
     tb = b.timing()
-    # and the unscreened engine with the round-3 fallback (k_f64_hist: every feature walked
-    # in row order by one wave per feature group) instead of per-(node, feature) chains
+    # the exact fallback both ways: every flagged node walked in row order by one wave per
+    # (node, feature group) (k_f64_hist), and every flagged node bucketed + chained per
+    # (node, feature) (the default splits them by node size, SBAG_F64_WALK_MAX)
     monkeypatch.setenv("SBAG_F64_FALLBACK", "hist")
     c = _fit(ctx, X, y2, 6, 9)
+    monkeypatch.setenv("SBAG_F64_FALLBACK", "chain")
+    d = _fit(ctx, X, y2, 6, 9)
     for t in range(6):
-        (na, sa), (nb, sb_), (nc, sc) = a.tree(t), b.tree(t), c.tree(t)
-        assert na.tobytes() == nb.tobytes() == nc.tobytes(), f"tree {t}"
-        assert sa.tobytes() == sb_.tobytes() == sc.tobytes()
+        (na, sa), (nb, sb_), (nc, sc), (nd, sd) = a.tree(t), b.tree(t), c.tree(t), d.tree(t)
+        assert na.tobytes() == nb.tobytes() == nc.tobytes() == nd.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes() == sc.tobytes() == sd.tobytes()
     assert tb["exact_fallbacks"] >= ta["exact_fallbacks"]
     if case in ("cpusmall_pi", "cpusmall_sqrt"):
         assert ta["exact_fallbacks"] < tb["exact_fallbacks"] / 2  # the screen decides most nodes
