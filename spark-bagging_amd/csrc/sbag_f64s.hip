@@ -236,7 +236,7 @@ __device__ __forceinline__ void rstore64(__amdgpu_buffer_rsrc_t r, uint32_t off,
 }
 
 // per piece: entries per bin of the task's feature, entries going left (bin <= s).  Each
-// thread takes 4 entries per step, their loads (clamped indices: no branches, so the
+// thread takes 8 entries per step, their loads (clamped indices: no branches, so the
 // gathers are issued back to back) and gathers before the atomics.
 __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   const F64TPiece pc = A.pieces[blockIdx.x];
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   block_sync();
   const __amdgpu_buffer_rsrc_t rc = task_col_rsrc(A, t);
   uint32_t nl = 0;
-  constexpr int U = 4;
+  constexpr int U = 8;
   const int64_t last = pc.b - 1;
   for (int64_t i0 = pc.a; i0 < pc.b; i0 += 256 * U) {
     uint64_t e[U];
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const F64TPiece pc = A.pieces[pi];
   const F64Task t = A.tasks[pc.task];
   const int NB = A.NB;
-  const bool chain = t.kbase >= 0;
+  const bool chain = __builtin_amdgcn_readfirstlane((int)(t.kbase >= 0)) != 0;  // (uniform: SGPR resources)
   int64_t* sb = s_base[wv];
   for (int b = lane; b < NB; b += 64) sb[b] = chain ? A.pbase[pi * NB + b] : 0;
   int64_t lrun = t.part ? A.plbase[pi] : 0;
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(A.bky + (chain ? t.kbase : 0), nk * 8);
   const __amdgpu_buffer_rsrc_t rkc = rsrc_of(A.bkc + (chain ? t.kbase : 0), nk);
   const __amdgpu_buffer_rsrc_t ro = rsrc_of(A.ent_out + t.a, t.part ? (uint64_t)(t.b - t.a) * 8 : 0);
-  const __amdgpu_buffer_rsrc_t ry = rsrc_of(A.y, chain ? 0xFFFFFFFFull : 0);
+  const __amdgpu_buffer_rsrc_t ry = rsrc_of(A.y, 0xFFFFFFFFull);  // (routing-only tasks load them too)
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t last = pc.b - 1;
   // kScU rounds of 64 entries per step: all their entry loads, then all their bin and label
@@ -390,16 +390,16 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   }
 }
 
-// Spark's row-order fp64 sums of every bucket: one lane per (task, bin), 16 chains per
+// Spark's row-order fp64 sums of every bucket: one lane per (task, bin), kChC chains per
 // wave.  The chains' labels and counts stream through LDS: the whole wave loads each
 // chain's next kChT labels and counts with contiguous loads two stages ahead and writes
-// them to LDS; then lane l < 16 adds its own slice in order, each label count times
+// them to LDS; then lane l < kChC adds its own slice in order, each label count times
 // (sum += y, sumSq += y*y: instanceWeight 1.0 per draw, DTStatsAggregator.update; a row
-// drawn c times is c consecutive rows).
-constexpr int kChC = 16;    // chains per wave
-constexpr int kChT = 64;    // entries per chain per stage
-constexpr int kChPitch = kChT + 1;
+// drawn c times is c consecutive rows).  (kChC * kChT = 1024 entries per stage.)
+template <int kChC>
 __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
+  constexpr int kChT = 1024 / kChC;  // entries per chain per stage
+  constexpr int kChPitch = kChT + 1;
   __shared__ double s_y[kChC * kChPitch];
   __shared__ uint8_t s_c[kChC * kChPitch];
   const int NB = A.NB, lane = threadIdx.x;
@@ -437,10 +437,12 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
     for (int u = 0; u < kLd; u++) {
       const int j = u / kPer;
       const int64_t x = off + (u % kPer) * 64 + lane;
-      const int64_t at = jlen[j] > 0 ? jlo[j] + (x < jlen[j] ? x : 0) : 0;  // (empty: entry 0)
+      // (past the chain's end: its last entry, or the one before an empty chain -- min/max,
+      // no select on the wave-uniform length, which the compiler turns into branches)
+      const int64_t at = max(min(jlo[j] + x, jlo[j] + jlen[j] - 1), (int64_t)0);
       yv[u] = A.bky[at];
-      cv[u] = x < jlen[j] ? (uint32_t)A.bkc[at] : 0u;
-    }
+      cv[u] = (uint32_t)A.bkc[at];  // (unconditional: a masked load would make the
+    }                               //  compiler wait for every load in flight)
   };
   double yA[kLd], yB[kLd];
   uint32_t cA[kLd], cB[kLd];
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
       const int j = u / kPer;
       const int x = (u % kPer) * 64 + lane;
       s_y[j * kChPitch + x] = yA[u];
-      s_c[j * kChPitch + x] = (uint8_t)cA[u];
+      s_c[j * kChPitch + x] = off + x < jlen[j] ? (uint8_t)cA[u] : (uint8_t)0;
     }
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
@@ -511,9 +513,16 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
     hipLaunchKernelGGL(k_fb_scatter, dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
                        npieces, nbits);
   const int64_t lanes = (int64_t)nchain * a.NB;
-  if (lanes > 0)
-    hipLaunchKernelGGL(k_fb_chain, dim3((unsigned)((lanes + kChC - 1) / kChC)), dim3(64), 0, st, a,
-                       nchain);
+  // The serial adds are VALU-issue-bound: every wave-instruction serves kChC chains, so
+  // sixteen per wave wherever there are enough chains to fill the GPU (C3 shape, serialized,
+  // ms per fit: 16 everywhere 109; 1 / 4 / 16 by chain count 154) -- one or four only for a
+  // booster's few chains
+  if (lanes >= 4096)
+    hipLaunchKernelGGL(k_fb_chain<16>, dim3((unsigned)((lanes + 15) / 16)), dim3(64), 0, st, a, nchain);
+  else if (lanes >= 512)
+    hipLaunchKernelGGL(k_fb_chain<4>, dim3((unsigned)((lanes + 3) / 4)), dim3(64), 0, st, a, nchain);
+  else if (lanes > 0)
+    hipLaunchKernelGGL(k_fb_chain<1>, dim3((unsigned)lanes), dim3(64), 0, st, a, nchain);
 }
 
 // ---------------------------------------------------------------- finish
