@@ -3259,12 +3259,52 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   TRY(h2d(c, d_pos, h_pos.data(), h_pos.size()));
   TRY(h2d(c, d_nbins, h_nbins.data(), h_nbins.size()));
 
+  // Packed rows for the histograms (identity bins under feature subspaces, C5): each entry's
+  // row gather then pulls a row of roundup(F_r) bytes instead of the whole code row, most of
+  // it other replicas' features (C5: 64 of 128 bytes).  Built per fit: R N S_p bytes.  The
+  // partition keeps the shared column copy in global feature coordinates (h_pos).  Opt-in
+  // (SBAG_PACK_ROWS=1): measured on the C5 shard it does not pay -- hist 71.8 -> 69.8 ms per
+  // fit (k_hist is bound by its per-entry instructions, not by the row bytes), k_pack_rows
+  // 46 ms for 51 GB (profiles/r04m/).
+  const uint8_t* hbins = d_bins;
+  int64_t hb_rstride = bins_rstride;
+  int32_t hS = S;
+  int16_t* hpos = d_pos;
+  std::vector<int16_t> h_hpos = h_pos;
+  {
+    const int Sp = row_stride(Fmax);
+    bool sub_any = false;
+    for (int r = 0; r < R && !sub_any; r++)
+      for (int fl = 0; fl < h_Fr[r]; fl++)
+        if (h_pos[(size_t)r * Fmax + fl] != fl) sub_any = true;
+    const int pack_env = getenv("SBAG_PACK_ROWS") ? atoi(getenv("SBAG_PACK_ROWS")) : -1;
+    const bool can = identity && bins_rstride == 0 && sub_any && Sp < S && ds->code_bytes == 1 &&
+                     S % 4 == 0 && (double)R * N * Sp <= bins_budget(c);
+    const bool pack = can && pack_env == 1;
+    if (pack) {
+      int h = tm.begin(T_BIN);
+      uint8_t* d_pk;
+      TRY(ws_typed(c, "packed_rows", (size_t)R * N * Sp + 256, &d_pk));
+      launch_pack_rows(c->stream, (const uint8_t*)ds->d_codes, N, S, d_sub, d_Fr, Fmax, R, d_pk, Sp);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemsetAsync(d_pk + (size_t)R * N * Sp, 0, 256, c->stream));  // zero slack
+      for (int r = 0; r < R; r++)
+        for (int fl = 0; fl < Fmax; fl++) h_hpos[(size_t)r * Fmax + fl] = (int16_t)(fl < h_Fr[r] ? fl : 0);
+      TRY(ws_typed(c, "pos_hist", h_hpos.size(), &hpos));
+      TRY(h2d(c, hpos, h_hpos.data(), h_hpos.size()));
+      tm.end(h);
+      hbins = d_pk;
+      hb_rstride = (int64_t)N * Sp;
+      hS = Sp;
+    }
+  }
+
   hmark(12);
   // ---- 6. level-wise growth
   HistGeom g;
-  if (!hist_geometry(S, Fmax, NB, NS, gini, g, rl_mode_for(h_pos, S)))
+  if (!hist_geometry(hS, Fmax, NB, NS, gini, g, rl_mode_for(h_hpos, hS)))
     return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
-  TRY(maybe_grouped(g, S, NB));
+  TRY(maybe_grouped(g, hS, NB));
   if (ha.hct == 0) ha.hct = hist_layout_tile(g);  // else the optimistic root's layout
   const int64_t slot_words = (int64_t)Fmax * NB * NS;
   std::vector<std::vector<HNode>> trees(R);
@@ -3274,10 +3314,10 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     trees[r].push_back(HNode{});
     slots[r] = {r, 0};
   }
-  ha.bins = d_bins;
-  ha.bins_rstride = bins_rstride;
-  ha.S = S;
-  ha.pos = d_pos;
+  ha.bins = hbins;
+  ha.bins_rstride = hb_rstride;
+  ha.S = hS;
+  ha.pos = hpos;
   ha.NB = NB;
   ha.NS = NS;
   ha.count_only = 0;

@@ -257,6 +257,10 @@ void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, co
 void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
                         const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
                         const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out);
+// identity bins packed per replica: out[r][n][fl] = codes[n][sub[r][fl]], S_out % 4 == 0,
+// S_codes % 4 == 0
+void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
+                      const int32_t* d_Fr, int32_t Fmax, int R, uint8_t* out, int32_t S_out);
 void launch_synth(hipStream_t st, uint8_t* codes, int32_t S, int64_t N, int32_t F, uint64_t seed,
                   int32_t num_classes, int32_t* labk);
 void launch_predict(hipStream_t st, const double* X, const void* codes, int code_bytes,

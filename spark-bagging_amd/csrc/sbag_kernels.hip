@@ -3235,6 +3235,45 @@ void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64
                        S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
 }
 
+// Per-replica packed rows of identity bins: out[r][n][fl] = codes[n][sub[r][fl]] (0 past the
+// replica's F_r), S_out bytes per row.  A workgroup takes 16 rows: their code rows into LDS
+// (coalesced), then per replica one 4-byte word of the 16 x S_out output bytes per thread
+// (coalesced stores).
+__global__ __launch_bounds__(256) void k_pack_rows(const uint8_t* __restrict__ codes, int64_t N,
+                                                   int32_t S_codes, const int32_t* __restrict__ sub,
+                                                   const int32_t* __restrict__ Fr, int32_t Fmax, int R,
+                                                   uint8_t* __restrict__ out, int32_t S_out) {
+  extern __shared__ __align__(16) uint8_t s_rows[];  // [16][S_codes]
+  const int tid = threadIdx.x;
+  const int64_t n0 = (int64_t)blockIdx.x * 16;
+  const int nr = (int)min<int64_t>(16, N - n0);
+  for (int k = tid; k < nr * S_codes / 4; k += 256)
+    ((uint32_t*)s_rows)[k] = ((const uint32_t*)(codes + n0 * S_codes))[k];
+  block_sync();
+  const int wpr = S_out / 4;  // output words per row
+  for (int r = 0; r < R; r++) {
+    const int fr = Fr[r];
+    const int32_t* sr = sub + (int64_t)r * Fmax;
+    for (int q = tid; q < nr * wpr; q += 256) {
+      const int row = q / wpr, w = q - row * wpr;
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int fl = 4 * w + k;
+        if (fl < fr) v |= (uint32_t)s_rows[row * S_codes + sr[fl]] << (8 * k);
+      }
+      ((uint32_t*)(out + ((int64_t)r * N + n0) * S_out))[q] = v;
+    }
+  }
+}
+
+void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
+                      const int32_t* d_Fr, int32_t Fmax, int R, uint8_t* out, int32_t S_out) {
+  const unsigned blocks = (unsigned)((N + 15) / 16);
+  hipLaunchKernelGGL(k_pack_rows, dim3(blocks), dim3(256), (size_t)16 * S_codes, st, codes, N, S_codes,
+                     d_sub, d_Fr, Fmax, R, out, S_out);
+}
+
 // Per-replica bins of a wide (u32-coded) dataset: the bin of a code is the number of the
 // feature's thresholds below its value, i.e. of code cuts (#{dict values <= t}) at or
 // below the code; a binary search over the replica's cuts (padded with ~0u).
