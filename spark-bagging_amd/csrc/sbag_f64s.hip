@@ -34,6 +34,7 @@
 // label); upstream RandomForest.findBestSplits / binsToBestSplit (Spark 2.4.3).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 
@@ -247,6 +248,8 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   for (int b = tid; b < NB; b += 256) s_c[b] = 0u;
   block_sync();
   const __amdgpu_buffer_rsrc_t rc = task_col_rsrc(A, t);
+  // the gathered bins, kept for k_fb_scatter (which then reads them in order)
+  const __amdgpu_buffer_rsrc_t re = rsrc_of(A.ebin + t.ebase, (uint64_t)(t.b - t.a));
   uint32_t nl = 0;
   constexpr int U = 8;
   const int64_t last = pc.b - 1;
@@ -258,11 +261,15 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
 #pragma unroll
     for (int u = 0; u < U; u++) bin[u] = rbin(rc, e[u]);
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      if (i0 + u * 256 + tid < pc.b) {
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + u * 256 + tid;
+      // (lanes past the piece store past the resource: dropped)
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bin[u], re, i < pc.b ? (int)(i - t.a) : -1, 0, 0);
+      if (i < pc.b) {
         atomicAdd(&s_c[bin[u]], 1u);
         nl += bin[u] <= (uint32_t)t.s ? 1u : 0u;
       }
+    }
   }
   for (int o = 32; o > 0; o >>= 1) nl += __shfl_down(nl, o);
   if ((tid & 63) == 0) s_l[tid >> 6] = nl;
@@ -333,14 +340,21 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   for (int b = lane; b < NB; b += 64) sb[b] = chain ? A.pbase[pi * NB + b] : 0;
   int64_t lrun = t.part ? A.plbase[pi] : 0;
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
-  const __amdgpu_buffer_rsrc_t rc = task_col_rsrc(A, t);
+  // the entries' bins as k_fb_count gathered them (in entry order: coalesced)
+  const __amdgpu_buffer_rsrc_t re = rsrc_of(A.ebin + t.ebase, (uint64_t)(t.b - t.a));
   // the task's buckets (labels and counts) and its children's segment (each < 4 GB: a
   // node's entries); the labels (rows < 2^29)
   const uint64_t nk = chain ? (uint64_t)(t.b - t.a) : 0;
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(A.bky + (chain ? t.kbase : 0), nk * 8);
   const __amdgpu_buffer_rsrc_t rkc = rsrc_of(A.bkc + (chain ? t.kbase : 0), nk);
   const __amdgpu_buffer_rsrc_t ro = rsrc_of(A.ent_out + t.a, t.part ? (uint64_t)(t.b - t.a) * 8 : 0);
-  const __amdgpu_buffer_rsrc_t ry = rsrc_of(A.y, 0xFFFFFFFFull);  // (routing-only tasks load them too)
+  // the entries' labels: carried in entry order (coalesced; and the children's written),
+  // or, without the carried copy (ey_in null: too big), gathered by row
+  const bool carried = A.ey_in != nullptr;
+  const __amdgpu_buffer_rsrc_t ry =
+      carried ? rsrc_of(A.ey_in + t.a, (uint64_t)(t.b - t.a) * 8) : rsrc_of(A.y, 0xFFFFFFFFull);
+  const __amdgpu_buffer_rsrc_t roy =
+      rsrc_of(carried ? A.ey_out + t.a : A.ey_out, carried && t.part ? (uint64_t)(t.b - t.a) * 8 : 0);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t last = pc.b - 1;
   // kScU rounds of 64 entries per step: all their entry loads, then all their bin and label
@@ -356,8 +370,9 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
     for (int u = 0; u < kScU; u++) ev[u] = A.ent_in[min(i0 + 64 * u + lane, last)];
 #pragma unroll
     for (int u = 0; u < kScU; u++) {
-      bv[u] = rbin(rc, ev[u]);
-      yv[u] = __builtin_amdgcn_raw_buffer_load_b64(ry, (int)((uint32_t)ev[u] * 8u), 0, 0);
+      bv[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(re, (int)(min(i0 + 64 * u + lane, last) - t.a), 0, 0);
+      const int yoff = carried ? (int)(min(i0 + 64 * u + lane, last) - t.a) * 8 : (int)((uint32_t)ev[u] * 8u);
+      yv[u] = __builtin_amdgcn_raw_buffer_load_b64(ry, yoff, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kScU; u++) {
@@ -385,6 +400,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
       const int64_t lr = __popcll(lm & lt);
       const int64_t pos = left ? lrun + lr : nl + (i - t.a - lrun - lr);  // within the segment
       rstore64(ro, valid ? (uint32_t)pos * 8u : 0xFFFFFFF0u, e);
+      __builtin_amdgcn_raw_buffer_store_b64(yv[u], roy, valid ? (int)((uint32_t)pos * 8u) : -16, 0, 0);
       lrun += __popcll(lm);
     }
   }
@@ -500,6 +516,25 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
     o[1] = s1;
     o[2] = s2;
   }
+}
+
+// the labels of the root entries, in entry order: what the scatter reads (and carries to
+// the children) instead of gathering y[row] per entry at every level
+__global__ __launch_bounds__(256) void k_entry_labels(const uint64_t* __restrict__ ent,
+                                                      const double* __restrict__ y,
+                                                      double* __restrict__ ey, int64_t cap,
+                                                      const int64_t* __restrict__ nent) {
+  const int r = blockIdx.y;
+  const int64_t n = nent[r];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    ey[r * cap + i] = y[(uint32_t)ent[r * cap + i]];
+}
+
+void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap,
+                         const int64_t* d_nent, int R, int64_t max_nent) {
+  if (R <= 0 || max_nent <= 0) return;
+  const unsigned bx = (unsigned)std::min<int64_t>((max_nent + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_entry_labels, dim3(bx, (unsigned)R), dim3(256), 0, st, ent, y, ey, cap, d_nent);
 }
 
 void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain) {

@@ -408,6 +408,7 @@ struct F64Task {            // one (node, feature) whose entries are bucketed / 
   int64_t piece0, piece1;   // its pieces
   int32_t r, col, s, part;  // replica, column of the column-major bins (-1: every entry in
                             // bin 0, the node total), split bin, route?
+  int64_t ebase;            // its entries' bins at ebin[ebase, ebase + b - a) (k_fb_count)
 };
 struct F64TPiece {
   int64_t a, b;
@@ -424,6 +425,7 @@ struct F64BucketArgs {
   uint64_t* ent_out;        // children: left [a, a + nleft), right [a + nleft, b), row order
   double* bky;              // the buckets: the node's entries' labels grouped by bin, row
   uint8_t* bkc;             //   order kept, and their draw counts
+  uint8_t* ebin;            // every task's entries' bins, gathered once by k_fb_count
   uint32_t* pcnt;           // [piece][NB] entries per bin
   uint32_t* plcnt;          // [piece] entries going left
   int64_t* pbase;           // [piece][NB] bucket position of the piece's first entry per bin
@@ -431,8 +433,13 @@ struct F64BucketArgs {
   int64_t* nleft;           // [task]
   int64_t* kb_off;          // [task][NB + 1] bucket bounds in entK
   const double* y;          // [N] labels
+  const double* ey_in;      // the labels of ent_in's entries (same positions)
+  double* ey_out;           // the labels of ent_out's entries
   double* chist;            // [task][NB][3] count, sum, sumSq in Spark's row order
 };
+// ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]
+void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap,
+                         const int64_t* d_nent, int R, int64_t max_nent);
 struct F64FinishNode {
   int32_t t, t0;            // task of the chosen feature; task of the first feature with
                             // splits (root: the parent stats), -1 when not needed

@@ -197,10 +197,15 @@ def test_screened_engine_equals_unscreened(ctx, cpusmall, monkeypatch, case):
     c = _fit(ctx, X, y2, 6, 9)
     monkeypatch.setenv("SBAG_F64_FALLBACK", "chain")
     d = _fit(ctx, X, y2, 6, 9)
+    # and the scatter gathering y[row] instead of reading the labels carried with the entries
+    monkeypatch.delenv("SBAG_F64_SCREEN")
+    monkeypatch.delenv("SBAG_F64_FALLBACK")
+    monkeypatch.setenv("SBAG_F64_NO_CARRY", "1")
+    e = _fit(ctx, X, y2, 6, 9)
     for t in range(6):
-        (na, sa), (nb, sb_), (nc, sc), (nd, sd) = a.tree(t), b.tree(t), c.tree(t), d.tree(t)
-        assert na.tobytes() == nb.tobytes() == nc.tobytes() == nd.tobytes(), f"tree {t}"
-        assert sa.tobytes() == sb_.tobytes() == sc.tobytes() == sd.tobytes()
+        (na, sa), (nb, sb_), (nc, sc), (nd, sd), (ne, se) = a.tree(t), b.tree(t), c.tree(t), d.tree(t), e.tree(t)
+        assert na.tobytes() == nb.tobytes() == nc.tobytes() == nd.tobytes() == ne.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes() == sc.tobytes() == sd.tobytes() == se.tobytes()
     assert tb["exact_fallbacks"] >= ta["exact_fallbacks"]
     if case in ("cpusmall_pi", "cpusmall_sqrt"):
         assert ta["exact_fallbacks"] < tb["exact_fallbacks"] / 2  # the screen decides most nodes
