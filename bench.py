@@ -23,6 +23,7 @@ import sbag_loader  # noqa: E402
 SEED_REG = -1395689524  # default seed of BaggingRegressor (class-name hashCode)
 SEED_CLS = 42087812     # default seed of BaggingClassifier
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
+MFMA_I8_PEAK_TOPS = 5000.0  # dense int8 MFMA, 2x the ~2.5 PF dense BF16 (MI355X_MICROARCH.md, matrix cores)
 # ds_add_u64 throughput measured on MI355X by scripts/micro/lds_atomic.hip:
 # 7.16 cycles per wave-instruction per CU (4 x 512-thread workgroups per CU), 256 CUs, 2.4 GHz
 LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
@@ -49,7 +50,8 @@ def pmc_traffic(workload):
         except (OSError, ValueError):
             continue
         for k, v in d.items():
-            if k.startswith("sbag::k_hist") and "hbm_bytes_per_launch" in v:
+            # (the level histograms' kernel; the MFMA root is reported apart)
+            if (k.startswith("sbag::k_hist<") or k.startswith("sbag::k_hist_rl<")) and "hbm_bytes_per_launch" in v:
                 return round(v["hbm_bytes_per_launch"]), rel, k
     return None, None, None
 
@@ -290,6 +292,19 @@ def main():
                                "unit": "G wave-instr/s (%s peak, scripts/micro/lds_atomic.hip)"
                                        % ("ds_add_u32" if cls else "ds_add_u64"),
                                "frac": round(lds_rate / lds_peak, 4)}}
+    # the root histogram as an int8 MFMA contraction (k_hist_mfma): its
+    # dense int8 operations over its HIP-event time against the dense int8 MFMA peak
+    root_ms = sum(t.get("root_ms", 0.0) for t in timings)
+    root_ops = sum(t.get("root_mfma_ops", 0.0) for t in timings)
+    if root_ms > 0 and root_ops > 0:
+        tops = root_ops / (root_ms / 1e3) / 1e12
+        roofline["root_mfma"] = {"kernel": "sbag::k_hist_mfma (root histogram, int8 MFMA)",
+                                 "bound": "mfma", "achieved": round(tops, 1), "peak": MFMA_I8_PEAK_TOPS,
+                                 "unit": "TOPS", "frac": round(tops / MFMA_I8_PEAK_TOPS, 4),
+                                 "ms_per_fit": round(root_ms, 3),
+                                 "ops_def": "2 x 32^3 int8 ops per v_mfma_i32_32x32x32_i8 issued: "
+                                            "ceil(N/32) row steps x F x ceil(R/32) replica tiles "
+                                            "x (1 + label digit planes)"}
     breakdown = {k: round(v, 3) for k, v in timings[-1].items() if k.endswith("_ms")}
     # the sampler's cost depends on rows per partition stream (Poisson.scala:53-56 reseeds
     # per partition): one extra fit, outside the timed region, at P = nproc
