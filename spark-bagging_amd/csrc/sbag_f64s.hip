@@ -486,15 +486,28 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
     if (lane < kChC) {
       const double* sy = s_y + lane * kChPitch;
       const uint8_t* sc = s_c + lane * kChPitch;
-      // (4 entries' LDS reads ahead of their adds; every bucket entry is drawn, c >= 1)
+      // (4 entries' LDS reads ahead of their adds; every bucket entry is drawn, c >= 1.)
+      // A lane's adds are one dependent chain, so the instructions between two adds pace a
+      // long chain: the second to fourth draws are added branch-free (a draw past c adds
+      // -0.0, which leaves every sum unchanged, -0.0 included), the loop takes only c > 4
+      // (scripts/micro/chain_lat.hip: a per-entry count loop costs 4.5x the adds).
+      const bool multi = A.cmax > 1;
       auto add = [&](double y, uint32_t c) {
         const double w = 1.0 * y;  // instanceWeight * label
         const double wy = w * y;   // instanceWeight * label * label
         s1 += w;
         s2 += wy;
-        for (uint32_t k = 1; k < c; k++) {
-          s1 += w;
-          s2 += wy;
+        if (multi) {
+          s1 += c >= 2 ? w : -0.0;
+          s2 += c >= 2 ? wy : -0.0;
+          s1 += c >= 3 ? w : -0.0;
+          s2 += c >= 3 ? wy : -0.0;
+          s1 += c >= 4 ? w : -0.0;
+          s2 += c >= 4 ? wy : -0.0;
+          for (uint32_t k = 4; k < c; k++) {
+            s1 += w;
+            s2 += wy;
+          }
         }
         cnt += c;
       };

@@ -1927,6 +1927,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.kb_off = d_kboff;
       ba.y = d_y64;
       ba.chist = chist;
+      ba.cmax = (int32_t)G.cmax;
       launch_fb_route(c->stream, ba, np, nchain);
       HIP_TRY(hipGetLastError());
       if (nleft_out) {
@@ -2155,8 +2156,22 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       double* d_chist;
       TRY(ws_typed(c, "fb_chist", (size_t)std::max(1, nchain0 + nchain1) * NB * 3, &d_chist));
       int h = G.tm.begin(T_CHAIN);
-      TRY(run_tasks(tasks[0], nchain0, kb[0], d_chist, &nleft));
-      TRY(run_tasks(tasks[1], nchain1, kb[1], d_chist + (size_t)nchain0 * NB * 3, nullptr));
+      // one launch sequence for both passes: the root's chains of the chosen features and of
+      // the first features run side by side (the root has few, long chains: 2 x 2048 per C3
+      // half, each ~200k entries, and a lone chain's adds are latency-bound)
+      std::vector<F64Task> all;
+      all.reserve(tasks[0].size() + tasks[1].size());
+      all.insert(all.end(), tasks[0].begin(), tasks[0].begin() + nchain0);
+      for (F64Task t : tasks[1]) {
+        t.kbase += kb[0];
+        all.push_back(t);
+      }
+      all.insert(all.end(), tasks[0].begin() + nchain0, tasks[0].end());
+      std::vector<int64_t> nl_all;
+      TRY(run_tasks(all, nchain0 + nchain1, kb[0] + kb[1], d_chist, &nl_all));
+      nleft.assign(tasks[0].size(), 0);
+      for (size_t t = 0; t < tasks[0].size(); t++)
+        nleft[t] = nl_all[(int)t < nchain0 ? t : t + nchain1];
       G.tm.end(h);
       if (!fin.empty()) {
         F64FinishNode* d_fn;

@@ -436,6 +436,7 @@ struct F64BucketArgs {
   const double* ey_in;      // the labels of ent_in's entries (same positions)
   double* ey_out;           // the labels of ent_out's entries
   double* chist;            // [task][NB][3] count, sum, sumSq in Spark's row order
+  int32_t cmax, pad;        // largest draw count of an entry (1: no count loop)
 };
 // ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]
 void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap,
