@@ -350,8 +350,12 @@ def main():
                      "value": round(L * N * args.nondyadic_steps / el, 1),
                      "unit": "estimator*rows/s",
                      "breakdown_ms": {k: round(v, 3) for k, v in tl[-1].items() if k.endswith("_ms")},
-                     "engine": "row-order fp64 histograms (LDS fp64 atomics), device "
-                               "binsToBestSplit, stable partition (DESIGN.md §4.7)"}
+                     "exact_fallbacks": int(tl[-1]["exact_fallbacks"]),
+                     "engine": "screened fp64 engine: splits chosen from integer histograms of the "
+                               "labels' fixed-point image under a rigorous error bound, the chosen "
+                               "feature's bins summed in Spark's row order (bucketing + chains), "
+                               "flagged nodes ('exact_fallbacks') summed exactly on every feature "
+                               "(DESIGN.md §4.7)"}
     out = {
         "metric": "estimator×rows trained/sec", "value": round(value, 1),
         "unit": "estimator*rows/s", "n_gpus": world, "backend": args.backend if world > 1 else None,
