@@ -447,9 +447,10 @@ __global__ __launch_bounds__(64) void k_f64_split(F64SplitArgs A) {
   }
   double best_gain = 0.0;
   int best_f = -1, best_s = -1, best_valid = 0;
+  const uint8_t* fm = A.fmask ? A.fmask + (int64_t)q * A.Fmax : nullptr;
   for (int fl = lane; fl < Fr; fl += 64) {
     const int nsp = nbins[fl] - 1;
-    if (nsp <= 0) continue;
+    if (nsp <= 0 || (fm && !fm[fl])) continue;
     const double* fa = h + (int64_t)fl * NB * 3;
     double t0 = fa[0], t1 = fa[1], t2 = fa[2];
     for (int s = 1; s <= nsp; s++) {

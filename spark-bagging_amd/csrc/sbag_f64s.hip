@@ -156,11 +156,16 @@ __global__ __launch_bounds__(256) void k_f64_screen(F64ScreenArgs A) {
   const int bfl = s_fl[0], bs = s_s[0];
   const double dn = A.dnode[slot], dp = A.dpar[slot];
   block_sync();
-  // pass 2: candidates whose upper bound reaches the best's lower bound (the best too)
+  // pass 2: candidates whose upper bound reaches the best's lower bound (the best too), and
+  // per feature whether it holds one: a flagged node's exact fallback needs only those
+  // features (every other candidate's exact gain is below the best's, so it can be neither
+  // Spark's argmax nor tie with it)
   int cnt = 0;
-  if (bfl != INT_MAX) {
-    const double thr = gb - ab - 2.0 * dn;
-    for (int fl = tid; fl < Fr; fl += 256) {
+  uint8_t* cm = A.cmask + (int64_t)slot * A.Fmax;
+  const double thr = gb - ab - 2.0 * dn;
+  for (int fl = tid; fl < Fr; fl += 256) {
+    int fc = 0;
+    if (bfl != INT_MAX) {
       const int nsp = nb_r[fl] - 1;
       const uint64_t* h = hs + (int64_t)fl * NB * 3;
       int64_t lc = 0, lsk = 0;
@@ -170,9 +175,11 @@ __global__ __launch_bounds__(256) void k_f64_screen(F64ScreenArgs A) {
         if (lc < A.min_inst || tc - lc < A.min_inst) continue;
         double g, a;
         screen_cand(lc, lsk, tc, tsk, n, is, eps, &g, &a);
-        if (!(g + a < thr)) cnt++;  // NaN counts as a contender
+        if (!(g + a < thr)) fc++;  // NaN counts as a contender
       }
     }
+    cm[fl] = fc > 0 ? 1 : 0;
+    cnt += fc;
   }
   s_cnt[tid] = cnt;
   block_sync();

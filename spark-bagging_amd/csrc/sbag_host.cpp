@@ -1827,6 +1827,9 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     // ---- 1. screen (level D only happens for maxDepth 0: the root's stats, exactly)
     std::vector<F64ScreenOut> so(M);
     for (auto& o : so) o.flag = 1;
+    // per node, the features whose exact sums a flagged node needs (the screen's contenders;
+    // every feature when the screen did not run)
+    std::vector<uint8_t> cmask((size_t)M * Fmax, 1);
     if (screen_on && level < D) {
       std::vector<int32_t> h_slot_r(M);
       std::vector<double> hdn(M), hdp(M);
@@ -1860,12 +1863,21 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       sa.dnode = d_dn;
       sa.dpar = d_dp;
       sa.out = d_so;
+      uint8_t* d_cm;
+      TRY(ws_typed(c, "f64_cmask", (size_t)M * Fmax, &d_cm));
+      sa.cmask = d_cm;
       int h = G.tm.begin(T_SPLIT);
       launch_f64_screen(c->stream, sa, M);
       HIP_TRY(hipGetLastError());
       G.tm.end(h);
       TRY(d2h(c, so.data(), d_so, (size_t)M));
+      const bool all_features = getenv("SBAG_F64_FALLBACK_ALL") != nullptr;  // (A/B, tests)
+      if (!all_features) TRY(d2h(c, cmask.data(), d_cm, cmask.size()));
     }
+    // ... and the first feature with splits of the node's replica (at the root its bins
+    // give Spark's parent stats; a node without any valid candidate takes its first split)
+    for (int i = 0; i < M; i++)
+      if (f0[cur[i].r] >= 0) cmask[(size_t)i * Fmax + f0[cur[i].r]] = 1;
     // Buckets + routing of a task list (launch_fb_route): the chain sums of its first
     // `nchain` tasks land at chist (task-major [NB][3]); nleft (optional) gets the left
     // entries of every routing task.  Bucket space: the chain tasks' entries.
@@ -1982,7 +1994,9 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       double used = 0;
       while (k1 < X.size() && (k1 < nwalk) == walk_fallback) {
         const LNode& q = cur[X[k1]];
-        const double need = walk_fallback ? 1.0 : (double)(q.b - q.a) * (G.h_Fr[q.r] + 1);
+        int nf = 1;
+        for (int fl = 0; fl < G.h_Fr[q.r]; fl++) nf += cmask[(size_t)X[k1] * Fmax + fl];
+        const double need = walk_fallback ? 1.0 : (double)(q.b - q.a) * nf;
         if (k1 > k0 && used + need > (walk_fallback ? 4096.0 : budget)) break;
         used += need;
         k1++;
@@ -2049,7 +2063,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
             t.r = q.r;
             t.s = -1;
             t.part = 0;
-            const bool real = fl < G.h_Fr[q.r] || (fl == G.h_Fr[q.r] && f0[q.r] < 0);
+            const bool real = (fl < G.h_Fr[q.r] && cmask[(size_t)X[k0 + k] * Fmax + fl]) ||
+                              (fl == G.h_Fr[q.r] && f0[q.r] < 0);
             if (real) {
               t.a = q.a;
               t.b = q.b;
@@ -2086,6 +2101,16 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       sa.min_inst = G.tp.min_instances_per_node;
       sa.min_gain = G.tp.min_info_gain;
       sa.out = d_out;
+      {
+        std::vector<uint8_t> fm((size_t)A * Fmax);
+        for (int k = 0; k < A; k++)
+          std::copy(cmask.begin() + (size_t)X[k0 + k] * Fmax, cmask.begin() + (size_t)(X[k0 + k] + 1) * Fmax,
+                    fm.begin() + (size_t)k * Fmax);
+        uint8_t* d_fm;
+        TRY(ws_typed(c, "f64_fmask", fm.size(), &d_fm));
+        TRY(h2d(c, d_fm, fm.data(), fm.size()));
+        sa.fmask = d_fm;
+      }
       launch_f64_split(c->stream, sa, A);
       HIP_TRY(hipGetLastError());
       G.tm.end(h);
@@ -2827,9 +2852,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     ha.count_only = 0;
     // Variance with every replica on every feature of <= 32 codes, counts <= 127: the root
     // histogram as an int8 MFMA contraction (sbag_mfma.hip; SBAG_ROOT_MFMA=0: k_hist_rl)
-    const int mfma_env = getenv("SBAG_ROOT_MFMA") ? atoi(getenv("SBAG_ROOT_MFMA")) : 1;
-    bool mfma_root = !gini && mfma_env != 0 && ncmax <= 32 && N % 16 == 0 && cmax <= 127 &&
-                     Fmax == F && !getenv("SBAG_NO_LAYOUT_CACHE");
+    const int mfma_env = getenv("SBAG_ROOT_MFMA") ? atoi(getenv("SBAG_ROOT_MFMA")) : -1;
+    // (its cost goes with ceil(R / 32) tiles, the atomics' with R: below 16 replicas -- a
+    // booster's single tree -- the atomics are cheaper; SBAG_ROOT_MFMA=1 forces it)
+    bool mfma_root = !gini && mfma_env != 0 && (R >= 16 || mfma_env == 1) && ncmax <= 32 &&
+                     N % 16 == 0 && cmax <= 127 && Fmax == F && !getenv("SBAG_NO_LAYOUT_CACHE");
     for (int r = 0; r < R && mfma_root; r++) {
       if (h_Fr[r] != F) mfma_root = false;
       for (int fl = 0; fl < h_Fr[r] && mfma_root; fl++)

@@ -345,6 +345,8 @@ struct F64SplitArgs {
   int32_t Fmax, NB, min_inst, pad;
   double min_gain;
   F64SplitOut* out;
+  const uint8_t* fmask;    // [node][Fmax] features to consider (null: all); the others hold
+                           // no sums (the screen proved none of their candidates can win)
 };
 struct F64PartNode {  // a split node: entries [a, b), pieces [piece0, piece1)
   int64_t a, b, piece0, piece1;
@@ -401,6 +403,7 @@ struct F64ScreenArgs {
                             //     candidate's child part (lw imp(L) + rw imp(R)) of the gain
   const double* dpar;       // [M] bound on the error of the node's own impurity
   F64ScreenOut* out;        // [M]
+  uint8_t* cmask;           // [M][Fmax] the feature holds a contender (pass 2)
 };
 struct F64Task {            // one (node, feature) whose entries are bucketed / routed
   int64_t a, b;             // entries [a, b) of ent_in (row order)
