@@ -52,6 +52,7 @@ def synthetic_line(n):
         t1 = time.perf_counter()
         p = nat.predict_dataset(ctx, f, ds, nat.AGG_MEAN)
         t2 = time.perf_counter()
+        bd = {k: round(v, 2) for k, v in f.timing().items() if k.endswith("_ms") and v}
         f.free()
         res = res - 0.5 * p
         fit_ms.append(1e3 * (t1 - t0))
@@ -62,7 +63,7 @@ def synthetic_line(n):
                       "data": "device synthetic codes, labels 1.1 y + 0.3", "fit_s": round(dt, 3),
                       "ms_per_booster": round(1e3 * dt / a.learners, 2),
                       "booster_fit_ms": round(sum(fit_ms) / len(fit_ms), 2),
-                      "predict_ms": round(sum(pred_ms) / len(pred_ms), 2),
+                      "predict_ms": round(sum(pred_ms) / len(pred_ms), 2), "breakdown_last": bd,
                       "rows_x_boosters_per_s": round(n * a.learners / dt, 1)}), flush=True)
 
 

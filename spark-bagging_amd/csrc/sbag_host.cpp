@@ -1351,7 +1351,9 @@ static bool hist_geometry(int S, int Fmax, int NB, int NS, bool gini_layout, His
   g.lds = lds_for(g.FT, ct);
   g.rl = 0;
   // row lanes when they carry fewer dump lanes than 64-feature lane groups
-  if (rl_mode && roundup(g.FT, hist_rl_lanes()) < roundup(g.FT, 64)) {
+  // (SBAG_HIST_RL_FORCE=1: whenever the layout allows them, for A/B)
+  static const bool rl_force = getenv("SBAG_HIST_RL_FORCE") && atoi(getenv("SBAG_HIST_RL_FORCE")) != 0;
+  if (rl_mode && (rl_force || roundup(g.FT, hist_rl_lanes()) < roundup(g.FT, 64))) {
     const size_t b = hist_rl_lds_bytes(NB, ct, g.FPH, gini_layout);
     if (b <= hard) {
       g.rl = rl_mode;
