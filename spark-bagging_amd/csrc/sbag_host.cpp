@@ -329,6 +329,7 @@ struct LabelSet {
   bool label_ok = false;                  // representable as |k| < 2^23
   int64_t kmin = 0, kmax = 0;
   bool integral = false;                  // all labels integers >= 0 (classifiable)
+  bool finite = true;                     // no NaN / inf
   // labels that are not dyadic (fp64 path): the fixed-point image k = round(y 2^ashift),
   // |k| <= 2^22, which the integer histograms screen splits with (|y - k 2^-ashift| <=
   // 2^-ashift-1), and the labels' largest |y| and y*y (the screen's error bounds)
@@ -375,90 +376,115 @@ static int32_t row_stride(int32_t F) {
   return (F + 127) / 128 * 128;
 }
 
-static void analyze_labels(LabelSet& L) {
-  L.label_ok = false;
-  L.integral = true;
-  for (double v : L.y)
-    if (!(v >= 0 && v == std::floor(v) && v < 8388608.0)) {
-      L.integral = false;
-      break;
-    }
-  for (int s = 0; s <= 40 && !L.label_ok; s++) {
-    bool ok = true;
-    int64_t mn = 0, mx = 0;
-    bool first = true;
-    for (double v : L.y) {
+// chunks of [0, N) on the host pool (one chunk per worker; serial without a pool)
+static void par_range(HostPool* pool, int64_t N, const std::function<void(int64_t, int64_t, int)>& f,
+                      int* nw_out = nullptr) {
+  const int nw = pool && N >= (1 << 16) ? HostPool::width() : 1;
+  if (nw_out) *nw_out = nw;
+  auto body = [&](int w) {
+    const int64_t lo = N * w / nw, hi = N * (w + 1) / nw;
+    f(lo, hi, w);
+  };
+  if (nw == 1)
+    body(0);
+  else
+    pool->run(nw, body);
+}
+
+// The label column's integer images: dyadic fixed point (k = y 2^s exactly, |k| < 2^23, s
+// minimal and <= 40), or for any other finite labels the fp64 engine's screening image
+// k = round(y 2^ashift), |k| <= 2^22; also whether the labels are class indices and their
+// largest |y| (the screen's bounds).  One pass: the smallest s making y integral is read off
+// y's binary exponent and trailing zeros, and k's range is y's range times 2^s.
+static void analyze_labels(LabelSet& L, HostPool* pool = nullptr) {
+  const int64_t N = (int64_t)L.y.size();
+  struct Acc {
+    bool finite = true, integral = true;
+    int smax = 0;
+    double ymin = INFINITY, ymax = -INFINITY, amax = 0.0;
+  };
+  std::vector<Acc> acc(std::max(1, HostPool::width()));
+  int nw = 1;
+  par_range(pool, N, [&](int64_t lo, int64_t hi, int w) {
+    Acc a;
+    for (int64_t i = lo; i < hi; i++) {
+      const double v = L.y[i];
       if (!std::isfinite(v)) {
-        ok = false;
-        break;
+        a.finite = false;
+        a.integral = false;
+        continue;
       }
-      const double k = std::ldexp(v, s);
-      if (k != std::floor(k) || std::fabs(k) >= 8388608.0) {
-        ok = false;
-        break;
+      int si = 0;
+      if (v != 0.0) {
+        uint64_t bits;
+        std::memcpy(&bits, &v, 8);
+        const int E = (int)((bits >> 52) & 0x7FF);
+        const uint64_t M = bits & ((1ull << 52) - 1);
+        const uint64_t sig = E ? (M | (1ull << 52)) : M;
+        const int low = (E ? E - 1075 : -1074) + __builtin_ctzll(sig);  // v = odd * 2^low
+        si = low < 0 ? -low : 0;
       }
-      const int64_t ki = (int64_t)k;
-      if (first) {
-        mn = mx = ki;
-        first = false;
-      }
-      mn = std::min(mn, ki);
-      mx = std::max(mx, ki);
+      a.smax = std::max(a.smax, si);
+      if (!(v >= 0 && si == 0 && v < 8388608.0)) a.integral = false;
+      a.ymin = std::min(a.ymin, v);
+      a.ymax = std::max(a.ymax, v);
+      a.amax = std::max(a.amax, std::fabs(v));
     }
-    if (ok) {
-      L.label_ok = true;
-      L.shift = s;
-      L.kmin = mn;
-      L.kmax = mx;
-    }
+    acc[w] = a;
+  }, &nw);
+  Acc t;
+  for (int w = 0; w < nw; w++) {
+    t.finite = t.finite && acc[w].finite;
+    t.integral = t.integral && acc[w].integral;
+    t.smax = std::max(t.smax, acc[w].smax);
+    t.ymin = std::min(t.ymin, acc[w].ymin);
+    t.ymax = std::max(t.ymax, acc[w].ymax);
+    t.amax = std::max(t.amax, acc[w].amax);
+  }
+  L.finite = t.finite;
+  L.integral = t.integral;
+  L.label_ok = false;
+  if (t.finite && t.smax <= 40 && std::ldexp(t.amax, t.smax) < 8388608.0) {
+    L.label_ok = true;
+    L.shift = t.smax;
+    L.kmin = N ? (int64_t)std::ldexp(t.ymin, t.smax) : 0;
+    L.kmax = N ? (int64_t)std::ldexp(t.ymax, t.smax) : 0;
   }
   L.approx_ok = false;
-  L.ymax_abs = L.ymax_sq = 0.0;
-  bool finite = true;
-  for (double v : L.y) {
-    if (!std::isfinite(v)) {
-      finite = false;
-      break;
-    }
-    L.ymax_abs = std::max(L.ymax_abs, std::fabs(v));
-    L.ymax_sq = std::max(L.ymax_sq, v * v);
-  }
-  if (!L.label_ok && finite && L.ymax_abs > 0.0) {
-    // 2^e <= max|y| < 2^(e+1): max|y| 2^(21-e) < 2^22
-    L.ashift = 21 - std::ilogb(L.ymax_abs);
-    int64_t mn = 0, mx = 0;
-    for (double v : L.y) {
-      const int64_t k = (int64_t)std::nearbyint(std::ldexp(v, L.ashift));
-      mn = std::min(mn, k);
-      mx = std::max(mx, k);
-    }
-    L.akmin = mn;
-    L.akmax = mx;
+  L.ymax_abs = t.finite ? t.amax : 0.0;
+  L.ymax_sq = t.finite ? t.amax * t.amax : 0.0;
+  if (!L.label_ok && t.finite && t.amax > 0.0) {
+    // 2^e <= max|y| < 2^(e+1): max|y| 2^(21-e) < 2^22 (the image's range includes 0)
+    L.ashift = 21 - std::ilogb(t.amax);
+    L.akmin = std::min<int64_t>(0, (int64_t)std::nearbyint(std::ldexp(t.ymin, L.ashift)));
+    L.akmax = std::max<int64_t>(0, (int64_t)std::nearbyint(std::ldexp(t.ymax, L.ashift)));
     L.approx_ok = true;
   }
 }
-static void analyze_labels(sbag_dataset* ds) { analyze_labels(ds->lab); }
+static void analyze_labels(sbag_dataset* ds) { analyze_labels(ds->lab, &ds->ctx->pool); }
 
 // the labels' fixed point image (exact for dyadic labels, else the screening approximation
 // of the fp64 path, else zeros) into dst [N] on the device
-static int labk_image(const LabelSet& L, int32_t* dst) {
+static int labk_image(const LabelSet& L, int32_t* dst, HostPool* pool = nullptr) {
   const int64_t N = (int64_t)L.y.size();
   if (!L.label_ok && !L.approx_ok) {
     HIP_TRY(hipMemset(dst, 0, (size_t)std::max<int64_t>(N, 1) * 4));
     return SBAG_OK;
   }
   std::vector<int32_t> k(N);
-  if (L.label_ok)
-    for (int64_t i = 0; i < N; i++) k[i] = (int32_t)std::ldexp(L.y[i], L.shift);
-  else
-    for (int64_t i = 0; i < N; i++) k[i] = (int32_t)std::nearbyint(std::ldexp(L.y[i], L.ashift));
+  par_range(pool, N, [&](int64_t lo, int64_t hi, int) {
+    if (L.label_ok)
+      for (int64_t i = lo; i < hi; i++) k[i] = (int32_t)std::ldexp(L.y[i], L.shift);
+    else
+      for (int64_t i = lo; i < hi; i++) k[i] = (int32_t)std::nearbyint(std::ldexp(L.y[i], L.ashift));
+  });
   HIP_TRY(hipMemcpy(dst, k.data(), (size_t)N * 4, hipMemcpyHostToDevice));
   return SBAG_OK;
 }
 
 static int upload_labels(sbag_dataset* ds) {
   HIP_TRY(hipMalloc(&ds->lab.d_labk, std::max<int64_t>(ds->N, 1) * 4));
-  return labk_image(ds->lab, ds->lab.d_labk);
+  return labk_image(ds->lab, ds->lab.d_labk, &ds->ctx->pool);
 }
 
 static int upload_dict(sbag_dataset* ds) {
@@ -2198,8 +2224,38 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
         all.push_back(t);
       }
       all.insert(all.end(), tasks[0].begin() + nchain0, tasks[0].end());
+      // ... in chunks of consecutive tasks whose bucket entries stay within a budget of 2^32
+      // (39 GB of labels and counts; the C4 shard's root holds 2 x 4.0e9: two chunks).  The
+      // chain tasks lead the list, so a chunk's chain sums land at its first task's index.
+      const int nch = nchain0 + nchain1;
       std::vector<int64_t> nl_all;
-      TRY(run_tasks(all, nchain0 + nchain1, kb[0] + kb[1], d_chist, &nl_all));
+      {
+        const int64_t kBudget =
+            getenv("SBAG_F64_BUCKET_BUDGET") ? atoll(getenv("SBAG_F64_BUCKET_BUDGET")) : ((int64_t)1 << 32);
+        size_t t0 = 0;
+        while (t0 < all.size()) {
+          size_t t1 = t0;
+          int64_t ent = 0;
+          while (t1 < all.size()) {
+            const int64_t e = (int)t1 < nch ? all[t1].b - all[t1].a : 0;
+            if (t1 > t0 && ent + e > kBudget) break;
+            ent += e;
+            t1++;
+          }
+          std::vector<F64Task> sub(all.begin() + t0, all.begin() + t1);
+          int64_t kbc = 0;
+          for (size_t t = 0; t < sub.size(); t++)
+            if ((int)(t0 + t) < nch) {
+              sub[t].kbase = kbc;
+              kbc += sub[t].b - sub[t].a;
+            }
+          const int sub_chains = (int)std::max<int64_t>(0, std::min<int64_t>((int64_t)t1, nch) - (int64_t)t0);
+          std::vector<int64_t> nl;
+          TRY(run_tasks(sub, sub_chains, kbc, d_chist + t0 * (size_t)NB * 3, &nl));
+          nl_all.insert(nl_all.end(), nl.begin(), nl.end());
+          t0 = t1;
+        }
+      }
       nleft.assign(tasks[0].size(), 0);
       for (size_t t = 0; t < tasks[0].size(); t++)
         nleft[t] = nl_all[(int)t < nchain0 ? t : t + nchain1];
@@ -2360,8 +2416,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   const bool force_f64 = getenv("SBAG_F64") && atoi(getenv("SBAG_F64")) != 0;
   const bool f64 = !gini && (!lab.label_ok || force_f64);
   if (f64) {
-    for (double v : lab.y)
-      if (!std::isfinite(v)) return fail(SBAG_EINVAL, "labels must be finite");
+    if (!lab.finite) return fail(SBAG_EINVAL, "labels must be finite");
     if (!lab.label_ok && !lab.approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
     // (the bucketing kernels address the labels with 32-bit byte offsets)
     if (ds->N >= ((int64_t)1 << 29))
@@ -4705,9 +4760,14 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
   for (int k = 0; k < Fr; k++)
     if (sub[k] < 0 || sub[k] >= F || (k > 0 && sub[k] <= sub[k - 1]))
       return fail(SBAG_EINVAL, "subspace indices must be increasing and within [0, num_features)");
-  for (int64_t r = 0; r < N; r++)
-    if (!std::isfinite(labels[r]))
-      return fail(SBAG_EUNSUPPORTED, "booster labels must be finite");
+  // the residuals as a label set (copied and analyzed on the host pool)
+  LabelSet lab;
+  lab.y.resize(N);
+  par_range(&c->pool, N, [&](int64_t lo, int64_t hi, int) {
+    std::copy(labels + lo, labels + hi, lab.y.begin() + lo);
+  });
+  analyze_labels(lab, &c->pool);
+  if (!lab.finite) return fail(SBAG_EUNSUPPORTED, "booster labels must be finite");
   std::vector<int64_t> poff;
   TRY(check_partitions(bp->num_partitions, bp->partition_offsets, N, poff));
   HIP_TRY(hipSetDevice(c->device));
@@ -4723,11 +4783,8 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
         return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
                                  "empty one.");
     }
-    LabelSet lab;
-    lab.y.assign(labels, labels + N);
-    analyze_labels(lab);
     TRY(ws_typed(c, "bt_labk", (size_t)N, &lab.d_labk));
-    TRY(labk_image(lab, lab.d_labk));
+    TRY(labk_image(lab, lab.d_labk, &c->pool));
     TRY(ws_typed(c, "bt_y64", (size_t)N + 1, &lab.d_y64));
     TRY(h2d(c, lab.d_y64, labels, (size_t)N));
     HIP_TRY(hipMemsetAsync(lab.d_y64 + N, 0, 8, c->stream));

@@ -226,3 +226,22 @@ def test_c3_shape_nondyadic_screened(ctx):
     t = forest.timing()
     nodes = sum(len(forest.tree(i)[0]) for i in range(L))
     assert t["exact_fallbacks"] <= 0.02 * nodes, (t["exact_fallbacks"], nodes)
+
+
+def test_bucket_budget_chunks_equal_one_launch(ctx, cpusmall, monkeypatch):
+    """The decided nodes' bucketing tasks run in chunks when their buckets exceed a budget
+    (the C4 shard's root: 73 GB at once); the chunked fit equals the one-launch fit byte for
+    byte, and the oracle."""
+    X, y = cpusmall
+    y2 = y * np.pi
+    a = _fit(ctx, X, y2, 4, 7)
+    monkeypatch.setenv("SBAG_F64_BUCKET_BUDGET", "3000")  # a few nodes per chunk
+    b = _fit(ctx, X, y2, 4, 7)
+    for t in range(4):
+        (na, sa), (nb, sb_) = a.tree(t), b.tree(t)
+        assert na.tobytes() == nb.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes()
+    N, F = X.shape
+    counts = oracle.bag(True, 1.0, 0, 4, SEED_REG, [0, N], N)
+    subs = [oracle.subspace(1.0, F, SEED_REG + i) for i in range(4)]
+    assert_forest_equal(b, oracle_forest(X, y2, counts, subs, 7, 32, False))
