@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 
 #include "sbag_internal.h"
 
@@ -538,6 +539,109 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
   }
 }
 
+// k_fb_chain with every lane a chain (64 per wave): the serial adds are VALU-issue-bound
+// where chains are many (the deep levels), and a wave-instruction then serves 64 chains
+// instead of 16.  A stage is 16 entries per chain; load u covers chains 4u .. 4u + 3, 16
+// lanes each (so the chains' bounds are per lane, fetched once with shuffles).
+__global__ __launch_bounds__(64) void k_fb_chain64(F64BucketArgs A, int nchain) {
+  constexpr int kT = 16;          // entries per chain per stage
+  constexpr int kP = kT + 1;
+  constexpr int kLd = 64 * kT / 64;  // 16 loads per stage
+  __shared__ double s_y[64 * kP];
+  __shared__ uint8_t s_c[64 * kP];
+  const int NB = A.NB, lane = threadIdx.x;
+  const int64_t nlanes = (int64_t)nchain * NB;
+  const int64_t g = (int64_t)blockIdx.x * 64 + lane;
+  int64_t lo = 0, hi = 0;
+  if (g < nlanes) {
+    const int64_t task = g / NB;
+    const int b = (int)(g - task * NB);
+    const int64_t* ko = A.kb_off + task * (NB + 1);
+    lo = ko[b];
+    hi = ko[b + 1];
+  }
+  const int64_t len = hi - lo;
+  int64_t maxlen = len;
+  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
+  const int seg = lane >> 4, x16 = lane & 15;
+  // the chains' bounds in LDS (load u reads chain 4u + seg's: per lane, not per wave)
+  __shared__ int64_t s_lo[64], s_len[64];
+  s_lo[lane] = lo;
+  s_len[lane] = len;
+  auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&cv)[kLd]) {
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      const int64_t ul = s_lo[4 * u + seg], un = s_len[4 * u + seg];
+      const int64_t x = off + x16;
+      const int64_t at = max(min(ul + x, ul + un - 1), (int64_t)0);
+      yv[u] = A.bky[at];
+      cv[u] = (uint32_t)A.bkc[at];
+    }
+  };
+  double yA[kLd], yB[kLd];
+  uint32_t cA[kLd], cB[kLd];
+  if (maxlen > 0) {
+    load(0, yA, cA);
+    load(kT, yB, cB);
+  }
+  double s1 = 0.0, s2 = 0.0;
+  uint64_t cnt = 0;
+  const bool multi = A.cmax > 1;
+  for (int64_t off = 0; off < maxlen; off += kT) {
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      const int j = 4 * u + seg;
+      s_y[j * kP + x16] = yA[u];
+      s_c[j * kP + x16] = off + x16 < s_len[j] ? (uint8_t)cA[u] : (uint8_t)0;
+    }
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      yA[u] = yB[u];
+      cA[u] = cB[u];
+    }
+    if (off + 2 * kT < maxlen) load(off + 2 * kT, yB, cB);
+    const int n = (int)min((int64_t)kT, max((int64_t)0, len - off));
+    const double* sy = s_y + lane * kP;
+    const uint8_t* sc = s_c + lane * kP;
+    // (as k_fb_chain: the second to fourth draws branch-free, -0.0 for absent ones)
+    auto add = [&](double y, uint32_t c) {
+      const double w = 1.0 * y;  // instanceWeight * label
+      const double wy = w * y;   // instanceWeight * label * label
+      s1 += w;
+      s2 += wy;
+      if (multi) {
+        s1 += c >= 2 ? w : -0.0;
+        s2 += c >= 2 ? wy : -0.0;
+        s1 += c >= 3 ? w : -0.0;
+        s2 += c >= 3 ? wy : -0.0;
+        s1 += c >= 4 ? w : -0.0;
+        s2 += c >= 4 ? wy : -0.0;
+        for (uint32_t k = 4; k < c; k++) {
+          s1 += w;
+          s2 += wy;
+        }
+      }
+      cnt += c;
+    };
+    int x = 0;
+    for (; x + 4 <= n; x += 4) {
+      const double y0 = sy[x], y1 = sy[x + 1], y2 = sy[x + 2], y3 = sy[x + 3];
+      const uint32_t c0 = sc[x], c1 = sc[x + 1], c2 = sc[x + 2], c3 = sc[x + 3];
+      add(y0, c0);
+      add(y1, c1);
+      add(y2, c2);
+      add(y3, c3);
+    }
+    for (; x < n; x++) add(sy[x], sc[x]);
+  }
+  if (g < nlanes) {
+    double* o = A.chist + g * 3;
+    o[0] = (double)cnt;  // count += 1.0 per draw
+    o[1] = s1;
+    o[2] = s2;
+  }
+}
+
 // the labels of the root entries, in entry order: what the scatter reads (and carries to
 // the children) instead of gathering y[row] per entry at every level
 __global__ __launch_bounds__(256) void k_entry_labels(const uint64_t* __restrict__ ent,
@@ -572,11 +676,18 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
   // sixteen per wave wherever there are enough chains to fill the GPU (C3 shape, serialized,
   // ms per fit: 16 everywhere 109; 1 / 4 / 16 by chain count 154) -- one or four only for a
   // booster's few chains
-  if (lanes >= 4096)
+  // (SBAG_F64_CHAIN_C=1|4|16|64 forces the width, for A/B)
+  const int cenv = getenv("SBAG_F64_CHAIN_C") ? atoi(getenv("SBAG_F64_CHAIN_C")) : 0;
+  const int cw = cenv == 1 || cenv == 4 || cenv == 16 || cenv == 64 ? cenv
+                 : lanes >= 4096 ? 16 : lanes >= 512 ? 4 : 1;
+  if (lanes <= 0) return;
+  if (cw == 64)
+    hipLaunchKernelGGL(k_fb_chain64, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st, a, nchain);
+  else if (cw == 16)
     hipLaunchKernelGGL(k_fb_chain<16>, dim3((unsigned)((lanes + 15) / 16)), dim3(64), 0, st, a, nchain);
-  else if (lanes >= 512)
+  else if (cw == 4)
     hipLaunchKernelGGL(k_fb_chain<4>, dim3((unsigned)((lanes + 3) / 4)), dim3(64), 0, st, a, nchain);
-  else if (lanes > 0)
+  else
     hipLaunchKernelGGL(k_fb_chain<1>, dim3((unsigned)lanes), dim3(64), 0, st, a, nchain);
 }
 
