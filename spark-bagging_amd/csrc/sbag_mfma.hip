@@ -39,11 +39,10 @@ constexpr int kMfChunk = 256;        // rows per LDS chunk of A
 constexpr int kMfPitch = kMfChunk + 16;  // LDS bytes per replica row (bank spread)
 constexpr int64_t kMfSlice = 65536;  // rows per workgroup (int32 accumulators exact)
 
-// 4 bytes x of a column vs bin b: 0x01 in every byte equal to b
-__device__ __forceinline__ uint32_t eq_bytes(uint32_t x, uint32_t bb) {
+// 4 bytes x of a column vs bin b: 0x80 in every byte equal to b
+__device__ __forceinline__ uint32_t eq_hi(uint32_t x, uint32_t bb) {
   const uint32_t t = x ^ bb;
-  const uint32_t hi = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
-  return hi >> 7;
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
 }
 }  // namespace
 
@@ -126,14 +125,22 @@ __global__ __launch_bounds__(kMfWaves * 64, 1) void k_hist_mfma(MfmaHistArgs A) 
       for (int ks = 0; ks < kMfChunk; ks += 32) {
         // B: the column's 16 rows of this lane half vs bin b (rows past N are 0 with 0 counts)
         const uint4 x = *(const uint4*)(cX + ks + 16 * h);
+        // 0x01 (count plane) and 0xFF (digit mask) in every matching byte: from the 0x80
+        // mask by a shift, and (hi - lo) | hi -- not (lo << 8) - lo, which the compiler
+        // turns into a quarter-rate v_mul_lo_u32 by 255
+        const uint32_t h0 = eq_hi(x.x, bb), h1 = eq_hi(x.y, bb), h2 = eq_hi(x.z, bb), h3 = eq_hi(x.w, bb);
         v4i be;
-        be.x = (int)eq_bytes(x.x, bb);
-        be.y = (int)eq_bytes(x.y, bb);
-        be.z = (int)eq_bytes(x.z, bb);
-        be.w = (int)eq_bytes(x.w, bb);
+        be.x = (int)(h0 >> 7);
+        be.y = (int)(h1 >> 7);
+        be.z = (int)(h2 >> 7);
+        be.w = (int)(h3 >> 7);
         v4i bd[ND > 0 ? ND : 1];
         if constexpr (ND > 0) {
-          const v4i ff = (be << 8) - be;  // 0xFF in every matching byte
+          v4i ff;
+          ff.x = (int)((h0 - (h0 >> 7)) | h0);
+          ff.y = (int)((h1 - (h1 >> 7)) | h1);
+          ff.z = (int)((h2 - (h2 >> 7)) | h2);
+          ff.w = (int)((h3 - (h3 >> 7)) | h3);
 #pragma unroll
           for (int j = 0; j < ND; j++) {
             const uint4 d = *(const uint4*)(cD + j * kMfChunk + ks + 16 * h);
