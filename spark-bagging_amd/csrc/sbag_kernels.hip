@@ -984,14 +984,15 @@ __global__ __launch_bounds__(64) void k_split_sample(
 // gaps depend only on its XORShift stream, so every lane steps the stream to its own draw of
 // a block of 64 (the stream is sequential: each lane runs the 64 steps, keeps the one it
 // owns), the gaps' prefix gives the block's 64 taken item positions, and the wave streams the
-// partition's count bytes (1024 rows per chunk, one chunk ahead) and resolves the positions
+// partition's count bytes (4096 rows per chunk in aligned 16-byte loads, one chunk ahead) and
+// resolves the positions
 // that fall in each chunk to their rows.  The same items as the one-lane walk, in the same
 // order: the row list is identical.
 __global__ __launch_bounds__(64) void k_split_sample_gap(
     const uint8_t* __restrict__ counts, int64_t N, const int64_t* __restrict__ part_off, int P,
     const int32_t* __restrict__ reps, const uint64_t* __restrict__ part_state,
     const double* __restrict__ frac, uint32_t* __restrict__ rows_out, int64_t cap,
-    uint32_t* __restrict__ nrows) {
+    uint32_t* __restrict__ nrows, int64_t counts_len) {
   __shared__ int64_t s_t[64];
   __shared__ uint32_t s_rows[64];
   const int ri = blockIdx.y, p = blockIdx.x, lane = threadIdx.x;
@@ -1001,23 +1002,48 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
   const uint8_t* cr = counts + (int64_t)r * N;
   const int64_t r0 = part_off[p], r1 = part_off[p + 1];
   uint32_t* out = rows_out + (int64_t)ri * cap;
-  // the current chunk: rows [c0, c0 + 1024), lane l's 16 rows [c0 + 16 l, c0 + 16 l + 16)
-  auto load16 = [&](int64_t c0, uint32_t (&w)[16]) {
+  // the current chunk: 4096 rows from the 16-byte aligned address at or below the
+  // partition's first row, lane l's 64 rows [c0 + 64 l, c0 + 64 l + 64) as four aligned
+  // 16-byte loads (clamped inside the counts buffer: every lane loads, no branch); rows
+  // outside [r0, r1) count 0
+  // (the buffer holds counts_len >= 1 bytes; device allocations come in >= 4 KB pages, so a
+  // 16-byte load clamped to its start stays mapped)
+  const uint8_t* cbase = counts;
+  const uint8_t* climit = counts + max(counts_len - 16, (int64_t)0);
+  const int64_t a0 = r0 - (int64_t)(((uintptr_t)(cr + r0)) & 15u);  // row of the aligned start
+  auto load64 = [&](int64_t c0, uint32_t (&w)[16]) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int64_t row = c0 + 16 * lane + k;
-      w[k] = row < r1 ? (uint32_t)cr[row] : 0u;
+    for (int q = 0; q < 4; q++) {
+      const int64_t row = c0 + 64 * lane + 16 * q;
+      const uint8_t* pa = cr + row;
+      const uint8_t* pc = pa < cbase ? cbase : (pa > climit ? climit : pa);
+      const uint4 v = *(const uint4*)pc;
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+          const int64_t rr = row + 4 * d + bb;
+          m |= (rr >= r0 && rr < r1) ? (0xFFu << (8 * bb)) : 0u;
+        }
+        w[4 * q + d] = pc == pa ? (vv[d] & m) : 0u;
+      }
     }
   };
-  int64_t c0 = r0;
+  auto bsum = [](uint32_t x) {  // sum of the 4 bytes
+    x = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
+    return (x & 0xFFFFu) + (x >> 16);
+  };
+  int64_t c0 = a0;
   uint32_t cw[16], nw[16];
-  load16(c0, cw);
-  load16(c0 + 1024, nw);
+  load64(c0, cw);
+  load64(c0 + 4096, nw);
   // items before the chunk, and this lane's item range inside it
   int64_t ib = 0;
   uint32_t lsum = 0;
 #pragma unroll
-  for (int k = 0; k < 16; k++) lsum += cw[k];
+  for (int k = 0; k < 16; k++) lsum += bsum(cw[k]);
   uint32_t incl = lsum;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1056,18 +1082,18 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
     for (int j = 0; j < 64;) {
       const int64_t t = s_t[j];  // (LDS, same wave: in order)
       if (t >= ib + (int64_t)ctot) {  // past this chunk: the next one
-        if (c0 + 1024 >= r1) {
+        if (c0 + 4096 >= r1) {
           done = true;
           break;
         }
         ib += ctot;
-        c0 += 1024;
+        c0 += 4096;
 #pragma unroll
         for (int k = 0; k < 16; k++) cw[k] = nw[k];
-        load16(c0 + 1024, nw);
+        load64(c0 + 4096, nw);
         lsum = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) lsum += cw[k];
+        for (int k = 0; k < 16; k++) lsum += bsum(cw[k]);
         incl = lsum;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1083,10 +1109,13 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
       const uint64_t m = __ballot(mine);
       const int owner = __ffsll((unsigned long long)m) - 1;
       if (lane == owner) {
+        // the word, then the byte among the lane's 64 rows
         uint32_t acc = incl - lsum;
         int k = 0;
-        while (k < 15 && (int64_t)(acc + cw[k]) <= o) acc += cw[k++];
-        s_rows[nfound] = (uint32_t)(c0 + 16 * lane + k);
+        while (k < 15 && (int64_t)(acc + bsum(cw[k])) <= o) acc += bsum(cw[k++]);
+        int bb = 0;
+        while (bb < 3 && (int64_t)(acc + ((cw[k] >> (8 * bb)) & 0xFFu)) <= o) acc += (cw[k] >> (8 * bb++)) & 0xFFu;
+        s_rows[nfound] = (uint32_t)(c0 + 64 * lane + 4 * k + bb);
       }
       nfound++;
       j++;
@@ -1182,7 +1211,7 @@ void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, int64
   static const bool lanes_env = getenv("SBAG_SPLIT_SAMPLE_LANES") && atoi(getenv("SBAG_SPLIT_SAMPLE_LANES"));
   if (P < 64 && gap_sampling && !lanes_env) {
     hipLaunchKernelGGL(k_split_sample_gap, dim3((unsigned)P, (unsigned)nrep), dim3(64), 0, st, counts,
-                       N, d_part_off, P, d_reps, d_part_state, d_frac, d_rows, cap, d_nrows);
+                       N, d_part_off, P, d_reps, d_part_state, d_frac, d_rows, cap, d_nrows, R * N);
     return;
   }
   const int64_t ng = split_sample_groups(R * N);
