@@ -539,6 +539,179 @@ __global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
   }
 }
 
+// k_fb_chain with the draws exploded in LDS: the same sums, but the serial lanes' loop is
+// one 16-byte LDS read and two adds per draw, with no per-entry count logic.  The whole
+// wave turns a stage of 512 entries (kChT per chain, kChC chains) into draw streams: the
+// (sumSq term) products and the draw positions (a scan of the counts per chain) are
+// computed in parallel, entry e of count c is written c times as (w, w*y), and every chain
+// is padded to the wave's longest stream with (-0.0, -0.0), which leaves a sum unchanged
+// (-0.0 included), so the serial loop runs a uniform trip count.  A stage's draws beyond
+// kDcap per chain go through further windows.  The count is the integer sum of the draws.
+template <int kChC>
+__global__ __launch_bounds__(64) void k_fb_chainx(F64BucketArgs A, int nchain) {
+  constexpr int kChT = 512 / kChC;     // entries per chain per stage
+  constexpr int kLd = 8;               // 512 entries = 8 loads of 64
+  constexpr int kDcap = 2 * kChT;      // draws per chain per window
+  constexpr int kDp = kDcap + 1;       // odd pitch (16-byte units): conflict-free serial reads
+  __shared__ double2 s_d[kChC * kDp + 8];
+  const int NB = A.NB, lane = threadIdx.x;
+  const int nbits = min(8, 32 - (int)__builtin_clz((uint32_t)max(A.cmax, 1)));  // of a count
+  const int64_t nlanes = (int64_t)nchain * NB;
+  const int64_t g = (int64_t)blockIdx.x * kChC + lane;
+  int64_t lo = 0, hi = 0;
+  if (lane < kChC && g < nlanes) {
+    const int64_t task = g / NB;
+    const int b = (int)(g - task * NB);
+    const int64_t* ko = A.kb_off + task * (NB + 1);
+    lo = ko[b];
+    hi = ko[b + 1];
+  }
+  const int64_t len = hi - lo;
+  int64_t maxlen = len;
+  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
+  // load u, lane l: slot 64u + l = chain j's entry x of the stage
+  int64_t ulo[kLd], ulen[kLd];
+  int ux[kLd], uj[kLd];
+#pragma unroll
+  for (int u = 0; u < kLd; u++) {
+    const int slot = 64 * u + lane;
+    uj[u] = slot / kChT;
+    ux[u] = slot % kChT;
+    ulo[u] = __shfl(lo, uj[u]);
+    ulen[u] = __shfl(len, uj[u]);
+  }
+  auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&cv)[kLd]) {
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      const int64_t at = max(min(ulo[u] + off + ux[u], ulo[u] + ulen[u] - 1), (int64_t)0);
+      yv[u] = A.bky[at];
+      cv[u] = (uint32_t)A.bkc[at];
+    }
+  };
+  double yA[kLd], yB[kLd];
+  uint32_t cA[kLd], cB[kLd];
+  if (maxlen > 0) {
+    load(0, yA, cA);
+    load(kChT, yB, cB);
+  }
+  double s1 = 0.0, s2 = 0.0;
+  uint64_t cnt = 0;
+  for (int64_t off = 0; off < maxlen; off += kChT) {
+    uint32_t cc[kLd];
+    double w[kLd], wy[kLd];
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      cc[u] = off + ux[u] < ulen[u] ? cA[u] : 0u;
+      w[u] = 1.0 * yA[u];    // instanceWeight * label
+      wy[u] = w[u] * yA[u];  // instanceWeight * label * label
+    }
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      yA[u] = yB[u];
+      cA[u] = cB[u];
+    }
+    if (off + 2 * kChT < maxlen) load(off + 2 * kChT, yB, cB);
+    // draw positions: exclusive prefix of the counts per chain from ballots of their bits
+    // (lanes below this one in its chain's segment: mbcnt), D[j] = chain j's draws
+    uint32_t pre[kLd];
+    int D[kChC], T[kLd];  // T: a whole load's draws (kChT >= 64)
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      pre[u] = 0;
+      T[u] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kChC; j++) D[j] = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      if (b >= nbits) break;
+#pragma unroll
+      for (int u = 0; u < kLd; u++) {
+        const uint64_t bal = __ballot((cc[u] >> b) & 1u);
+        uint32_t mlo, mhi;
+        if constexpr (kChT >= 64) {
+          mlo = (uint32_t)bal;
+          mhi = (uint32_t)(bal >> 32);
+        } else {  // this lane's kChT-lane segment
+          const uint64_t seg = ((1ull << kChT) - 1) << (lane & ~(kChT - 1));
+          mlo = (uint32_t)(bal & seg);
+          mhi = (uint32_t)((bal & seg) >> 32);
+        }
+        pre[u] += __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u)) << b;
+        if constexpr (kChT >= 64) {
+          T[u] += __popcll(bal) << b;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 64 / kChT; q++)
+            D[u * (64 / kChT) + q] += __popcll(bal & (((1ull << kChT) - 1) << (q * kChT))) << b;
+        }
+      }
+    }
+    if constexpr (kChT >= 64) {  // + the chain's earlier loads of the stage
+      constexpr int kPer = kChT / 64;
+#pragma unroll
+      for (int u = 0; u < kLd; u++) {
+#pragma unroll
+        for (int v = u - u % kPer; v < u; v++) pre[u] += (uint32_t)T[v];
+        D[u / kPer] += T[u];
+      }
+    }
+    int maxD = 0, myD = 0;
+#pragma unroll
+    for (int j = 0; j < kChC; j++) {
+      maxD = max(maxD, D[j]);
+      myD = lane == j ? D[j] : myD;
+    }
+    cnt += (uint32_t)myD;  // count += 1.0 per draw (an integer sum: order-free)
+    for (int wnd = 0; wnd < maxD; wnd += kDcap) {
+#pragma unroll
+      for (int u = 0; u < kLd; u++) {
+        const int p = (int)pre[u] - wnd;
+        const int k1 = min((int)cc[u], kDcap - p);
+        double2 v;
+        v.x = w[u];
+        v.y = wy[u];
+        for (int k = max(0, -p); k < k1; k++) s_d[uj[u] * kDp + p + k] = v;
+      }
+      block_sync();
+      if (lane < kChC) {
+        // this chain's draws of the window, padded to a multiple of 8 with (-0.0, -0.0) by
+        // its own lane; 8 draws per step, the next 8 read ahead (the array's 8-entry tail
+        // keeps the last chain's over-read inside it)
+        const int n = min(max(myD - wnd, 0), kDcap);
+        const int n8 = (n + 7) & ~7;
+        double2* sd = s_d + lane * kDp;
+        double2 z;
+        z.x = -0.0;
+        z.y = -0.0;
+        for (int i = n; i < n8; i++) sd[i] = z;
+        double2 a[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) a[k] = sd[k];
+        for (int d = 0; d < n8; d += 8) {
+          double2 b[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) b[k] = sd[d + 8 + k];
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            s1 += a[k].x;
+            s2 += a[k].y;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; k++) a[k] = b[k];
+        }
+      }
+      block_sync();
+    }
+  }
+  if (lane < kChC && g < nlanes) {
+    double* o = A.chist + g * 3;
+    o[0] = (double)cnt;
+    o[1] = s1;
+    o[2] = s2;
+  }
+}
+
 // k_fb_chain with every lane a chain (64 per wave): the serial adds are VALU-issue-bound
 // where chains are many (the deep levels), and a wave-instruction then serves 64 chains
 // instead of 16.  A stage is 16 entries per chain; load u covers chains 4u .. 4u + 3, 16
@@ -672,15 +845,29 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
     hipLaunchKernelGGL(k_fb_scatter, dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
                        npieces, nbits);
   const int64_t lanes = (int64_t)nchain * a.NB;
-  // The serial adds are VALU-issue-bound: every wave-instruction serves kChC chains, so
-  // sixteen per wave wherever there are enough chains to fill the GPU (C3 shape, serialized,
-  // ms per fit: 16 everywhere 109; 1 / 4 / 16 by chain count 154) -- one or four only for a
-  // booster's few chains
-  // (SBAG_F64_CHAIN_C=1|4|16|64 forces the width, for A/B)
+  // k_fb_chainx (the default; SBAG_F64_CHAIN_X=0: the per-entry k_fb_chain): the serial
+  // lanes are latency-bound, so a wave takes as few chains as keep >= 2048 waves (two per
+  // SIMD: the VGPR budget's occupancy) -- C3 shape, serialized fit, ms: 16 everywhere 331,
+  // by this rule 305 (root 37 instead of 51); a booster's few chains get a wave each
+  // (GBM 10M x 100: chains 71 -> 16 ms per booster).  k_fb_chain (per-entry loop) kept for
+  // A/B: 16 per wave wherever there are enough chains, else 4 or 1.
+  // (SBAG_F64_CHAIN_C=1|4|16|64 forces the width, for A/B; 64 is k_fb_chain64)
   const int cenv = getenv("SBAG_F64_CHAIN_C") ? atoi(getenv("SBAG_F64_CHAIN_C")) : 0;
+  const char* xenv = getenv("SBAG_F64_CHAIN_X");
+  const bool xpl = !(xenv && atoi(xenv) == 0);
   const int cw = cenv == 1 || cenv == 4 || cenv == 16 || cenv == 64 ? cenv
-                 : lanes >= 4096 ? 16 : lanes >= 512 ? 4 : 1;
+                 : xpl ? (lanes >= 16 * 2048 ? 16 : lanes >= 4 * 2048 ? 4 : 1)
+                       : (lanes >= 4096 ? 16 : lanes >= 512 ? 4 : 1);
   if (lanes <= 0) return;
+  if (xpl && cw != 64) {
+    if (cw == 16)
+      hipLaunchKernelGGL(k_fb_chainx<16>, dim3((unsigned)((lanes + 15) / 16)), dim3(64), 0, st, a, nchain);
+    else if (cw == 4)
+      hipLaunchKernelGGL(k_fb_chainx<4>, dim3((unsigned)((lanes + 3) / 4)), dim3(64), 0, st, a, nchain);
+    else
+      hipLaunchKernelGGL(k_fb_chainx<1>, dim3((unsigned)lanes), dim3(64), 0, st, a, nchain);
+    return;
+  }
   if (cw == 64)
     hipLaunchKernelGGL(k_fb_chain64, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st, a, nchain);
   else if (cw == 16)
