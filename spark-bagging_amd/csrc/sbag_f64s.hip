@@ -330,15 +330,26 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
 // child (left from the segment start, right after the left block, both in row order).
 // Every lane issues the same memory operations each round (loads at clamped indices, one
 // bucket store, one child store, buffer operations whose out-of-range offsets are dropped),
-// so the compiler's vmcnt waits stay counted.  (The wave's LDS operations on sb execute in
+// so the compiler's vmcnt waits stay counted.  (The wave's LDS operations execute in
 // order, and the compiler keeps a store to sb[x] before a later load of sb[y] it cannot
 // prove distinct: no fence, which would drain the vector memory counter too.)
+// kStage (the default): a step's 512 entries are first ordered by bin in LDS, so the
+// bucket stores leave as runs of consecutive positions (a 64-entry round spreads over up to
+// NB buckets: 2-entry runs of 8-byte labels and 1-byte counts, written back ~1.7x their
+// bytes as measured by WRITE_SIZE).
+constexpr int kScU = 8;  // rounds of 64 entries per step
+template <bool kStage>
 __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits) {
   // (the wave index in an SGPR: the piece, its task and the buffer resources built from them
   // are then wave-uniform, with no per-lane waterfall loop around the buffer operations)
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t pi = (int64_t)blockIdx.x * 4 + wv;
   __shared__ int64_t s_base[4][256];
+  // staging (kStage): per wave the step's bin counts and offsets, and its entries by bin
+  __shared__ uint32_t s_scnt[kStage ? 4 : 1][256], s_soff[kStage ? 4 : 1][256];
+  __shared__ v2u32 s_sy[kStage ? 4 : 1][64 * kScU];
+  __shared__ uint32_t s_skp[kStage ? 4 : 1][64 * kScU];
+  __shared__ uint8_t s_sc[kStage ? 4 : 1][64 * kScU];
   if (pi >= npieces) return;  // whole waves only; no block-wide barrier below
   const F64TPiece pc = A.pieces[pi];
   const F64Task t = A.tasks[pc.task];
@@ -346,6 +357,10 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const bool chain = __builtin_amdgcn_readfirstlane((int)(t.kbase >= 0)) != 0;  // (uniform: SGPR resources)
   int64_t* sb = s_base[wv];
   for (int b = lane; b < NB; b += 64) sb[b] = chain ? A.pbase[pi * NB + b] : 0;
+  uint32_t* scnt = s_scnt[kStage ? wv : 0];
+  uint32_t* soff = s_soff[kStage ? wv : 0];
+  if (kStage)
+    for (int b = lane; b < 256; b += 64) scnt[b] = 0u;
   int64_t lrun = t.part ? A.plbase[pi] : 0;
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
   // the entries' bins as k_fb_count gathered them (in entry order: coalesced)
@@ -369,11 +384,11 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   // gathers, then the rounds' ballots and stores -- one memory latency per step, not per
   // round (vmcnt counts stores and loads in order on gfx9, so loads carried across steps
   // would wait for the stores issued after them anyway)
-  constexpr int kScU = 8;
   for (int64_t i0 = pc.a; i0 < pc.b; i0 += 64 * kScU) {
     uint64_t ev[kScU];
     uint32_t bv[kScU];
     v2u32 yv[kScU];
+    uint32_t rs[kScU];  // (kStage) rank among the step's entries of the same bin
 #pragma unroll
     for (int u = 0; u < kScU; u++) ev[u] = A.ent_in[min(i0 + 64 * u + lane, last)];
 #pragma unroll
@@ -397,12 +412,18 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
         eq &= bit ? m : ~m;
       }
       const int rank = __popcll(eq & lt), cnt = __popcll(eq);
-      const int64_t base = sb[bin];
-      // (positions relative to the task's buckets; invalid lanes store past the end: dropped)
-      const uint32_t kp = valid ? (uint32_t)(base - t.kbase + rank) : 0x1FFFFFFEu;
-      __builtin_amdgcn_raw_buffer_store_b64(yv[u], rk, (int)(kp * 8u), 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(e >> 32), rkc, (int)kp, 0, 0);
-      if (valid && rank == cnt - 1) sb[bin] = base + cnt;
+      if constexpr (kStage) {
+        const uint32_t so = scnt[bin];
+        rs[u] = so + (uint32_t)rank;
+        if (valid && rank == cnt - 1) scnt[bin] = so + (uint32_t)cnt;
+      } else {
+        const int64_t base = sb[bin];
+        // (positions relative to the task's buckets; invalid lanes store past the end: dropped)
+        const uint32_t kp = valid ? (uint32_t)(base - t.kbase + rank) : 0x1FFFFFFEu;
+        __builtin_amdgcn_raw_buffer_store_b64(yv[u], rk, (int)(kp * 8u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(e >> 32), rkc, (int)kp, 0, 0);
+        if (valid && rank == cnt - 1) sb[bin] = base + cnt;
+      }
       const bool left = valid && bin <= (uint32_t)t.s;
       const uint64_t lm = __ballot(left);
       const int64_t lr = __popcll(lm & lt);
@@ -410,6 +431,67 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
       rstore64(ro, valid ? (uint32_t)pos * 8u : 0xFFFFFFF0u, e);
       __builtin_amdgcn_raw_buffer_store_b64(yv[u], roy, valid ? (int)((uint32_t)pos * 8u) : -16, 0, 0);
       lrun += __popcll(lm);
+    }
+    if constexpr (kStage) {
+      if (chain) {
+        // step offsets per bin (exclusive scan over the bins, 4 per lane), then every entry
+        // to its slot: bins in order, row order inside a bin
+        __builtin_amdgcn_wave_barrier();
+        uint32_t c4[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          c4[k] = scnt[4 * lane + k];
+          sum += c4[k];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t v = __shfl_up(incl, o);
+          if (lane >= o) incl += v;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          soff[4 * lane + k] = run;
+          run += c4[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        v2u32* sy = s_sy[wv];
+        uint32_t* skp = s_skp[wv];
+        uint8_t* sc = s_sc[wv];
+#pragma unroll
+        for (int u = 0; u < kScU; u++) {
+          const bool valid = i0 + 64 * u + lane < pc.b;
+          const uint32_t bin = valid ? bv[u] : 0u;
+          if (valid) {
+            const uint32_t slot = soff[bin] + rs[u];
+            sy[slot] = yv[u];
+            sc[slot] = (uint8_t)(ev[u] >> 32);
+            skp[slot] = (uint32_t)(sb[bin] - t.kbase) + rs[u];
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // bucket positions advance by the step's counts; the counts restart
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int b = 4 * lane + k;
+          if (b < NB) sb[b] += c4[k];
+          scnt[b] = 0u;
+        }
+        const int nst = (int)min((int64_t)(64 * kScU), pc.b - i0);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < kScU; k++) {
+          const int q = 64 * k + lane;
+          const bool ok = q < nst;
+          const uint32_t kp = ok ? skp[q] : 0x1FFFFFFEu;
+          const v2u32 y = sy[ok ? q : 0];
+          const uint32_t cb = sc[ok ? q : 0];
+          __builtin_amdgcn_raw_buffer_store_b64(y, rk, (int)(kp * 8u), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)cb, rkc, (int)kp, 0, 0);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
     }
   }
 }
@@ -837,12 +919,16 @@ void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, d
 void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain) {
   int nbits = 0;
   while ((1 << nbits) < a.NB) nbits++;
+  // SBAG_F64_SCATTER_STAGE=0: the bucket stores straight from the rounds (A/B)
+  const char* senv = getenv("SBAG_F64_SCATTER_STAGE");
+  const bool scatter_stage = !(senv && atoi(senv) == 0);
   if (npieces > 0)
     hipLaunchKernelGGL(k_fb_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
   if (a.ntasks > 0)  // (tasks without pieces still get their bucket bounds)
     hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)a.ntasks), dim3(256), 0, st, a);
   if (npieces > 0)
-    hipLaunchKernelGGL(k_fb_scatter, dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
+    hipLaunchKernelGGL(scatter_stage ? k_fb_scatter<true> : k_fb_scatter<false>,
+                       dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
                        npieces, nbits);
   const int64_t lanes = (int64_t)nchain * a.NB;
   // k_fb_chainx (the default; SBAG_F64_CHAIN_X=0: the per-entry k_fb_chain): the serial
