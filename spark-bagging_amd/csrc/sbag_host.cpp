@@ -1851,7 +1851,6 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     G.tm.end(h);
   }
   const size_t node_words = (size_t)(Fmax + 1) * NB * 3;
-  const int64_t batch = std::max<int64_t>(1, ((int64_t)4 << 30) / (int64_t)(node_words * 8));
   for (int level = 0; level <= D && !cur.empty(); level++) {
     G.levels++;
     G.tm.level = level;
@@ -2169,7 +2168,22 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       tasks[pass].push_back(t);
       return (int)tasks[pass].size() - 1;
     };
-    for (int i = 0; i < M; i++) {
+    // tasks in order of their bin column: k_fb_count's bin gathers (one byte per entry, a
+    // line each where a deep node's rows are sparse) then hit the same column from the
+    // many replicas' tasks in flight together (SBAG_F64_TASK_ORDER=0: node order)
+    std::vector<int> norder(M);
+    for (int i = 0; i < M; i++) norder[i] = i;
+    {
+      static const char* oenv = getenv("SBAG_F64_TASK_ORDER");
+      if (!(oenv && atoi(oenv) == 0)) {
+        auto colkey = [&](int i) -> int64_t {
+          return so[i].flag || so[i].f < 0 ? INT64_MAX : (int64_t)G.h_pos[(size_t)cur[i].r * Fmax + so[i].f];
+        };
+        std::stable_sort(norder.begin(), norder.end(), [&](int x, int y) { return colkey(x) < colkey(y); });
+      }
+    }
+    for (int ii = 0; ii < M; ii++) {
+      const int i = norder[ii];
       if (so[i].flag) continue;
       const LNode& q = cur[i];
       const int f = so[i].f, s = so[i].s;
