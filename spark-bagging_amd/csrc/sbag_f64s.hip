@@ -897,6 +897,78 @@ __global__ __launch_bounds__(64) void k_fb_chain64(F64BucketArgs A, int nchain) 
   }
 }
 
+// ---------------------------------------------------------------- label column
+// analyze_labels (sbag_host.cpp) on the device: per label, finite / integral and the
+// smallest s with y 2^s integral (from the exponent and the significand's trailing zeros),
+// the range and the largest |y|; wave reductions, then one atomic per wave and quantity
+__device__ __forceinline__ uint64_t dkey(double v) {  // order-preserving key of a double
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__global__ __launch_bounds__(256) void k_label_stats(const double* __restrict__ y, int64_t N,
+                                                     uint64_t* __restrict__ acc) {
+  uint32_t nf = 0, ni = 0;
+  int smax = 0;
+  uint64_t kmin = ~0ull, kmax = 0, amax = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256) {
+    const double v = y[i];
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const int E = (int)((bits >> 52) & 0x7FF);
+    if (E == 0x7FF) {  // NaN / inf
+      nf = 1;
+      ni = 1;
+      continue;
+    }
+    int si = 0;
+    if (v != 0.0) {
+      const uint64_t M = bits & ((1ull << 52) - 1);
+      const uint64_t sig = E ? (M | (1ull << 52)) : M;
+      const int low = (E ? E - 1075 : -1074) + (int)__builtin_ctzll(sig);  // v = odd 2^low
+      si = low < 0 ? -low : 0;
+    }
+    smax = max(smax, si);
+    if (!(v >= 0 && si == 0 && v < 8388608.0)) ni = 1;
+    const uint64_t k = dkey(v);
+    kmin = min(kmin, k);
+    kmax = max(kmax, k);
+    amax = max(amax, bits & 0x7FFFFFFFFFFFFFFFull);  // |v|: its bits order as the value
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    nf |= (uint32_t)__shfl_xor((int)nf, o);
+    ni |= (uint32_t)__shfl_xor((int)ni, o);
+    smax = max(smax, __shfl_xor(smax, o));
+    kmin = min(kmin, (uint64_t)__shfl_xor((long long)kmin, o));
+    kmax = max(kmax, (uint64_t)__shfl_xor((long long)kmax, o));
+    amax = max(amax, (uint64_t)__shfl_xor((long long)amax, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (nf) atomicOr((unsigned long long*)&acc[0], 1ull);
+    if (ni) atomicOr((unsigned long long*)&acc[1], 1ull);
+    atomicMax((unsigned long long*)&acc[2], (unsigned long long)smax);
+    atomicMin((unsigned long long*)&acc[3], (unsigned long long)kmin);
+    atomicMax((unsigned long long*)&acc[4], (unsigned long long)kmax);
+    atomicMax((unsigned long long*)&acc[5], (unsigned long long)amax);
+  }
+}
+
+void launch_label_stats(hipStream_t st, const double* y, int64_t N, uint64_t* acc) {
+  const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((N + 255) / 256, 2048));
+  hipLaunchKernelGGL(k_label_stats, dim3(bx), dim3(256), 0, st, y, N, acc);
+}
+
+__global__ __launch_bounds__(256) void k_label_image(const double* __restrict__ y, int64_t N,
+                                                     int shift, int dyadic, int32_t* __restrict__ k) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256) {
+    const double v = ldexp(y[i], shift);
+    k[i] = (int32_t)(dyadic ? v : rint(v));
+  }
+}
+
+void launch_label_image(hipStream_t st, const double* y, int64_t N, int shift, bool dyadic, int32_t* k) {
+  const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((N + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_label_image, dim3(bx), dim3(256), 0, st, y, N, shift, dyadic ? 1 : 0, k);
+}
+
 // the labels of the root entries, in entry order: what the scatter reads (and carries to
 // the children) instead of gathering y[row] per entry at every level
 __global__ __launch_bounds__(256) void k_entry_labels(const uint64_t* __restrict__ ent,

@@ -396,6 +396,29 @@ static void par_range(HostPool* pool, int64_t N, const std::function<void(int64_
 // k = round(y 2^ashift), |k| <= 2^22; also whether the labels are class indices and their
 // largest |y| (the screen's bounds).  One pass: the smallest s making y integral is read off
 // y's binary exponent and trailing zeros, and k's range is y's range times 2^s.
+static void set_label_stats(LabelSet& L, int64_t N, bool finite, bool integral, int smax, double ymin,
+                            double ymax, double amax) {
+  L.finite = finite;
+  L.integral = integral;
+  L.label_ok = false;
+  if (finite && smax <= 40 && std::ldexp(amax, smax) < 8388608.0) {
+    L.label_ok = true;
+    L.shift = smax;
+    L.kmin = N ? (int64_t)std::ldexp(ymin, smax) : 0;
+    L.kmax = N ? (int64_t)std::ldexp(ymax, smax) : 0;
+  }
+  L.approx_ok = false;
+  L.ymax_abs = finite ? amax : 0.0;
+  L.ymax_sq = finite ? amax * amax : 0.0;
+  if (!L.label_ok && finite && amax > 0.0) {
+    // 2^e <= max|y| < 2^(e+1): max|y| 2^(21-e) < 2^22 (the image's range includes 0)
+    L.ashift = 21 - std::ilogb(amax);
+    L.akmin = std::min<int64_t>(0, (int64_t)std::nearbyint(std::ldexp(ymin, L.ashift)));
+    L.akmax = std::max<int64_t>(0, (int64_t)std::nearbyint(std::ldexp(ymax, L.ashift)));
+    L.approx_ok = true;
+  }
+}
+
 static void analyze_labels(LabelSet& L, HostPool* pool = nullptr) {
   const int64_t N = (int64_t)L.y.size();
   struct Acc {
@@ -441,25 +464,7 @@ static void analyze_labels(LabelSet& L, HostPool* pool = nullptr) {
     t.ymax = std::max(t.ymax, acc[w].ymax);
     t.amax = std::max(t.amax, acc[w].amax);
   }
-  L.finite = t.finite;
-  L.integral = t.integral;
-  L.label_ok = false;
-  if (t.finite && t.smax <= 40 && std::ldexp(t.amax, t.smax) < 8388608.0) {
-    L.label_ok = true;
-    L.shift = t.smax;
-    L.kmin = N ? (int64_t)std::ldexp(t.ymin, t.smax) : 0;
-    L.kmax = N ? (int64_t)std::ldexp(t.ymax, t.smax) : 0;
-  }
-  L.approx_ok = false;
-  L.ymax_abs = t.finite ? t.amax : 0.0;
-  L.ymax_sq = t.finite ? t.amax * t.amax : 0.0;
-  if (!L.label_ok && t.finite && t.amax > 0.0) {
-    // 2^e <= max|y| < 2^(e+1): max|y| 2^(21-e) < 2^22 (the image's range includes 0)
-    L.ashift = 21 - std::ilogb(t.amax);
-    L.akmin = std::min<int64_t>(0, (int64_t)std::nearbyint(std::ldexp(t.ymin, L.ashift)));
-    L.akmax = std::max<int64_t>(0, (int64_t)std::nearbyint(std::ldexp(t.ymax, L.ashift)));
-    L.approx_ok = true;
-  }
+  set_label_stats(L, N, t.finite, t.integral, t.smax, t.ymin, t.ymax, t.amax);
 }
 static void analyze_labels(sbag_dataset* ds) { analyze_labels(ds->lab, &ds->ctx->pool); }
 
@@ -4774,14 +4779,47 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
   for (int k = 0; k < Fr; k++)
     if (sub[k] < 0 || sub[k] >= F || (k > 0 && sub[k] <= sub[k - 1]))
       return fail(SBAG_EINVAL, "subspace indices must be increasing and within [0, num_features)");
-  // the residuals as a label set (copied and analyzed on the host pool)
+  // host-side phase timing of the booster set-up (SBAG_PROFILE_HOST=1 prints it)
+  const bool bprof = getenv("SBAG_PROFILE_HOST") != nullptr;
+  auto bnow = [] {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  double bt[6] = {0}, b0 = bnow();
+  auto bmark = [&](int k) {
+    const double t = bnow();
+    bt[k] += t - b0;
+    b0 = t;
+  };
+  // the residuals as a label set: uploaded, then analyzed on the device (analyze_labels'
+  // quantities, k_label_stats) -- no host pass over the column
   LabelSet lab;
-  lab.y.resize(N);
-  par_range(&c->pool, N, [&](int64_t lo, int64_t hi, int) {
-    std::copy(labels + lo, labels + hi, lab.y.begin() + lo);
-  });
-  analyze_labels(lab, &c->pool);
+  HIP_TRY(hipSetDevice(c->device));
+  TRY(ws_typed(c, "bt_y64", (size_t)N + 1, &lab.d_y64));
+  TRY(h2d(c, lab.d_y64, labels, (size_t)N));
+  HIP_TRY(hipMemsetAsync(lab.d_y64 + N, 0, 8, c->stream));
+  {
+    uint64_t* d_acc;
+    TRY(ws_typed(c, "bt_lacc", 6, &d_acc));
+    const uint64_t init[6] = {0, 0, 0, ~0ull, 0, 0};
+    TRY(h2d(c, d_acc, init, 6));
+    launch_label_stats(c->stream, lab.d_y64, N, d_acc);
+    HIP_TRY(hipGetLastError());
+    uint64_t acc[6];
+    TRY(d2h(c, acc, d_acc, 6));
+    auto from_key = [](uint64_t k) {
+      const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+      double v;
+      std::memcpy(&v, &b, 8);
+      return v;
+    };
+    double amax;
+    std::memcpy(&amax, &acc[5], 8);
+    const bool finite = acc[0] == 0;
+    set_label_stats(lab, N, finite, acc[1] == 0, (int)acc[2], finite ? from_key(acc[3]) : 0.0,
+                    finite ? from_key(acc[4]) : 0.0, amax);
+  }
   if (!lab.finite) return fail(SBAG_EUNSUPPORTED, "booster labels must be finite");
+  bmark(0);  // upload + analysis
   std::vector<int64_t> poff;
   TRY(check_partitions(bp->num_partitions, bp->partition_offsets, N, poff));
   HIP_TRY(hipSetDevice(c->device));
@@ -4797,11 +4835,15 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
         return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
                                  "empty one.");
     }
+    bmark(1);  // items
     TRY(ws_typed(c, "bt_labk", (size_t)N, &lab.d_labk));
-    TRY(labk_image(lab, lab.d_labk, &c->pool));
-    TRY(ws_typed(c, "bt_y64", (size_t)N + 1, &lab.d_y64));
-    TRY(h2d(c, lab.d_y64, labels, (size_t)N));
-    HIP_TRY(hipMemsetAsync(lab.d_y64 + N, 0, 8, c->stream));
+    if (lab.label_ok || lab.approx_ok)
+      launch_label_image(c->stream, lab.d_y64, N, lab.label_ok ? lab.shift : lab.ashift, lab.label_ok,
+                         lab.d_labk);
+    else
+      HIP_TRY(hipMemsetAsync(lab.d_labk, 0, (size_t)N * 4, c->stream));
+    HIP_TRY(hipGetLastError());
+    bmark(2);  // fixed-point image
     FitExt ext{bp->counts, sub, &lab};
     sbag_fit_params fp{};
     fp.sampler.replacement = 1;
@@ -4818,6 +4860,10 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
     const int rc = fit_range(c, const_cast<sbag_dataset*>(ds), &fp, &f, &ext);
     if (rc == kSplitRange) return fail(SBAG_EUNSUPPORTED, "the booster's bins exceed the device budget");
     TRY(rc);
+    bmark(4);  // fit
+    if (bprof)
+      fprintf(stderr, "[sbag] booster host ms: upload+analysis %.2f items %.2f image %.2f fit %.2f\n",
+              bt[0], bt[1], bt[2], bt[4]);
     *out = f;
     return SBAG_OK;
   }

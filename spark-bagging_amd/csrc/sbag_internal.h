@@ -442,6 +442,13 @@ struct F64BucketArgs {
   int32_t cmax, pad;        // largest draw count of an entry (1: no count loop)
 };
 // ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]
+// A label column's analysis on the device (sbag_fit_booster's residuals): acc[6] =
+// {not finite, not integral, largest scale s making a label integral, order key of the
+// smallest and of the largest label, bits of the largest |y|}; acc must hold the
+// launch_label_stats_init values.  k_label_image: k = y 2^shift (dyadic) or
+// rint(y 2^shift) (the fp64 screen's image).
+void launch_label_stats(hipStream_t st, const double* y, int64_t N, uint64_t* acc);
+void launch_label_image(hipStream_t st, const double* y, int64_t N, int shift, bool dyadic, int32_t* k);
 void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap,
                          const int64_t* d_nent, int R, int64_t max_nent);
 struct F64FinishNode {
