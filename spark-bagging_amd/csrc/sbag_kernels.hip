@@ -984,17 +984,16 @@ __global__ __launch_bounds__(64) void k_split_sample(
 // gaps depend only on its XORShift stream, so every lane steps the stream to its own draw of
 // a block of 64 (the stream is sequential: each lane runs the 64 steps, keeps the one it
 // owns), the gaps' prefix gives the block's 64 taken item positions, and the wave streams the
-// partition's count bytes (4096 rows per chunk in aligned 16-byte loads, one chunk ahead) and
-// resolves the positions
-// that fall in each chunk to their rows.  The same items as the one-lane walk, in the same
-// order: the row list is identical.
+// partition's count bytes (4096 rows per chunk in aligned 16-byte loads, three chunks ahead);
+// the lanes whose items fall in a chunk resolve their rows in parallel.  The same items as
+// the one-lane walk, in the same order: the row list is identical.
 __global__ __launch_bounds__(64) void k_split_sample_gap(
     const uint8_t* __restrict__ counts, int64_t N, const int64_t* __restrict__ part_off, int P,
     const int32_t* __restrict__ reps, const uint64_t* __restrict__ part_state,
     const double* __restrict__ frac, uint32_t* __restrict__ rows_out, int64_t cap,
     uint32_t* __restrict__ nrows, int64_t counts_len) {
-  __shared__ int64_t s_t[64];
-  __shared__ uint32_t s_rows[64];
+  __shared__ uint32_t s_incl[64];
+  __shared__ uint32_t s_words[64 * 16];
   const int ri = blockIdx.y, p = blockIdx.x, lane = threadIdx.x;
   const int r = reps[ri];
   const double lnq = frac[2 * ri + 1];
@@ -1035,26 +1034,18 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
     x = (x & 0x00FF00FFu) + ((x >> 8) & 0x00FF00FFu);
     return (x & 0xFFFFu) + (x >> 16);
   };
+  // kAhead - 1 chunks in flight behind the current one (the wave walks the partition's counts
+  // chunk after chunk)
+  constexpr int kAhead = 4;
   int64_t c0 = a0;
-  uint32_t cw[16], nw[16];
+  uint32_t cw[16], nw[kAhead - 1][16];
   load64(c0, cw);
-  load64(c0 + 4096, nw);
-  // items before the chunk, and this lane's item range inside it
-  int64_t ib = 0;
-  uint32_t lsum = 0;
 #pragma unroll
-  for (int k = 0; k < 16; k++) lsum += bsum(cw[k]);
-  uint32_t incl = lsum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_up(incl, o);
-    if (lane >= o) incl += u;
-  }
-  uint32_t ctot = __shfl(incl, 63);
+  for (int a = 0; a < kAhead - 1; a++) load64(c0 + 4096 * (a + 1), nw[a]);
+  // a block of 64 draws: lane j holds taken item j (every lane steps the shared stream and
+  // keeps its own draw); bhi = the block's last item
   int64_t next = 0;  // item index of the next draw's gap origin
-  bool done = r0 >= r1;
-  while (!done) {
-    // 64 gaps: lane j keeps draw j of the block (every lane steps the shared stream)
+  auto gen_block = [&](int64_t& tgt) {
     double myu = 0.0;
     for (int j = 0; j < 64; j++) {
       st = xs_step_s(st);
@@ -1074,59 +1065,99 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
       const int64_t u = __shfl_up(d, o);
       if (lane >= o) d += u;
     }
-    const int64_t tgt = next + d - 1;
-    s_t[lane] = tgt;
+    tgt = next + d - 1;
     next = next + __shfl(d, 63);
-    int nfound = 0;
-    // resolve the block's targets against the streamed chunks
-    for (int j = 0; j < 64;) {
-      const int64_t t = s_t[j];  // (LDS, same wave: in order)
-      if (t >= ib + (int64_t)ctot) {  // past this chunk: the next one
-        if (c0 + 4096 >= r1) {
-          done = true;
-          break;
+  };
+  int64_t tgt;
+  gen_block(tgt);
+  int64_t ib = 0;  // items before the chunk
+  // Chunk-major: each chunk's words and lane prefixes go to LDS, and every lane whose taken
+  // item falls in the chunk resolves its row in parallel (the owner lane by a binary
+  // search over the prefixes, then its 64 rows' bytes) -- no per-item serial loop
+  while (c0 < r1) {
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) lsum += bsum(cw[k]);
+    uint32_t incl = lsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
+    }
+    const uint32_t ctot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    s_incl[lane] = incl;
+#pragma unroll
+    for (int k = 0; k < 16; k++) s_words[16 * lane + k] = cw[k];
+    __builtin_amdgcn_wave_barrier();
+    const int64_t iend = ib + (int64_t)ctot;
+    for (;;) {
+      const bool in = tgt >= ib && tgt < iend;
+      const uint64_t im = __ballot(in);
+      if (im) {
+        uint32_t row = 0;
+        if (in) {
+          const uint32_t o = (uint32_t)(tgt - ib);
+          // owner: the first lane w with incl[w] > o
+          int w = 0;
+#pragma unroll
+          for (int stp = 32; stp > 0; stp >>= 1)
+            if (s_incl[w + stp - 1] <= o) w += stp;
+          uint32_t acc = s_incl[w];
+          uint32_t wv[16];
+#pragma unroll
+          for (int k = 0; k < 16; k++) wv[k] = s_words[16 * w + k];
+#pragma unroll
+          for (int k = 0; k < 16; k++) acc -= bsum(wv[k]);  // items before lane w's rows
+          // the word, then the byte, holding item o
+          int kk = 0;
+          uint32_t run = acc;
+#pragma unroll
+          for (int k = 0; k < 16; k++) {
+            const uint32_t nx = run + bsum(wv[k]);
+            const bool before = nx <= o && k == kk;
+            run = before ? nx : run;
+            kk += before ? 1 : 0;
+          }
+          uint32_t x = wv[0];
+#pragma unroll
+          for (int k = 1; k < 16; k++) x = kk == k ? wv[k] : x;
+          int bb = 0;
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            const uint32_t nx = run + ((x >> (8 * q)) & 0xFFu);
+            const bool before = nx <= o && q == bb;
+            run = before ? nx : run;
+            bb += before ? 1 : 0;
+          }
+          row = (uint32_t)(c0 + 64 * w + 4 * kk + bb);
         }
-        ib += ctot;
-        c0 += 4096;
-#pragma unroll
-        for (int k = 0; k < 16; k++) cw[k] = nw[k];
-        load64(c0 + 4096, nw);
-        lsum = 0;
-#pragma unroll
-        for (int k = 0; k < 16; k++) lsum += bsum(cw[k]);
-        incl = lsum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t u = __shfl_up(incl, o);
-          if (lane >= o) incl += u;
-        }
-        ctot = __shfl(incl, 63);
+        // append the chunk's rows of this block in item order (one atomic)
+        const int n = __popcll(im);
+        uint32_t k0 = 0;
+        if (lane == 0) k0 = atomicAdd(&nrows[ri], (uint32_t)n);
+        k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+        const int rk = __popcll(im & ((1ull << lane) - 1));
+        if (in && (int64_t)k0 + rk < cap) out[k0 + rk] = row;
+      }
+      // the whole block lies before the chunk's end: the next block (it may start here too)
+      const int64_t bhi = (int64_t)__builtin_amdgcn_readlane((int)(uint32_t)tgt, 63) |
+                          ((int64_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)tgt >> 32), 63) << 32);
+      if (bhi < iend) {
+        gen_block(tgt);
         continue;
       }
-      // the lane whose rows hold item t, then the row among its 16
-      const int64_t o = t - ib;
-      const bool mine = o >= (int64_t)(incl - lsum) && o < (int64_t)incl;
-      const uint64_t m = __ballot(mine);
-      const int owner = __ffsll((unsigned long long)m) - 1;
-      if (lane == owner) {
-        // the word, then the byte among the lane's 64 rows
-        uint32_t acc = incl - lsum;
-        int k = 0;
-        while (k < 15 && (int64_t)(acc + bsum(cw[k])) <= o) acc += bsum(cw[k++]);
-        int bb = 0;
-        while (bb < 3 && (int64_t)(acc + ((cw[k] >> (8 * bb)) & 0xFFu)) <= o) acc += (cw[k] >> (8 * bb++)) & 0xFFu;
-        s_rows[nfound] = (uint32_t)(c0 + 64 * lane + 4 * k + bb);
-      }
-      nfound++;
-      j++;
+      break;
     }
-    // append the block's rows (one atomic per block)
-    if (nfound > 0) {
-      uint32_t k0 = 0;
-      if (lane == 0) k0 = atomicAdd(&nrows[ri], (uint32_t)nfound);
-      k0 = (uint32_t)__shfl((int)k0, 0);
-      if (lane < nfound && (int64_t)k0 + lane < cap) out[k0 + lane] = s_rows[lane];
-    }
+    __builtin_amdgcn_wave_barrier();
+    ib = iend;
+    c0 += 4096;
+#pragma unroll
+    for (int k = 0; k < 16; k++) cw[k] = nw[0][k];
+#pragma unroll
+    for (int a = 0; a + 1 < kAhead - 1; a++)
+#pragma unroll
+      for (int k = 0; k < 16; k++) nw[a][k] = nw[a + 1][k];
+    load64(c0 + 4096 * (kAhead - 1), nw[kAhead - 2]);
   }
 }
 
