@@ -1017,7 +1017,13 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
       const uint8_t* pa = cr + row;
       const uint8_t* pc = pa < cbase ? cbase : (pa > climit ? climit : pa);
       const uint4 v = *(const uint4*)pc;
-      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      // clamped at the buffer's end (its last < 16 rows): the wanted bytes pa.. are the
+      // loaded bytes from pa - pc on, the rest past the buffer (0): a 128-bit right shift
+      const uint32_t s8 = 8u * (uint32_t)(pa > pc ? pa - pc : 0);
+      const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+      const uint64_t nlo = s8 == 0 ? lo : s8 < 64 ? (lo >> s8) | (hi << (64 - s8)) : hi >> (s8 - 64);
+      const uint64_t nhi = s8 < 64 ? hi >> s8 : 0ull;
+      const uint32_t vv[4] = {(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
 #pragma unroll
       for (int d = 0; d < 4; d++) {
         uint32_t m = 0;
@@ -1026,7 +1032,7 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
           const int64_t rr = row + 4 * d + bb;
           m |= (rr >= r0 && rr < r1) ? (0xFFu << (8 * bb)) : 0u;
         }
-        w[4 * q + d] = pc == pa ? (vv[d] & m) : 0u;
+        w[4 * q + d] = pa < cbase ? 0u : (vv[d] & m);
       }
     }
   };

@@ -129,6 +129,18 @@ def test_fuzz_shapes_parity(ctx, seed):
     forest.free()
 
 
+# scripts/fuzz_parity.py seeds that failed in round 4 (gpurun_out/r04au/fuzz.log, 78 of 1956
+# draws): k_split_sample_gap's aligned 16-byte count loads were clamped to the buffer's last
+# 16 bytes and then dropped whole, so the last replica lost its last (N*R mod 16) rows' items
+# from the split-finding sample -- always the last tree of a P < 64 fit with continuous
+# features.  The clamped load is now shifted into place.
+@pytest.mark.parametrize("seed", [81005, 81008, 81059, 81172, 81076])
+def test_split_sample_gap_buffer_tail(ctx, seed):
+    forest, orf = _fit_fuzz(ctx, seed)
+    assert_forest_equal(forest, orf)
+    forest.free()
+
+
 def test_split_sample_one_more_threshold(ctx):
     """scripts/fuzz_parity.py --big seed 90000 (2.87M rows, 32 learners, subspace ratio 0.3 of
     its own, fp64 labels): a split-finding sample larger than numSamples passes one more
