@@ -248,7 +248,9 @@ __device__ __forceinline__ void rstore64(__amdgpu_buffer_rsrc_t r, uint32_t off,
 // thread takes 8 entries per step, their loads (clamped indices: no branches, so the
 // gathers are issued back to back) and gathers before the atomics.
 __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
-  const F64TPiece pc = A.pieces[blockIdx.x];
+  // (porder: the dispatch order of the pieces, XCD-aware; the outputs stay per piece)
+  const int64_t pix = A.porder ? (int64_t)A.porder[blockIdx.x] : (int64_t)blockIdx.x;
+  const F64TPiece pc = A.pieces[pix];
   const F64Task t = A.tasks[pc.task];
   const int NB = A.NB, tid = threadIdx.x;
   __shared__ uint32_t s_c[256];
@@ -282,8 +284,8 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   for (int o = 32; o > 0; o >>= 1) nl += __shfl_down(nl, o);
   if ((tid & 63) == 0) s_l[tid >> 6] = nl;
   block_sync();
-  for (int b = tid; b < NB; b += 256) A.pcnt[(int64_t)blockIdx.x * NB + b] = s_c[b];
-  if (tid == 0) A.plcnt[blockIdx.x] = s_l[0] + s_l[1] + s_l[2] + s_l[3];
+  for (int b = tid; b < NB; b += 256) A.pcnt[pix * NB + b] = s_c[b];
+  if (tid == 0) A.plcnt[pix] = s_l[0] + s_l[1] + s_l[2] + s_l[3];
 }
 
 // per task: bucket bounds (bins in order, each bin's entries in row order), each piece's

@@ -1976,6 +1976,40 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.y = d_y64;
       ba.chist = chist;
       ba.cmax = (int32_t)G.cmax;
+      // XCD-aware dispatch of k_fb_count (workgroup w runs on XCD w mod 8, each with its own
+      // L2): a piece goes to the XCD of its position within its node's entries, a proxy of
+      // its rows' slice of [0, N), so each XCD's bin gathers stay in one eighth of a column
+      // (SBAG_F64_XCD_ORDER=0: in order)
+      ba.porder = nullptr;
+      {
+        static const char* xenv = getenv("SBAG_F64_XCD_ORDER");
+        if (!(xenv && atoi(xenv) == 0) && np >= 64) {
+          std::vector<std::vector<int32_t>> q(8);
+          for (int64_t i = 0; i < np; i++) {
+            const F64Task& t = tk[pcs[i].task];
+            const int64_t len = std::max<int64_t>(1, t.b - t.a);
+            const int64_t mid = (pcs[i].a + pcs[i].b) / 2 - t.a;
+            q[(size_t)std::min<int64_t>(7, mid * 8 / len)].push_back((int32_t)i);
+          }
+          std::vector<int32_t> ord;
+          ord.reserve((size_t)np);
+          std::vector<size_t> head(8, 0);
+          for (int64_t w = 0; w < np; w++) {
+            int k = (int)(w & 7);
+            if (head[k] >= q[k].size()) {  // that slice is done: the earliest remaining piece
+              int best = -1;
+              for (int j = 0; j < 8; j++)
+                if (head[j] < q[j].size() && (best < 0 || q[j][head[j]] < q[best][head[best]])) best = j;
+              k = best;
+            }
+            ord.push_back(q[k][head[k]++]);
+          }
+          int32_t* d_ord;
+          TRY(ws_typed(c, "fb_porder", (size_t)np, &d_ord));
+          TRY(h2d(c, d_ord, ord.data(), ord.size()));
+          ba.porder = d_ord;
+        }
+      }
       launch_fb_route(c->stream, ba, np, nchain);
       HIP_TRY(hipGetLastError());
       if (nleft_out) {

@@ -440,6 +440,7 @@ struct F64BucketArgs {
   double* ey_out;           // the labels of ent_out's entries
   double* chist;            // [task][NB][3] count, sum, sumSq in Spark's row order
   int32_t cmax, pad;        // largest draw count of an entry (1: no count loop)
+  const int32_t* porder;    // k_fb_count's piece of each workgroup (null: in order)
 };
 // ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]
 // A label column's analysis on the device (sbag_fit_booster's residuals): acc[6] =
