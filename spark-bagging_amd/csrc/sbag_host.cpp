@@ -1982,7 +1982,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       // (SBAG_F64_XCD_ORDER=0: in order)
       ba.porder = nullptr;
       {
-        static const char* xenv = getenv("SBAG_F64_XCD_ORDER");
+        const char* xenv = getenv("SBAG_F64_XCD_ORDER");
         if (!(xenv && atoi(xenv) == 0) && np >= 64) {
           std::vector<std::vector<int32_t>> q(8);
           for (int64_t i = 0; i < np; i++) {
@@ -2213,7 +2213,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     std::vector<int> norder(M);
     for (int i = 0; i < M; i++) norder[i] = i;
     {
-      static const char* oenv = getenv("SBAG_F64_TASK_ORDER");
+      const char* oenv = getenv("SBAG_F64_TASK_ORDER");
       if (!(oenv && atoi(oenv) == 0)) {
         auto colkey = [&](int i) -> int64_t {
           return so[i].flag || so[i].f < 0 ? INT64_MAX : (int64_t)G.h_pos[(size_t)cur[i].r * Fmax + so[i].f];

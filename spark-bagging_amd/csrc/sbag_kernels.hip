@@ -992,8 +992,10 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
     const int32_t* __restrict__ reps, const uint64_t* __restrict__ part_state,
     const double* __restrict__ frac, uint32_t* __restrict__ rows_out, int64_t cap,
     uint32_t* __restrict__ nrows, int64_t counts_len) {
+  constexpr int kGapBuf = 2048;
   __shared__ uint32_t s_incl[64];
   __shared__ uint32_t s_words[64 * 16];
+  __shared__ uint32_t s_buf[kGapBuf];
   const int ri = blockIdx.y, p = blockIdx.x, lane = threadIdx.x;
   const int r = reps[ri];
   const double lnq = frac[2 * ri + 1];
@@ -1010,17 +1012,28 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
   const uint8_t* cbase = counts;
   const uint8_t* climit = counts + max(counts_len - 16, (int64_t)0);
   const int64_t a0 = r0 - (int64_t)(((uintptr_t)(cr + r0)) & 15u);  // row of the aligned start
-  auto load64 = [&](int64_t c0, uint32_t (&w)[16]) {
+  // issue: the chunk's four 16-byte loads per lane, raw (the data is not touched here, so
+  // the loads stay in flight behind the current chunk); finish: the chunk's words, shifted
+  // into place where a load was clamped to the buffer's last 16 bytes, rows outside
+  // [r0, r1) masked to 0
+  auto issue = [&](int64_t c0, uint4 (&v)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint8_t* pa = cr + c0 + 64 * lane + 16 * q;
+      const uint8_t* pc = pa < cbase ? cbase : (pa > climit ? climit : pa);
+      v[q] = *(const uint4*)pc;
+    }
+  };
+  auto finish = [&](int64_t c0, const uint4 (&v)[4], uint32_t (&w)[16]) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int64_t row = c0 + 64 * lane + 16 * q;
       const uint8_t* pa = cr + row;
       const uint8_t* pc = pa < cbase ? cbase : (pa > climit ? climit : pa);
-      const uint4 v = *(const uint4*)pc;
       // clamped at the buffer's end (its last < 16 rows): the wanted bytes pa.. are the
       // loaded bytes from pa - pc on, the rest past the buffer (0): a 128-bit right shift
       const uint32_t s8 = 8u * (uint32_t)(pa > pc ? pa - pc : 0);
-      const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+      const uint64_t lo = ((uint64_t)v[q].y << 32) | v[q].x, hi = ((uint64_t)v[q].w << 32) | v[q].z;
       const uint64_t nlo = s8 == 0 ? lo : s8 < 64 ? (lo >> s8) | (hi << (64 - s8)) : hi >> (s8 - 64);
       const uint64_t nhi = s8 < 64 ? hi >> s8 : 0ull;
       const uint32_t vv[4] = {(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
@@ -1044,10 +1057,12 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
   // chunk after chunk)
   constexpr int kAhead = 4;
   int64_t c0 = a0;
-  uint32_t cw[16], nw[kAhead - 1][16];
-  load64(c0, cw);
+  uint32_t cw[16];
+  // ring of kAhead chunks in flight; the chunk loop is unrolled kAhead times so each slot
+  // is a fixed set of registers (moving an in-flight load's destination would wait for it)
+  uint4 ring[kAhead][4];
 #pragma unroll
-  for (int a = 0; a < kAhead - 1; a++) load64(c0 + 4096 * (a + 1), nw[a]);
+  for (int a = 0; a < kAhead; a++) issue(c0 + 4096 * a, ring[a]);
   // a block of 64 draws: lane j holds taken item j (every lane steps the shared stream and
   // keeps its own draw); bhi = the block's last item
   int64_t next = 0;  // item index of the next draw's gap origin
@@ -1076,11 +1091,22 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
   };
   int64_t tgt;
   gen_block(tgt);
+  int nbuf = 0;  // rows in s_buf
+  auto flush = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    uint32_t k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&nrows[ri], (uint32_t)nbuf);
+    k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+    for (int i = lane; i < nbuf; i += 64)
+      if ((int64_t)k0 + i < cap) out[k0 + i] = s_buf[i];
+    __builtin_amdgcn_wave_barrier();
+    nbuf = 0;
+  };
   int64_t ib = 0;  // items before the chunk
   // Chunk-major: each chunk's words and lane prefixes go to LDS, and every lane whose taken
   // item falls in the chunk resolves its row in parallel (the owner lane by a binary
   // search over the prefixes, then its 64 rows' bytes) -- no per-item serial loop
-  while (c0 < r1) {
+  auto process = [&]() {
     uint32_t lsum = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) lsum += bsum(cw[k]);
@@ -1137,13 +1163,14 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
           }
           row = (uint32_t)(c0 + 64 * w + 4 * kk + bb);
         }
-        // append the chunk's rows of this block in item order (one atomic)
+        // the chunk's rows of this block, in item order, to the LDS buffer (appended to the
+        // replica's list with one atomic per kGapBuf rows: a returning atomic in the chunk
+        // loop would wait for the chunk loads in flight, vmcnt counting in order)
         const int n = __popcll(im);
-        uint32_t k0 = 0;
-        if (lane == 0) k0 = atomicAdd(&nrows[ri], (uint32_t)n);
-        k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
         const int rk = __popcll(im & ((1ull << lane) - 1));
-        if (in && (int64_t)k0 + rk < cap) out[k0 + rk] = row;
+        if (in) s_buf[nbuf + rk] = row;
+        nbuf += n;
+        if (nbuf > kGapBuf - 64) flush();
       }
       // the whole block lies before the chunk's end: the next block (it may start here too)
       const int64_t bhi = (int64_t)__builtin_amdgcn_readlane((int)(uint32_t)tgt, 63) |
@@ -1156,15 +1183,21 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
     }
     __builtin_amdgcn_wave_barrier();
     ib = iend;
-    c0 += 4096;
+  };
+  bool more = c0 < r1;
+  while (more) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) cw[k] = nw[0][k];
-#pragma unroll
-    for (int a = 0; a + 1 < kAhead - 1; a++)
-#pragma unroll
-      for (int k = 0; k < 16; k++) nw[a][k] = nw[a + 1][k];
-    load64(c0 + 4096 * (kAhead - 1), nw[kAhead - 2]);
+    for (int a = 0; a < kAhead; a++) {
+      if (more) {
+        finish(c0, ring[a], cw);
+        issue(c0 + 4096 * kAhead, ring[a]);
+        process();
+        c0 += 4096;
+        more = c0 < r1;
+      }
+    }
   }
+  if (nbuf > 0) flush();
 }
 
 // Phase 2, grid (sample chunks of kSvcRows, replicas): each sampled row adds its value codes

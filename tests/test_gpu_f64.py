@@ -245,3 +245,44 @@ def test_bucket_budget_chunks_equal_one_launch(ctx, cpusmall, monkeypatch):
     counts = oracle.bag(True, 1.0, 0, 4, SEED_REG, [0, N], N)
     subs = [oracle.subspace(1.0, F, SEED_REG + i) for i in range(4)]
     assert_forest_equal(b, oracle_forest(X, y2, counts, subs, 7, 32, False))
+
+
+def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
+    """The bench's real-valued-label fit at full size (10M x 100, 128 learners, depth 8,
+    P = 128), where the oracle cannot follow: the default engine (screen, staged bucket
+    scatter, column-ordered and XCD-dispatched tasks, exploded chains) gives the same trees
+    byte for byte as (a) the same screen with round 4's first bucketing and chain kernels and
+    (b) the unscreened engine, every node of every level summed by round 3's row-order walk
+    (k_f64_hist) -- two independent exact paths."""
+    N, F, L = 10_000_000, 100, 128
+    ds = nat.DeviceDataset.synthetic(N, F, seed=20261015, ctx=ctx)
+    try:
+        ds.set_labels(ds.labels() * 1.1 + 0.3)
+        part = [round(i * N / 128) for i in range(129)]
+
+        def fit():
+            return nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=-1395689524,
+                           learner_begin=0, learner_end=L, partition_offsets=part, max_depth=8,
+                           max_bins=32, impurity=nat.IMPURITY_VARIANCE)
+
+        a = fit()
+        for k in ("SBAG_F64_CHAIN_X", "SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER",
+                  "SBAG_F64_XCD_ORDER"):
+            monkeypatch.setenv(k, "0")
+        b = fit()
+        for k in ("SBAG_F64_CHAIN_X", "SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER",
+                  "SBAG_F64_XCD_ORDER"):
+            monkeypatch.delenv(k)
+        monkeypatch.setenv("SBAG_F64_SCREEN", "0")
+        monkeypatch.setenv("SBAG_F64_FALLBACK", "hist")
+        c = fit()
+    finally:
+        ds.free()
+    ta, tc = a.timing(), c.timing()
+    assert ta["exact_fallbacks"] < tc["exact_fallbacks"] / 20, (ta["exact_fallbacks"], tc["exact_fallbacks"])
+    for t in range(L):
+        (na, sa), (nb, sb_), (nc, sc) = a.tree(t), b.tree(t), c.tree(t)
+        assert na.tobytes() == nb.tobytes() == nc.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes() == sc.tobytes(), f"tree {t} stats"
+    for f in (a, b, c):
+        f.free()
