@@ -328,7 +328,8 @@ def main():
     else:
         os.environ["SBAG_OVERLAP"] = prev
     # The same fit on real-valued labels: y' = 1.1 y + 0.3 is not dyadic,
-    # so sbag_fit takes the row-order fp64 path (Spark's DTStatsAggregator sums, sbag_f64.hip).
+    # so sbag_fit takes the screened fp64 path (Spark's DTStatsAggregator row-order sums of the
+    # chosen features, sbag_f64s.hip).
     # Reported beside the headline; not part of `value`.
     nondyadic = None
     if not cls and world == 1 and not args.no_nondyadic:
@@ -353,7 +354,8 @@ def main():
                      "exact_fallbacks": int(tl[-1]["exact_fallbacks"]),
                      "engine": "screened fp64 engine: splits chosen from integer histograms of the "
                                "labels' fixed-point image under a rigorous error bound, the chosen "
-                               "feature's bins summed in Spark's row order (bucketing + chains), "
+                               "feature's bins summed in Spark's row order (bucketing staged by bin, "
+                               "chains with the draws exploded in LDS), "
                                "flagged nodes ('exact_fallbacks') summed exactly on every feature "
                                "(DESIGN.md §4.7)"}
     out = {
