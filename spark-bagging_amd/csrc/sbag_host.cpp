@@ -1535,21 +1535,67 @@ static bool overlap_fits(sbag_ctx* c, const sbag_dataset* ds, int learners) {
   return 2.0 * part <= 0.9 * ((double)fr + mine);
 }
 
+static int fit_learners_halving(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out);
 // one context: fit_range, or halves of the learner range when per-replica bins exceed
 // the device budget (learners are independent, so concatenation is exact)
 static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
+  // Continuous features (more distinct values than maxBins) get thresholds of their own per
+  // replica, so their bins are materialized per replica: when those of the whole range
+  // exceed the budget, split it up front into parts that fit -- a fit_range that finds out
+  // only after the sampling and the split finding would redo them for every halving
+  // (C3-sized continuous fit: 3 wasted attempts)
+  {
+    const int lb = fp->sampler.learner_begin, le = fp->sampler.learner_end;
+    bool cont = false;
+    for (const auto& d : ds->dict) cont = cont || (int64_t)d.size() > fp->tree.max_bins;
+    if (cont && le - lb > 1) {
+      const double per = (double)ds->N * row_stride(ds->F) + (double)ds->F * (double)((ds->N + 63) / 64 * 64);
+      const double budget = bins_budget(c);
+      const int fitn = (int)std::max(1.0, std::floor(budget / per));
+      if (fitn < le - lb) {
+        const int parts = (le - lb + fitn - 1) / fitn;
+        std::unique_ptr<sbag_forest> acc;
+        for (int k = 0; k < parts; k++) {
+          sbag_fit_params h = *fp;
+          h.sampler.learner_begin = lb + (int)((int64_t)(le - lb) * k / parts);
+          h.sampler.learner_end = lb + (int)((int64_t)(le - lb) * (k + 1) / parts);
+          sbag_forest* f = nullptr;
+          {
+            const int st = fit_range(c, ds, &h, &f);
+            if (st == kSplitRange) {  // the estimate was short: halve as before
+              TRY(fit_learners_halving(c, ds, &h, &f));
+            } else {
+              TRY(st);
+            }
+          }
+          std::unique_ptr<sbag_forest> ff(f);
+          if (!acc) {
+            acc = std::move(ff);
+          } else {
+            merge_forests(acc.get(), ff.get());
+          }
+        }
+        *out = acc.release();
+        return SBAG_OK;
+      }
+    }
+  }
+  return fit_learners_halving(c, ds, fp, out);
+}
+
+static int fit_learners_halving(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
   const int st = fit_range(c, ds, fp, out);
   if (st != kSplitRange) return st;
   const int lb = fp->sampler.learner_begin, le = fp->sampler.learner_end, mid = lb + (le - lb) / 2;
   sbag_fit_params h = *fp;
   h.sampler.learner_end = mid;
   sbag_forest* a = nullptr;
-  TRY(fit_learners(c, ds, &h, &a));
+  TRY(fit_learners_halving(c, ds, &h, &a));
   std::unique_ptr<sbag_forest> fa(a);
   h.sampler.learner_begin = mid;
   h.sampler.learner_end = le;
   sbag_forest* b = nullptr;
-  TRY(fit_learners(c, ds, &h, &b));
+  TRY(fit_learners_halving(c, ds, &h, &b));
   std::unique_ptr<sbag_forest> fb(b);
   merge_forests(fa.get(), fb.get());
   *out = fa.release();
@@ -3029,7 +3075,16 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
           vc[vcoff[(size_t)r * Fmax + fl] + k] = (uint32_t)cnt;
         }
       }
-  } else if (!wide) {
+  } else if (!wide && [&] {
+               // the subbag's value counts serve only replicas whose thresholds come from the
+               // whole subbag (numExamples <= required); the others are thresholded on their
+               // split-finding sample (3b) -- a C3-sized continuous fit skips 8.1e10 atomics
+               for (int r = 0; r < R; r++)
+                 if (std::max<int64_t>(std::min<int64_t>(tp.max_bins, nw[r]) * std::min<int64_t>(tp.max_bins, nw[r]),
+                                       10000) >= nw[r])
+                   return true;
+               return false;
+             }()) {
     int h = tm.begin(T_VC);
     HistGeom g;
     if (ds->code_bytes == 1 && hist_geometry(ds->S, Fmax, ncmax, 1, true, g)) {

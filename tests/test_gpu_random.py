@@ -189,3 +189,24 @@ def test_max_bins_256_refused_for_every_seed(ctx, seed):
         f.free()
     finally:
         ds.free()
+
+
+def test_per_replica_bins_split_learner_range(ctx, monkeypatch):
+    """Continuous features get per-replica thresholds and materialized per-replica bins;
+    when those exceed the bins budget the learner range is split up front into parts that
+    fit (each part samples and bins only its learners).  A budget of a few replicas forces
+    several parts: the same forest byte for byte as one part, and the oracle's."""
+    X, y, cls, f64, part, p, kind = fuzz_case(81005)  # 57 239 x 65 mixed features, 9 learners
+    a, orf = _fit_fuzz(ctx, 81005)
+    N, F = X.shape
+    per_replica_mb = (N * (F + 127) // 128 * 128 + F * ((N + 63) // 64 * 64)) / 2**20
+    monkeypatch.setenv("SBAG_BINS_BUDGET_MB", str(3.5 * per_replica_mb))  # 3 learners per part
+    b, _ = _fit_fuzz(ctx, 81005)
+    assert len(a) == len(b) == p["L"]
+    for t in range(p["L"]):
+        (na, sa), (nb, sb_) = a.tree(t), b.tree(t)
+        assert na.tobytes() == nb.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes()
+    assert_forest_equal(b, orf)
+    a.free()
+    b.free()
