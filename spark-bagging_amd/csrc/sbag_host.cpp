@@ -3355,6 +3355,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   int plane_nsp = 0;
   int32_t S;
   std::vector<int16_t> h_pos((size_t)R * Fmax, 0);
+  uint8_t* cols_direct = nullptr;  // per-replica column copy written by the materialization
   {
     int h = tm.begin(T_BIN);
     uint8_t* d_lut;
@@ -3431,8 +3432,17 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         TRY(ws_typed(c, "lutoff", vcoff.size(), &d_lutoff));
         TRY(h2d(c, d_lut, lut.data(), lut.size()));
         TRY(h2d(c, d_lutoff, vcoff.data(), vcoff.size()));
-        launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
-                           d_lut, d_lutoff, d_b, S);
+        // the column copy for k_partition written by the same pass (no transpose re-reading
+        // the bins: 46 ms per 43-replica part of a C3-sized continuous fit)
+        int ncol_r = 1;
+        for (int r = 0; r < R; r++) ncol_r = std::max(ncol_r, (int)h_Fr[r]);
+        const int64_t npad_r = (N + 63) / 64 * 64;
+        uint8_t* d_c;
+        TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_r, &d_c));
+        if (launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
+                               d_lut, d_lutoff, d_b, S, getenv("SBAG_MATERIALIZE_NO_COLS") ? nullptr : d_c,
+                               ncol_r, npad_r))
+          cols_direct = d_c;
       }
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemsetAsync(d_b + (size_t)R * N * S, 0, 256, c->stream));  // zero slack
@@ -3481,10 +3491,12 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         plane_nsp = ds->planes_nsp;
       }
     } else {
-      uint8_t* d_c;
-      TRY(ws_typed(c, "cols", (size_t)Rc * ncol * npad, &d_c));
-      launch_transpose(c->stream, d_bins, N, S, ncol, d_c, npad, Rc, bins_rstride, cols_rstride);
-      HIP_TRY(hipGetLastError());
+      uint8_t* d_c = cols_direct;
+      if (!d_c) {
+        TRY(ws_typed(c, "cols", (size_t)Rc * ncol * npad, &d_c));
+        launch_transpose(c->stream, d_bins, N, S, ncol, d_c, npad, Rc, bins_rstride, cols_rstride);
+        HIP_TRY(hipGetLastError());
+      }
       d_cols = d_c;
       if (bins_rstride == 0 && planes_fit(ncol, plane_nsp)) {
         uint32_t* d_pl;

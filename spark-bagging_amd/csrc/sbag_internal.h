@@ -254,9 +254,13 @@ void launch_zero_slots(hipStream_t st, void* hist, const int32_t* d_slots, int n
                        int64_t u32_words_per_slot);
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words);
-void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
+// per-replica bins out[r][n][fl] = lut[lutoff[r][fl] + codes[n][sub[r][fl]]]; with cols, the
+// column-major copy cols[r][fl < ncol][npad] is written by the same pass when the kernel
+// can (returns true; else the caller transposes)
+bool launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
                         const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
-                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out);
+                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out,
+                        uint8_t* cols = nullptr, int32_t ncol = 0, int64_t npad = 0);
 // identity bins packed per replica: out[r][n][fl] = codes[n][sub[r][fl]], S_out % 4 == 0,
 // S_codes % 4 == 0
 void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,

@@ -3334,8 +3334,11 @@ __global__ __launch_bounds__(256) void k_materialize_rows(const CT* __restrict__
                                                           const int32_t* __restrict__ Fr, int32_t Fmax,
                                                           const uint8_t* __restrict__ lut,
                                                           const int64_t* __restrict__ lutoff,
-                                                          uint8_t* __restrict__ out, int32_t S_out) {
-  extern __shared__ __align__(16) uint8_t s_codes[];  // [kMatRows][S_codes] CT
+                                                          uint8_t* __restrict__ out, int32_t S_out,
+                                                          uint8_t* __restrict__ cols, int32_t ncol,
+                                                          int64_t npad) {
+  // [kMatRows][S_codes] CT codes, then (cols) [kMatRows][S_out] bins
+  extern __shared__ __align__(16) uint8_t s_codes[];
   const int r = blockIdx.y, tid = threadIdx.x;
   const int64_t n0 = (int64_t)blockIdx.x * kMatRows;
   const int nr = (int)min<int64_t>(kMatRows, N - n0);
@@ -3358,25 +3361,43 @@ __global__ __launch_bounds__(256) void k_materialize_rows(const CT* __restrict__
       if (fl < fr) v |= (uint32_t)lut[lo[fl] + (int64_t)sc[row * S_codes + sr[fl]]] << (8 * k);
     }
     o[q] = v;
+    if (cols) ((uint32_t*)(s_codes + (size_t)kMatRows * S_codes * sizeof(CT)))[q] = v;
+  }
+  if (!cols) return;
+  // the column-major copy (k_partition's gathers): per feature the block's 64 rows are 64
+  // consecutive bytes (rows past N: 0)
+  block_sync();
+  const uint8_t* sb = s_codes + (size_t)kMatRows * S_codes * sizeof(CT);
+  uint8_t* cr = cols + (int64_t)r * ncol * npad + n0;
+  for (int q = tid; q < ncol * (kMatRows / 4); q += 256) {
+    const int fl = q / (kMatRows / 4), wd = q - fl * (kMatRows / 4);
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int row = 4 * wd + k;
+      if (row < nr) v |= (uint32_t)sb[row * S_out + fl] << (8 * k);
+    }
+    ((uint32_t*)(cr + (int64_t)fl * npad))[wd] = v;
   }
 }
 
-void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
+bool launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
                         const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
-                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out) {
-  if (S_out % 4 == 0 && (S_codes * code_bytes) % 4 == 0 && (int64_t)kMatRows * S_codes * code_bytes <= 64 * 1024 &&
+                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out,
+                        uint8_t* cols, int32_t ncol, int64_t npad) {
+  const size_t lds = (size_t)kMatRows * S_codes * code_bytes + (cols ? (size_t)kMatRows * S_out : 0);
+  if (S_out % 4 == 0 && (S_codes * code_bytes) % 4 == 0 && lds <= 64 * 1024 && npad % kMatRows == 0 &&
       !getenv("SBAG_MATERIALIZE_ROWWISE")) {
     const dim3 g((unsigned)((N + kMatRows - 1) / kMatRows), (unsigned)R);
-    const size_t lds = (size_t)kMatRows * S_codes * code_bytes;
     set_max_lds(code_bytes == 1 ? (const void*)k_materialize_rows<uint8_t> : (const void*)k_materialize_rows<uint16_t>,
                 (int)lds);
     if (code_bytes == 1)
       hipLaunchKernelGGL(k_materialize_rows<uint8_t>, g, dim3(256), lds, st, (const uint8_t*)codes, N, S_codes,
-                         d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
+                         d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad);
     else
       hipLaunchKernelGGL(k_materialize_rows<uint16_t>, g, dim3(256), lds, st, (const uint16_t*)codes, N,
-                         S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
-    return;
+                         S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad);
+    return cols != nullptr;
   }
   dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
   if (code_bytes == 1)
@@ -3385,6 +3406,7 @@ void launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64
   else
     hipLaunchKernelGGL(k_materialize<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)codes, N,
                        S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
+  return false;
 }
 
 // Per-replica packed rows of identity bins: out[r][n][fl] = codes[n][sub[r][fl]] (0 past the
