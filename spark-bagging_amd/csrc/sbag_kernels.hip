@@ -3336,10 +3336,10 @@ __global__ __launch_bounds__(256) void k_materialize_rows(const CT* __restrict__
                                                           const int64_t* __restrict__ lutoff,
                                                           uint8_t* __restrict__ out, int32_t S_out,
                                                           uint8_t* __restrict__ cols, int32_t ncol,
-                                                          int64_t npad) {
+                                                          int64_t npad, int R, int rb) {
   // [kMatRows][S_codes] CT codes, then (cols) [kMatRows][S_out] bins
   extern __shared__ __align__(16) uint8_t s_codes[];
-  const int r = blockIdx.y, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int64_t n0 = (int64_t)blockIdx.x * kMatRows;
   const int nr = (int)min<int64_t>(kMatRows, N - n0);
   const int rw = S_codes * (int)sizeof(CT) / 4;  // 4-byte words per code row (S_codes % 4 == 0)
@@ -3347,6 +3347,9 @@ __global__ __launch_bounds__(256) void k_materialize_rows(const CT* __restrict__
   for (int k = tid; k < nr * rw; k += 256) ((uint32_t*)s_codes)[k] = src[k];
   block_sync();
   const CT* sc = (const CT*)s_codes;
+  // rb replicas per workgroup share the staged code rows
+  for (int r = blockIdx.y * rb; r < min(R, (int)(blockIdx.y + 1) * rb); r++) {
+  if (cols) block_sync();  // (the previous replica's column pass read the bins tile)
   const int fr = Fr[r];
   const int32_t* sr = sub + (int64_t)r * Fmax;
   const int64_t* lo = lutoff + (int64_t)r * Fmax;
@@ -3363,7 +3366,7 @@ __global__ __launch_bounds__(256) void k_materialize_rows(const CT* __restrict__
     o[q] = v;
     if (cols) ((uint32_t*)(s_codes + (size_t)kMatRows * S_codes * sizeof(CT)))[q] = v;
   }
-  if (!cols) return;
+  if (!cols) continue;
   // the column-major copy (k_partition's gathers): per feature the block's 64 rows are 64
   // consecutive bytes (rows past N: 0)
   block_sync();
@@ -3379,6 +3382,7 @@ __global__ __launch_bounds__(256) void k_materialize_rows(const CT* __restrict__
     }
     ((uint32_t*)(cr + (int64_t)fl * npad))[wd] = v;
   }
+  }
 }
 
 bool launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
@@ -3388,15 +3392,18 @@ bool launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64
   const size_t lds = (size_t)kMatRows * S_codes * code_bytes + (cols ? (size_t)kMatRows * S_out : 0);
   if (S_out % 4 == 0 && (S_codes * code_bytes) % 4 == 0 && lds <= 64 * 1024 && npad % kMatRows == 0 &&
       !getenv("SBAG_MATERIALIZE_ROWWISE")) {
-    const dim3 g((unsigned)((N + kMatRows - 1) / kMatRows), (unsigned)R);
+    // four replicas per workgroup share the staged code rows (C3-sized continuous fit:
+    // 927 / 894 / 890 ms at 1 / 2 / 4; SBAG_MATERIALIZE_RB overrides)
+    const int rb = std::max(1, std::min(R, getenv("SBAG_MATERIALIZE_RB") ? atoi(getenv("SBAG_MATERIALIZE_RB")) : 4));
+    const dim3 g((unsigned)((N + kMatRows - 1) / kMatRows), (unsigned)((R + rb - 1) / rb));
     set_max_lds(code_bytes == 1 ? (const void*)k_materialize_rows<uint8_t> : (const void*)k_materialize_rows<uint16_t>,
                 (int)lds);
     if (code_bytes == 1)
       hipLaunchKernelGGL(k_materialize_rows<uint8_t>, g, dim3(256), lds, st, (const uint8_t*)codes, N, S_codes,
-                         d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad);
+                         d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad, R, rb);
     else
       hipLaunchKernelGGL(k_materialize_rows<uint16_t>, g, dim3(256), lds, st, (const uint16_t*)codes, N,
-                         S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad);
+                         S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad, R, rb);
     return cols != nullptr;
   }
   dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
