@@ -991,12 +991,15 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
     const uint8_t* __restrict__ counts, int64_t N, const int64_t* __restrict__ part_off, int P,
     const int32_t* __restrict__ reps, const uint64_t* __restrict__ part_state,
     const double* __restrict__ frac, uint32_t* __restrict__ rows_out, int64_t cap,
-    uint32_t* __restrict__ nrows, int64_t counts_len) {
+    uint32_t* __restrict__ nrows, int64_t counts_len, int W) {
   constexpr int kGapBuf = 2048;
   __shared__ uint32_t s_incl[64];
   __shared__ uint32_t s_words[64 * 16];
   __shared__ uint32_t s_buf[kGapBuf];
-  const int ri = blockIdx.y, p = blockIdx.x, lane = threadIdx.x;
+  // W waves per (replica, partition): wave w resolves the items of its share of the chunks
+  // (every wave steps the whole gap stream -- cheap scalar work -- and skips the items
+  // before its share, whose count it sums from the counts first)
+  const int ri = blockIdx.y, p = blockIdx.x / W, wv = blockIdx.x % W, lane = threadIdx.x;
   const int r = reps[ri];
   const double lnq = frac[2 * ri + 1];
   uint64_t st = part_state[p];
@@ -1056,13 +1059,40 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
   // kAhead - 1 chunks in flight behind the current one (the wave walks the partition's counts
   // chunk after chunk)
   constexpr int kAhead = 4;
-  int64_t c0 = a0;
+  const int64_t nch = r1 > a0 ? (r1 - a0 + 4095) / 4096 : 0;  // the partition's chunks
+  const int64_t cs = nch * wv / W, ce = nch * (wv + 1) / W;    // this wave's share
+  const int64_t c_end = min(r1, a0 + 4096 * ce);
   uint32_t cw[16];
   // ring of kAhead chunks in flight; the chunk loop is unrolled kAhead times so each slot
   // is a fixed set of registers (moving an in-flight load's destination would wait for it)
   uint4 ring[kAhead][4];
+  // items before the share: the counts of chunks [0, cs), summed through the same ring
+  int64_t c0 = a0;
+  uint32_t before = 0;
+  {
+    const int64_t pre_end = a0 + 4096 * cs;
 #pragma unroll
-  for (int a = 0; a < kAhead; a++) issue(c0 + 4096 * a, ring[a]);
+    for (int a = 0; a < kAhead; a++) issue(c0 + 4096 * a, ring[a]);
+    bool pm = c0 < pre_end;
+    while (pm) {
+#pragma unroll
+      for (int a = 0; a < kAhead; a++) {
+        if (pm) {
+          finish(c0, ring[a], cw);
+          issue(c0 + 4096 * kAhead, ring[a]);
+#pragma unroll
+          for (int k = 0; k < 16; k++) before += bsum(cw[k]);
+          c0 += 4096;
+          pm = c0 < pre_end;
+        }
+      }
+    }
+    // (the ring now holds chunks c0 .. c0 + kAhead - 1 in slot order only when cs is a
+    // multiple of kAhead: reissue them in slot order)
+#pragma unroll
+    for (int a = 0; a < kAhead; a++) issue(c0 + 4096 * a, ring[a]);
+  }
+  for (int o = 32; o > 0; o >>= 1) before += (uint32_t)__shfl_xor((int)before, o);
   // a block of 64 draws: lane j holds taken item j (every lane steps the shared stream and
   // keeps its own draw); bhi = the block's last item
   int64_t next = 0;  // item index of the next draw's gap origin
@@ -1102,7 +1132,7 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
     __builtin_amdgcn_wave_barrier();
     nbuf = 0;
   };
-  int64_t ib = 0;  // items before the chunk
+  int64_t ib = (int64_t)before;  // items before the chunk
   // Chunk-major: each chunk's words and lane prefixes go to LDS, and every lane whose taken
   // item falls in the chunk resolves its row in parallel (the owner lane by a binary
   // search over the prefixes, then its 64 rows' bytes) -- no per-item serial loop
@@ -1184,7 +1214,7 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
     __builtin_amdgcn_wave_barrier();
     ib = iend;
   };
-  bool more = c0 < r1;
+  bool more = c0 < c_end;
   while (more) {
 #pragma unroll
     for (int a = 0; a < kAhead; a++) {
@@ -1193,7 +1223,7 @@ __global__ __launch_bounds__(64) void k_split_sample_gap(
         issue(c0 + 4096 * kAhead, ring[a]);
         process();
         c0 += 4096;
-        more = c0 < r1;
+        more = c0 < c_end;
       }
     }
   }
@@ -1280,8 +1310,11 @@ void launch_split_sample(hipStream_t st, const uint8_t* counts, int64_t N, int64
   // else k_split_sample's lanes walk the partitions (SBAG_SPLIT_SAMPLE_LANES=1 forces them)
   static const bool lanes_env = getenv("SBAG_SPLIT_SAMPLE_LANES") && atoi(getenv("SBAG_SPLIT_SAMPLE_LANES"));
   if (P < 64 && gap_sampling && !lanes_env) {
-    hipLaunchKernelGGL(k_split_sample_gap, dim3((unsigned)P, (unsigned)nrep), dim3(64), 0, st, counts,
-                       N, d_part_off, P, d_reps, d_part_state, d_frac, d_rows, cap, d_nrows, R * N);
+    // waves per (replica, partition): enough for ~32 waves per replica (SBAG_GAP_WAVES)
+    const int W = getenv("SBAG_GAP_WAVES") ? std::max(1, atoi(getenv("SBAG_GAP_WAVES")))
+                                           : std::max(1, std::min(32, 64 / P));
+    hipLaunchKernelGGL(k_split_sample_gap, dim3((unsigned)(P * W), (unsigned)nrep), dim3(64), 0, st, counts,
+                       N, d_part_off, P, d_reps, d_part_state, d_frac, d_rows, cap, d_nrows, R * N, W);
     return;
   }
   const int64_t ng = split_sample_groups(R * N);
