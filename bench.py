@@ -34,7 +34,7 @@ LDS_ATOMIC_PEAK_U32 = 256 * 2.4e9 / 5.97
 PMC_SUMMARIES = {"c3": ["profiles/r04bn/c3/summary.json", "profiles/r04ac/c3/summary.json", "profiles/r04o/c3/summary.json", "profiles/r03y/c3/summary.json", "profiles/r03r/c3/summary.json", "profiles/r03g/c3/summary.json", "profiles/r02g/c3/summary.json", "profiles/r02f/c3/summary.json",
                         "profiles/r02e/c3/summary.json", "profiles/r01g/summary.json"],
                  "c4": ["profiles/r04o/c4/summary.json", "profiles/r02g/c4/summary.json", "profiles/r02f/c4/summary.json"],
-                 "c5": ["profiles/r03y/c5/summary.json", "profiles/r02g/c5/summary.json", "profiles/r02f/c5/summary.json",
+                 "c5": ["profiles/r05a/c5/summary.json", "profiles/r03y/c5/summary.json", "profiles/r02g/c5/summary.json", "profiles/r02f/c5/summary.json",
                         "profiles/r02e/c5/summary.json", "profiles/r01g_c5/summary.json"]}
 
 
@@ -117,6 +117,8 @@ def parse():
     ap.add_argument("--no-nondyadic", action="store_true",
                     help="skip the extra timing of the same fit on real-valued (non-dyadic) labels")
     ap.add_argument("--nondyadic-steps", type=int, default=2)
+    ap.add_argument("--no-continuous", action="store_true",
+                    help="skip the extra timing of the C3 shape on continuous features")
     a = ap.parse_args()
     w = WORKLOADS[a.workload]
     for k in ("rows", "features", "learners", "depth"):
@@ -150,6 +152,56 @@ def cpu_baseline(args):
             "sample": f"{n} rows x {args.features} features, {L} learners, depth {args.depth}, "
                       f"{args.partitions} partitions; oracle/sbag_oracle.c fit only "
                       f"({dt:.1f} s, restatement, not Spark)"}
+
+
+def continuous_data(N, F, seed=20261017):
+    """Continuous features of the C3 shape: ~2400-38000 distinct values per feature (tiles of one
+    rounded-normal block, each shifted), dyadic labels."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    blk = min(N, 1_000_000)
+    B = np.round(rng.standard_normal((blk, F), dtype=np.float32) * 300).astype(np.float64) / 8
+    X = np.empty((N, F))
+    for k in range(0, N, blk):
+        n = min(blk, N - k)
+        X[k:k + n] = B[:n] + (k // blk) / 16.0
+    y = np.round((X[:, 0] * 0.37 - X[:, 1] * 1.3 + X[:, 2] * 0.05) * 16) / 16
+    return X, y
+
+
+def continuous_fit(nat, ctx, N, F, L, depth, bins, part, steps=1):
+    """Fit the continuous-feature dataset (ingested from host fp64 rows, timed apart) with the
+    headline's tree parameters; returns the report dict."""
+    t0 = time.perf_counter()
+    X, y = continuous_data(N, F)
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    del X
+    t_ingest = time.perf_counter() - t0
+
+    def fit(lend):
+        return nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                       learner_end=lend, partition_offsets=part, max_depth=depth, max_bins=bins,
+                       impurity=nat.IMPURITY_VARIANCE)
+
+    fit(2).free()  # warm
+    import torch
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        f = fit(L)
+        tm = f.timing()
+        f.free()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    ds.free()
+    return {"data": "continuous: ~2400-38000 distinct values per feature (host fp64 rows), dyadic "
+                    "labels; per-replica thresholds from each replica's split-finding sample, "
+                    "per-replica bins materialized on the device",
+            "rows": N, "features": F, "learners": L, "steps": steps,
+            "ms_per_step": round(1000.0 * el / steps, 3), "value": round(L * N * steps / el, 1),
+            "unit": "estimator*rows/s", "ingest_s_untimed": round(t_ingest, 2),
+            "breakdown_ms": {k: round(v, 3) for k, v in tm.items() if k.endswith("_ms")}}
 
 
 def nproc():
@@ -345,12 +397,25 @@ def main():
             f.free()
         torch.cuda.synchronize()
         el = time.perf_counter() - t1
+        # per-stage times from one more fit with the learner halves serialized, as for the
+        # headline's breakdown (the overlapped steps stretch each stage by the other half's)
+        prev_ov = os.environ.get("SBAG_OVERLAP")
+        os.environ["SBAG_OVERLAP"] = "0"
+        f = step()
+        tser = f.timing()
+        f.free()
+        if prev_ov is None:
+            os.environ.pop("SBAG_OVERLAP", None)
+        else:
+            os.environ["SBAG_OVERLAP"] = prev_ov
         ds.set_labels(y0)
         nondyadic = {"labels": "1.1 * y + 0.3 (fp64, not dyadic)", "steps": args.nondyadic_steps,
                      "ms_per_step": round(1000.0 * el / args.nondyadic_steps, 3),
                      "value": round(L * N * args.nondyadic_steps / el, 1),
                      "unit": "estimator*rows/s",
-                     "breakdown_ms": {k: round(v, 3) for k, v in tl[-1].items() if k.endswith("_ms")},
+                     "breakdown_ms": {k: round(v, 3) for k, v in tser.items() if k.endswith("_ms")},
+                     "breakdown_def": "one extra fit with the learner halves serialized "
+                                      "(SBAG_OVERLAP=0), HIP events per stage",
                      "exact_fallbacks": int(tl[-1]["exact_fallbacks"]),
                      "engine": "screened fp64 engine: splits chosen from integer histograms of the "
                                "labels' fixed-point image under a rigorous error bound, the chosen "
@@ -358,6 +423,13 @@ def main():
                                "chains with the draws exploded in LDS), "
                                "flagged nodes ('exact_fallbacks') summed exactly on every feature "
                                "(DESIGN.md §4.7)"}
+    # The C3 shape on continuous features: thousands of distinct values per
+    # feature, so every replica is thresholded on its own split-finding sample and its bins are
+    # materialized per replica.  Reported beside the headline; not `value`.
+    continuous = None
+    if args.workload == "c3" and world == 1 and not args.no_continuous:
+        ds.free()
+        continuous = continuous_fit(nat, ctx, N, F, L, args.depth, args.bins, part, steps=1)
     out = {
         "metric": "estimator×rows trained/sec", "value": round(value, 1),
         "unit": "estimator*rows/s", "n_gpus": world, "backend": args.backend if world > 1 else None,
@@ -372,7 +444,7 @@ def main():
                    "classes": args.classes, "replacement": args.replacement,
                    "sample_ratio": args.ratio, "parallelism": f"learner-shard x{world}"},
         "roofline": roofline, "breakdown_ms": breakdown, "sampler_at_nproc_partitions": sampler_p,
-        "nondyadic_labels": nondyadic, "replication": replication,
+        "nondyadic_labels": nondyadic, "continuous_features": continuous, "replication": replication,
         "value_incl_replication": (round(world * L * N * args.steps / (elapsed + replication["seconds"]), 1)
                                    if replication else None),
         "kernel_timing": "roofline and breakdown_ms: one extra fit after the timed steps with "

@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 # kernel durations of each launch alone (the bench's roofline fit does the same)
 export SBAG_OVERLAP=0
-BENCH="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --sampler-partitions 128 $*"
+BENCH="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-continuous --sampler-partitions 128 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- $BENCH > $OUT/trace.log 2>&1 || { echo "trace failed rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- $BENCH > $OUT/fetch.log 2>&1 || { echo "pmc fetch failed rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- $BENCH > $OUT/write.log 2>&1 || { echo "pmc write failed rc=$?"; exit 1; }

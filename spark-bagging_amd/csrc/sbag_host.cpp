@@ -1445,6 +1445,9 @@ static void build_work(const std::vector<std::pair<int64_t, int64_t>>& segs, int
 // fit_range's request to be called again on halves of its learner range: per-replica bins
 // (thresholds that differ across replicas) of all its replicas exceed the device budget
 static constexpr int kSplitRange = -1000;
+// fit_range_impl's integer engine cannot hold the dyadic labels' sums exactly (the packed
+// LDS word or the 2^53 bound on the sum of squares): fit_range refits on the fp64 engine
+static constexpr int kIntRange = -1001;
 
 // device bytes per-replica bins may take: SBAG_BINS_BUDGET_MB, else 40 % of the device
 static double bins_budget(sbag_ctx* c) {
@@ -2492,8 +2495,22 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   return SBAG_OK;
 }
 
+static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out,
+                          const FitExt* ext, bool int_overflow_f64);
+
+// Dyadic labels go to the exact integer engine unless their sums do not fit its words
+// (integer targets of 10^5 at 10^6 rows, e.g. a GBM's first residuals): then the fit is
+// redone on the screened fp64 engine, which sums dyadic labels bit-identically to Spark
+// (SBAG_F64=1 forces it; tests/test_gpu_gbm.py::test_gbm_large_integer_labels).
 static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out,
                      const FitExt* ext) {
+  const int st = fit_range_impl(c, ds, fp, out, ext, false);
+  if (st != kIntRange) return st;
+  return fit_range_impl(c, ds, fp, out, ext, true);
+}
+
+static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out,
+                          const FitExt* ext, bool int_overflow_f64) {
   const LabelSet& lab = ext ? *ext->lab : ds->lab;
   const sbag_tree_params& tp = fp->tree;
   TRY(check_sampler(&fp->sampler));
@@ -2513,7 +2530,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   // fp64 path (f64 mode, sbag_f64s.hip / sbag_f64.hip): Spark's sums depend on their order
   // there. SBAG_F64=1 forces it on dyadic labels too (both paths then agree bit for bit).
   const bool force_f64 = getenv("SBAG_F64") && atoi(getenv("SBAG_F64")) != 0;
-  const bool f64 = !gini && (!lab.label_ok || force_f64);
+  const bool f64 = !gini && (!lab.label_ok || force_f64 || int_overflow_f64);
   if (f64) {
     if (!lab.finite) return fail(SBAG_EINVAL, "labels must be finite");
     if (!lab.label_ok && !lab.approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
@@ -2643,8 +2660,14 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   int64_t flush_limit = (int64_t)1 << 22;
   int cshift = 40;
   for (;; flush_limit /= 2) {
-    if (flush_limit < 256)
+    if (flush_limit < 256) {
+      if (!gini && !f64) {
+        (void)hipEventDestroy(ev_start);
+        (void)hipEventDestroy(ev_stop);
+        return kIntRange;
+      }
       return fail(SBAG_EUNSUPPORTED, "label range too wide for the packed LDS histogram");
+    }
     const double wmax = (double)flush_limit * cmax;
     if (gini) {
       if (wmax < 4294967295.0) break;
@@ -2659,8 +2682,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   // the row-lane histogram builds the word as (c << cshift) + c*(k + K0) with a 32-bit
   // low half: raise cshift to 32 when the count field keeps room for flush_limit * cmax
   if (!gini && cshift < 32 && (double)flush_limit * cmax < 4294967296.0) cshift = 32;
-  if (!gini && !f64 && (double)N * cmax * kabs * kabs >= std::ldexp(1.0, 53))
-    return fail(SBAG_EUNSUPPORTED, "sum of squared labels would exceed 2^53 (not exact in fp64)");
+  if (!gini && !f64 && (double)N * cmax * kabs * kabs >= std::ldexp(1.0, 53)) {
+    (void)hipEventDestroy(ev_start);
+    (void)hipEventDestroy(ev_stop);
+    return kIntRange;
+  }
 
   // ---- per-replica tables
   std::vector<int32_t> h_sub((size_t)R * Fmax, 0), h_Fr(R);
@@ -3236,10 +3262,13 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     }
   }
 
-  // ---- 4. thresholds, LUTs (code -> bin), numSplits per (replica, feature)
+  // ---- 4. thresholds, code cuts (bin(code) = #{j : cut_j <= code}), numSplits per (replica,
+  // feature).  SBAG_BIN_LUT=1: the round-4 per-code LUTs and their gather kernel (A/B only)
   std::vector<std::vector<double>> thr((size_t)R * Fmax);
+  std::vector<std::vector<uint32_t>> cuts((size_t)R * Fmax);
   std::vector<int32_t> h_nbins((size_t)R * Fmax, 1);
-  std::vector<uint8_t> lut((size_t)std::max<int64_t>(vc_total, 1), 0);
+  static const bool bin_lut = getenv("SBAG_BIN_LUT") && atoi(getenv("SBAG_BIN_LUT")) != 0;
+  std::vector<uint8_t> lut(bin_lut ? (size_t)std::max<int64_t>(vc_total, 1) : 0, 0);
   std::vector<int32_t> exact(R, 1);
   bool identity = ds->code_bytes == 1;
   int NB = 1;
@@ -3291,6 +3320,11 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
             const int nt = find_splits(sv, sc.data(), szero, nw[r], nsamp, tp.max_bins, t);
             h_nbins[(size_t)r * Fmax + fl] = nt + 1;
             t_nb[w] = std::max(t_nb[w], nt + 1);
+            const auto& d = ds->dict[g];
+            std::vector<uint32_t>& cu = cuts[(size_t)r * Fmax + fl];
+            cu.resize(t.size());
+            for (size_t j = 0; j < t.size(); j++)
+              cu[j] = (uint32_t)(std::upper_bound(d.begin(), d.end(), t[j]) - d.begin());
           }
           continue;
         }
@@ -3303,12 +3337,24 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
           h_nbins[(size_t)r * Fmax + fl] = nt + 1;
           t_nb[w] = std::max(t_nb[w], nt + 1);
           const auto& d = ds->dict[g];
-          for (size_t k = 0; k < d.size(); k++) {
-            const int b = (int)(std::lower_bound(t.begin(), t.end(), d[k]) - t.begin());  // #{t < v}
-            lut[o + k] = (uint8_t)b;
-            if (b != (int)k) t_id[w] = 0;
+          // cut_j = #{dict values <= t_j}: #{t < d[k]} = #{j : cut_j <= k}
+          std::vector<uint32_t>& cu = cuts[(size_t)r * Fmax + fl];
+          cu.resize(t.size());
+          for (size_t j = 0; j < t.size(); j++)
+            cu[j] = (uint32_t)(std::upper_bound(d.begin(), d.end(), t[j]) - d.begin());
+          // the codes are the bins when bin(k) = k for every code k < d.size()
+          if ((int)d.size() > nt + 1) {
+            t_id[w] = 0;
+          } else {
+            for (size_t j = 0; j + 1 < d.size(); j++)
+              if (cu[j] != (uint32_t)(j + 1)) {
+                t_id[w] = 0;
+                break;
+              }
           }
-          if ((int)d.size() > nt + 1) t_id[w] = 0;
+          if (bin_lut)
+            for (size_t k = 0; k < d.size(); k++)
+              lut[o + k] = (uint8_t)(std::lower_bound(t.begin(), t.end(), d[k]) - t.begin());  // #{t < v}
         }
       }
     };
@@ -3328,22 +3374,42 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     NB = ncmax;  // the codes-as-bins root histogram already has this layout
     root_done = true;
   }
-  // per global feature: is the LUT the same for every replica that uses it?
+  // per global feature: are the cuts (the code -> bin map) the same for every replica that
+  // uses it?
   bool shared = !wide;
+  std::vector<int64_t> first_rf(F, -1);
   if (shared) {
-    std::vector<int64_t> first_off(F, -1);
     for (int r = 0; r < R && shared; r++)
       for (int fl = 0; fl < h_Fr[r] && shared; fl++) {
         const int g = sub[r][fl];
-        const int64_t o = vcoff[(size_t)r * Fmax + fl];
-        if (first_off[g] < 0) {
-          first_off[g] = o;
-        } else if (!std::equal(lut.begin() + o, lut.begin() + o + (int64_t)ds->dict[g].size(),
-                               lut.begin() + first_off[g])) {
+        const int64_t rf = (int64_t)r * Fmax + fl;
+        if (first_rf[g] < 0)
+          first_rf[g] = rf;
+        else if (cuts[rf] != cuts[first_rf[g]])
           shared = false;
-        }
       }
   }
+  // the cut table [rows][Fmax'][ncp] (padded with ~0u) and its groups of 32 per (row, feature)
+  size_t maxcuts = 1;
+  for (const auto& cu : cuts) maxcuts = std::max(maxcuts, cu.size());
+  const int32_t ncp = (int32_t)((maxcuts + 31) / 32 * 32);
+  auto upload_cuts = [&](int rows, int fw, const std::function<const std::vector<uint32_t>*(int, int)>& at,
+                         uint32_t** d_cut, int32_t** d_ng) -> int {
+    std::vector<uint32_t> tab((size_t)rows * fw * ncp, 0xffffffffu);
+    std::vector<int32_t> ngv((size_t)rows * fw, 0);
+    for (int a = 0; a < rows; a++)
+      for (int b = 0; b < fw; b++) {
+        const std::vector<uint32_t>* cu = at(a, b);
+        if (!cu) continue;
+        std::copy(cu->begin(), cu->end(), tab.begin() + ((size_t)a * fw + b) * ncp);
+        ngv[(size_t)a * fw + b] = (int32_t)((cu->size() + 31) / 32);
+      }
+    TRY(ws_typed(c, "cut", tab.size(), d_cut));
+    TRY(ws_typed(c, "cut_ng", ngv.size(), d_ng));
+    TRY(h2d(c, *d_cut, tab.data(), tab.size()));
+    TRY(h2d(c, *d_ng, ngv.data(), ngv.size()));
+    return SBAG_OK;
+  };
   hmark(11);
   // ---- 5. bins
   const uint8_t* d_bins;
@@ -3356,6 +3422,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
   int32_t S;
   std::vector<int16_t> h_pos((size_t)R * Fmax, 0);
   uint8_t* cols_direct = nullptr;  // per-replica column copy written by the materialization
+  int64_t cols_direct_npad = 0;    // (its row padding)
   {
     int h = tm.begin(T_BIN);
     uint8_t* d_lut;
@@ -3364,8 +3431,29 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
       d_bins = (const uint8_t*)ds->d_codes;
       S = ds->S;
       h_pos = h_pos_codes;
-    } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30)) {
+    } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30) && !bin_lut) {
       // one bins matrix in global feature coordinates
+      S = row_stride(F);
+      std::vector<int32_t> gsub(F), gF(1, F);
+      for (int g = 0; g < F; g++) gsub[g] = g;
+      int32_t *d_gsub, *d_gF, *d_ng;
+      uint32_t* d_cut;
+      TRY(ws_typed(c, "gsub", (size_t)F, &d_gsub));
+      TRY(ws_typed(c, "gF", 1, &d_gF));
+      TRY(h2d(c, d_gsub, gsub.data(), (size_t)F));
+      TRY(h2d(c, d_gF, gF.data(), 1));
+      TRY(upload_cuts(1, F, [&](int, int g) { return first_rf[g] < 0 ? nullptr : &cuts[first_rf[g]]; },
+                      &d_cut, &d_ng));
+      uint8_t* d_b;
+      TRY(ws_typed(c, "bins", (size_t)N * S + 256, &d_b));
+      launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_cut, ncp, d_ng,
+                      d_b, S, 0, nullptr, 0, 0, 0);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemsetAsync(d_b + (size_t)N * S, 0, 256, c->stream));  // zero slack
+      d_bins = d_b;
+      h_pos = h_pos_codes;
+    } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30)) {
+      // (SBAG_BIN_LUT=1) the same through per-code LUTs
       S = row_stride(F);
       std::vector<int32_t> gsub(F), gF(1, F);
       for (int g = 0; g < F; g++) gsub[g] = g;
@@ -3409,24 +3497,27 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         return fail(SBAG_EUNSUPPORTED, "per-replica bins of one learner exceed the device budget");
       }
       uint8_t* d_b;
-      TRY(ws_typed(c, "bins", (size_t)R * N * S, &d_b));
-      if (wide) {
-        // bin(code) = #{t < dict[code]} = #{j : cut_j <= code}, cut_j = #{dict values <= t_j}
-        const int nc = std::max(NB - 1, 1);
-        std::vector<uint32_t> cut((size_t)R * Fmax * nc, 0xffffffffu);
-        for (int r = 0; r < R; r++)
-          for (int fl = 0; fl < h_Fr[r]; fl++) {
-            const auto& d = ds->dict[sub[r][fl]];
-            const auto& t = thr[(size_t)r * Fmax + fl];
-            for (size_t j = 0; j < t.size(); j++)
-              cut[((size_t)r * Fmax + fl) * nc + j] =
-                  (uint32_t)(std::upper_bound(d.begin(), d.end(), t[j]) - d.begin());
-          }
+      TRY(ws_typed(c, "bins", (size_t)R * N * S + 256, &d_b));
+      int ncol_r = 1;
+      for (int r = 0; r < R; r++) ncol_r = std::max(ncol_r, (int)h_Fr[r]);
+      const int64_t npad_r = (N + 63) / 64 * 64;
+      if (!bin_lut) {
+        // bin(code) = #{t < dict[code]} = #{j : cut_j <= code} by VALU compares (k_bin_cuts),
+        // the partition's column copy written by the same pass
+        int32_t* d_ng;
         uint32_t* d_cut;
-        TRY(ws_typed(c, "cut", cut.size(), &d_cut));
-        TRY(h2d(c, d_cut, cut.data(), cut.size()));
-        launch_materialize_cut(c->stream, (const uint32_t*)ds->d_codes, N, ds->S, d_sub, d_Fr, Fmax,
-                               R, d_cut, nc, d_b, S);
+        TRY(upload_cuts(R, Fmax, [&](int r, int fl) { return fl < h_Fr[r] ? &cuts[(size_t)r * Fmax + fl] : nullptr; },
+                        &d_cut, &d_ng));
+        uint8_t* d_c;
+        const int64_t npad_c = (N + 127) / 128 * 128;
+        TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_c, &d_c));
+        if (launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R, d_cut, ncp,
+                            d_ng, d_b, S, (int64_t)N * S, d_c, ncol_r, npad_c, (int64_t)ncol_r * npad_c)) {
+          cols_direct = d_c;
+          cols_direct_npad = npad_c;
+        }
+      } else if (wide) {
+        return fail(SBAG_EUNSUPPORTED, "SBAG_BIN_LUT: wide codes have no LUT form");
       } else {
         TRY(ws_typed(c, "lut", lut.size(), &d_lut));
         TRY(ws_typed(c, "lutoff", vcoff.size(), &d_lutoff));
@@ -3434,15 +3525,14 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
         TRY(h2d(c, d_lutoff, vcoff.data(), vcoff.size()));
         // the column copy for k_partition written by the same pass (no transpose re-reading
         // the bins: 46 ms per 43-replica part of a C3-sized continuous fit)
-        int ncol_r = 1;
-        for (int r = 0; r < R; r++) ncol_r = std::max(ncol_r, (int)h_Fr[r]);
-        const int64_t npad_r = (N + 63) / 64 * 64;
         uint8_t* d_c;
         TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_r, &d_c));
         if (launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
                                d_lut, d_lutoff, d_b, S, getenv("SBAG_MATERIALIZE_NO_COLS") ? nullptr : d_c,
-                               ncol_r, npad_r))
+                               ncol_r, npad_r)) {
           cols_direct = d_c;
+          cols_direct_npad = npad_r;
+        }
       }
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemsetAsync(d_b + (size_t)R * N * S, 0, 256, c->stream));  // zero slack
@@ -3456,7 +3546,7 @@ static int fit_range(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, s
     for (int r = 0; r < R; r++)
       for (int fl = 0; fl < h_Fr[r]; fl++) ncol = std::max(ncol, (int)h_pos[(size_t)r * Fmax + fl] + 1);
     const int Rc = bins_rstride ? R : 1;
-    npad = (N + 63) / 64 * 64;
+    npad = cols_direct ? cols_direct_npad : (N + 63) / 64 * 64;
     cols_rstride = bins_rstride ? (int64_t)ncol * npad : 0;
     plane_nw32 = (N + 31) / 32;
     plane_nsp = NB - 1;

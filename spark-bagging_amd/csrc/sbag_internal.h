@@ -226,10 +226,14 @@ void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                             const void* codes, int code_bytes, int32_t S, const int32_t* d_sub,
                             const int32_t* d_Fr, int32_t Fmax, const int64_t* d_vcoff, uint32_t* vc,
                             int lds_words);
-// per-replica bins of u32 codes: bin = #{j < nc : cut[r][fl][j] <= code} (cut padded with ~0u)
-void launch_materialize_cut(hipStream_t st, const uint32_t* codes, int64_t N, int32_t S_codes,
-                            const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
-                            const uint32_t* d_cut, int nc, uint8_t* out, int32_t S_out);
+// per-replica bins out[r][n][fl] = #{j : cut[r][fl][j] <= codes[n][sub[r][fl]]} (cut [R][Fmax][ncp]
+// ascending, padded with ~0u; ng[r][fl] groups of 32 cuts tested), zero past F_r; with cols the
+// column copy cols[r][fl < ncol][npad] is written by the same pass when the kernel can (returns
+// true; else the caller transposes)
+bool launch_bin_cuts(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
+                     const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut,
+                     int32_t ncp, const int32_t* d_ng, uint8_t* out, int32_t S_out, int64_t out_rstride,
+                     uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride);
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
                     unsigned long long* d_wsum, unsigned int* d_cmax, unsigned long long* d_sqsum);

@@ -3488,27 +3488,128 @@ void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S
                      d_sub, d_Fr, Fmax, R, out, S_out);
 }
 
-// Per-replica bins of a wide (u32-coded) dataset: the bin of a code is the number of the
-// feature's thresholds below its value, i.e. of code cuts (#{dict values <= t}) at or
-// below the code; a binary search over the replica's cuts (padded with ~0u).
-__global__ __launch_bounds__(256) void k_materialize_cut(const uint32_t* __restrict__ codes,
-                                                         int64_t N, int32_t S_codes,
-                                                         const int32_t* __restrict__ sub,
-                                                         const int32_t* __restrict__ Fr, int32_t Fmax,
-                                                         const uint32_t* __restrict__ cut, int nc,
-                                                         uint8_t* __restrict__ out, int32_t S_out) {
+// Per-replica bins by counting code cuts: bin(code) = #{j : cut_j <= code}, cut_j = #{dictionary
+// values <= t_j} of the (replica, feature)'s thresholds t_j -- TreePoint.findBin's binary search
+// over the thresholds (#{t < value}).  cut: [R][Fmax][ncp] u32 ascending, padded with 0xffffffff
+// (never <= a code); ng: [R][Fmax] groups of 32 cuts to test.
+//
+// k_bin_cuts (round 5): a workgroup takes kRows rows and rb replicas.  The rows' codes are staged
+// in LDS once (coalesced; pitch S*sizeof(CT) + 4 bytes, so a column read by 64 consecutive rows
+// hits 64 banks), then for each replica every wave bins groups of 4 features for all kRows rows
+// (kRows/64 per lane) with the (replica, feature)'s cuts wave-uniform in SGPRs -- VALU compares,
+// no gathers -- packs a row's 4 bins into a word of an LDS tile [kRows][S_out + 4], and the tile
+// goes out row-major (the histograms' rows) and as k_partition's column copy (4 rows per word).
+// The LUT form it replaces gathered one byte per (row, feature, replica) from multi-MB tables in
+// L2 (955 ms of a C3-sized continuous fit, profiles/r04bf/).
+template <typename CT, int kRows>
+__global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, int64_t N, int32_t S_codes,
+                                                  const int32_t* __restrict__ sub,
+                                                  const int32_t* __restrict__ Fr, int32_t Fmax,
+                                                  const uint32_t* __restrict__ cut, int32_t ncp,
+                                                  const int32_t* __restrict__ ng, uint8_t* __restrict__ out,
+                                                  int32_t S_out, int64_t out_rstride,
+                                                  uint8_t* __restrict__ cols, int32_t ncol, int64_t npad,
+                                                  int64_t cols_rstride, int R, int rb) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  constexpr int kRpl = kRows / 64;  // rows per lane
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pc = S_codes * (int)sizeof(CT) + 4;  // code row pitch in LDS (bytes)
+  const int pb = S_out + 4;                      // bin row pitch
+  uint8_t* sc = smem;
+  uint8_t* sb = smem + (size_t)kRows * pc;
+  const int64_t n0 = (int64_t)blockIdx.x * kRows;
+  const int nr = (int)min<int64_t>(kRows, N - n0);
+  {
+    const int rw = S_codes * (int)sizeof(CT) / 4;  // dwords per code row
+    const uint32_t* src = (const uint32_t*)(codes + n0 * S_codes);
+    for (int k = tid; k < kRows * rw; k += 256) {
+      const int row = k / rw, w = k - row * rw;
+      *(uint32_t*)(sc + row * pc + 4 * w) = row < nr ? src[k] : 0u;
+    }
+  }
+  block_sync();
+  const int ngrp4 = S_out / 4;
+  for (int r = blockIdx.y * rb; r < min(R, (int)(blockIdx.y + 1) * rb); r++) {
+    const int fr = Fr[r];
+    for (int q = wave; q < ngrp4; q += 4) {
+      uint32_t wv[kRpl];
+#pragma unroll
+      for (int i = 0; i < kRpl; i++) wv[i] = 0u;
+      for (int k = 0; k < 4; k++) {
+        const int fl = 4 * q + k;
+        if (fl >= fr) break;
+        const int64_t rf = (int64_t)r * Fmax + fl;
+        const int g = sub[rf];
+        uint32_t cv[kRpl], b[kRpl];
+#pragma unroll
+        for (int i = 0; i < kRpl; i++) {
+          cv[i] = (uint32_t) * (const CT*)(sc + (lane + 64 * i) * pc + g * (int)sizeof(CT));
+          b[i] = 0u;
+        }
+        const uint32_t* cu = cut + rf * ncp;
+        const int ngr = ng[rf];
+        for (int gg = 0; gg < ngr; gg++) {
+#pragma unroll
+          for (int j = 0; j < 32; j++) {
+            const uint32_t cj = cu[32 * gg + j];
+#pragma unroll
+            for (int i = 0; i < kRpl; i++) b[i] += cv[i] >= cj ? 1u : 0u;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kRpl; i++) wv[i] |= b[i] << (8 * k);
+      }
+#pragma unroll
+      for (int i = 0; i < kRpl; i++) *(uint32_t*)(sb + (lane + 64 * i) * pb + 4 * q) = wv[i];
+    }
+    block_sync();
+    {
+      const int wpr = S_out / 4;  // output words per row
+      uint32_t* o = (uint32_t*)(out + (int64_t)r * out_rstride + n0 * S_out);
+      for (int k = tid; k < nr * wpr; k += 256) {
+        const int row = k / wpr, w = k - row * wpr;
+        o[k] = *(const uint32_t*)(sb + row * pb + 4 * w);
+      }
+    }
+    if (cols) {  // per feature the block's kRows rows are kRows consecutive bytes (rows past N: 0)
+      uint8_t* cr = cols + (int64_t)r * cols_rstride + n0;
+      for (int k = tid; k < ncol * (kRows / 4); k += 256) {
+        const int fl = k / (kRows / 4), wd = k - fl * (kRows / 4);
+        uint32_t v = 0;
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+          const int row = 4 * wd + kk;
+          if (row < nr) v |= (uint32_t)sb[row * pb + fl] << (8 * kk);
+        }
+        *(uint32_t*)(cr + (int64_t)fl * npad + 4 * wd) = v;
+      }
+    }
+    block_sync();  // the tile is rewritten by the next replica
+  }
+}
+
+// Fallback for rows too wide for the staged tiles: a thread per row, a binary search over the
+// cuts per feature (no column copy).
+template <typename CT>
+__global__ __launch_bounds__(256) void k_bin_cuts_rows(const CT* __restrict__ codes, int64_t N, int32_t S_codes,
+                                                       const int32_t* __restrict__ sub,
+                                                       const int32_t* __restrict__ Fr, int32_t Fmax,
+                                                       const uint32_t* __restrict__ cut, int32_t ncp,
+                                                       uint8_t* __restrict__ out, int32_t S_out,
+                                                       int64_t out_rstride) {
   const int r = blockIdx.y;
   const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (row >= N) return;
   const int fr = Fr[r];
-  uint8_t* o = out + ((int64_t)r * N + row) * S_out;
-  const uint32_t* cr = codes + row * S_codes;
+  uint8_t* o = out + (int64_t)r * out_rstride + row * S_out;
+  const CT* cr = codes + row * S_codes;
   for (int fl = 0; fl < S_out; fl++) {
     uint32_t b = 0;
     if (fl < fr) {
-      const uint32_t code = cr[sub[(int64_t)r * Fmax + fl]];
-      const uint32_t* cu = cut + ((int64_t)r * Fmax + fl) * nc;
-      int lo = 0, hi = nc;  // first j with cu[j] > code
+      const uint32_t code = (uint32_t)cr[sub[(int64_t)r * Fmax + fl]];
+      const uint32_t* cu = cut + ((int64_t)r * Fmax + fl) * ncp;
+      int lo = 0, hi = ncp;  // first j with cu[j] > code
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (cu[mid] <= code)
@@ -3522,12 +3623,52 @@ __global__ __launch_bounds__(256) void k_materialize_cut(const uint32_t* __restr
   }
 }
 
-void launch_materialize_cut(hipStream_t st, const uint32_t* codes, int64_t N, int32_t S_codes,
-                            const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
-                            const uint32_t* d_cut, int nc, uint8_t* out, int32_t S_out) {
-  dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
-  hipLaunchKernelGGL(k_materialize_cut, grid, dim3(256), 0, st, codes, N, S_codes, d_sub, d_Fr, Fmax,
-                     d_cut, nc, out, S_out);
+template <typename CT>
+static bool launch_bin_cuts_t(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
+                              const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
+                              const int32_t* d_ng, uint8_t* out, int32_t S_out, int64_t out_rstride,
+                              uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride) {
+  // four replicas per workgroup share the staged code rows (SBAG_BIN_RB overrides)
+  static const int rb_env = getenv("SBAG_BIN_RB") ? atoi(getenv("SBAG_BIN_RB")) : 4;
+  const int rb = std::max(1, std::min(R, rb_env));
+  auto lds_for = [&](int rows) {
+    return (size_t)rows * (S_codes * sizeof(CT) + 4) + (size_t)rows * (S_out + 4);
+  };
+  const bool fits128 = sizeof(CT) <= 2 && lds_for(128) <= 64 * 1024;
+  const bool fits64 = lds_for(64) <= 80 * 1024;
+  if ((fits128 || fits64) && S_out % 4 == 0 && (S_codes * sizeof(CT)) % 4 == 0 && npad % 128 == 0 &&
+      !getenv("SBAG_BIN_ROWWISE")) {
+    if (fits128) {
+      const dim3 g((unsigned)((N + 127) / 128), (unsigned)((R + rb - 1) / rb));
+      set_max_lds((const void*)k_bin_cuts<CT, 128>, (int)lds_for(128));
+      hipLaunchKernelGGL((k_bin_cuts<CT, 128>), g, dim3(256), lds_for(128), st, codes, N, S_codes, d_sub, d_Fr,
+                         Fmax, d_cut, ncp, d_ng, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb);
+    } else {
+      const dim3 g((unsigned)((N + 63) / 64), (unsigned)((R + rb - 1) / rb));
+      set_max_lds((const void*)k_bin_cuts<CT, 64>, (int)lds_for(64));
+      hipLaunchKernelGGL((k_bin_cuts<CT, 64>), g, dim3(256), lds_for(64), st, codes, N, S_codes, d_sub, d_Fr,
+                         Fmax, d_cut, ncp, d_ng, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb);
+    }
+    return cols != nullptr;
+  }
+  const dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
+  hipLaunchKernelGGL(k_bin_cuts_rows<CT>, grid, dim3(256), 0, st, codes, N, S_codes, d_sub, d_Fr, Fmax, d_cut,
+                     ncp, out, S_out, out_rstride);
+  return false;
+}
+
+bool launch_bin_cuts(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
+                     const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut,
+                     int32_t ncp, const int32_t* d_ng, uint8_t* out, int32_t S_out, int64_t out_rstride,
+                     uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride) {
+  if (code_bytes == 1)
+    return launch_bin_cuts_t(st, (const uint8_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_ng, out,
+                             S_out, out_rstride, cols, ncol, npad, cols_rstride);
+  if (code_bytes == 2)
+    return launch_bin_cuts_t(st, (const uint16_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_ng, out,
+                             S_out, out_rstride, cols, ncol, npad, cols_rstride);
+  return launch_bin_cuts_t(st, (const uint32_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_ng, out,
+                           S_out, out_rstride, cols, ncol, npad, cols_rstride);
 }
 
 // Value counts with global atomics (u16 codes / dictionaries too large for LDS)

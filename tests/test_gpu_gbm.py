@@ -84,6 +84,41 @@ def test_booster_sampled_split_finding_partitions(ctx):
     _booster_vs_oracle(ctx, X, lab, counts, np.arange(f, dtype=np.int32), depth=7, part=part)
 
 
+def test_booster_large_integer_labels(ctx):
+    """Integer labels of ~1e5 at 1.2e5 rows: their sums of squares pass 2^53, so the exact
+    integer engine cannot hold them and the fit is redone on the screened fp64 engine
+    (sbag_host.cpp fit_range) -- a GBM's first booster sees the raw
+    labels.  Bit-exact against the oracle; before, SBAG_EUNSUPPORTED."""
+    rng = np.random.default_rng(17)
+    n, f = 120_000, 6
+    X = np.round(rng.normal(size=(n, f)) * 3) / 3
+    lab = np.round(rng.normal(size=n) * 4e4 + 1e5 + X[:, 1] * 2e4)
+    assert n * 8 * np.abs(lab).max() ** 2 > 2.0 ** 53
+    counts = oracle.bag(True, 1.0, 0, 1, 21, [0, n], n)[0]
+    _booster_vs_oracle(ctx, X, lab, counts, np.arange(f, dtype=np.int32), depth=6)
+
+
+def test_bagging_large_integer_labels(ctx):
+    """The same fallback for a bagging regressor (several replicas, P = 2)."""
+    rng = np.random.default_rng(23)
+    n, f = 100_000, 5
+    X = np.round(rng.normal(size=(n, f)) * 2) / 2
+    y = np.round(rng.normal(size=n) * 1e5 + 3e5 * (X[:, 0] > 0))
+    part = [0, 40_000, n]
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        forest = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=77, learner_begin=0,
+                         learner_end=3, max_depth=5, max_bins=32, partition_offsets=part,
+                         impurity=nat.IMPURITY_VARIANCE)
+    finally:
+        ds.free()
+    counts = oracle.bag(True, 1.0, 0, 3, 77, part, n)
+    subs = [np.arange(f, dtype=np.int32)] * 3
+    orf = oracle.fit(X, y, counts, subs, max_depth=5, max_bins=32, part=part)
+    for t in range(3):
+        assert_tree_equal(forest, t, orf, t)
+
+
 @pytest.mark.parametrize("loss,lr,repl,ratio,sratio", [
     ("squared", 0.1, True, 1.0, 0.7),
     ("squared", 1.0, False, 0.8, 1.0),
