@@ -10,6 +10,7 @@
 #     c3 | c4 | c5            bench.py --workload <w>, short (env passes through, e.g. SBAG_*)
 #     cont                    scripts/bench_continuous.py (C3 shape on continuous features)
 #     gbm                     scripts/bench_gbm.py
+#     f64probe                scripts/f64_probe.py, serialized, per-level stage times
 #     trace_c3 | trace_c5 | trace_c4   rocprofv3 --kernel-trace --stats of the bench command
 #     prof_c3 | prof_c5 | prof_c4      trace + separate PMC passes (scripts/profile.sh)
 #     fuzz[=<minutes>]        scripts/fuzz_parity.py; fuzzb: --booster; fuzzbig: --big
@@ -61,9 +62,21 @@ run_step() {
     cont)
       timeout -k 10 400 python3 -u scripts/bench_continuous.py > "$OUT/cont$tag.log" 2>&1
       rc=$?; tail -4 "$OUT/cont$tag.log"; return $rc ;;
+    f64probe)
+      SBAG_OVERLAP=0 SBAG_LEVEL_TRACE=1 timeout -k 10 300 python3 -u scripts/f64_probe.py > "$OUT/f64probe$tag.log" 2>&1
+      rc=$?; grep "f64 level" "$OUT/f64probe$tag.log" | tail -9; tail -1 "$OUT/f64probe$tag.log" | cut -c1-700; return $rc ;;
     gbm)
       timeout -k 10 400 python3 -u scripts/bench_gbm.py > "$OUT/gbm$tag.log" 2>&1
       rc=$?; tail -4 "$OUT/gbm$tag.log"; return $rc ;;
+    trace_f64)
+      local d="$OUT/trace_f64$tag"
+      mkdir -p "$d"
+      SBAG_OVERLAP=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o trace -- \
+        python3 scripts/f64_probe.py > "$d/trace.log" 2>&1
+      rc=$?; [ $rc -ne 0 ] && { tail -20 "$d/trace.log"; return $rc; }
+      tail -1 "$d/trace.log" | cut -c1-400
+      f=$(find "$d" -name "*kernel_stats.csv" | head -1); head -20 "$f" | cut -d, -f1-5 | cut -c1-160
+      return 0 ;;
     trace_cont)
       local d="$OUT/trace_cont$tag"
       mkdir -p "$d"
@@ -96,7 +109,10 @@ run_step() {
       name=${spec%%=*}; spec=${spec#*=}; vals=${spec%%:*}; inner=${spec#*:}
       for v in ${vals//,/ }; do
         echo "== $name=$v $inner"
-        env "$name=$v" bash -c "$(declare -f summ run_step); OUT='$OUT' RUN='$RUN'; run_step '$inner' '_${name}_$v'" || return $?
+        # (a value may carry more settings: ab:A=1,0+B=1:step runs A=1, then A=0 B=1)
+        local first=${v%%+*} more="" tagv=${v//[+=]/_}
+        [ "$v" != "$first" ] && more=${v#*+}
+        env "$name=$first" ${more//+/ } bash -c "$(declare -f summ run_step); OUT='$OUT' RUN='$RUN'; run_step '$inner' '_${name}_$tagv'" || return $?
       done
       return 0 ;;
     *) echo "unknown step $st"; return 2 ;;

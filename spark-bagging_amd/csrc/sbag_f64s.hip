@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
   const F64Task t = A.tasks[task];
   __shared__ int64_t s_start[257];
   __shared__ int64_t s_wave[4];
-  if (t.kbase >= 0) {
+  if (t.kbase >= 0 && !A.fused) {
     int64_t tot = 0;
     if (tid < NB)
       for (int64_t p = t.piece0; p < t.piece1; p++) tot += A.pcnt[p * NB + tid];
@@ -356,7 +356,8 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const F64TPiece pc = A.pieces[pi];
   const F64Task t = A.tasks[pc.task];
   const int NB = A.NB;
-  const bool chain = __builtin_amdgcn_readfirstlane((int)(t.kbase >= 0)) != 0;  // (uniform: SGPR resources)
+  // (uniform: SGPR resources; fused: k_fb_bchain sums the buckets, this only routes)
+  const bool chain = __builtin_amdgcn_readfirstlane((int)(t.kbase >= 0 && !A.fused)) != 0;
   int64_t* sb = s_base[wv];
   for (int b = lane; b < NB; b += 64) sb[b] = chain ? A.pbase[pi * NB + b] : 0;
   uint32_t* scnt = s_scnt[kStage ? wv : 0];
@@ -899,6 +900,211 @@ __global__ __launch_bounds__(64) void k_fb_chain64(F64BucketArgs A, int nchain) 
   }
 }
 
+// ---------------------------------------------------------------- fused bucket chains
+// Bucketing and chains fused (round 5, SBAG_F64_FUSED=1; the default stays the global buckets of
+// k_fb_scatter + k_fb_chainx, which measured faster: 260 vs 294 ms per serialized C3-shape fit,
+// gpurun_out/r05h/ -- the root's few long tasks expose each block's latency).  One workgroup per chain task walks the task's entries
+// (ent_in / ey_in [t.a, t.b): the node's rows in row order, bins from k_fb_count's ebin) in
+// blocks of kE.  A block is ordered by bin in LDS, stably: each 64-entry round ranks its
+// entries among the same bin's with ballots over the bin bits and counts their draws with
+// ballots over the count bits, a scan over (bin, round) places every round's draws, and each
+// entry's label is written c times (a row drawn c times is c consecutive rows,
+// sql/bfunctions.scala:42-44).  Then thread b adds bin b's records in order -- sum += y,
+// sumSq += y * y (instanceWeight 1.0) -- its sums carried across the blocks: Spark's
+// row-order cell sums (DTStatsAggregator.update) bit for bit, with no bucket written to or
+// read from HBM (the global buckets moved ~176 GB per C3-shape fit, profiles/r04am/).  A bin's
+// records are padded to a multiple of 8 with -0.0 (sum += -0.0 and sumSq += +0.0 leave both
+// unchanged: sumSq >= +0.0), so the serial loop takes 8 records a step.  The round bookkeeping
+// is double-buffered, so the next block's ranking overlaps the bin threads' adds: three
+// barriers per block.  A block whose records exceed kD goes through several windows.
+template <int kE, bool kCarried>
+__global__ __launch_bounds__(256) void k_fb_bchain(F64BucketArgs A, int nchain, int nbits, int cbits) {
+  constexpr int kR = kE / 64;   // rounds
+  constexpr int kRW = kR / 4;   // rounds per wave
+  constexpr int kD = kE * 5 / 2;  // records per window
+  const int task = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int NB = A.NB;
+  extern __shared__ __align__(16) uint8_t smem[];
+  double* sd = (double*)smem;                                // [kD] records
+  uint32_t* src = (uint32_t*)(smem + (size_t)kD * 8);        // [2][kR][NB] round draws -> slots
+  uint32_t* sbs = src + 2 * kR * NB;                         // [NB + 1] bin starts (padded)
+  uint32_t* sbn = sbs + NB + 1;                              // [NB] bin draws
+  __shared__ int64_t swave[4];  // (static: a pointer rebuilt from an integer is a flat pointer,
+                                //  whose accesses wait for every global load in flight)
+  const F64Task t = A.tasks[task];
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t above = ~(lt | (1ull << lane));
+  constexpr bool carried = kCarried;  // the labels travel with the entries (ey_in), else y[row]
+  for (int k = tid; k < 2 * kR * NB; k += 256) src[k] = 0u;
+  double s1 = 0.0, s2 = 0.0;  // thread b < NB: bin b's sums, carried across the blocks
+  uint64_t cnt = 0;
+  const int64_t n = t.b - t.a;
+  // (every load unconditional, past the task's end at its last entry -- masked at use: a
+  // select on a loaded value, or a branch around a load, makes the compiler wait for it)
+  auto load = [&](int64_t blk, uint64_t (&e)[kRW], double (&y)[kRW], uint32_t (&bn)[kRW]) {
+#pragma unroll
+    for (int u = 0; u < kRW; u++) {
+      const int64_t ic = min(blk + 64 * (kRW * wave + u) + lane, n - 1);  // round kRW wave + u
+      e[u] = A.ent_in[t.a + ic];
+      y[u] = carried ? A.ey_in[t.a + ic] : 0.0;
+      bn[u] = (uint32_t)A.ebin[t.ebase + ic];
+    }
+    if (!carried)
+#pragma unroll
+      for (int u = 0; u < kRW; u++) y[u] = A.y[(uint32_t)e[u]];
+  };
+  // two blocks' loads in flight ahead of the one being ordered (a task's blocks follow each
+  // other; with one workgroup per CU -- the root's few long tasks -- a block's work is shorter
+  // than the memory latency)
+  uint64_t eA[kRW], eB[kRW], eC[kRW];
+  double yA[kRW], yB[kRW], yC[kRW];
+  uint32_t bA[kRW], bB[kRW], bC[kRW];
+  if (n > 0) {
+    load(0, eA, yA, bA);
+    load(kE, eB, yB, bB);
+  }
+  block_sync();
+  int buf = 0;
+  // the block body (fixed registers per block: rotating buffers whose loads are in flight
+  // would make the compiler wait for them)
+  auto body = [&](int64_t blk, const uint64_t (&eX)[kRW], const double (&yX)[kRW], const uint32_t (&bX)[kRW]) {
+    uint32_t* rc = src + buf * kR * NB;
+    // A: ranks among the round's entries of the same bin (in draws), the round's draws per bin
+    uint32_t pre[kRW], cc[kRW];
+#pragma unroll
+    for (int u = 0; u < kRW; u++) {
+      const int q = kRW * wave + u;
+      const bool valid = blk + 64 * q + lane < n;
+      const uint32_t c = valid ? (uint32_t)(eX[u] >> 32) & 0xffu : 0u;  // past the end: no draws
+      cc[u] = c;
+      const uint32_t bin = bX[u];
+      uint64_t eq = __ballot(c != 0u);
+      for (int k = 0; k < nbits; k++) {
+        const bool bit = (bin >> k) & 1u;
+        const uint64_t m = __ballot(bit);
+        eq &= bit ? m : ~m;
+      }
+      uint32_t p = 0, tot = 0;
+      for (int k = 0; k < cbits; k++) {
+        const uint64_t m = __ballot((c >> k) & 1u) & eq;
+        p += (uint32_t)__popcll(m & lt) << k;
+        tot += (uint32_t)__popcll(m) << k;
+      }
+      pre[u] = p;
+      if (c != 0u && (eq & above) == 0ull) rc[q * NB + bin] = tot;  // the bin's last lane
+    }
+    block_sync();
+    // B: per bin the rounds' offsets, the padded bin sizes, their scan over the bins
+    uint32_t bd = 0, bp = 0;
+    uint32_t ro[kR];  // (all reads first: a read after a write of the same array waits for it)
+    if (tid < NB) {
+#pragma unroll
+      for (int q = 0; q < kR; q++) ro[q] = rc[q * NB + tid];
+#pragma unroll
+      for (int q = 0; q < kR; q++) {
+        const uint32_t v = ro[q];
+        ro[q] = bd;
+        bd += v;
+      }
+      bp = (bd + 7u) & ~7u;
+    }
+    uint32_t ex, all;
+    if (NB <= 64) {
+      if (wave == 0) {
+        uint32_t incl = bp;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t v = __shfl_up(incl, o);
+          if (lane >= o) incl += v;
+        }
+        ex = incl - bp;
+        all = __shfl(incl, 63);
+      }
+    } else {
+      int64_t a64;
+      ex = (uint32_t)scan256((int64_t)bp, swave, &a64);
+      all = (uint32_t)a64;
+    }
+    if (tid < NB) {
+      sbs[tid] = ex;
+      sbn[tid] = bd;
+#pragma unroll
+      for (int q = 0; q < kR; q++) rc[q * NB + tid] = ro[q] + ex;
+      if (tid == 0) sbs[NB] = all;
+    }
+    block_sync();
+    const uint32_t total = sbs[NB];
+    for (uint32_t wnd = 0; wnd < total; wnd += kD) {
+      // C: the window's records -- every entry's draws, each bin's padding
+#pragma unroll
+      for (int u = 0; u < kRW; u++) {
+        if (cc[u] == 0u) continue;
+        const uint32_t at = rc[(kRW * wave + u) * NB + bX[u]] + pre[u];
+        for (uint32_t k = 0; k < cc[u]; k++) {
+          const uint32_t x = at + k;
+          if (x - wnd < (uint32_t)kD) sd[x - wnd] = yX[u];
+        }
+      }
+      if (tid < NB) {
+        const uint32_t b0 = sbs[tid] + sbn[tid], b1 = sbs[tid + 1];
+        for (uint32_t x = max(b0, wnd); x < min(b1, wnd + (uint32_t)kD); x++) sd[x - wnd] = -0.0;
+      }
+      block_sync();
+      // D: thread b adds bin b's records of the window, 8 a step, the next 8 read ahead
+      if (tid < NB) {
+        const uint32_t lo = max(sbs[tid], wnd), hi = min(sbs[tid + 1], wnd + (uint32_t)kD);
+        const int m = (int)(hi > lo ? hi - lo : 0u);  // a multiple of 8 (bins and windows are)
+        const double* p = sd + (lo - wnd);
+        double a[8];
+        if (m > 0)
+#pragma unroll
+          for (int k = 0; k < 8; k++) a[k] = p[k];
+        for (int x = 0; x < m; x += 8) {
+          double b8[8];
+          if (x + 8 < m)
+#pragma unroll
+            for (int k = 0; k < 8; k++) b8[k] = p[x + 8 + k];
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            s1 += a[k];          // instanceWeight * label
+            s2 += a[k] * a[k];   // instanceWeight * label * label
+          }
+#pragma unroll
+          for (int k = 0; k < 8; k++) a[k] = b8[k];
+        }
+        if (wnd + kD >= total) {  // the block's last window: its rounds' slots are spent
+          cnt += sbn[tid];
+          for (int q = 0; q < kR; q++) rc[q * NB + tid] = 0u;
+        }
+      }
+      if (wnd + kD < total) block_sync();  // (more windows: the records are rewritten)
+    }
+    buf ^= 1;
+  };
+  for (int64_t blk = 0; blk < n;) {
+    load(blk + 2 * kE, eC, yC, bC);
+    body(blk, eA, yA, bA);
+    if ((blk += kE) >= n) break;
+    load(blk + 2 * kE, eA, yA, bA);
+    body(blk, eB, yB, bB);
+    if ((blk += kE) >= n) break;
+    load(blk + 2 * kE, eB, yB, bB);
+    body(blk, eC, yC, bC);
+    blk += kE;
+  }
+  if (task < nchain && tid < NB) {
+    double* o = A.chist + ((int64_t)task * NB + tid) * 3;
+    o[0] = (double)cnt;  // count += 1.0 per draw (an integer sum: order-free)
+    o[1] = s1;
+    o[2] = s2;
+  }
+}
+
+static size_t bchain_lds(int kE, int NB) {
+  return (size_t)kE * 5 / 2 * 8 + ((size_t)2 * (kE / 64) * NB + 2 * NB + 1) * 4;
+}
+
 // ---------------------------------------------------------------- label column
 // analyze_labels (sbag_host.cpp) on the device: per label, finite / integral and the
 // smallest s with y 2^s integral (from the exponent and the significand's trailing zeros),
@@ -1004,6 +1210,28 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
     hipLaunchKernelGGL(scatter_stage ? k_fb_scatter<true> : k_fb_scatter<false>,
                        dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
                        npieces, nbits);
+  if (a.fused) {  // the chain tasks' sums by k_fb_bchain (no buckets: k_fb_scatter routed only)
+    int cbits = 1;
+    while (cbits < 8 && (a.cmax >> cbits) != 0) cbits++;
+    // 1024-entry blocks: ~25 KB of LDS at 32 bins, six workgroups per CU (SBAG_F64_BCHAIN_E=512|2048)
+    static const int be = getenv("SBAG_F64_BCHAIN_E") ? atoi(getenv("SBAG_F64_BCHAIN_E")) : 1024;
+    if (nchain > 0 && a.NB <= 256) {
+      const bool cy = a.ey_in != nullptr;
+      auto go = [&](const void* fn, int e) {
+        const size_t lds = bchain_lds(e, a.NB);
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        void* args[] = {(void*)&a, (void*)&nchain, (void*)&nbits, (void*)&cbits};
+        (void)hipLaunchKernel(fn, dim3((unsigned)nchain), dim3(256), args, lds, st);
+      };
+      if (be == 512)
+        go(cy ? (const void*)k_fb_bchain<512, true> : (const void*)k_fb_bchain<512, false>, 512);
+      else if (be == 2048)
+        go(cy ? (const void*)k_fb_bchain<2048, true> : (const void*)k_fb_bchain<2048, false>, 2048);
+      else
+        go(cy ? (const void*)k_fb_bchain<1024, true> : (const void*)k_fb_bchain<1024, false>, 1024);
+    }
+    return;
+  }
   const int64_t lanes = (int64_t)nchain * a.NB;
   // k_fb_chainx (the default; SBAG_F64_CHAIN_X=0: the per-entry k_fb_chain): the serial
   // lanes are latency-bound, so a wave takes as few chains as keep >= 2048 waves (two per

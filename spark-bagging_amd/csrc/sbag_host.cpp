@@ -1997,8 +1997,14 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       TRY(ws_typed(c, "fb_kboff", (size_t)nt * (NB + 1), &d_kboff));
       uint8_t* d_ebin;
       TRY(ws_typed(c, "fb_ebin", (size_t)std::max<int64_t>(1, ebase), &d_ebin));
-      TRY(ws_typed(c, "fb_bky", (size_t)std::max<int64_t>(1, nlabels), &d_bky));
-      TRY(ws_typed(c, "fb_bkc", (size_t)std::max<int64_t>(1, nlabels), &d_bkc));
+      // SBAG_F64_FUSED=1: bucketing fused into the chains in LDS (k_fb_bchain, no bucket space);
+      // measured slower than the global buckets + k_fb_chainx on the C3 shape (serialized fit
+      // 294 vs 260 ms, gpurun_out/r05h/: a task's blocks are ordered one after another by one
+      // workgroup, so the root's 256 long tasks expose each block's latency), kept for A/B.
+      // (read per call: the tests switch it between fits)
+      const bool fused = getenv("SBAG_F64_FUSED") && atoi(getenv("SBAG_F64_FUSED")) != 0 && NB <= 256;
+      TRY(ws_typed(c, "fb_bky", (size_t)std::max<int64_t>(1, fused ? 1 : nlabels), &d_bky));
+      TRY(ws_typed(c, "fb_bkc", (size_t)std::max<int64_t>(1, fused ? 1 : nlabels), &d_bkc));
       TRY(h2d(c, d_tk, tk.data(), (size_t)nt));
       TRY(h2d(c, d_pc, pcs.data(), pcs.size()));
       F64BucketArgs ba{};
@@ -2025,6 +2031,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.y = d_y64;
       ba.chist = chist;
       ba.cmax = (int32_t)G.cmax;
+      ba.fused = fused ? 1 : 0;
       // XCD-aware dispatch of k_fb_count (workgroup w runs on XCD w mod 8, each with its own
       // L2): a piece goes to the XCD of its position within its node's entries, a proxy of
       // its rows' slice of [0, N), so each XCD's bin gathers stay in one eighth of a column
@@ -3389,25 +3396,27 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
           shared = false;
       }
   }
-  // the cut table [rows][Fmax'][ncp] (padded with ~0u) and its groups of 32 per (row, feature)
+  // the cut table [rows][Fmax'][ncp] (padded with ~0u, ncp a power of two >= 32; k_bin_cuts
+  // binary-searches it)
   size_t maxcuts = 1;
   for (const auto& cu : cuts) maxcuts = std::max(maxcuts, cu.size());
-  const int32_t ncp = (int32_t)((maxcuts + 31) / 32 * 32);
+  int32_t ncp = 32;
+  while ((size_t)ncp < maxcuts + 1) ncp *= 2;
   auto upload_cuts = [&](int rows, int fw, const std::function<const std::vector<uint32_t>*(int, int)>& at,
-                         uint32_t** d_cut, int32_t** d_ng) -> int {
+                         uint32_t** d_cut) -> int {
     std::vector<uint32_t> tab((size_t)rows * fw * ncp, 0xffffffffu);
-    std::vector<int32_t> ngv((size_t)rows * fw, 0);
     for (int a = 0; a < rows; a++)
       for (int b = 0; b < fw; b++) {
         const std::vector<uint32_t>* cu = at(a, b);
         if (!cu) continue;
+        // (a threshold is a midpoint of two values, so at least the smallest value lies below
+        // it: every cut >= 1, which the kernel's keys cut - 1 rely on)
+        for (uint32_t v : *cu)
+          if (v == 0) return fail(SBAG_EDEVICE, "internal: a threshold below every value");
         std::copy(cu->begin(), cu->end(), tab.begin() + ((size_t)a * fw + b) * ncp);
-        ngv[(size_t)a * fw + b] = (int32_t)((cu->size() + 31) / 32);
       }
     TRY(ws_typed(c, "cut", tab.size(), d_cut));
-    TRY(ws_typed(c, "cut_ng", ngv.size(), d_ng));
     TRY(h2d(c, *d_cut, tab.data(), tab.size()));
-    TRY(h2d(c, *d_ng, ngv.data(), ngv.size()));
     return SBAG_OK;
   };
   hmark(11);
@@ -3436,17 +3445,17 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       S = row_stride(F);
       std::vector<int32_t> gsub(F), gF(1, F);
       for (int g = 0; g < F; g++) gsub[g] = g;
-      int32_t *d_gsub, *d_gF, *d_ng;
+      int32_t *d_gsub, *d_gF;
       uint32_t* d_cut;
       TRY(ws_typed(c, "gsub", (size_t)F, &d_gsub));
       TRY(ws_typed(c, "gF", 1, &d_gF));
       TRY(h2d(c, d_gsub, gsub.data(), (size_t)F));
       TRY(h2d(c, d_gF, gF.data(), 1));
       TRY(upload_cuts(1, F, [&](int, int g) { return first_rf[g] < 0 ? nullptr : &cuts[first_rf[g]]; },
-                      &d_cut, &d_ng));
+                      &d_cut));
       uint8_t* d_b;
       TRY(ws_typed(c, "bins", (size_t)N * S + 256, &d_b));
-      launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_cut, ncp, d_ng,
+      launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_cut, ncp,
                       d_b, S, 0, nullptr, 0, 0, 0);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemsetAsync(d_b + (size_t)N * S, 0, 256, c->stream));  // zero slack
@@ -3504,15 +3513,14 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       if (!bin_lut) {
         // bin(code) = #{t < dict[code]} = #{j : cut_j <= code} by VALU compares (k_bin_cuts),
         // the partition's column copy written by the same pass
-        int32_t* d_ng;
         uint32_t* d_cut;
         TRY(upload_cuts(R, Fmax, [&](int r, int fl) { return fl < h_Fr[r] ? &cuts[(size_t)r * Fmax + fl] : nullptr; },
-                        &d_cut, &d_ng));
+                        &d_cut));
         uint8_t* d_c;
         const int64_t npad_c = (N + 127) / 128 * 128;
         TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_c, &d_c));
         if (launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R, d_cut, ncp,
-                            d_ng, d_b, S, (int64_t)N * S, d_c, ncol_r, npad_c, (int64_t)ncol_r * npad_c)) {
+                            d_b, S, (int64_t)N * S, d_c, ncol_r, npad_c, (int64_t)ncol_r * npad_c)) {
           cols_direct = d_c;
           cols_direct_npad = npad_c;
         }

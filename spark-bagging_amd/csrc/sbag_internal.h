@@ -227,13 +227,13 @@ void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                             const int32_t* d_Fr, int32_t Fmax, const int64_t* d_vcoff, uint32_t* vc,
                             int lds_words);
 // per-replica bins out[r][n][fl] = #{j : cut[r][fl][j] <= codes[n][sub[r][fl]]} (cut [R][Fmax][ncp]
-// ascending, padded with ~0u; ng[r][fl] groups of 32 cuts tested), zero past F_r; with cols the
+// ascending, every cut >= 1, padded with ~0u; ncp a power of two), zero past F_r; with cols the
 // column copy cols[r][fl < ncol][npad] is written by the same pass when the kernel can (returns
 // true; else the caller transposes)
 bool launch_bin_cuts(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
                      const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut,
-                     int32_t ncp, const int32_t* d_ng, uint8_t* out, int32_t S_out, int64_t out_rstride,
-                     uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride);
+                     int32_t ncp, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
+                     int64_t npad, int64_t cols_rstride);
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
                     unsigned long long* d_wsum, unsigned int* d_cmax, unsigned long long* d_sqsum);
@@ -447,7 +447,8 @@ struct F64BucketArgs {
   const double* ey_in;      // the labels of ent_in's entries (same positions)
   double* ey_out;           // the labels of ent_out's entries
   double* chist;            // [task][NB][3] count, sum, sumSq in Spark's row order
-  int32_t cmax, pad;        // largest draw count of an entry (1: no count loop)
+  int32_t cmax;             // largest draw count of an entry (1: no count loop)
+  int32_t fused;            // k_fb_bchain sums the chain tasks (no global buckets)
   const int32_t* porder;    // k_fb_count's piece of each workgroup (null: in order)
 };
 // ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]

@@ -3493,99 +3493,143 @@ void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S
 // over the thresholds (#{t < value}).  cut: [R][Fmax][ncp] u32 ascending, padded with 0xffffffff
 // (never <= a code); ng: [R][Fmax] groups of 32 cuts to test.
 //
-// k_bin_cuts (round 5): a workgroup takes kRows rows and rb replicas.  The rows' codes are staged
-// in LDS once (coalesced; pitch S*sizeof(CT) + 4 bytes, so a column read by 64 consecutive rows
-// hits 64 banks), then for each replica every wave bins groups of 4 features for all kRows rows
-// (kRows/64 per lane) with the (replica, feature)'s cuts wave-uniform in SGPRs -- VALU compares,
-// no gathers -- packs a row's 4 bins into a word of an LDS tile [kRows][S_out + 4], and the tile
-// goes out row-major (the histograms' rows) and as k_partition's column copy (4 rows per word).
-// The LUT form it replaces gathered one byte per (row, feature, replica) from multi-MB tables in
-// L2 (955 ms of a C3-sized continuous fit, profiles/r04bf/).
-template <typename CT, int kRows>
+// k_bin_cuts (round 5): a workgroup takes rb replicas and a chunk of row blocks.  The rb
+// replicas' cuts go to LDS once, as keys cut - 1 (u16 for u8/u16 codes: a cut is at most the
+// dictionary size, and a key 0xffff -- also the padding -- is never below a code; u32 for wide
+// codes), and the bin of a code is a branch-free binary search over the (replica, feature)'s
+// ncp keys: log2(ncp) steps of one LDS read (at most 16 distinct words of 32 consecutive banks
+// per wave: no conflicts), a compare and a select.  Per row block of kRows rows the codes are
+// staged in LDS (pitch S*sizeof(CT) + 4 bytes: a column read by 64 consecutive rows hits 64
+// banks); for each replica every wave bins groups of 4 features for all the rows (kRows/64 per
+// lane), packs a row's 4 bins into a word of an LDS tile [kRows][S_out + 4], and the tile goes
+// out row-major (the histograms' rows) and as k_partition's column copy (4 rows per word).
+// The LUT form it replaces gathered one byte per (row, feature, replica) from multi-MB tables
+// in L2 (955 ms of a C3-sized continuous fit, profiles/r04bf/); a count of the cuts by VALU
+// compares took 32 compares per bin (380 ms, gpurun_out/r05e/).
+template <typename CT, typename KT, int kRows>
 __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, int64_t N, int32_t S_codes,
                                                   const int32_t* __restrict__ sub,
                                                   const int32_t* __restrict__ Fr, int32_t Fmax,
-                                                  const uint32_t* __restrict__ cut, int32_t ncp,
-                                                  const int32_t* __restrict__ ng, uint8_t* __restrict__ out,
-                                                  int32_t S_out, int64_t out_rstride,
+                                                  const uint32_t* __restrict__ cut, int32_t ncp, int32_t lg,
+                                                  uint8_t* __restrict__ out, int32_t S_out, int64_t out_rstride,
                                                   uint8_t* __restrict__ cols, int32_t ncol, int64_t npad,
-                                                  int64_t cols_rstride, int R, int rb) {
+                                                  int64_t cols_rstride, int R, int rb, int64_t rows_per_chunk) {
   extern __shared__ __align__(16) uint8_t smem[];
   constexpr int kRpl = kRows / 64;  // rows per lane
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r0 = blockIdx.y * rb, nrep = min(rb, R - r0);
   const int pc = S_codes * (int)sizeof(CT) + 4;  // code row pitch in LDS (bytes)
   const int pb = S_out + 4;                      // bin row pitch
-  uint8_t* sc = smem;
-  uint8_t* sb = smem + (size_t)kRows * pc;
-  const int64_t n0 = (int64_t)blockIdx.x * kRows;
-  const int nr = (int)min<int64_t>(kRows, N - n0);
-  {
-    const int rw = S_codes * (int)sizeof(CT) / 4;  // dwords per code row
-    const uint32_t* src = (const uint32_t*)(codes + n0 * S_codes);
-    for (int k = tid; k < kRows * rw; k += 256) {
-      const int row = k / rw, w = k - row * rw;
-      *(uint32_t*)(sc + row * pc + 4 * w) = row < nr ? src[k] : 0u;
-    }
+  KT* sk = (KT*)smem;                            // [rb][Fmax][ncp] keys
+  const size_t kbytes = ((size_t)rb * Fmax * ncp * sizeof(KT) + 15) & ~(size_t)15;
+  uint8_t* sc = smem + kbytes;
+  uint8_t* sb = sc + (size_t)kRows * pc;
+  for (int64_t k = tid; k < (int64_t)nrep * Fmax * ncp; k += 256) {
+    const uint32_t c = cut[(int64_t)r0 * Fmax * ncp + k];
+    sk[k] = c == 0xffffffffu ? (KT)~(KT)0 : (KT)(c - 1u);
   }
-  block_sync();
+  const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk, c1 = min(N, c0 + rows_per_chunk);
   const int ngrp4 = S_out / 4;
-  for (int r = blockIdx.y * rb; r < min(R, (int)(blockIdx.y + 1) * rb); r++) {
-    const int fr = Fr[r];
-    for (int q = wave; q < ngrp4; q += 4) {
-      uint32_t wv[kRpl];
+  // the code rows of a block as 16-byte pieces, kPv per thread, loaded one block ahead into
+  // registers (a load-then-store loop waited out the memory latency for every piece)
+  const int rq = S_codes * (int)sizeof(CT) / 16;  // 16-byte pieces per code row
+  constexpr int kPv = 8;                           // pieces per thread (rows of <= 256 bytes)
+  uint4 pv[kPv];
+  // (unconditional loads, clamped to the last row: rows past a block's end are binned but never
+  // stored; a select on a loaded value, or a branch around a load, makes the compiler wait)
+  auto load_block = [&](int64_t nb) {
+    nb = min(nb, N - 1);
+    const uint4* src = (const uint4*)(codes + nb * S_codes);
+    const int64_t lim = (min(N, nb + kRows) - nb) * rq;  // pieces of the block's real rows
 #pragma unroll
-      for (int i = 0; i < kRpl; i++) wv[i] = 0u;
-      for (int k = 0; k < 4; k++) {
-        const int fl = 4 * q + k;
-        if (fl >= fr) break;
-        const int64_t rf = (int64_t)r * Fmax + fl;
-        const int g = sub[rf];
-        uint32_t cv[kRpl], b[kRpl];
+    for (int v = 0; v < kPv; v++) pv[v] = src[min((int64_t)(tid + 256 * v), lim - 1)];
+  };
+  if (c0 < c1) load_block(c0);
+  for (int64_t n0 = c0; n0 < c1; n0 += kRows) {
+    const int nr = (int)min<int64_t>(kRows, c1 - n0);
+    block_sync();  // (the previous block's tile reads; the keys at the first block)
 #pragma unroll
-        for (int i = 0; i < kRpl; i++) {
-          cv[i] = (uint32_t) * (const CT*)(sc + (lane + 64 * i) * pc + g * (int)sizeof(CT));
-          b[i] = 0u;
+    for (int v = 0; v < kPv; v++) {
+      const int k = tid + 256 * v;
+      if (k < kRows * rq) {
+        const int row = k / rq, w = k - row * rq;
+        uint32_t* d = (uint32_t*)(sc + row * pc + 16 * w);
+        d[0] = pv[v].x;
+        d[1] = pv[v].y;
+        d[2] = pv[v].z;
+        d[3] = pv[v].w;
+      }
+    }
+    load_block(n0 + kRows);  // the next block's codes in flight
+    block_sync();
+    for (int ri = 0; ri < nrep; ri++) {
+      const int r = r0 + ri;
+      const int fr = Fr[r];
+      for (int q = wave; q < ngrp4; q += 4) {
+        if (4 * q >= fr) {  // past the replica's features: zero bins
+#pragma unroll
+          for (int i = 0; i < kRpl; i++) *(uint32_t*)(sb + (lane + 64 * i) * pb + 4 * q) = 0u;
+          continue;
         }
-        const uint32_t* cu = cut + rf * ncp;
-        const int ngr = ng[rf];
-        for (int gg = 0; gg < ngr; gg++) {
+        uint32_t wv[kRpl];
 #pragma unroll
-          for (int j = 0; j < 32; j++) {
-            const uint32_t cj = cu[32 * gg + j];
+        for (int i = 0; i < kRpl; i++) wv[i] = 0u;
+        // the group's 4 features x kRpl rows: 4 kRpl independent searches, their LDS reads
+        // interleaved (one search alone waits out each read's latency)
+        const KT* ks[4];
+        uint32_t cv[4][kRpl], idx[4][kRpl];
 #pragma unroll
-            for (int i = 0; i < kRpl; i++) b[i] += cv[i] >= cj ? 1u : 0u;
+        for (int k = 0; k < 4; k++) {
+          const int fl = min(4 * q + k, fr - 1);  // (features past F_r search a real one; masked below)
+          const int g = sub[(int64_t)r * Fmax + fl];
+          ks[k] = sk + ((size_t)ri * Fmax + fl) * ncp;
+#pragma unroll
+          for (int i = 0; i < kRpl; i++) {
+            cv[k][i] = (uint32_t) * (const CT*)(sc + (lane + 64 * i) * pc + g * (int)sizeof(CT));
+            idx[k][i] = 0u;
           }
         }
+        // idx = #{keys < code} (keys ascending): steps of ncp / 2, ..., 1
+        for (int st = lg - 1; st >= 0; st--) {
+          const uint32_t h = 1u << st;
 #pragma unroll
-        for (int i = 0; i < kRpl; i++) wv[i] |= b[i] << (8 * k);
-      }
+          for (int k = 0; k < 4; k++)
 #pragma unroll
-      for (int i = 0; i < kRpl; i++) *(uint32_t*)(sb + (lane + 64 * i) * pb + 4 * q) = wv[i];
-    }
-    block_sync();
-    {
-      const int wpr = S_out / 4;  // output words per row
-      uint32_t* o = (uint32_t*)(out + (int64_t)r * out_rstride + n0 * S_out);
-      for (int k = tid; k < nr * wpr; k += 256) {
-        const int row = k / wpr, w = k - row * wpr;
-        o[k] = *(const uint32_t*)(sb + row * pb + 4 * w);
-      }
-    }
-    if (cols) {  // per feature the block's kRows rows are kRows consecutive bytes (rows past N: 0)
-      uint8_t* cr = cols + (int64_t)r * cols_rstride + n0;
-      for (int k = tid; k < ncol * (kRows / 4); k += 256) {
-        const int fl = k / (kRows / 4), wd = k - fl * (kRows / 4);
-        uint32_t v = 0;
-#pragma unroll
-        for (int kk = 0; kk < 4; kk++) {
-          const int row = 4 * wd + kk;
-          if (row < nr) v |= (uint32_t)sb[row * pb + fl] << (8 * kk);
+            for (int i = 0; i < kRpl; i++) idx[k][i] += (uint32_t)ks[k][idx[k][i] + h - 1u] < cv[k][i] ? h : 0u;
         }
-        *(uint32_t*)(cr + (int64_t)fl * npad + 4 * wd) = v;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (4 * q + k < fr)
+#pragma unroll
+            for (int i = 0; i < kRpl; i++) wv[i] |= idx[k][i] << (8 * k);
+#pragma unroll
+        for (int i = 0; i < kRpl; i++) *(uint32_t*)(sb + (lane + 64 * i) * pb + 4 * q) = wv[i];
       }
+      block_sync();
+      {
+        const int wpr = S_out / 4;  // output words per row
+        uint32_t* o = (uint32_t*)(out + (int64_t)r * out_rstride + n0 * S_out);
+        for (int k = tid; k < nr * wpr; k += 256) {
+          const int row = k / wpr, w = k - row * wpr;
+          o[k] = *(const uint32_t*)(sb + row * pb + 4 * w);
+        }
+      }
+      if (cols) {  // per feature the block's rows are consecutive bytes (rows past N: 0)
+        uint8_t* cr = cols + (int64_t)r * cols_rstride + n0;
+        for (int k = tid; k < ncol * (kRows / 4); k += 256) {
+          const int fl = k / (kRows / 4), wd = k - fl * (kRows / 4);
+          uint32_t v = 0;
+#pragma unroll
+          for (int kk = 0; kk < 4; kk++) {
+            const int row = 4 * wd + kk;
+            if (row < nr) v |= (uint32_t)sb[row * pb + fl] << (8 * kk);
+          }
+          *(uint32_t*)(cr + (int64_t)fl * npad + 4 * wd) = v;
+        }
+      }
+      if (ri + 1 < nrep) block_sync();  // the tile is rewritten by the next replica
     }
-    block_sync();  // the tile is rewritten by the next replica
   }
 }
 
@@ -3623,34 +3667,51 @@ __global__ __launch_bounds__(256) void k_bin_cuts_rows(const CT* __restrict__ co
   }
 }
 
-template <typename CT>
+template <typename CT, typename KT>
 static bool launch_bin_cuts_t(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
                               const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
-                              const int32_t* d_ng, uint8_t* out, int32_t S_out, int64_t out_rstride,
-                              uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride) {
-  // four replicas per workgroup share the staged code rows (SBAG_BIN_RB overrides)
-  static const int rb_env = getenv("SBAG_BIN_RB") ? atoi(getenv("SBAG_BIN_RB")) : 4;
-  const int rb = std::max(1, std::min(R, rb_env));
-  auto lds_for = [&](int rows) {
-    return (size_t)rows * (S_codes * sizeof(CT) + 4) + (size_t)rows * (S_out + 4);
-  };
-  const bool fits128 = sizeof(CT) <= 2 && lds_for(128) <= 64 * 1024;
-  const bool fits64 = lds_for(64) <= 80 * 1024;
-  if ((fits128 || fits64) && S_out % 4 == 0 && (S_codes * sizeof(CT)) % 4 == 0 && npad % 128 == 0 &&
-      !getenv("SBAG_BIN_ROWWISE")) {
-    if (fits128) {
-      const dim3 g((unsigned)((N + 127) / 128), (unsigned)((R + rb - 1) / rb));
-      set_max_lds((const void*)k_bin_cuts<CT, 128>, (int)lds_for(128));
-      hipLaunchKernelGGL((k_bin_cuts<CT, 128>), g, dim3(256), lds_for(128), st, codes, N, S_codes, d_sub, d_Fr,
-                         Fmax, d_cut, ncp, d_ng, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb);
-    } else {
-      const dim3 g((unsigned)((N + 63) / 64), (unsigned)((R + rb - 1) / rb));
-      set_max_lds((const void*)k_bin_cuts<CT, 64>, (int)lds_for(64));
-      hipLaunchKernelGGL((k_bin_cuts<CT, 64>), g, dim3(256), lds_for(64), st, codes, N, S_codes, d_sub, d_Fr,
-                         Fmax, d_cut, ncp, d_ng, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb);
-    }
-    return cols != nullptr;
-  }
+                              uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
+                              int64_t npad, int64_t cols_rstride) {
+  constexpr int kRows = 128;
+  const size_t tiles = (size_t)kRows * (S_codes * sizeof(CT) + 4) + (size_t)kRows * (S_out + 4);
+  const size_t per_rep = (size_t)Fmax * ncp * sizeof(KT);
+  // replicas per workgroup: up to 4 (they share the staged codes) within ~72 KB of LDS, so two
+  // workgroups fit a CU (SBAG_BIN_RB overrides)
+  static const int rb_env = getenv("SBAG_BIN_RB") ? atoi(getenv("SBAG_BIN_RB")) : 0;
+  int rb = rb_env > 0 ? rb_env : 4;
+  while (rb > 1 && tiles + rb * per_rep + 16 > 72 * 1024) rb--;
+  rb = std::max(1, std::min(rb, R));
+  const size_t lds = tiles + ((rb * per_rep + 15) & ~(size_t)15);
+  int lg = 0;
+  while ((1 << lg) < ncp) lg++;
+  // (the staged code rows: 16-byte pieces, at most 8 per thread per block)
+  if (lds > 150 * 1024 || (1 << lg) != ncp || S_out % 4 != 0 || (S_codes * sizeof(CT)) % 16 != 0 ||
+      (size_t)kRows * S_codes * sizeof(CT) > 8 * 16 * 256 || npad % kRows != 0 || getenv("SBAG_BIN_ROWWISE"))
+    return false;
+  // chunks of row blocks: about 2048 workgroups over the replica groups
+  const int ngrp = (R + rb - 1) / rb;
+  const int64_t nblk = (N + kRows - 1) / kRows;
+  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(nblk, (2048 + ngrp - 1) / ngrp));
+  const int64_t rpc = (nblk + nch - 1) / nch * kRows;
+  const dim3 g((unsigned)((N + rpc - 1) / rpc), (unsigned)ngrp);
+  set_max_lds((const void*)k_bin_cuts<CT, KT, kRows>, (int)lds);
+  hipLaunchKernelGGL((k_bin_cuts<CT, KT, kRows>), g, dim3(256), lds, st, codes, N, S_codes, d_sub, d_Fr, Fmax,
+                     d_cut, ncp, lg, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb, rpc);
+  return true;
+}
+
+template <typename CT>
+static bool launch_bin_cuts_any(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
+                                const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
+                                uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
+                                int64_t npad, int64_t cols_rstride) {
+  const bool ok = sizeof(CT) <= 2
+                      ? launch_bin_cuts_t<CT, uint16_t>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
+                                                        S_out, out_rstride, cols, ncol, npad, cols_rstride)
+                      : launch_bin_cuts_t<CT, uint32_t>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
+                                                        S_out, out_rstride, cols, ncol, npad, cols_rstride);
+  if (ok) return cols != nullptr;
+  // rows too wide for the staged tiles: a thread per row (no column copy)
   const dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
   hipLaunchKernelGGL(k_bin_cuts_rows<CT>, grid, dim3(256), 0, st, codes, N, S_codes, d_sub, d_Fr, Fmax, d_cut,
                      ncp, out, S_out, out_rstride);
@@ -3659,16 +3720,16 @@ static bool launch_bin_cuts_t(hipStream_t st, const CT* codes, int64_t N, int32_
 
 bool launch_bin_cuts(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
                      const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut,
-                     int32_t ncp, const int32_t* d_ng, uint8_t* out, int32_t S_out, int64_t out_rstride,
-                     uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride) {
+                     int32_t ncp, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
+                     int64_t npad, int64_t cols_rstride) {
   if (code_bytes == 1)
-    return launch_bin_cuts_t(st, (const uint8_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_ng, out,
-                             S_out, out_rstride, cols, ncol, npad, cols_rstride);
+    return launch_bin_cuts_any(st, (const uint8_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
+                               S_out, out_rstride, cols, ncol, npad, cols_rstride);
   if (code_bytes == 2)
-    return launch_bin_cuts_t(st, (const uint16_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_ng, out,
+    return launch_bin_cuts_any(st, (const uint16_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
+                               S_out, out_rstride, cols, ncol, npad, cols_rstride);
+  return launch_bin_cuts_any(st, (const uint32_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
                              S_out, out_rstride, cols, ncol, npad, cols_rstride);
-  return launch_bin_cuts_t(st, (const uint32_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_ng, out,
-                           S_out, out_rstride, cols, ncol, npad, cols_rstride);
 }
 
 // Value counts with global atomics (u16 codes / dictionaries too large for LDS)

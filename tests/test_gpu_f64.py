@@ -15,7 +15,7 @@ import pytest
 
 import oracle
 from conftest import DATA
-from parity_utils import assert_forest_equal, oracle_forest
+from parity_utils import assert_forest_equal, assert_tree_equal, oracle_forest
 
 import spark_bagging_amd as sb
 from spark_bagging_amd import _native as nat
@@ -251,7 +251,8 @@ def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
     """The bench's real-valued-label fit at full size (10M x 100, 128 learners, depth 8,
     P = 128), where the oracle cannot follow: the default engine (screen, staged bucket
     scatter, column-ordered and XCD-dispatched tasks, exploded chains) gives the same trees
-    byte for byte as (a) the same screen with round 4's first bucketing and chain kernels and
+    byte for byte as (a) the same screen with round 4's first bucketing and chain kernels,
+    (a') the bucketing fused into the chains in LDS (SBAG_F64_FUSED=1) and
     (b) the unscreened engine, every node of every level summed by round 3's row-order walk
     (k_f64_hist) -- two independent exact paths."""
     N, F, L = 10_000_000, 100, 128
@@ -273,6 +274,9 @@ def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
         for k in ("SBAG_F64_CHAIN_X", "SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER",
                   "SBAG_F64_XCD_ORDER"):
             monkeypatch.delenv(k)
+        monkeypatch.setenv("SBAG_F64_FUSED", "1")  # the fused bucket chains
+        d = fit()
+        monkeypatch.delenv("SBAG_F64_FUSED")
         monkeypatch.setenv("SBAG_F64_SCREEN", "0")
         monkeypatch.setenv("SBAG_F64_FALLBACK", "hist")
         c = fit()
@@ -281,8 +285,32 @@ def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
     ta, tc = a.timing(), c.timing()
     assert ta["exact_fallbacks"] < tc["exact_fallbacks"] / 20, (ta["exact_fallbacks"], tc["exact_fallbacks"])
     for t in range(L):
-        (na, sa), (nb, sb_), (nc, sc) = a.tree(t), b.tree(t), c.tree(t)
-        assert na.tobytes() == nb.tobytes() == nc.tobytes(), f"tree {t}"
-        assert sa.tobytes() == sb_.tobytes() == sc.tobytes(), f"tree {t} stats"
-    for f in (a, b, c):
+        (na, sa), (nb, sb_), (nc, sc), (nd, sd) = a.tree(t), b.tree(t), c.tree(t), d.tree(t)
+        assert na.tobytes() == nb.tobytes() == nc.tobytes() == nd.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes() == sc.tobytes() == sd.tobytes(), f"tree {t} stats"
+    for f in (a, b, c, d):
         f.free()
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_chain_windows_many_bins_large_counts(ctx, monkeypatch, fused):
+    """Spark's row-order sums with every row drawn 9 times (a 1024-entry block holds 9216
+    draw records: k_fb_bchain's several LDS windows), maxBins 255 on features with ~1000
+    distinct values (up to 255 chains per task), fp64 labels -- the booster engine, fused
+    bucket chains (SBAG_F64_FUSED=1, round 5) and the global buckets (the default), bit-exact
+    against the oracle."""
+    monkeypatch.setenv("SBAG_F64_FUSED", fused)
+    rng = np.random.default_rng(29)
+    n, f = 20_000, 6
+    X = np.round(rng.normal(size=(n, f)) * 150) / 7
+    lab = rng.normal(size=n) * 3.3 + X[:, 2] * 0.01
+    counts = np.full(n, 9, np.uint8)
+    counts[rng.random(n) < 0.1] = 0
+    sub = np.arange(f, dtype=np.int32)
+    ds = nat.DeviceDataset.from_numpy(X, np.zeros(n), ctx)
+    try:
+        fb = nat.fit_booster(ctx, ds, lab, counts, sub, max_depth=6, max_bins=255)
+    finally:
+        ds.free()
+    orf = oracle.fit(X, lab, counts[None, :], [sub], max_depth=6, max_bins=255)
+    assert_tree_equal(fb, 0, orf, 0)
