@@ -77,6 +77,17 @@ run_step() {
       tail -1 "$d/trace.log" | cut -c1-400
       f=$(find "$d" -name "*kernel_stats.csv" | head -1); head -20 "$f" | cut -d, -f1-5 | cut -c1-160
       return 0 ;;
+    pmc_cont|pmc_f64)
+      # two PMC passes (one counter block set each, no trace domains) of the continuous bench /
+      # the f64 probe: issue mix and LDS behaviour
+      local d="$OUT/$st$tag" cmd="python3 scripts/bench_continuous.py"
+      [ "$st" = pmc_f64 ] && cmd="python3 scripts/f64_probe.py"
+      mkdir -p "$d"
+      timeout -s KILL 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY \
+        --output-format csv -d "$d/p1" -o p1 -- $cmd > "$d/p1.log" 2>&1 || { tail -5 "$d/p1.log"; return 1; }
+      timeout -s KILL 400 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_ANY \
+        --output-format csv -d "$d/p2" -o p2 -- $cmd > "$d/p2.log" 2>&1 || { tail -5 "$d/p2.log"; return 1; }
+      return 0 ;;
     trace_cont)
       local d="$OUT/trace_cont$tag"
       mkdir -p "$d"

@@ -3519,8 +3519,11 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
         uint8_t* d_c;
         const int64_t npad_c = (N + 127) / 128 * 128;
         TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_c, &d_c));
+        // (SBAG_BIN_NO_COLS=1: the column copy by k_transpose afterwards, A/B)
+        static const bool no_cols = getenv("SBAG_BIN_NO_COLS") != nullptr;
         if (launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R, d_cut, ncp,
-                            d_b, S, (int64_t)N * S, d_c, ncol_r, npad_c, (int64_t)ncol_r * npad_c)) {
+                            d_b, S, (int64_t)N * S, no_cols ? nullptr : d_c, ncol_r, npad_c,
+                            (int64_t)ncol_r * npad_c)) {
           cols_direct = d_c;
           cols_direct_npad = npad_c;
         }

@@ -3534,7 +3534,7 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
   // the code rows of a block as 16-byte pieces, kPv per thread, loaded one block ahead into
   // registers (a load-then-store loop waited out the memory latency for every piece)
   const int rq = S_codes * (int)sizeof(CT) / 16;  // 16-byte pieces per code row
-  constexpr int kPv = 8;                           // pieces per thread (rows of <= 256 bytes)
+  constexpr int kPv = kRows / 16;                  // pieces per thread (rows of <= 256 bytes)
   uint4 pv[kPv];
   // (unconditional loads, clamped to the last row: rows past a block's end are binned but never
   // stored; a select on a loaded value, or a branch around a load, makes the compiler wait)
@@ -3565,8 +3565,16 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
     block_sync();
     for (int ri = 0; ri < nrep; ri++) {
       const int r = r0 + ri;
-      const int fr = Fr[r];
-      for (int q = wave; q < ngrp4; q += 4) {
+      // the replica's feature count and this wave's features' code offsets, by vector loads
+      // once per replica (lane 4 j + k: feature 4 (wave + 4 j) + k) -- scalar loads inside
+      // the group loop would wait on lgkmcnt, which also counts the searches' LDS reads
+      const int fr = __builtin_amdgcn_readfirstlane(Fr[r]);
+      int gv;
+      {
+        const int fl = min(4 * (wave + 4 * (lane >> 2)) + (lane & 3), fr - 1);
+        gv = sub[(int64_t)r * Fmax + fl] * (int)sizeof(CT);
+      }
+      for (int q = wave, j = 0; q < ngrp4; q += 4, j++) {
         if (4 * q >= fr) {  // past the replica's features: zero bins
 #pragma unroll
           for (int i = 0; i < kRpl; i++) *(uint32_t*)(sb + (lane + 64 * i) * pb + 4 * q) = 0u;
@@ -3582,21 +3590,30 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const int fl = min(4 * q + k, fr - 1);  // (features past F_r search a real one; masked below)
-          const int g = sub[(int64_t)r * Fmax + fl];
+          const int gb = __builtin_amdgcn_readlane(gv, 4 * j + k);
           ks[k] = sk + ((size_t)ri * Fmax + fl) * ncp;
 #pragma unroll
           for (int i = 0; i < kRpl; i++) {
-            cv[k][i] = (uint32_t) * (const CT*)(sc + (lane + 64 * i) * pc + g * (int)sizeof(CT));
+            cv[k][i] = (uint32_t) * (const CT*)(sc + (lane + 64 * i) * pc + gb);
             idx[k][i] = 0u;
           }
         }
-        // idx = #{keys < code} (keys ascending): steps of ncp / 2, ..., 1
-        for (int st = lg - 1; st >= 0; st--) {
-          const uint32_t h = 1u << st;
+        // idx = #{keys < code} (keys ascending): steps of ncp / 2, ..., 1 (unrolled for the
+        // common 32 keys)
+        auto step = [&](uint32_t h) {
 #pragma unroll
           for (int k = 0; k < 4; k++)
 #pragma unroll
             for (int i = 0; i < kRpl; i++) idx[k][i] += (uint32_t)ks[k][idx[k][i] + h - 1u] < cv[k][i] ? h : 0u;
+        };
+        if (lg == 5) {
+          step(16u);
+          step(8u);
+          step(4u);
+          step(2u);
+          step(1u);
+        } else {
+          for (int st = lg - 1; st >= 0; st--) step(1u << st);
         }
 #pragma unroll
         for (int k = 0; k < 4; k++)
@@ -3667,37 +3684,53 @@ __global__ __launch_bounds__(256) void k_bin_cuts_rows(const CT* __restrict__ co
   }
 }
 
-template <typename CT, typename KT>
-static bool launch_bin_cuts_t(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
+template <typename CT, typename KT, int kRows>
+static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
                               const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
                               uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
                               int64_t npad, int64_t cols_rstride) {
-  constexpr int kRows = 128;
   const size_t tiles = (size_t)kRows * (S_codes * sizeof(CT) + 4) + (size_t)kRows * (S_out + 4);
   const size_t per_rep = (size_t)Fmax * ncp * sizeof(KT);
-  // replicas per workgroup: up to 4 (they share the staged codes) within ~72 KB of LDS, so two
-  // workgroups fit a CU (SBAG_BIN_RB overrides)
+  // replicas per workgroup: up to 4 (they share the staged codes) within the LDS target, so that
+  // several workgroups fit a CU (SBAG_BIN_RB / SBAG_BIN_LDS_KB override)
   static const int rb_env = getenv("SBAG_BIN_RB") ? atoi(getenv("SBAG_BIN_RB")) : 0;
+  static const int lds_kb = getenv("SBAG_BIN_LDS_KB") ? atoi(getenv("SBAG_BIN_LDS_KB")) : 52;
   int rb = rb_env > 0 ? rb_env : 4;
-  while (rb > 1 && tiles + rb * per_rep + 16 > 72 * 1024) rb--;
+  while (rb > 1 && tiles + rb * per_rep + 16 > (size_t)lds_kb * 1024) rb--;
   rb = std::max(1, std::min(rb, R));
   const size_t lds = tiles + ((rb * per_rep + 15) & ~(size_t)15);
   int lg = 0;
   while ((1 << lg) < ncp) lg++;
-  // (the staged code rows: 16-byte pieces, at most 8 per thread per block)
+  // (the staged code rows: 16-byte pieces, at most kRows / 16 per thread per block)
   if (lds > 150 * 1024 || (1 << lg) != ncp || S_out % 4 != 0 || (S_codes * sizeof(CT)) % 16 != 0 ||
-      (size_t)kRows * S_codes * sizeof(CT) > 8 * 16 * 256 || npad % kRows != 0 || getenv("SBAG_BIN_ROWWISE"))
+      (size_t)kRows * S_codes * sizeof(CT) > (size_t)kRows / 16 * 16 * 256 || npad % kRows != 0 ||
+      getenv("SBAG_BIN_ROWWISE"))
     return false;
-  // chunks of row blocks: about 2048 workgroups over the replica groups
+  // chunks of row blocks: about 4096 workgroups over the replica groups
   const int ngrp = (R + rb - 1) / rb;
   const int64_t nblk = (N + kRows - 1) / kRows;
-  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(nblk, (2048 + ngrp - 1) / ngrp));
+  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(nblk, (4096 + ngrp - 1) / ngrp));
   const int64_t rpc = (nblk + nch - 1) / nch * kRows;
   const dim3 g((unsigned)((N + rpc - 1) / rpc), (unsigned)ngrp);
   set_max_lds((const void*)k_bin_cuts<CT, KT, kRows>, (int)lds);
   hipLaunchKernelGGL((k_bin_cuts<CT, KT, kRows>), g, dim3(256), lds, st, codes, N, S_codes, d_sub, d_Fr, Fmax,
                      d_cut, ncp, lg, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb, rpc);
   return true;
+}
+
+template <typename CT, typename KT>
+static bool launch_bin_cuts_t(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
+                              const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
+                              uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
+                              int64_t npad, int64_t cols_rstride) {
+  // 64-row blocks (one row per lane: ~50 KB of LDS with four replicas, three workgroups per CU)
+  // unless SBAG_BIN_ROWS=128 (C3-sized continuous fit 563 vs 604 ms, gpurun_out/r05k/)
+  static const int rows = getenv("SBAG_BIN_ROWS") ? atoi(getenv("SBAG_BIN_ROWS")) : 64;
+  if (rows == 128)
+    return launch_bin_cuts_r<CT, KT, 128>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out, S_out,
+                                          out_rstride, cols, ncol, npad, cols_rstride);
+  return launch_bin_cuts_r<CT, KT, 64>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out, S_out,
+                                       out_rstride, cols, ncol, npad, cols_rstride);
 }
 
 template <typename CT>
