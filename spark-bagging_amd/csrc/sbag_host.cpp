@@ -3790,6 +3790,11 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     hist_pregrouped = true;
   }
   std::string hist_nxt_name = "histB", hist_cur_name = "histA";
+  // gini: the larger children's histograms are derived (parent - smaller child) inside the next
+  // level's split search (k_split_gini), not by k_subtract; SBAG_NO_FUSED_SUB=1: k_subtract
+  static const bool fused_sub = !getenv("SBAG_NO_FUSED_SUB");
+  void* hist_prev = nullptr;        // the previous level's histograms (the derived slots' parents)
+  std::vector<int32_t> derive;      // [2 slot] (parent slot, smaller-child slot) or -1
   int levels = 0;
   // exact sum of count*k^2 of every slot's node (variance screening): root from k_compact
   std::vector<uint64_t> slot_sq(R);
@@ -3830,6 +3835,14 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     sa.out = d_sout;
     sa.stats = d_sstats;
     sa.plane = (int64_t)M * NS;
+    if (gini && fused_sub && !derive.empty()) {
+      int32_t* d_der;
+      TRY(ws_typed(c, "derive", derive.size(), &d_der));
+      TRY(h2d(c, d_der, derive.data(), derive.size()));
+      sa.derive = d_der;
+      sa.par_hist = hist_prev;
+      sa.hist_w = hist_cur;
+    }
     if (!gini) {
       uint64_t* d_nsq;
       TRY(ws_typed(c, "node_sq", (size_t)M, &d_nsq));
@@ -4275,7 +4288,15 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     ha.hist = hist_nxt;
     TRY(launch(g, gini ? kHistGini : kHistVar, T_HIST, hseg, hpar));
     pre_hist = nullptr;
-    if (!triples.empty()) {
+    derive.clear();
+    if (!triples.empty() && gini && fused_sub) {
+      // the next level's split search derives them (SplitArgs.derive)
+      derive.assign((size_t)2 * Mn, -1);
+      for (size_t k = 0; k + 2 < triples.size() + 1; k += 3) {
+        derive[2 * (size_t)triples[k]] = triples[k + 1];
+        derive[2 * (size_t)triples[k] + 1] = triples[k + 2];
+      }
+    } else if (!triples.empty()) {
       int32_t* d_tri;
       TRY(ws_typed(c, "triples", triples.size(), &d_tri));
       TRY(h2d(c, d_tri, triples.data(), triples.size()));
@@ -4284,6 +4305,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       HIP_TRY(hipGetLastError());
       tm.end(h);
     }
+    hist_prev = hist_cur;
     seg = nseg;
     if (tile_res) tseg.swap(ntseg);
     slots = next_slots;

@@ -154,6 +154,13 @@ struct SplitArgs {
   const uint64_t* node_sq;        // screen: [M] exact sum of count*k^2 of each node
   int32_t hct;                    // gini layout class tile (HistArgs.hct)
   int32_t pad;
+  // gini: slots whose histogram is the sibling = parent - smaller child, derived while staged
+  // (k_subtract fused into the split search): derive[2 slot] = the parent's slot in par_hist,
+  // derive[2 slot + 1] = the smaller child's slot in hist (-1: the slot's histogram is built);
+  // the derived histogram is written to hist_w for the next level's parents
+  const int32_t* derive;
+  const void* par_hist;
+  void* hist_w;
 };
 
 struct DevNode {  // packed tree node for predict

@@ -3005,9 +3005,12 @@ __host__ __device__ inline int split_fstride(int NB, int NS) {
   const int NSP = NS + 1;
   return NB * NSP + (((NB - 1) * NSP - NB * NSP) % 64 + 64) % 64;
 }
+// (ps, hw: a derived slot -- the staged words are parent ps - smaller child hs, and are also
+// written to hw, the slot's own histogram for the next level)
 __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ hs, int f0, int g,
                                                    int NB, int NS, int Fmax, int hct,
-                                                   uint32_t* pre) {
+                                                   uint32_t* pre, const uint32_t* __restrict__ ps = nullptr,
+                                                   uint32_t* __restrict__ hw = nullptr) {
   // features [f0, f0 + g) of each layout class tile t are one contiguous run of g*NB*hct
   // words (gini_cell); staged as pre[fl][b][c] with the class row padded to NS + 1
   const int tid = threadIdx.x;
@@ -3018,7 +3021,14 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
     const int hct4 = hct >> 2, per_t4 = (int)(per_t >> 2), n4 = ntc * per_t4;
     auto src4 = [&](int q) {
       const int t = q / per_t4, rem = q - t * per_t4;
-      return ((const uint4*)(hs + ((int64_t)t * Fmax + f0) * NB * hct))[rem];
+      const int64_t o = ((int64_t)t * Fmax + f0) * NB * hct;
+      uint4 v = ((const uint4*)(hs + o))[rem];
+      if (ps) {
+        const uint4 pv = ((const uint4*)(ps + o))[rem];
+        v = make_uint4(pv.x - v.x, pv.y - v.y, pv.z - v.z, pv.w - v.w);
+        ((uint4*)(hw + o))[rem] = v;
+      }
+      return v;
     };
     auto put = [&](int q, const uint4& v) {
       const int t = q / per_t4, rem = q - t * per_t4;
@@ -3046,8 +3056,13 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
       const int64_t rem = q - (int64_t)t * per_t;
       const int row = (int)(rem / hct), c = t * hct + (int)(rem - (int64_t)row * hct);
       const int fl = row / NB;
-      pre[(size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c] =
-          hs[((int64_t)t * Fmax + f0) * NB * hct + rem];
+      const int64_t o = ((int64_t)t * Fmax + f0) * NB * hct + rem;
+      uint32_t v = hs[o];
+      if (ps) {
+        v = ps[o] - v;
+        hw[o] = v;
+      }
+      pre[(size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c] = v;
     }
   }
   block_sync();
@@ -3071,6 +3086,15 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   const int NB = A.NB, NS = A.NS, NSP = NS + 1, FS = split_fstride(NB, NS);
   const int64_t slot_words = (int64_t)A.Fmax * NB * NS;
   const uint32_t* hs = (const uint32_t*)A.hist + (int64_t)slot * slot_words;
+  // a derived slot (the larger child): staged as parent - smaller child, written to its own
+  // histogram on the way (k_subtract fused in)
+  const uint32_t* ps = nullptr;
+  uint32_t* hw = nullptr;
+  if (A.derive && A.derive[2 * slot] >= 0) {
+    ps = (const uint32_t*)A.par_hist + (int64_t)A.derive[2 * slot] * slot_words;
+    hw = (uint32_t*)A.hist_w + (int64_t)slot * slot_words;
+    hs = (const uint32_t*)A.hist + (int64_t)A.derive[2 * slot + 1] * slot_words;
+  }
   const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
   int64_t* s_tot = (int64_t*)smem;                      // [NS]
   double* s_gain = (double*)(s_tot + NS);               // [256]
@@ -3079,7 +3103,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   double* s_wmax = (double*)(s_valid + 256);            // [2][4] per-wave best, by group parity
   uint32_t* pre = (uint32_t*)(s_wmax + 8);              // [G][NB][NS + 1] prefix over bins
   // group 0 first: the node totals are feature 0's last prefix
-  split_stage_prefix(hs, 0, min(G, Fr), NB, NS, A.Fmax, A.hct, pre);
+  split_stage_prefix(hs, 0, min(G, Fr), NB, NS, A.Fmax, A.hct, pre, ps, hw);
   for (int c = tid; c < NS; c += 256) s_tot[c] = (int64_t)pre[(size_t)(NB - 1) * NSP + c];
   block_sync();
   double ttot = 0.0;
@@ -3110,7 +3134,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
       const double* wm = s_wmax + ((grp - 1) & 1) * 4;
       block_sync();  // previous group's prefix no longer read; wm visible
       thr = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
-      split_stage_prefix(hs, f0, g, NB, NS, A.Fmax, A.hct, pre);
+      split_stage_prefix(hs, f0, g, NB, NS, A.Fmax, A.hct, pre, ps, hw);
     }
     for (int q = tid; q < g * (NB - 1); q += 256) {
       const int fl = q / (NB - 1), sp = q - fl * (NB - 1);
@@ -3218,16 +3242,22 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
     if (bf >= 0) {
       // bins of (bf, c) are hct words apart (gini_cell)
       const int hct = A.hct;
-      const uint32_t* h = hs + gini_cell(bf, 0, c, NB, A.Fmax, hct);
-      int sb = 0;
-      for (; sb + 8 <= bsp + 1; sb += 8) {
-        uint32_t v[8];
+      auto bins_sum = [&](const uint32_t* h) {
+        int64_t acc = 0;
+        int sb = 0;
+        for (; sb + 8 <= bsp + 1; sb += 8) {
+          uint32_t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = h[(int64_t)(sb + u) * hct];
+          for (int u = 0; u < 8; u++) v[u] = h[(int64_t)(sb + u) * hct];
 #pragma unroll
-        for (int u = 0; u < 8; u++) l += v[u];
-      }
-      for (; sb <= bsp; sb++) l += h[(int64_t)sb * hct];
+          for (int u = 0; u < 8; u++) acc += v[u];
+        }
+        for (; sb <= bsp; sb++) acc += h[(int64_t)sb * hct];
+        return acc;
+      };
+      const int64_t cell = gini_cell(bf, 0, c, NB, A.Fmax, hct);
+      // (a derived slot: parent - smaller child, read where this block did not write)
+      l = ps ? bins_sum(ps + cell) - bins_sum(hs + cell) : bins_sum(hs + cell);
     }
     so[c] = s_tot[c];
     so[A.plane + c] = l;
