@@ -340,7 +340,10 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
 // NB buckets: 2-entry runs of 8-byte labels and 1-byte counts, written back ~1.7x their
 // bytes as measured by WRITE_SIZE).
 constexpr int kScU = 8;  // rounds of 64 entries per step
-template <bool kStage>
+// kWide (datasets of >= 2^28 rows): the 8-byte labels, buckets and children are addressed by
+// 64-bit pointers with predicated stores -- a buffer resource spans at most 4 GB, and a task's
+// segment (up to a replica's every in-bag row) or the label column (8 N bytes) may not
+template <bool kStage, bool kWide>
 __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits) {
   // (the wave index in an SGPR: the piece, its task and the buffer resources built from them
   // are then wave-uniform, with no per-lane waterfall loop around the buffer operations)
@@ -397,8 +400,13 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
 #pragma unroll
     for (int u = 0; u < kScU; u++) {
       bv[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(re, (int)(min(i0 + 64 * u + lane, last) - t.a), 0, 0);
-      const int yoff = carried ? (int)(min(i0 + 64 * u + lane, last) - t.a) * 8 : (int)((uint32_t)ev[u] * 8u);
-      yv[u] = __builtin_amdgcn_raw_buffer_load_b64(ry, yoff, 0, 0);
+      if constexpr (kWide) {
+        const double* yp = carried ? A.ey_in + min(i0 + 64 * u + lane, last) : A.y + (uint32_t)ev[u];
+        yv[u] = *(const v2u32*)yp;
+      } else {
+        const int yoff = carried ? (int)(min(i0 + 64 * u + lane, last) - t.a) * 8 : (int)((uint32_t)ev[u] * 8u);
+        yv[u] = __builtin_amdgcn_raw_buffer_load_b64(ry, yoff, 0, 0);
+      }
     }
 #pragma unroll
     for (int u = 0; u < kScU; u++) {
@@ -423,16 +431,30 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
         const int64_t base = sb[bin];
         // (positions relative to the task's buckets; invalid lanes store past the end: dropped)
         const uint32_t kp = valid ? (uint32_t)(base - t.kbase + rank) : 0x1FFFFFFEu;
-        __builtin_amdgcn_raw_buffer_store_b64(yv[u], rk, (int)(kp * 8u), 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(e >> 32), rkc, (int)kp, 0, 0);
+        if constexpr (kWide) {
+          if (valid && chain) {
+            *(v2u32*)(A.bky + t.kbase + kp) = yv[u];
+            A.bkc[t.kbase + kp] = (uint8_t)(e >> 32);
+          }
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b64(yv[u], rk, (int)(kp * 8u), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(e >> 32), rkc, (int)kp, 0, 0);
+        }
         if (valid && rank == cnt - 1) sb[bin] = base + cnt;
       }
       const bool left = valid && bin <= (uint32_t)t.s;
       const uint64_t lm = __ballot(left);
       const int64_t lr = __popcll(lm & lt);
       const int64_t pos = left ? lrun + lr : nl + (i - t.a - lrun - lr);  // within the segment
-      rstore64(ro, valid ? (uint32_t)pos * 8u : 0xFFFFFFF0u, e);
-      __builtin_amdgcn_raw_buffer_store_b64(yv[u], roy, valid ? (int)((uint32_t)pos * 8u) : -16, 0, 0);
+      if constexpr (kWide) {
+        if (valid && t.part) {
+          A.ent_out[t.a + pos] = e;
+          if (carried) *(v2u32*)(A.ey_out + t.a + pos) = yv[u];
+        }
+      } else {
+        rstore64(ro, valid ? (uint32_t)pos * 8u : 0xFFFFFFF0u, e);
+        __builtin_amdgcn_raw_buffer_store_b64(yv[u], roy, valid ? (int)((uint32_t)pos * 8u) : -16, 0, 0);
+      }
       lrun += __popcll(lm);
     }
     if constexpr (kStage) {
@@ -490,8 +512,15 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
           const uint32_t kp = ok ? skp[q] : 0x1FFFFFFEu;
           const v2u32 y = sy[ok ? q : 0];
           const uint32_t cb = sc[ok ? q : 0];
-          __builtin_amdgcn_raw_buffer_store_b64(y, rk, (int)(kp * 8u), 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)cb, rkc, (int)kp, 0, 0);
+          if constexpr (kWide) {
+            if (ok) {
+              *(v2u32*)(A.bky + t.kbase + kp) = y;
+              A.bkc[t.kbase + kp] = (uint8_t)cb;
+            }
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b64(y, rk, (int)(kp * 8u), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)cb, rkc, (int)kp, 0, 0);
+          }
         }
         __builtin_amdgcn_wave_barrier();
       }
@@ -1206,10 +1235,15 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
     hipLaunchKernelGGL(k_fb_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
   if (a.ntasks > 0)  // (tasks without pieces still get their bucket bounds)
     hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)a.ntasks), dim3(256), 0, st, a);
-  if (npieces > 0)
-    hipLaunchKernelGGL(scatter_stage ? k_fb_scatter<true> : k_fb_scatter<false>,
-                       dim3((unsigned)((npieces + 3) / 4)), dim3(256), 0, st, a,
-                       npieces, nbits);
+  if (npieces > 0) {
+    const dim3 g((unsigned)((npieces + 3) / 4));
+    if (a.wide)
+      hipLaunchKernelGGL((scatter_stage ? k_fb_scatter<true, true> : k_fb_scatter<false, true>), g, dim3(256), 0,
+                         st, a, npieces, nbits);
+    else
+      hipLaunchKernelGGL((scatter_stage ? k_fb_scatter<true, false> : k_fb_scatter<false, false>), g, dim3(256), 0,
+                         st, a, npieces, nbits);
+  }
   if (a.fused) {  // the chain tasks' sums by k_fb_bchain (no buckets: k_fb_scatter routed only)
     int cbits = 1;
     while (cbits < 8 && (a.cmax >> cbits) != 0) cbits++;

@@ -2032,6 +2032,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.chist = chist;
       ba.cmax = (int32_t)G.cmax;
       ba.fused = fused ? 1 : 0;
+      // (a task's 8-byte arrays or the label column past 2^31 bytes; SBAG_F64_WIDE=1 forces it)
+      ba.wide = (G.N >= ((int64_t)1 << 28) || getenv("SBAG_F64_WIDE")) ? 1 : 0;
       // XCD-aware dispatch of k_fb_count (workgroup w runs on XCD w mod 8, each with its own
       // L2): a piece goes to the XCD of its position within its node's entries, a proxy of
       // its rows' slice of [0, N), so each XCD's bin gathers stay in one eighth of a column
@@ -2541,9 +2543,6 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   if (f64) {
     if (!lab.finite) return fail(SBAG_EINVAL, "labels must be finite");
     if (!lab.label_ok && !lab.approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
-    // (the bucketing kernels address the labels with 32-bit byte offsets)
-    if (ds->N >= ((int64_t)1 << 29))
-      return fail(SBAG_EUNSUPPORTED, "fp64 (non-dyadic) labels: at most 2^29 - 1 rows per dataset");
   }
   // the labels' fixed-point image in the entries: exact for dyadic labels, else (f64 path)
   // the screening approximation k = round(y 2^ashift)
@@ -2785,9 +2784,66 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   // Gini class tiles: regroup the entries to be histogrammed so that each (segment,
   // class tile) is contiguous (k_tile_count / k_tile_scatter into "entG"), and hand the
   // histogram one sub-segment per (segment, tile) with ParentInfo.tile.
+  // the (segment, class tile) entry counts of the next histogram when the host knows them
+  // (gini with every draw count 1: the split's class counts), [segs][ntc]; else null
+  const std::vector<int64_t>* known_tiles = nullptr;
   auto group_tiles = [&](const HistGeom& g, const std::vector<std::pair<int64_t, int64_t>>& segs,
                          const std::vector<ParentInfo>& par, uint64_t** ent_out) -> int {
     const int CT = g.CT, ntc = (NS + CT - 1) / CT;
+    if (known_tiles && known_tiles->size() == segs.size() * (size_t)ntc) {
+      // sub-segments from the known sizes; k_tile_scatter_known places the entries with
+      // atomic (segment, tile) cursors (no count pass, no round trip)
+      const std::vector<int64_t>& kt = *known_tiles;
+      std::vector<HistChunk> pcs;
+      const int64_t kp = tile_scatter_known_piece();
+      std::vector<unsigned long long> cur0(segs.size() * (size_t)ntc);
+      gsegs.clear();
+      gpar.clear();
+      gtile_bounds.assign(segs.size() * (ntc + 1), 0);
+      gtile_ct = CT;
+      for (size_t q = 0; q < segs.size(); q++) {
+        int64_t o = segs[q].first;
+        for (int t = 0; t < ntc; t++) {
+          gtile_bounds[q * (ntc + 1) + t] = o;
+          cur0[q * ntc + t] = (unsigned long long)o;
+          const int64_t n = kt[q * ntc + t];
+          if (n > 0) {
+            gsegs.push_back({o, o + n});
+            ParentInfo pi = par[q];
+            pi.tile = t;
+            gpar.push_back(pi);
+          }
+          o += n;
+        }
+        if (o != segs[q].second)
+          return fail(SBAG_EDEVICE, "internal: class-tile sizes differ from the segment's entries");
+        gtile_bounds[q * (ntc + 1) + ntc] = o;
+        for (int64_t a = segs[q].first; a < segs[q].second; a += kp)
+          pcs.push_back(HistChunk{(int32_t)q, 0, a, std::min(a + kp, segs[q].second), 0, 0, 0, 0});
+      }
+      const int np = (int)pcs.size();
+      HistChunk* d_pcs;
+      unsigned long long* d_cur;
+      uint64_t* d_entg;
+      TRY(ws_typed(c, "tg_pieces", std::max(np, 1), &d_pcs));
+      TRY(ws_typed(c, "tg_cursors", std::max<size_t>(cur0.size(), 1), &d_cur));
+      TRY(ws_typed(c, "entG", (size_t)R * cap, &d_entg));
+      TRY(h2d(c, d_pcs, pcs.data(), pcs.size()));
+      TRY(h2d(c, d_cur, cur0.data(), cur0.size()));
+      launch_tile_scatter_known(c->stream, d_pcs, np, ha.ent_in, CT, ntc, d_cur, d_entg);
+      HIP_TRY(hipGetLastError());
+      if (getenv("SBAG_TILE_CHECK")) {  // (tests: every cursor ends at its tile's end)
+        std::vector<unsigned long long> ce(cur0.size());
+        TRY(d2h(c, ce.data(), d_cur, ce.size()));
+        for (size_t q = 0; q < segs.size(); q++)
+          for (int t = 0; t < ntc; t++)
+            if ((int64_t)ce[q * ntc + t] != gtile_bounds[q * (ntc + 1) + t + 1])
+              return fail(SBAG_EDEVICE, "internal: class-tile cursor does not end at its tile's end");
+      }
+      *ent_out = d_entg;
+      gtile_ent = d_entg;
+      return SBAG_OK;
+    }
     std::vector<HistChunk> pcs;
     std::vector<int> pseg;
     constexpr int64_t kPiece = 1 << 16;
@@ -4164,6 +4220,13 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     std::vector<std::pair<int64_t, int64_t>> hseg;
     std::vector<ParentInfo> hpar;
     std::vector<std::pair<int64_t, int64_t>> ntseg;  // next slots' tile sub-segments
+    // gini bags whose every draw count is 1 (without replacement): a child's class counts are
+    // its entries per class, so the next histogram's class-tile grouping sizes are known
+    // (SBAG_TILE_KNOWN=0: counted on the device as before)
+    static const bool known_env = !(getenv("SBAG_TILE_KNOWN") && atoi(getenv("SBAG_TILE_KNOWN")) == 0);
+    const int kct = g.CT > 0 ? g.CT : NS, kntc = (NS + kct - 1) / kct;
+    const bool known_ok = gini && g.grouped && !tile_res && cmax <= 1 && known_env;
+    std::vector<int64_t> hknown;
     for (int q = 0; q < NPn; q++) {
       const Split& sp = psplit[q];
       HNode& L = trees[sp.r][sp.li];
@@ -4249,6 +4312,12 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       } else if (hs >= 0) {
         hseg.push_back(nseg[hs]);
         hpar.push_back(ParentInfo{sp.r, -1, 0, 0, 0, hs, 0, 0});
+        if (known_ok) {  // its class counts are its entries per class: sizes per class tile
+          const HNode& ch = trees[sp.r][sp.li + (hs == sl ? 0 : 1)];
+          const size_t b0 = hknown.size();
+          hknown.resize(b0 + (size_t)kntc, 0);
+          for (int k = 0; k < NS; k++) hknown[b0 + (size_t)(k / kct)] += ch.stats[k];
+        }
       }
     }
     hmark(5);
@@ -4286,7 +4355,9 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     };
     ha.ent_in = ent_nxt;
     ha.hist = hist_nxt;
+    known_tiles = known_ok && hknown.size() == hseg.size() * (size_t)kntc ? &hknown : nullptr;
     TRY(launch(g, gini ? kHistGini : kHistVar, T_HIST, hseg, hpar));
+    known_tiles = nullptr;
     pre_hist = nullptr;
     derive.clear();
     if (!triples.empty() && gini && fused_sub) {

@@ -292,6 +292,11 @@ void launch_quantize(hipStream_t st, const double* X, int64_t n, int32_t F, cons
                      const int64_t* toff, uint16_t* codes, int32_t S);
 void launch_predict_tiled(hipStream_t st, const PredictArgs& a);
 // class-tile grouping of gini histogram entries (one workgroup per piece)
+// the grouping with known (segment, tile) sizes: cursors[q ntc + t] start at the tile's first
+// position and advance by atomics; pieces of tile_scatter_known_piece() entries
+void launch_tile_scatter_known(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
+                               int CT, int ntc, unsigned long long* cursors, uint64_t* ent_out);
+int tile_scatter_known_piece();
 void launch_tile_count(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
                        int CT, int ntc, uint32_t* counts);
 void launch_tile_scatter(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
@@ -456,6 +461,7 @@ struct F64BucketArgs {
   double* chist;            // [task][NB][3] count, sum, sumSq in Spark's row order
   int32_t cmax;             // largest draw count of an entry (1: no count loop)
   int32_t fused;            // k_fb_bchain sums the chain tasks (no global buckets)
+  int32_t wide, pad2;       // >= 2^28 rows: k_fb_scatter addresses by 64-bit pointers
   const int32_t* porder;    // k_fb_count's piece of each workgroup (null: in order)
 };
 // ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]

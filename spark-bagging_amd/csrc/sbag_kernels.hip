@@ -2324,6 +2324,55 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const HistChunk* 
   }
 }
 
+// The grouping when every (segment, tile) size is known on the host (gini with every draw
+// count 1, e.g. bags without replacement: the split's class counts are the children's entry
+// counts): a workgroup takes a kTkPiece-entry piece of one segment (HistChunk.parent), ranks
+// its entries per tile with returning LDS atomics, reserves each tile's run with one global
+// atomic on the (segment, tile) cursor (set by the host to the tile's start), and writes the
+// entries from registers -- no count pass and no host round trip between them.
+constexpr int kTkPer = 16;                              // entries per thread
+constexpr int kTkPiece = kTkPer * kTileThreads;         // 4096
+__global__ __launch_bounds__(kTileThreads) void k_tile_scatter_known(const HistChunk* __restrict__ pieces,
+                                                                     const uint64_t* __restrict__ ent,
+                                                                     int CT, int ntc,
+                                                                     unsigned long long* __restrict__ cursors,
+                                                                     uint64_t* __restrict__ ent_out) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  unsigned long long* base = (unsigned long long*)smem;  // [ntc] the piece's run of each tile
+  uint32_t* cnt = (uint32_t*)(base + ntc);                // [ntc]
+  const HistChunk pc = pieces[blockIdx.x];
+  const int tid = threadIdx.x;
+  for (int t = tid; t < ntc; t += kTileThreads) cnt[t] = 0u;
+  block_sync();
+  uint64_t e[kTkPer];
+  uint32_t tl[kTkPer], rk[kTkPer];
+  const int64_t last = pc.b - 1;
+#pragma unroll
+  for (int u = 0; u < kTkPer; u++) e[u] = ent[min(pc.a + (int64_t)u * kTileThreads + tid, last)];
+#pragma unroll
+  for (int u = 0; u < kTkPer; u++) {
+    const bool valid = pc.a + (int64_t)u * kTileThreads + tid < pc.b;
+    tl[u] = (uint32_t)(((int32_t)(e[u] >> 32) >> 8) / CT);
+    rk[u] = valid ? atomicAdd(&cnt[tl[u]], 1u) : 0u;
+  }
+  block_sync();
+  for (int t = tid; t < ntc; t += kTileThreads)
+    base[t] = cnt[t] ? atomicAdd(&cursors[(int64_t)pc.parent * ntc + t], (unsigned long long)cnt[t]) : 0ull;
+  block_sync();
+#pragma unroll
+  for (int u = 0; u < kTkPer; u++)
+    if (pc.a + (int64_t)u * kTileThreads + tid < pc.b) ent_out[base[tl[u]] + rk[u]] = e[u];
+}
+
+void launch_tile_scatter_known(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
+                               int CT, int ntc, unsigned long long* cursors, uint64_t* ent_out) {
+  if (npieces <= 0) return;
+  set_max_lds((const void*)k_tile_scatter_known, 160 * 1024);
+  hipLaunchKernelGGL(k_tile_scatter_known, dim3((unsigned)npieces), dim3(kTileThreads), (size_t)ntc * 12, st,
+                     pieces, ent, CT, ntc, cursors, ent_out);
+}
+int tile_scatter_known_piece() { return kTkPiece; }
+
 void launch_tile_count(hipStream_t st, const HistChunk* pieces, int npieces, const uint64_t* ent,
                        int CT, int ntc, uint32_t* counts) {
   if (npieces <= 0) return;

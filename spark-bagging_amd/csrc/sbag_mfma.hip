@@ -199,7 +199,7 @@ size_t mfma_hist_lds_bytes(int R, int ND) {
 
 template <int MT, int ND>
 static void launch_mfma_t(hipStream_t st, const MfmaHistArgs& a, int nblk, size_t lds) {
-  if constexpr (MT * (1 + ND) <= 10) {
+  if constexpr (MT * (1 + ND) <= 12) {
     (void)hipFuncSetAttribute((const void*)k_hist_mfma<MT, ND>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipLaunchKernelGGL((k_hist_mfma<MT, ND>), dim3(nblk), dim3(kMfWaves * 64), lds, st, a);
@@ -220,7 +220,10 @@ static void launch_mfma_m(hipStream_t st, const MfmaHistArgs& a, int nblk, size_
 
 // replicas go in launches of at most MT tiles, MT (1 + ND) <= 10 accumulators (160 VGPRs at
 // two waves per SIMD, no spills)
-int mfma_hist_tiles(int ND) { return std::min(4, 10 / (1 + ND)); }
+int mfma_hist_tiles(int ND) {
+  static const int acc = getenv("SBAG_MFMA_ACC") ? atoi(getenv("SBAG_MFMA_ACC")) : 12;
+  return std::max(1, std::min(4, std::min(12, acc) / (1 + ND)));
+}
 
 bool launch_hist_mfma(hipStream_t st, const MfmaHistArgs& a) {
   if (a.R <= 0 || a.ND < 1 || a.ND > 6 || a.ND1 < 1 || a.ND1 > a.ND || a.NB > 32 || a.F <= 0 || a.N <= 0 || a.N % 16 != 0)

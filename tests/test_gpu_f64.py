@@ -314,3 +314,49 @@ def test_chain_windows_many_bins_large_counts(ctx, monkeypatch, fused):
         ds.free()
     orf = oracle.fit(X, lab, counts[None, :], [sub], max_depth=6, max_bins=255)
     assert_tree_equal(fb, 0, orf, 0)
+
+
+def test_wide_addressing_equals_buffer_path(ctx, cpusmall, monkeypatch):
+    """k_fb_scatter's 64-bit-pointer variant (taken from 2^28 rows on; SBAG_F64_WIDE=1 forces
+    it) gives the buffer-resource variant's trees byte for byte, and the oracle's."""
+    X, y = cpusmall
+    y2 = y * np.pi
+    a = _fit(ctx, X, y2, 4, 7)
+    monkeypatch.setenv("SBAG_F64_WIDE", "1")
+    b = _fit(ctx, X, y2, 4, 7)
+    monkeypatch.setenv("SBAG_F64_NO_CARRY", "1")  # the labels gathered by row, 64-bit
+    c = _fit(ctx, X, y2, 4, 7)
+    for t in range(4):
+        (na, sa), (nb, sb_), (nc, sc) = a.tree(t), b.tree(t), c.tree(t)
+        assert na.tobytes() == nb.tobytes() == nc.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes() == sc.tobytes()
+    N, F = X.shape
+    counts = oracle.bag(True, 1.0, 0, 4, SEED_REG, [0, N], N)
+    subs = [oracle.subspace(1.0, F, SEED_REG + i) for i in range(4)]
+    assert_forest_equal(b, oracle_forest(X, y2, counts, subs, 7, 32, False))
+
+
+def test_fp64_engine_past_2_28_rows(ctx, monkeypatch):
+    """fp64 labels are no longer limited to < 2^29 rows: 2^28 + 4096 rows
+    take the 64-bit-addressed scatter.  The fp64 engine forced on dyadic labels (SBAG_F64=1)
+    must give the integer engine's tree byte for byte -- its row-order fp64 sums of dyadic
+    labels are exact."""
+    N, F = (1 << 28) + 4096, 2
+    ds = nat.DeviceDataset.synthetic(N, F, seed=7, ctx=ctx)
+    try:
+        part = [round(i * N / 256) for i in range(257)]
+
+        def fit():
+            return nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                           learner_end=1, partition_offsets=part, max_depth=3, max_bins=32,
+                           impurity=nat.IMPURITY_VARIANCE)
+
+        a = fit()
+        monkeypatch.setenv("SBAG_F64", "1")
+        b = fit()
+    finally:
+        ds.free()
+    (na, sa), (nb, sb_) = a.tree(0), b.tree(0)
+    assert len(na) > 1
+    assert na.tobytes() == nb.tobytes()
+    assert sa.tobytes() == sb_.tobytes()
