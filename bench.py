@@ -184,7 +184,7 @@ def continuous_fit(nat, ctx, N, F, L, depth, bins, part, steps=1):
                        learner_end=lend, partition_offsets=part, max_depth=depth, max_bins=bins,
                        impurity=nat.IMPURITY_VARIANCE)
 
-    fit(2).free()  # warm
+    fit(L).free()  # warmup: the same fit (its workspace -- ~100 GB of per-replica bins -- is allocated here)
     import torch
     torch.cuda.synchronize()
     t1 = time.perf_counter()

@@ -3785,10 +3785,13 @@ static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_
       (size_t)kRows * S_codes * sizeof(CT) > (size_t)kRows / 16 * 16 * 256 || npad % kRows != 0 ||
       getenv("SBAG_BIN_ROWWISE"))
     return false;
-  // chunks of row blocks: about 4096 workgroups over the replica groups
+  // chunks of row blocks: about 65536 workgroups over the replica groups (SBAG_BIN_WGS; C3-sized
+  // continuous fit 1024 / 4096 / 16384 / 65536 / 262144: 617 / 632 / 548 / 548 / 523 ms on one box,
+  // gpurun_out/r05t/)
+  static const int64_t wgs = getenv("SBAG_BIN_WGS") ? atoll(getenv("SBAG_BIN_WGS")) : 65536;
   const int ngrp = (R + rb - 1) / rb;
   const int64_t nblk = (N + kRows - 1) / kRows;
-  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(nblk, (4096 + ngrp - 1) / ngrp));
+  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(nblk, (wgs + ngrp - 1) / ngrp));
   const int64_t rpc = (nblk + nch - 1) / nch * kRows;
   const dim3 g((unsigned)((N + rpc - 1) / rpc), (unsigned)ngrp);
   set_max_lds((const void*)k_bin_cuts<CT, KT, kRows>, (int)lds);
