@@ -932,7 +932,7 @@ __global__ __launch_bounds__(64) void k_fb_chain64(F64BucketArgs A, int nchain) 
 // ---------------------------------------------------------------- fused bucket chains
 // Bucketing and chains fused (round 5, SBAG_F64_FUSED=1; the default stays the global buckets of
 // k_fb_scatter + k_fb_chainx, which measured faster: 260 vs 294 ms per serialized C3-shape fit,
-// gpurun_out/r05h/ -- the root's few long tasks expose each block's latency).  One workgroup per chain task walks the task's entries
+// profiles/r05logs/r05h/ -- the root's few long tasks expose each block's latency).  One workgroup per chain task walks the task's entries
 // (ent_in / ey_in [t.a, t.b): the node's rows in row order, bins from k_fb_count's ebin) in
 // blocks of kE.  A block is ordered by bin in LDS, stably: each 64-entry round ranks its
 // entries among the same bin's with ballots over the bin bits and counts their draws with

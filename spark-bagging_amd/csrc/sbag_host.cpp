@@ -1999,7 +1999,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       TRY(ws_typed(c, "fb_ebin", (size_t)std::max<int64_t>(1, ebase), &d_ebin));
       // SBAG_F64_FUSED=1: bucketing fused into the chains in LDS (k_fb_bchain, no bucket space);
       // measured slower than the global buckets + k_fb_chainx on the C3 shape (serialized fit
-      // 294 vs 260 ms, gpurun_out/r05h/: a task's blocks are ordered one after another by one
+      // 294 vs 260 ms, profiles/r05logs/r05h/: a task's blocks are ordered one after another by one
       // workgroup, so the root's 256 long tasks expose each block's latency), kept for A/B.
       // (read per call: the tests switch it between fits)
       const bool fused = getenv("SBAG_F64_FUSED") && atoi(getenv("SBAG_F64_FUSED")) != 0 && NB <= 256;

@@ -3584,7 +3584,7 @@ void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S
 // out row-major (the histograms' rows) and as k_partition's column copy (4 rows per word).
 // The LUT form it replaces gathered one byte per (row, feature, replica) from multi-MB tables
 // in L2 (955 ms of a C3-sized continuous fit, profiles/r04bf/); a count of the cuts by VALU
-// compares took 32 compares per bin (380 ms, gpurun_out/r05e/).
+// compares took 32 compares per bin (380 ms, profiles/r05logs/r05e/).
 template <typename CT, typename KT, int kRows>
 __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, int64_t N, int32_t S_codes,
                                                   const int32_t* __restrict__ sub,
@@ -3787,7 +3787,7 @@ static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_
     return false;
   // chunks of row blocks: about 65536 workgroups over the replica groups (SBAG_BIN_WGS; C3-sized
   // continuous fit 1024 / 4096 / 16384 / 65536 / 262144: 617 / 632 / 548 / 548 / 523 ms on one box,
-  // gpurun_out/r05t/)
+  // profiles/r05logs/r05t/)
   static const int64_t wgs = getenv("SBAG_BIN_WGS") ? atoll(getenv("SBAG_BIN_WGS")) : 65536;
   const int ngrp = (R + rb - 1) / rb;
   const int64_t nblk = (N + kRows - 1) / kRows;
@@ -3806,7 +3806,7 @@ static bool launch_bin_cuts_t(hipStream_t st, const CT* codes, int64_t N, int32_
                               uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
                               int64_t npad, int64_t cols_rstride) {
   // 64-row blocks (one row per lane: ~50 KB of LDS with four replicas, three workgroups per CU)
-  // unless SBAG_BIN_ROWS=128 (C3-sized continuous fit 563 vs 604 ms, gpurun_out/r05k/)
+  // unless SBAG_BIN_ROWS=128 (C3-sized continuous fit 563 vs 604 ms, profiles/r05logs/r05k/)
   static const int rows = getenv("SBAG_BIN_ROWS") ? atoi(getenv("SBAG_BIN_ROWS")) : 64;
   if (rows == 128)
     return launch_bin_cuts_r<CT, KT, 128>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out, S_out,

@@ -222,7 +222,7 @@ static void launch_mfma_m(hipStream_t st, const MfmaHistArgs& a, int nblk, size_
 // two waves per SIMD, no spills)
 int mfma_hist_tiles(int ND) {
   // (12 accumulators -- all 128 C3 replicas in one launch -- spill at two waves per SIMD: root
-  // frac 0.49 -> 0.38, gpurun_out/r05s/; SBAG_MFMA_ACC overrides)
+  // frac 0.49 -> 0.38, profiles/r05logs/r05s/; SBAG_MFMA_ACC overrides)
   static const int acc = getenv("SBAG_MFMA_ACC") ? atoi(getenv("SBAG_MFMA_ACC")) : 10;
   return std::max(1, std::min(4, std::min(12, acc) / (1 + ND)));
 }
