@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   // the entries' bins as k_fb_count gathered them (in entry order: coalesced)
   const __amdgpu_buffer_rsrc_t re = rsrc_of(A.ebin + t.ebase, (uint64_t)(t.b - t.a));
   // the task's buckets (labels and counts) and its children's segment (each < 4 GB: a
-  // node's entries); the labels (rows < 2^29)
+  // node's entries); the labels (rows < 2^28 on this path; kWide takes 64-bit pointers)
   const uint64_t nk = chain ? (uint64_t)(t.b - t.a) : 0;
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(A.bky + (chain ? t.kbase : 0), nk * 8);
   const __amdgpu_buffer_rsrc_t rkc = rsrc_of(A.bkc + (chain ? t.kbase : 0), nk);
