@@ -3070,7 +3070,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   int16_t* d_pos;
   TRY(ws_typed(c, "pos", h_pos_codes.size(), &d_pos));
   TRY(h2d(c, d_pos, h_pos_codes.data(), h_pos_codes.size()));
-  std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1), 0);
+  std::vector<uint32_t> vc;  // the subbag's value counts (filled below when a replica uses them)
   const bool optimistic = ds->code_bytes == 1 && ncmax <= tp.max_bins;
   // row-lane histogram: identity byte layout, packed variance words with cshift >= 32
   // (SBAG_HIST_RL: 0 = never, 1 = always 64-bit row addresses; tests pin both paths)
@@ -3085,6 +3085,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   bool root_done = false;
   HistGeom g0{};
   if (optimistic) {
+    vc.assign((size_t)std::max<int64_t>(vc_total, 1), 0);
     if (!hist_geometry(ds->S, Fmax, ncmax, NS, gini, g0, rl_mode_for(h_pos_codes, ds->S)))
       return fail(SBAG_EUNSUPPORTED, "histogram of one feature does not fit in LDS");
     TRY(maybe_grouped(g0, ds->S, ncmax));
@@ -3174,6 +3175,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
                    return true;
                return false;
              }()) {
+    vc.assign((size_t)std::max<int64_t>(vc_total, 1), 0);
     int h = tm.begin(T_VC);
     HistGeom g;
     if (ds->code_bytes == 1 && hist_geometry(ds->S, Fmax, ncmax, 1, true, g)) {
@@ -3225,6 +3227,14 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   // findSplitsForContinuousFeature then sees numSamples = (fraction * n).toInt
   std::vector<double> sfrac(R, 1.0);
   std::vector<uint32_t> vcs;
+  // the sampled replicas' thresholds and cuts from k_find_splits (dev_tc per (replica, feature));
+  // SBAG_SPLITS_HOST=1: the host walk over the value counts copied back (A/B)
+  static const bool bin_lut = getenv("SBAG_BIN_LUT") && atoi(getenv("SBAG_BIN_LUT")) != 0;
+  bool dev_splits = false;
+  const int dev_tc = std::min(520, tp.max_bins + 64);
+  std::vector<int32_t> dev_nt;
+  std::vector<double> dev_thr;
+  std::vector<uint32_t> dev_cut;
   // wide datasets: per replica the (row, weight) items split finding counts
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> items(wide ? R : 0);
   {
@@ -3297,6 +3307,60 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
                                ds->code_bytes, ds->S, d_sub, d_Fr, Fmax, d_svcoff, d_vcs, lds_words);
       HIP_TRY(hipGetLastError());
       tm.end(h);
+      const bool splits_host = getenv("SBAG_SPLITS_HOST") && atoi(getenv("SBAG_SPLITS_HOST")) != 0;
+      if (!wide && !bin_lut && !splits_host && !getenv("SBAG_DEBUG_SAMPLE") && ds->d_dict) {
+        std::vector<int64_t> knw(reps.size()), kns(reps.size());
+        for (size_t k = 0; k < reps.size(); k++) {
+          const int r = reps[k];
+          knw[k] = nw[r];
+          kns[k] = (int64_t)(int32_t)(sfrac[r] * (double)nw[r]);  // (fraction * numExamples).toInt
+        }
+        int32_t *d_zc, *d_nt;
+        int64_t *d_knw, *d_kns;
+        double* d_thr;
+        uint32_t* d_fcut;
+        TRY(ws_typed(c, "fs_zero", (size_t)F, &d_zc));
+        TRY(ws_typed(c, "fs_nw", knw.size(), &d_knw));
+        TRY(ws_typed(c, "fs_ns", kns.size(), &d_kns));
+        TRY(ws_typed(c, "fs_nt", (size_t)R * Fmax, &d_nt));
+        TRY(ws_typed(c, "fs_thr", (size_t)R * Fmax * dev_tc, &d_thr));
+        TRY(ws_typed(c, "fs_cut", (size_t)R * Fmax * dev_tc, &d_fcut));
+        TRY(h2d(c, d_zc, ds->zero_code.data(), (size_t)F));
+        TRY(h2d(c, d_knw, knw.data(), knw.size()));
+        TRY(h2d(c, d_kns, kns.data(), kns.size()));
+        HIP_TRY(hipMemsetAsync(d_nt, 0, (size_t)R * Fmax * 4, c->stream));
+        SplitFindArgs fa{};
+        fa.cnt = d_vcs;
+        fa.vcoff = d_svcoff;
+        fa.dict = ds->d_dict;
+        fa.dict_off = ds->d_dict_off;
+        fa.zero_code = d_zc;
+        fa.sub = d_sub;
+        fa.Fr = d_Fr;
+        fa.reps = d_reps;
+        fa.nw = d_knw;
+        fa.nsamp = d_kns;
+        fa.Fmax = Fmax;
+        fa.max_bins = tp.max_bins;
+        fa.tc = dev_tc;
+        fa.nrep = (int)reps.size();
+        fa.nt = d_nt;
+        fa.thr = d_thr;
+        fa.cut = d_fcut;
+        launch_find_splits(c->stream, fa);
+        HIP_TRY(hipGetLastError());
+        dev_nt.resize((size_t)R * Fmax);
+        TRY(d2h(c, dev_nt.data(), d_nt, dev_nt.size()));
+        dev_splits = true;
+        for (int32_t v : dev_nt)
+          if (v > dev_tc) dev_splits = false;  // (more thresholds than the table holds: host walk)
+        if (dev_splits) {
+          dev_thr.resize((size_t)R * Fmax * dev_tc);
+          dev_cut.resize((size_t)R * Fmax * dev_tc);
+          TRY(d2h(c, dev_thr.data(), d_thr, dev_thr.size()));
+          TRY(d2h(c, dev_cut.data(), d_fcut, dev_cut.size()));
+        }
+      }
       std::vector<uint32_t> snr(reps.size());
       TRY(d2h(c, snr.data(), d_snr, snr.size()));
       for (uint32_t k : snr)
@@ -3311,8 +3375,10 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
           for (uint32_t k = 0; k < snr[ri]; k++) it.emplace_back(rows[ri * cap + k], 1u);
         }
       }
-      vcs.assign((size_t)std::max<int64_t>(vc_total, 1), 0);
-      TRY(d2h(c, vcs.data(), d_vcs, vcs.size()));
+      if (!dev_splits) {
+        vcs.assign((size_t)std::max<int64_t>(vc_total, 1), 0);
+        TRY(d2h(c, vcs.data(), d_vcs, vcs.size()));
+      }
       if (getenv("SBAG_DEBUG_SAMPLE")) {
         for (int r : reps) {
           int64_t tot = 0;
@@ -3330,7 +3396,6 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   std::vector<std::vector<double>> thr((size_t)R * Fmax);
   std::vector<std::vector<uint32_t>> cuts((size_t)R * Fmax);
   std::vector<int32_t> h_nbins((size_t)R * Fmax, 1);
-  static const bool bin_lut = getenv("SBAG_BIN_LUT") && atoi(getenv("SBAG_BIN_LUT")) != 0;
   std::vector<uint8_t> lut(bin_lut ? (size_t)std::max<int64_t>(vc_total, 1) : 0, 0);
   std::vector<int32_t> exact(R, 1);
   bool identity = ds->code_bytes == 1;
@@ -3393,18 +3458,26 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
         }
         for (int fl = 0; fl < h_Fr[r]; fl++) {
           const int g = sub[r][fl];
-          const size_t o = (size_t)vcoff[(size_t)r * Fmax + fl];
-          std::vector<double>& t = thr[(size_t)r * Fmax + fl];
-          const int nt = find_splits(ds->dict[g], (sampled ? vcs.data() : vc.data()) + o, ds->zero_code[g],
-                                     nw[r], nsamp, tp.max_bins, t);
-          h_nbins[(size_t)r * Fmax + fl] = nt + 1;
-          t_nb[w] = std::max(t_nb[w], nt + 1);
+          const size_t rf = (size_t)r * Fmax + fl;
+          const size_t o = (size_t)vcoff[rf];
+          std::vector<double>& t = thr[rf];
+          std::vector<uint32_t>& cu = cuts[rf];
           const auto& d = ds->dict[g];
-          // cut_j = #{dict values <= t_j}: #{t < d[k]} = #{j : cut_j <= k}
-          std::vector<uint32_t>& cu = cuts[(size_t)r * Fmax + fl];
-          cu.resize(t.size());
-          for (size_t j = 0; j < t.size(); j++)
-            cu[j] = (uint32_t)(std::upper_bound(d.begin(), d.end(), t[j]) - d.begin());
+          int nt;
+          if (sampled && dev_splits) {  // k_find_splits' thresholds and cuts
+            nt = dev_nt[rf];
+            t.assign(dev_thr.begin() + rf * dev_tc, dev_thr.begin() + rf * dev_tc + nt);
+            cu.assign(dev_cut.begin() + rf * dev_tc, dev_cut.begin() + rf * dev_tc + nt);
+          } else {
+            nt = find_splits(d, (sampled ? vcs.data() : vc.data()) + o, ds->zero_code[g], nw[r], nsamp,
+                             tp.max_bins, t);
+            // cut_j = #{dict values <= t_j}: #{t < d[k]} = #{j : cut_j <= k}
+            cu.resize(t.size());
+            for (size_t j = 0; j < t.size(); j++)
+              cu[j] = (uint32_t)(std::upper_bound(d.begin(), d.end(), t[j]) - d.begin());
+          }
+          h_nbins[rf] = nt + 1;
+          t_nb[w] = std::max(t_nb[w], nt + 1);
           // the codes are the bins when bin(k) = k for every code k < d.size()
           if ((int)d.size() > nt + 1) {
             t_id[w] = 0;
@@ -3458,21 +3531,36 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   for (const auto& cu : cuts) maxcuts = std::max(maxcuts, cu.size());
   int32_t ncp = 32;
   while ((size_t)ncp < maxcuts + 1) ncp *= 2;
+  // A threshold is a midpoint of two sampled values, so it lies above the smallest dictionary
+  // value -- unless one of the two is the 0.0 that a sample short of numSamples implies for a
+  // feature without zeros: a positive feature's first threshold (0 + v_0) / 2 lies below every
+  // value (cut 0; the feature's bin 0 stays empty).  Such leading zero cuts leave the table
+  // (k_bin_cuts' keys are cut - 1) and are added back per (row, feature) from d_z0.
   auto upload_cuts = [&](int rows, int fw, const std::function<const std::vector<uint32_t>*(int, int)>& at,
-                         uint32_t** d_cut) -> int {
+                         uint32_t** d_cut, const uint8_t** d_z0) -> int {
     std::vector<uint32_t> tab((size_t)rows * fw * ncp, 0xffffffffu);
+    std::vector<uint8_t> z0((size_t)rows * fw, 0);
+    bool any_z0 = false;
     for (int a = 0; a < rows; a++)
       for (int b = 0; b < fw; b++) {
         const std::vector<uint32_t>* cu = at(a, b);
         if (!cu) continue;
-        // (a threshold is a midpoint of two values, so at least the smallest value lies below
-        // it: every cut >= 1, which the kernel's keys cut - 1 rely on)
-        for (uint32_t v : *cu)
-          if (v == 0) return fail(SBAG_EDEVICE, "internal: a threshold below every value");
-        std::copy(cu->begin(), cu->end(), tab.begin() + ((size_t)a * fw + b) * ncp);
+        size_t z = 0;
+        while (z < cu->size() && (*cu)[z] == 0u) z++;
+        if (z > 255) return fail(SBAG_EDEVICE, "internal: more than 255 thresholds below every value");
+        z0[(size_t)a * fw + b] = (uint8_t)z;
+        any_z0 = any_z0 || z > 0;
+        std::copy(cu->begin() + z, cu->end(), tab.begin() + ((size_t)a * fw + b) * ncp);
       }
     TRY(ws_typed(c, "cut", tab.size(), d_cut));
     TRY(h2d(c, *d_cut, tab.data(), tab.size()));
+    *d_z0 = nullptr;
+    if (any_z0) {
+      uint8_t* d;
+      TRY(ws_typed(c, "cut_z0", z0.size(), &d));
+      TRY(h2d(c, d, z0.data(), z0.size()));
+      *d_z0 = d;
+    }
     return SBAG_OK;
   };
   hmark(11);
@@ -3503,15 +3591,16 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       for (int g = 0; g < F; g++) gsub[g] = g;
       int32_t *d_gsub, *d_gF;
       uint32_t* d_cut;
+      const uint8_t* d_z0;
       TRY(ws_typed(c, "gsub", (size_t)F, &d_gsub));
       TRY(ws_typed(c, "gF", 1, &d_gF));
       TRY(h2d(c, d_gsub, gsub.data(), (size_t)F));
       TRY(h2d(c, d_gF, gF.data(), 1));
       TRY(upload_cuts(1, F, [&](int, int g) { return first_rf[g] < 0 ? nullptr : &cuts[first_rf[g]]; },
-                      &d_cut));
+                      &d_cut, &d_z0));
       uint8_t* d_b;
       TRY(ws_typed(c, "bins", (size_t)N * S + 256, &d_b));
-      launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_cut, ncp,
+      launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_cut, ncp, d_z0,
                       d_b, S, 0, nullptr, 0, 0, 0);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemsetAsync(d_b + (size_t)N * S, 0, 256, c->stream));  // zero slack
@@ -3570,15 +3659,16 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
         // bin(code) = #{t < dict[code]} = #{j : cut_j <= code} by VALU compares (k_bin_cuts),
         // the partition's column copy written by the same pass
         uint32_t* d_cut;
+        const uint8_t* d_z0;
         TRY(upload_cuts(R, Fmax, [&](int r, int fl) { return fl < h_Fr[r] ? &cuts[(size_t)r * Fmax + fl] : nullptr; },
-                        &d_cut));
+                        &d_cut, &d_z0));
         uint8_t* d_c;
         const int64_t npad_c = (N + 127) / 128 * 128;
         TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_c, &d_c));
         // (SBAG_BIN_NO_COLS=1: the column copy by k_transpose afterwards, A/B)
         static const bool no_cols = getenv("SBAG_BIN_NO_COLS") != nullptr;
         if (launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R, d_cut, ncp,
-                            d_b, S, (int64_t)N * S, no_cols ? nullptr : d_c, ncol_r, npad_c,
+                            d_z0, d_b, S, (int64_t)N * S, no_cols ? nullptr : d_c, ncol_r, npad_c,
                             (int64_t)ncol_r * npad_c)) {
           cols_direct = d_c;
           cols_direct_npad = npad_c;

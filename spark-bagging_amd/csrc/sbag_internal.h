@@ -233,13 +233,35 @@ void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                             const void* codes, int code_bytes, int32_t S, const int32_t* d_sub,
                             const int32_t* d_Fr, int32_t Fmax, const int64_t* d_vcoff, uint32_t* vc,
                             int lds_words);
+// RandomForest.findSplitsForContinuousFeature on the device for the replicas thresholded on their
+// split-finding sample (k_find_splits: a wave per (replica, feature) over its value counts): the
+// thresholds thr[r][fl][tc] and their code cuts cut[r][fl][tc] (#{dictionary values <= t}), and
+// the threshold count nt[r][fl] (may exceed tc: the caller then falls back to the host)
+struct SplitFindArgs {
+  const uint32_t* cnt;     // value counts, the (replica, feature)'s at vcoff[r * Fmax + fl]
+  const int64_t* vcoff;    // [R * Fmax + 1]
+  const double* dict;      // sorted distinct values of every feature, flat
+  const int64_t* dict_off; // [F + 1]
+  const int32_t* zero_code;  // [F]: the code of 0.0, -1 when absent
+  const int32_t* sub;      // [R][Fmax] global feature of a local one
+  const int32_t* Fr;       // [R]
+  const int32_t* reps;     // [nrep] replicas
+  const int64_t* nw;       // [nrep] numExamples (the subbag's weighted size)
+  const int64_t* nsamp;    // [nrep] numSamples ((fraction * numExamples).toInt)
+  int32_t Fmax, max_bins, tc, nrep;
+  int32_t* nt;             // [R * Fmax]
+  double* thr;             // [R * Fmax][tc]
+  uint32_t* cut;           // [R * Fmax][tc]
+};
+void launch_find_splits(hipStream_t st, const SplitFindArgs& a);
 // per-replica bins out[r][n][fl] = #{j : cut[r][fl][j] <= codes[n][sub[r][fl]]} (cut [R][Fmax][ncp]
-// ascending, every cut >= 1, padded with ~0u; ncp a power of two), zero past F_r; with cols the
+// ascending, every cut >= 1, padded with ~0u; ncp a power of two) + z0[r][fl] (leading zero cuts
+// left out of the table; nullptr: none), zero past F_r; with cols the
 // column copy cols[r][fl < ncol][npad] is written by the same pass when the kernel can (returns
 // true; else the caller transposes)
 bool launch_bin_cuts(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
                      const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut,
-                     int32_t ncp, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
+                     int32_t ncp, const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
                      int64_t npad, int64_t cols_rstride);
 void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, const int32_t* d_labk,
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,

@@ -1338,6 +1338,159 @@ void launch_split_sample_vc(hipStream_t st, const uint32_t* d_rows, int64_t cap,
                      d_vcoff, vc, lds_words);
 }
 
+// Spark 2.4.3 RandomForest.findSplitsForContinuousFeature (the spark-mllib dependency the
+// reference's DecisionTree learners call; the host's find_splits is the same walk) for one (replica, feature) per wave, over its value counts on the device: the weighted
+// (value, count) list is the dictionary order with zero counts dropped and 0.0 carrying
+// numSamples - (non-zero count), inserted at its sorted place when the dictionary lacks it.
+// Midpoints of consecutive values when there are at most numSplits + 1 of them; else the
+// stride walk: with current the running int count, a value's midpoint with its predecessor is
+// taken when |prev - target| < |current - target|, then target += stride.  prev and current are
+// prefix sums that do not depend on the choices, so a chunk of 64 entries evaluates the test in
+// every lane, takes the first lane that passes, advances target and retests the lanes after it
+// -- the host loop's order and fp64 operations exactly.  The cuts (#{values <= t}) are a binary
+// search of the dictionary per threshold.  It replaces the value counts' copy to the host (a
+// C3-sized continuous fit: 4 bytes per (replica, feature, dictionary value), 0.5 GB per learner
+// half) and the host walk over them.
+constexpr int kFindSplitsMaxTc = 520;
+__global__ __launch_bounds__(64) void k_find_splits(SplitFindArgs A) {
+  __shared__ double s_thr[kFindSplitsMaxTc];
+  const int lane = threadIdx.x;
+  const int k = blockIdx.y, fl = blockIdx.x;
+  const int r = A.reps[k];
+  if (fl >= A.Fr[r]) return;
+  const int64_t rf = (int64_t)r * A.Fmax + fl;
+  const int g = A.sub[rf];
+  const double* d = A.dict + A.dict_off[g];
+  const int64_t D = A.dict_off[g + 1] - A.dict_off[g];
+  const uint32_t* cn = A.cnt + A.vcoff[rf];
+  const int64_t z = A.zero_code[g];
+  // non-zero count and values other than 0.0 present
+  unsigned long long nnz = 0, nvz = 0;
+  for (int64_t c = lane; c < D; c += 64) {
+    const uint32_t v = cn[c];
+    if (c != z) {
+      nnz += v;
+      nvz += v != 0u ? 1ull : 0ull;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    nnz += __shfl_xor(nnz, o);
+    nvz += __shfl_xor(nvz, o);
+  }
+  if (nnz == 0) {  // featureSamples.isEmpty
+    if (lane == 0) A.nt[rf] = 0;
+    return;
+  }
+  const int64_t n = A.nw[k], num_samples = A.nsamp[k];
+  const int64_t num_splits = min((int64_t)A.max_bins, n) - 1;
+  const int64_t zeros = num_samples - (int64_t)nnz;
+  const int64_t possible = (int64_t)nvz + (zeros > 0 ? 1 : 0) - 1;
+  if (possible == 0) {
+    if (lane == 0) A.nt[rf] = 0;
+    return;
+  }
+  const bool mids = possible <= num_splits;
+  // the implied 0.0's place when the dictionary lacks it: #{values < 0}
+  int64_t zp = -1;
+  if (z < 0 && zeros > 0) {
+    int64_t lo = 0, hi = D;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (d[mid] < 0.0)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    zp = lo;
+  }
+  const int64_t X = D + (zp >= 0 ? 1 : 0);
+  const int tc = A.tc;
+  const double stride = (double)num_samples / (double)(num_splits + 1);
+  double target = stride;
+  bool have_prev = false;
+  double prev_val = 0.0;
+  uint32_t cur = 0;  // Java int running count (wraps as the host's int32_t)
+  int64_t rank = 0;  // valid entries before the chunk
+  int64_t nt = 0;
+  for (int64_t x0 = 0; x0 < X; x0 += 64) {
+    const int64_t x = x0 + lane;
+    double v = 0.0;
+    uint32_t cv = 0u;
+    if (x < X) {
+      if (x == zp) {
+        cv = (uint32_t)zeros;
+      } else {
+        const int64_t c = (zp >= 0 && x > zp) ? x - 1 : x;
+        if (c == z) {
+          cv = zeros > 0 ? (uint32_t)zeros : 0u;
+        } else {
+          cv = cn[c];
+          v = d[c];
+        }
+      }
+    }
+    const bool valid = cv != 0u;
+    const uint64_t vm = __ballot(valid);
+    if (!vm) continue;
+    uint32_t s = cv;  // inclusive prefix of the chunk's counts
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(s, o);
+      if (lane >= o) s += t;
+    }
+    const uint32_t cur_i = cur + s, prev_i = cur_i - cv;
+    const uint64_t below = vm & ((1ull << lane) - 1ull);
+    const int pl = below ? 63 - __clzll((long long)below) : 0;
+    const double pv_l = __shfl(v, pl);
+    const double pv = below ? pv_l : prev_val;
+    const bool cand = valid && (below != 0ull || have_prev);
+    const double mid = (pv + v) / 2.0;
+    if (mids) {
+      const int64_t rk = rank + __popcll(below);  // this entry's place among the valid ones
+      if (cand && rk - 1 < tc) s_thr[rk - 1] = mid;
+    } else {
+      uint64_t left = __ballot(cand);
+      while (left) {
+        const bool p = cand && fabs((double)(int32_t)prev_i - target) < fabs((double)(int32_t)cur_i - target);
+        const uint64_t pm = __ballot(p) & left;
+        if (!pm) break;
+        const int f = __ffsll((unsigned long long)pm) - 1;
+        const double m = __shfl(mid, f);
+        if (lane == 0 && nt < tc) s_thr[nt] = m;
+        nt++;
+        target += stride;
+        left &= f == 63 ? 0ull : ~((2ull << f) - 1ull);
+      }
+    }
+    const int lv = 63 - __clzll((long long)vm);
+    prev_val = __shfl(v, lv);
+    cur = __shfl(cur_i, 63);
+    have_prev = true;
+    rank += __popcll(vm);
+  }
+  if (mids) nt = possible;
+  __syncthreads();
+  if (lane == 0) A.nt[rf] = (int32_t)min<int64_t>(nt, 0x7fffffff);
+  const int64_t m = min<int64_t>(nt, tc);
+  for (int64_t j = lane; j < m; j += 64) {
+    const double t = s_thr[j];
+    int64_t lo = 0, hi = D;  // first value > t
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (d[mid] <= t)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    A.thr[rf * tc + j] = t;
+    A.cut[rf * tc + j] = (uint32_t)lo;
+  }
+}
+
+void launch_find_splits(hipStream_t st, const SplitFindArgs& a) {
+  if (a.nrep == 0 || a.Fmax == 0) return;
+  hipLaunchKernelGGL(k_find_splits, dim3((unsigned)a.Fmax, (unsigned)a.nrep), dim3(64), 0, st, a);
+}
+
 // ======================================================================
 // Bernoulli sampler: XORShiftRandom is GF(2)-linear; a thread jumps its
 // stream to row j0 with precomputed M^(2^k) matrices and then steps 256 rows.
@@ -3590,6 +3743,7 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
                                                   const int32_t* __restrict__ sub,
                                                   const int32_t* __restrict__ Fr, int32_t Fmax,
                                                   const uint32_t* __restrict__ cut, int32_t ncp, int32_t lg,
+                                                  const uint8_t* __restrict__ z0,
                                                   uint8_t* __restrict__ out, int32_t S_out, int64_t out_rstride,
                                                   uint8_t* __restrict__ cols, int32_t ncol, int64_t npad,
                                                   int64_t cols_rstride, int R, int rb, int64_t rows_per_chunk) {
@@ -3607,6 +3761,8 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
   for (int64_t k = tid; k < (int64_t)nrep * Fmax * ncp; k += 256) {
     const uint32_t c = cut[(int64_t)r0 * Fmax * ncp + k];
     sk[k] = c == 0xffffffffu ? (KT)~(KT)0 : (KT)(c - 1u);
+    // (slot ncp - 1, never read by the search: the (replica, feature)'s leading zero cuts)
+    if (z0 && (k & (ncp - 1)) == ncp - 1) sk[k] = (KT)z0[(int64_t)r0 * Fmax + k / ncp];
   }
   const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk, c1 = min(N, c0 + rows_per_chunk);
   const int ngrp4 = S_out / 4;
@@ -3694,6 +3850,13 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
         } else {
           for (int st = lg - 1; st >= 0; st--) step(1u << st);
         }
+        if (z0)
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t zk = (uint32_t)ks[k][ncp - 1];
+#pragma unroll
+            for (int i = 0; i < kRpl; i++) idx[k][i] += zk;
+          }
 #pragma unroll
         for (int k = 0; k < 4; k++)
           if (4 * q + k < fr)
@@ -3736,6 +3899,7 @@ __global__ __launch_bounds__(256) void k_bin_cuts_rows(const CT* __restrict__ co
                                                        const int32_t* __restrict__ sub,
                                                        const int32_t* __restrict__ Fr, int32_t Fmax,
                                                        const uint32_t* __restrict__ cut, int32_t ncp,
+                                                       const uint8_t* __restrict__ z0,
                                                        uint8_t* __restrict__ out, int32_t S_out,
                                                        int64_t out_rstride) {
   const int r = blockIdx.y;
@@ -3757,7 +3921,7 @@ __global__ __launch_bounds__(256) void k_bin_cuts_rows(const CT* __restrict__ co
         else
           hi = mid;
       }
-      b = (uint32_t)lo;
+      b = (uint32_t)lo + (z0 ? (uint32_t)z0[(int64_t)r * Fmax + fl] : 0u);
     }
     o[fl] = (uint8_t)b;
   }
@@ -3766,8 +3930,8 @@ __global__ __launch_bounds__(256) void k_bin_cuts_rows(const CT* __restrict__ co
 template <typename CT, typename KT, int kRows>
 static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
                               const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
-                              uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
-                              int64_t npad, int64_t cols_rstride) {
+                              const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols,
+                              int32_t ncol, int64_t npad, int64_t cols_rstride) {
   const size_t tiles = (size_t)kRows * (S_codes * sizeof(CT) + 4) + (size_t)kRows * (S_out + 4);
   const size_t per_rep = (size_t)Fmax * ncp * sizeof(KT);
   // replicas per workgroup: up to 4 (they share the staged codes) within the LDS target, so that
@@ -3796,55 +3960,55 @@ static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_
   const dim3 g((unsigned)((N + rpc - 1) / rpc), (unsigned)ngrp);
   set_max_lds((const void*)k_bin_cuts<CT, KT, kRows>, (int)lds);
   hipLaunchKernelGGL((k_bin_cuts<CT, KT, kRows>), g, dim3(256), lds, st, codes, N, S_codes, d_sub, d_Fr, Fmax,
-                     d_cut, ncp, lg, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb, rpc);
+                     d_cut, ncp, lg, d_z0, out, S_out, out_rstride, cols, ncol, npad, cols_rstride, R, rb, rpc);
   return true;
 }
 
 template <typename CT, typename KT>
 static bool launch_bin_cuts_t(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
                               const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
-                              uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
-                              int64_t npad, int64_t cols_rstride) {
+                              const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols,
+                              int32_t ncol, int64_t npad, int64_t cols_rstride) {
   // 64-row blocks (one row per lane: ~50 KB of LDS with four replicas, three workgroups per CU)
   // unless SBAG_BIN_ROWS=128 (C3-sized continuous fit 563 vs 604 ms, profiles/r05logs/r05k/)
   static const int rows = getenv("SBAG_BIN_ROWS") ? atoi(getenv("SBAG_BIN_ROWS")) : 64;
   if (rows == 128)
-    return launch_bin_cuts_r<CT, KT, 128>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out, S_out,
+    return launch_bin_cuts_r<CT, KT, 128>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0, out, S_out,
                                           out_rstride, cols, ncol, npad, cols_rstride);
-  return launch_bin_cuts_r<CT, KT, 64>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out, S_out,
+  return launch_bin_cuts_r<CT, KT, 64>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0, out, S_out,
                                        out_rstride, cols, ncol, npad, cols_rstride);
 }
 
 template <typename CT>
 static bool launch_bin_cuts_any(hipStream_t st, const CT* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
                                 const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
-                                uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
-                                int64_t npad, int64_t cols_rstride) {
+                                const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride,
+                                uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride) {
   const bool ok = sizeof(CT) <= 2
-                      ? launch_bin_cuts_t<CT, uint16_t>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
-                                                        S_out, out_rstride, cols, ncol, npad, cols_rstride)
-                      : launch_bin_cuts_t<CT, uint32_t>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
-                                                        S_out, out_rstride, cols, ncol, npad, cols_rstride);
+                      ? launch_bin_cuts_t<CT, uint16_t>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0,
+                                                        out, S_out, out_rstride, cols, ncol, npad, cols_rstride)
+                      : launch_bin_cuts_t<CT, uint32_t>(st, codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0,
+                                                        out, S_out, out_rstride, cols, ncol, npad, cols_rstride);
   if (ok) return cols != nullptr;
   // rows too wide for the staged tiles: a thread per row (no column copy)
   const dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
   hipLaunchKernelGGL(k_bin_cuts_rows<CT>, grid, dim3(256), 0, st, codes, N, S_codes, d_sub, d_Fr, Fmax, d_cut,
-                     ncp, out, S_out, out_rstride);
+                     ncp, d_z0, out, S_out, out_rstride);
   return false;
 }
 
 bool launch_bin_cuts(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
                      const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut,
-                     int32_t ncp, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols, int32_t ncol,
-                     int64_t npad, int64_t cols_rstride) {
+                     int32_t ncp, const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride,
+                     uint8_t* cols, int32_t ncol, int64_t npad, int64_t cols_rstride) {
   if (code_bytes == 1)
-    return launch_bin_cuts_any(st, (const uint8_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
-                               S_out, out_rstride, cols, ncol, npad, cols_rstride);
+    return launch_bin_cuts_any(st, (const uint8_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0,
+                               out, S_out, out_rstride, cols, ncol, npad, cols_rstride);
   if (code_bytes == 2)
-    return launch_bin_cuts_any(st, (const uint16_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
-                               S_out, out_rstride, cols, ncol, npad, cols_rstride);
-  return launch_bin_cuts_any(st, (const uint32_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, out,
-                             S_out, out_rstride, cols, ncol, npad, cols_rstride);
+    return launch_bin_cuts_any(st, (const uint16_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0,
+                               out, S_out, out_rstride, cols, ncol, npad, cols_rstride);
+  return launch_bin_cuts_any(st, (const uint32_t*)codes, N, S_codes, d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0,
+                             out, S_out, out_rstride, cols, ncol, npad, cols_rstride);
 }
 
 // Value counts with global atomics (u16 codes / dictionaries too large for LDS)

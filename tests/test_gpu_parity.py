@@ -437,6 +437,47 @@ def test_sampled_split_finding(ctx, n_rows, cls, P):
     assert_forest_equal(forest, orf)
 
 
+@pytest.mark.parametrize("cls", [False, True])
+def test_device_split_finding_edge_features(ctx, monkeypatch, cls):
+    """findSplitsForContinuousFeature on the device (k_find_splits, a wave per (replica,
+    feature)) on the cases its walk branches on: 0.0 in the dictionary or only implied by a
+    sample short of numSamples (inserted first, last or in the middle), at most numSplits + 1
+    values (midpoints), just above it (stride walk), a constant and an all-zero feature, mostly
+    zeros.  Bit-exact against the oracle, as is the host walk over the value counts copied back
+    (SBAG_SPLITS_HOST=1)."""
+    rng = np.random.default_rng(11 + int(cls))
+    n, P, L = 60000, 4, 4
+    c0 = np.round(rng.normal(size=n), 3)
+    c0[rng.random(n) < 0.1] = 0.0
+    c3 = np.round(rng.normal(size=n), 3)
+    c3[c3 == 0.0] = 0.5
+    c7 = np.where(rng.random(n) < 0.97, 0.0, np.round(rng.normal(size=n), 2))
+    X = np.stack([c0,
+                  np.round(rng.uniform(1, 2, n), 4),        # positive only: 0.0 implied first
+                  -np.round(rng.uniform(1, 2, n), 4),       # negative only: 0.0 implied last
+                  c3,                                       # both signs, no 0.0: in the middle
+                  rng.integers(0, 10, n).astype(np.float64),  # midpoints
+                  np.full(n, 3.0),                          # constant
+                  np.zeros(n),                              # all zeros
+                  c7,
+                  rng.choice(np.round(rng.normal(size=40), 3), n)], axis=1)  # stride, few values
+    y = (rng.integers(0, 4, n) if cls else rng.integers(-256, 256, n) / 16).astype(np.float64)
+    part = [int(round(i * n / P)) for i in range(P + 1)]
+    seed = SEED_CLS if cls else SEED_REG
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    kw = dict(replacement=True, sample_ratio=1.0, seed=seed, learner_begin=0, learner_end=L,
+              partition_offsets=part, max_depth=6, max_bins=32, subspace_ratio=1.0,
+              subspace_bug_compat=False, impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    forest = nat.fit(ctx, ds, **kw)
+    counts = oracle.bag(True, 1.0, 0, L, seed, part, n)
+    assert oracle.split_sample_fraction(int(counts[0].sum()), 32) < 1.0
+    subs = [oracle.subspace(1.0, X.shape[1], seed + i) for i in range(L)]
+    orf = oracle_forest(X, y, counts, subs, 6, 32, cls, part=part)
+    assert_forest_equal(forest, orf)
+    monkeypatch.setenv("SBAG_SPLITS_HOST", "1")
+    assert_forest_equal(nat.fit(ctx, ds, **kw), orf)
+
+
 @pytest.mark.parametrize("cls,replacement,ratio", [(False, True, 1.0), (True, True, 1.0),
                                                   (False, False, 0.1)])
 def test_wide_features_more_than_65536_values(ctx, cls, replacement, ratio):
