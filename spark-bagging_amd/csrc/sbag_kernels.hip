@@ -3753,7 +3753,8 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r0 = blockIdx.y * rb, nrep = min(rb, R - r0);
   const int pc = S_codes * (int)sizeof(CT) + 4;  // code row pitch in LDS (bytes)
-  const int pb = S_out + 4;                      // bin row pitch
+  // bin row pitch: an odd number of words (a row per lane writes 64 distinct banks)
+  const int pb = ((S_out / 4) & 1) ? S_out : S_out + 4;
   KT* sk = (KT*)smem;                            // [rb][Fmax][ncp] keys
   const size_t kbytes = ((size_t)rb * Fmax * ncp * sizeof(KT) + 15) & ~(size_t)15;
   uint8_t* sc = smem + kbytes;
@@ -3780,16 +3781,22 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
 #pragma unroll
     for (int v = 0; v < kPv; v++) pv[v] = src[min((int64_t)(tid + 256 * v), lim - 1)];
   };
+  // (each piece's LDS place, computed once: the division by rq is not per block)
+  int soff[kPv];
+#pragma unroll
+  for (int v = 0; v < kPv; v++) {
+    const int k = tid + 256 * v;
+    const int row = k / rq, w = k - row * rq;
+    soff[v] = k < kRows * rq ? row * pc + 16 * w : -1;
+  }
   if (c0 < c1) load_block(c0);
   for (int64_t n0 = c0; n0 < c1; n0 += kRows) {
     const int nr = (int)min<int64_t>(kRows, c1 - n0);
     block_sync();  // (the previous block's tile reads; the keys at the first block)
 #pragma unroll
     for (int v = 0; v < kPv; v++) {
-      const int k = tid + 256 * v;
-      if (k < kRows * rq) {
-        const int row = k / rq, w = k - row * rq;
-        uint32_t* d = (uint32_t*)(sc + row * pc + 16 * w);
+      if (soff[v] >= 0) {
+        uint32_t* d = (uint32_t*)(sc + soff[v]);
         d[0] = pv[v].x;
         d[1] = pv[v].y;
         d[2] = pv[v].z;
@@ -3841,6 +3848,9 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
 #pragma unroll
             for (int i = 0; i < kRpl; i++) idx[k][i] += (uint32_t)ks[k][idx[k][i] + h - 1u] < cv[k][i] ? h : 0u;
         };
+        // (measured on a C3-sized continuous fit: a two-level search with packed u16 counts, two
+        // dependent LDS reads instead of five, took the same 83.8 ms per launch -- the kernel's
+        // VALU issue, not the search's latency, bounds it; profiles/r05logs/r05z/)
         if (lg == 5) {
           step(16u);
           step(8u);
@@ -3867,24 +3877,47 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
       }
       block_sync();
       {
-        const int wpr = S_out / 4;  // output words per row
-        uint32_t* o = (uint32_t*)(out + (int64_t)r * out_rstride + n0 * S_out);
-        for (int k = tid; k < nr * wpr; k += 256) {
-          const int row = k / wpr, w = k - row * wpr;
-          o[k] = *(const uint32_t*)(sb + row * pb + 4 * w);
+        uint8_t* o = out + (int64_t)r * out_rstride + n0 * S_out;
+        if (pb == S_out) {  // the tile is the block's rows as they go out
+          const int nb = nr * S_out;
+          if ((((uintptr_t)o) & 15) == 0) {
+            for (int k = tid; k < nb / 16; k += 256) ((uint4*)o)[k] = ((const uint4*)sb)[k];
+            for (int k = nb / 16 * 4 + tid; k < nb / 4; k += 256) ((uint32_t*)o)[k] = ((const uint32_t*)sb)[k];
+          } else {
+            for (int k = tid; k < nb / 4; k += 256) ((uint32_t*)o)[k] = ((const uint32_t*)sb)[k];
+          }
+        } else {
+          const int wpr = S_out / 4;  // output words per row
+          for (int row = tid >> 5; row < nr; row += 8)
+            for (int w = tid & 31; w < wpr; w += 32)
+              ((uint32_t*)o)[row * wpr + w] = *(const uint32_t*)(sb + row * pb + 4 * w);
         }
       }
       if (cols) {  // per feature the block's rows are consecutive bytes (rows past N: 0)
+        // a thread takes a 4 x 4 byte block (rows 4 rq.., features 4 fq..): four word reads of
+        // the tile, a byte transpose by v_perm, one word per feature column
+        constexpr int kRq = kRows / 4;
         uint8_t* cr = cols + (int64_t)r * cols_rstride + n0;
-        for (int k = tid; k < ncol * (kRows / 4); k += 256) {
-          const int fl = k / (kRows / 4), wd = k - fl * (kRows / 4);
-          uint32_t v = 0;
+        for (int t = tid; t < (ncol + 3) / 4 * kRq; t += 256) {
+          const int fq = t / kRq, rq4 = t % kRq;
+          uint32_t d[4];
 #pragma unroll
           for (int kk = 0; kk < 4; kk++) {
-            const int row = 4 * wd + kk;
-            if (row < nr) v |= (uint32_t)sb[row * pb + fl] << (8 * kk);
+            const int row = 4 * rq4 + kk;
+            const uint32_t x = *(const uint32_t*)(sb + row * pb + 4 * fq);
+            d[kk] = row < nr ? x : 0u;
           }
-          *(uint32_t*)(cr + (int64_t)fl * npad + 4 * wd) = v;
+          const uint32_t lo01 = __builtin_amdgcn_perm(d[1], d[0], 0x05010400u);
+          const uint32_t hi01 = __builtin_amdgcn_perm(d[1], d[0], 0x07030602u);
+          const uint32_t lo23 = __builtin_amdgcn_perm(d[3], d[2], 0x05010400u);
+          const uint32_t hi23 = __builtin_amdgcn_perm(d[3], d[2], 0x07030602u);
+          const uint32_t f4[4] = {__builtin_amdgcn_perm(lo23, lo01, 0x05040100u),
+                                  __builtin_amdgcn_perm(lo23, lo01, 0x07060302u),
+                                  __builtin_amdgcn_perm(hi23, hi01, 0x05040100u),
+                                  __builtin_amdgcn_perm(hi23, hi01, 0x07060302u)};
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            if (4 * fq + i < ncol) *(uint32_t*)(cr + (int64_t)(4 * fq + i) * npad + 4 * rq4) = f4[i];
         }
       }
       if (ri + 1 < nrep) block_sync();  // the tile is rewritten by the next replica
@@ -3941,9 +3974,9 @@ static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_
   int rb = rb_env > 0 ? rb_env : 4;
   while (rb > 1 && tiles + rb * per_rep + 16 > (size_t)lds_kb * 1024) rb--;
   rb = std::max(1, std::min(rb, R));
-  const size_t lds = tiles + ((rb * per_rep + 15) & ~(size_t)15);
   int lg = 0;
   while ((1 << lg) < ncp) lg++;
+  const size_t lds = tiles + ((rb * per_rep + 15) & ~(size_t)15);
   // (the staged code rows: 16-byte pieces, at most kRows / 16 per thread per block)
   if (lds > 150 * 1024 || (1 << lg) != ncp || S_out % 4 != 0 || (S_codes * sizeof(CT)) % 16 != 0 ||
       (size_t)kRows * S_codes * sizeof(CT) > (size_t)kRows / 16 * 16 * 256 || npad % kRows != 0 ||
