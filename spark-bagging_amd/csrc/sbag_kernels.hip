@@ -3848,10 +3848,18 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
 #pragma unroll
             for (int i = 0; i < kRpl; i++) idx[k][i] += (uint32_t)ks[k][idx[k][i] + h - 1u] < cv[k][i] ? h : 0u;
         };
-        // (measured on a C3-sized continuous fit: a two-level search with packed u16 counts, two
-        // dependent LDS reads instead of five, took the same 83.8 ms per launch -- the kernel's
-        // VALU issue, not the search's latency, bounds it; profiles/r05logs/r05z/)
+        // (measured on a C3-sized continuous fit, 64 keys: a two-level search with packed u16
+        // counts took the same 83.8 ms per launch, profiles/r05logs/r05z/; one search per pair
+        // of replicas over their union of keys, half the searches, took 124 vs 78 ms -- its
+        // tables halve the workgroups per CU, profiles/r05logs/r05z5/)
         if (lg == 5) {
+          step(16u);
+          step(8u);
+          step(4u);
+          step(2u);
+          step(1u);
+        } else if (lg == 6) {  // (a replica's 32nd threshold: common on continuous features)
+          step(32u);
           step(16u);
           step(8u);
           step(4u);
@@ -3965,14 +3973,17 @@ static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_
                               const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
                               const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols,
                               int32_t ncol, int64_t npad, int64_t cols_rstride) {
-  const size_t tiles = (size_t)kRows * (S_codes * sizeof(CT) + 4) + (size_t)kRows * (S_out + 4);
+  const int pb = ((S_out / 4) & 1) ? S_out : S_out + 4;  // (the kernel's bin row pitch)
+  const size_t tiles = (size_t)kRows * (S_codes * sizeof(CT) + 4) + (size_t)kRows * pb;
   const size_t per_rep = (size_t)Fmax * ncp * sizeof(KT);
-  // replicas per workgroup: up to 4 (they share the staged codes) within the LDS target, so that
-  // several workgroups fit a CU (SBAG_BIN_RB / SBAG_BIN_LDS_KB override)
+  // replicas per workgroup (they share the staged codes) within the LDS target.  One by default:
+  // the occupancy it buys outweighs re-reading the codes per replica (C3-sized continuous fit,
+  // 64 keys: 57.7 ms per launch at one, 65.9 at two; profiles/r05logs/r05z6/).  SBAG_BIN_RB /
+  // SBAG_BIN_LDS_KB override
   static const int rb_env = getenv("SBAG_BIN_RB") ? atoi(getenv("SBAG_BIN_RB")) : 0;
   static const int lds_kb = getenv("SBAG_BIN_LDS_KB") ? atoi(getenv("SBAG_BIN_LDS_KB")) : 52;
-  int rb = rb_env > 0 ? rb_env : 4;
-  while (rb > 1 && tiles + rb * per_rep + 16 > (size_t)lds_kb * 1024) rb--;
+  int rb = rb_env > 0 ? rb_env : 1;
+  while (rb > 1 && tiles + rb * per_rep > (size_t)lds_kb * 1024) rb--;
   rb = std::max(1, std::min(rb, R));
   int lg = 0;
   while ((1 << lg) < ncp) lg++;
