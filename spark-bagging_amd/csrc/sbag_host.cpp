@@ -3525,12 +3525,15 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
           shared = false;
       }
   }
-  // the cut table [rows][Fmax'][ncp] (padded with ~0u, ncp a power of two >= 32; k_bin_cuts
-  // binary-searches it)
+  // the cut table [rows][Fmax'][ncp] (padded with ~0u, ncp a power of two >= 32 holding the most
+  // cuts: maxBins 32 with a 32nd threshold still takes 32 slots; k_bin_cuts binary-searches it)
   size_t maxcuts = 1;
   for (const auto& cu : cuts) maxcuts = std::max(maxcuts, cu.size());
   int32_t ncp = 32;
-  while ((size_t)ncp < maxcuts + 1) ncp *= 2;
+  while ((size_t)ncp < maxcuts) ncp *= 2;
+  if (getenv("SBAG_DEBUG_BINS"))
+    fprintf(stderr, "[sbag] cut table: maxcuts %zu ncp %d identity %d shared %d\n", maxcuts, ncp, (int)identity,
+            (int)shared);
   // A threshold is a midpoint of two sampled values, so it lies above the smallest dictionary
   // value -- unless one of the two is the 0.0 that a sample short of numSamples implies for a
   // feature without zeros: a positive feature's first threshold (0 + v_0) / 2 lies below every

@@ -3757,14 +3757,16 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
   const int pb = ((S_out / 4) & 1) ? S_out : S_out + 4;
   KT* sk = (KT*)smem;                            // [rb][Fmax][ncp] keys
   const size_t kbytes = ((size_t)rb * Fmax * ncp * sizeof(KT) + 15) & ~(size_t)15;
-  uint8_t* sc = smem + kbytes;
+  uint8_t* sz = smem + kbytes;                   // [rb][Fmax] leading zero cuts (with z0)
+  const size_t zbytes = z0 ? ((size_t)rb * Fmax + 15) & ~(size_t)15 : 0;
+  uint8_t* sc = sz + zbytes;
   uint8_t* sb = sc + (size_t)kRows * pc;
   for (int64_t k = tid; k < (int64_t)nrep * Fmax * ncp; k += 256) {
     const uint32_t c = cut[(int64_t)r0 * Fmax * ncp + k];
     sk[k] = c == 0xffffffffu ? (KT)~(KT)0 : (KT)(c - 1u);
-    // (slot ncp - 1, never read by the search: the (replica, feature)'s leading zero cuts)
-    if (z0 && (k & (ncp - 1)) == ncp - 1) sk[k] = (KT)z0[(int64_t)r0 * Fmax + k / ncp];
   }
+  if (z0)
+    for (int k = tid; k < nrep * Fmax; k += 256) sz[k] = z0[(int64_t)r0 * Fmax + k];
   const int64_t c0 = (int64_t)blockIdx.x * rows_per_chunk, c1 = min(N, c0 + rows_per_chunk);
   const int ngrp4 = S_out / 4;
   // the code rows of a block as 16-byte pieces, kPv per thread, loaded one block ahead into
@@ -3868,13 +3870,15 @@ __global__ __launch_bounds__(256) void k_bin_cuts(const CT* __restrict__ codes, 
         } else {
           for (int st = lg - 1; st >= 0; st--) step(1u << st);
         }
-        if (z0)
+        // the steps count the keys of slots 0 .. ncp - 2; slot ncp - 1 (a 32nd cut in 32 slots,
+        // else padding) by one more compare off the dependent chain, then the leading zero cuts
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const uint32_t zk = (uint32_t)ks[k][ncp - 1];
+        for (int k = 0; k < 4; k++) {
+          const uint32_t kl = (uint32_t)ks[k][ncp - 1];
+          const uint32_t zk = z0 ? (uint32_t)sz[ri * Fmax + min(4 * q + k, fr - 1)] : 0u;
 #pragma unroll
-            for (int i = 0; i < kRpl; i++) idx[k][i] += zk;
-          }
+          for (int i = 0; i < kRpl; i++) idx[k][i] += (kl < cv[k][i] ? 1u : 0u) + zk;
+        }
 #pragma unroll
         for (int k = 0; k < 4; k++)
           if (4 * q + k < fr)
@@ -3987,7 +3991,7 @@ static bool launch_bin_cuts_r(hipStream_t st, const CT* codes, int64_t N, int32_
   rb = std::max(1, std::min(rb, R));
   int lg = 0;
   while ((1 << lg) < ncp) lg++;
-  const size_t lds = tiles + ((rb * per_rep + 15) & ~(size_t)15);
+  const size_t lds = tiles + ((rb * per_rep + 15) & ~(size_t)15) + (d_z0 ? ((size_t)rb * Fmax + 15) & ~(size_t)15 : 0);
   // (the staged code rows: 16-byte pieces, at most kRows / 16 per thread per block)
   if (lds > 150 * 1024 || (1 << lg) != ncp || S_out % 4 != 0 || (S_codes * sizeof(CT)) % 16 != 0 ||
       (size_t)kRows * S_codes * sizeof(CT) > (size_t)kRows / 16 * 16 * 256 || npad % kRows != 0 ||

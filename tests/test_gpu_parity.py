@@ -438,7 +438,7 @@ def test_sampled_split_finding(ctx, n_rows, cls, P):
 
 
 @pytest.mark.parametrize("cls", [False, True])
-def test_device_split_finding_edge_features(ctx, monkeypatch, cls):
+def test_device_split_finding_edge_features(ctx, monkeypatch, capfd, cls):
     """findSplitsForContinuousFeature on the device (k_find_splits, a wave per (replica,
     feature)) on the cases its walk branches on: 0.0 in the dictionary or only implied by a
     sample short of numSamples (inserted first, last or in the middle), at most numSplits + 1
@@ -468,7 +468,12 @@ def test_device_split_finding_edge_features(ctx, monkeypatch, cls):
     kw = dict(replacement=True, sample_ratio=1.0, seed=seed, learner_begin=0, learner_end=L,
               partition_offsets=part, max_depth=6, max_bins=32, subspace_ratio=1.0,
               subspace_bug_compat=False, impurity=nat.IMPURITY_GINI if cls else nat.IMPURITY_VARIANCE)
+    monkeypatch.setenv("SBAG_DEBUG_BINS", "1")
     forest = nat.fit(ctx, ds, **kw)
+    # a sample above numSamples passes a 32nd target: 32 cuts fill the 32-slot table, whose last
+    # slot k_bin_cuts counts apart from its binary search
+    assert "maxcuts 32 ncp 32" in capfd.readouterr().err
+    monkeypatch.delenv("SBAG_DEBUG_BINS")
     counts = oracle.bag(True, 1.0, 0, L, seed, part, n)
     assert oracle.split_sample_fraction(int(counts[0].sum()), 32) < 1.0
     subs = [oracle.subspace(1.0, X.shape[1], seed + i) for i in range(L)]
