@@ -56,6 +56,8 @@ def fuzz_case(seed):
             levels = int(rng.choice([2, 3, 7, 31, 200, 5000]))
             X[:, f] = np.round(rng.normal(size=N) * levels) / 8.0
             X[rng.random(N) < 0.1, f] = 0.0
+            if rng.random() < 0.2:  # one sign, no 0.0: a short split-finding sample implies one
+                X[:, f] = (np.abs(X[:, f]) + 0.125) * rng.choice([-1.0, 1.0])
     f64 = False
     if cls:
         C = int(rng.choice([2, 3, 5, 9, 17, 33, 64, 80]))
