@@ -48,6 +48,7 @@ def fuzz_case(seed):
     F = int(rng.choice([1, 3, 12, 40, 64, 65, 100, 140]))
     cls = bool(rng.integers(0, 2))
     kind = rng.choice(["mixed", "u8"])
+    sign_rng = np.random.default_rng(seed + 7919)  # (apart, so a seed's other draws stay put)
     if kind == "u8":  # 32-level integer columns: identity codes, the bench's layout
         X = rng.integers(0, 32, size=(N, F)).astype(np.float64)
     else:
@@ -56,8 +57,8 @@ def fuzz_case(seed):
             levels = int(rng.choice([2, 3, 7, 31, 200, 5000]))
             X[:, f] = np.round(rng.normal(size=N) * levels) / 8.0
             X[rng.random(N) < 0.1, f] = 0.0
-            if rng.random() < 0.2:  # one sign, no 0.0: a short split-finding sample implies one
-                X[:, f] = (np.abs(X[:, f]) + 0.125) * rng.choice([-1.0, 1.0])
+            if sign_rng.random() < 0.2:  # one sign, no 0.0: a short split-finding sample implies one
+                X[:, f] = (np.abs(X[:, f]) + 0.125) * sign_rng.choice([-1.0, 1.0])
     f64 = False
     if cls:
         C = int(rng.choice([2, 3, 5, 9, 17, 33, 64, 80]))
