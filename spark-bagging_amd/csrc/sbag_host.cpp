@@ -1551,8 +1551,25 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
     const int lb = fp->sampler.learner_begin, le = fp->sampler.learner_end;
     bool cont = false;
     for (const auto& d : ds->dict) cont = cont || (int64_t)d.size() > fp->tree.max_bins;
-    if (cont && le - lb > 1) {
-      const double per = (double)ds->N * row_stride(ds->F) + (double)ds->F * (double)((ds->N + 63) / 64 * 64);
+    // (every replica holds every row once -- bags without replacement at ratio 1 -- : the
+    // thresholds are shared and one bins matrix serves all)
+    const bool whole = !fp->sampler.replacement && fp->sampler.sample_ratio >= 1.0;
+    if (cont && le - lb > 1 && !whole) {
+      // the per-replica rows hold the subspace's features (not all of them)
+      const double sratio = fp->subspace_bug_compat ? fp->sampler.sample_ratio : fp->subspace_ratio;
+      int fmax = 0;
+      std::vector<int32_t> idx(ds->F);
+      for (int l = lb; l < le; l++) {
+        int n = 0;
+        if (sbag_subspace(sratio, ds->F, (int64_t)((uint64_t)fp->sampler.seed + (uint64_t)(int64_t)l), idx.data(),
+                          &n) != SBAG_OK) {
+          fmax = ds->F;
+          break;
+        }
+        fmax = std::max(fmax, n);
+      }
+      fmax = std::max(fmax, 1);
+      const double per = (double)ds->N * row_stride(fmax) + (double)fmax * (double)((ds->N + 127) / 128 * 128);
       const double budget = bins_budget(c);
       const int fitn = (int)std::max(1.0, std::floor(budget / per));
       if (fitn < le - lb) {

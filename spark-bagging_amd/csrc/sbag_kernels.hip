@@ -1468,7 +1468,7 @@ __global__ __launch_bounds__(64) void k_find_splits(SplitFindArgs A) {
     rank += __popcll(vm);
   }
   if (mids) nt = possible;
-  __syncthreads();
+  block_sync();
   if (lane == 0) A.nt[rf] = (int32_t)min<int64_t>(nt, 0x7fffffff);
   const int64_t m = min<int64_t>(nt, tc);
   for (int64_t j = lane; j < m; j += 64) {

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void k_label_digits(const int32_t* __restrict_
                                                       uint8_t* __restrict__ digits) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256) {
     const int64_t k = labk[i];
-    const uint64_t kp = (uint64_t)(k + K0), k2 = (uint64_t)(k * k);
+    const uint64_t kp = (uint64_t)(k + K0), k2 = (uint64_t)((int64_t)k * k);
     for (int j = 0; j < nd1; j++) digits[(int64_t)j * N + i] = (uint8_t)((kp >> (7 * j)) & 127u);
     for (int j = 0; j < nd2; j++) digits[(int64_t)(nd1 + j) * N + i] = (uint8_t)((k2 >> (7 * j)) & 127u);
   }
