@@ -4007,7 +4007,8 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       TRY(h2d(c, d_der, derive.data(), derive.size()));
       sa.derive = d_der;
       sa.par_hist = hist_prev;
-      sa.hist_w = hist_cur;
+      // (the derived histograms serve the next level's derivations: none after the last split)
+      sa.hist_w = level + 1 < D ? hist_cur : nullptr;
     }
     if (!gini) {
       uint64_t* d_nsq;

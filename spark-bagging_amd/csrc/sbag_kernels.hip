@@ -3208,7 +3208,7 @@ __host__ __device__ inline int split_fstride(int NB, int NS) {
   return NB * NSP + (((NB - 1) * NSP - NB * NSP) % 64 + 64) % 64;
 }
 // (ps, hw: a derived slot -- the staged words are parent ps - smaller child hs, and are also
-// written to hw, the slot's own histogram for the next level)
+// written to hw, the slot's own histogram for the next level; hw null: no next level)
 __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ hs, int f0, int g,
                                                    int NB, int NS, int Fmax, int hct,
                                                    uint32_t* pre, const uint32_t* __restrict__ ps = nullptr,
@@ -3228,7 +3228,7 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
       if (ps) {
         const uint4 pv = ((const uint4*)(ps + o))[rem];
         v = make_uint4(pv.x - v.x, pv.y - v.y, pv.z - v.z, pv.w - v.w);
-        ((uint4*)(hw + o))[rem] = v;
+        if (hw) ((uint4*)(hw + o))[rem] = v;
       }
       return v;
     };
@@ -3262,7 +3262,7 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
       uint32_t v = hs[o];
       if (ps) {
         v = ps[o] - v;
-        hw[o] = v;
+        if (hw) hw[o] = v;
       }
       pre[(size_t)fl * FS + (size_t)(row - fl * NB) * NSP + c] = v;
     }
@@ -3294,7 +3294,7 @@ __global__ __launch_bounds__(256) void k_split_gini(SplitArgs A, int G) {
   uint32_t* hw = nullptr;
   if (A.derive && A.derive[2 * slot] >= 0) {
     ps = (const uint32_t*)A.par_hist + (int64_t)A.derive[2 * slot] * slot_words;
-    hw = (uint32_t*)A.hist_w + (int64_t)slot * slot_words;
+    hw = A.hist_w ? (uint32_t*)A.hist_w + (int64_t)slot * slot_words : nullptr;
     hs = (const uint32_t*)A.hist + (int64_t)A.derive[2 * slot + 1] * slot_words;
   }
   const int32_t* nb_r = A.nbins + (int64_t)r * A.Fmax;
