@@ -1555,7 +1555,14 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
     // thresholds are shared and one bins matrix serves all)
     const bool whole = !fp->sampler.replacement && fp->sampler.sample_ratio >= 1.0;
     if (cont && le - lb > 1 && !whole) {
-      // the per-replica rows hold the subspace's features (not all of them)
+      // the per-replica rows hold the subspace's features (not all of them), and
+      // with integer labels only the in-bag rows (k_bin_ranked): 1 - e^-ratio of them for
+      // Poisson bags, the ratio for Bernoulli ones (a short estimate falls back to halving)
+      const bool ranked = (fp->tree.impurity == SBAG_IMPURITY_GINI || ds->lab.label_ok) &&
+                          (!getenv("SBAG_BIN_RANKED") || atoi(getenv("SBAG_BIN_RANKED")) != 0);
+      const double ratio = fp->sampler.sample_ratio;
+      const double frac = ranked ? std::min(1.0, (fp->sampler.replacement ? 1.0 - std::exp(-ratio) : ratio) * 1.02 + 1e-3)
+                                 : 1.0;
       const double sratio = fp->subspace_bug_compat ? fp->sampler.sample_ratio : fp->subspace_ratio;
       int fmax = 0;
       std::vector<int32_t> idx(ds->F);
@@ -1569,7 +1576,8 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
         fmax = std::max(fmax, n);
       }
       fmax = std::max(fmax, 1);
-      const double per = (double)ds->N * row_stride(fmax) + (double)fmax * (double)((ds->N + 127) / 128 * 128);
+      const double rows = frac * (double)ds->N + 192.0;
+      const double per = rows * row_stride(fmax) + (double)fmax * rows;
       const double budget = bins_budget(c);
       const int fitn = (int)std::max(1.0, std::floor(budget / per));
       if (fitn < le - lb) {
@@ -2337,9 +2345,11 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     const int nchain1 = (int)tasks[1].size();
     std::vector<F64SplitOut> fo(fin.size());
     std::vector<int64_t> nleft;
+    double* dbg_chist = nullptr;  // (SBAG_F64_DEBUG: the chain histograms, for a violation report)
     if (!tasks[0].empty()) {
       double* d_chist;
       TRY(ws_typed(c, "fb_chist", (size_t)std::max(1, nchain0 + nchain1) * NB * 3, &d_chist));
+      dbg_chist = d_chist;
       int h = G.tm.begin(T_CHAIN);
       // one launch sequence for both passes: the root's chains of the chosen features and of
       // the first features run side by side (the root has few, long chains: 2 x 2048 per C3
@@ -2418,8 +2428,29 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       const LNode& q = cur[i];
       const bool decided = !so[i].flag;
       const F64SplitOut& o = decided ? fo[fin_of[i]] : xo[xi[i]];
-      if (decided && (o.s != so[i].s || !o.valid || !(o.gain > 0.0) || o.gain < G.tp.min_info_gain))
+      if (decided && (o.s != so[i].s || !o.valid || !(o.gain > 0.0) || o.gain < G.tp.min_info_gain)) {
+        if (getenv("SBAG_F64_DEBUG")) {
+          fprintf(stderr,
+                  "[sbag] screen violation level %d slot %d r %d entries %lld: screen f %d s %d gain %.17g margin "
+                  "%.17g | exact f %d s %d gain %.17g valid %d | min_gain %.17g | node calc %.17g %.17g %.17g\n",
+                  level, i, q.r, (long long)(q.b - q.a), so[i].f, so[i].s, so[i].gain, so[i].margin, o.f, o.s,
+                  o.gain, o.valid, G.tp.min_info_gain, trees[q.r][q.node].calc[0], trees[q.r][q.node].calc[1],
+                  trees[q.r][q.node].calc[2]);
+          std::vector<uint64_t> ih((size_t)NB * 3);
+          (void)d2h(c, ih.data(), (const uint64_t*)hist_cur + ((size_t)i * Fmax + so[i].f) * NB * 3, ih.size());
+          std::vector<double> ch((size_t)NB * 3, 0.0);
+          if (dbg_chist) (void)d2h(c, ch.data(), dbg_chist + (size_t)fin[fin_of[i]].t * NB * 3, ch.size());
+          const F64FinishNode& fnd = fin[fin_of[i]];
+          fprintf(stderr, "[sbag]   finish t %d f %d s %d nsp %d set %d impurity %.17g calc %.17g %.17g %.17g NB %d\n",
+                  fnd.t, fnd.f, fnd.s, fnd.nsp, fnd.ch.set, fnd.ch.impurity, fnd.ch.calc[0], fnd.ch.calc[1],
+                  fnd.ch.calc[2], NB);
+          for (int b = 0; b < NB; b++)
+            if (ih[b * 3] || ch[b * 3] != 0.0)
+              fprintf(stderr, "[sbag]   bin %d: int count %llu sck %lld | chain %.17g %.17g %.17g\n", b,
+                      (unsigned long long)ih[b * 3], (long long)ih[b * 3 + 1], ch[b * 3], ch[b * 3 + 1], ch[b * 3 + 2]);
+        }
         return fail(SBAG_EDEVICE, "internal: the fp64 screen's split is not Spark's (bound violated)");
+      }
       const int r = q.r;
       {
         BtNode& n = trees[r][q.node];
@@ -3495,8 +3526,10 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
           }
           h_nbins[rf] = nt + 1;
           t_nb[w] = std::max(t_nb[w], nt + 1);
-          // the codes are the bins when bin(k) = k for every code k < d.size()
-          if ((int)d.size() > nt + 1) {
+          // the codes are the bins when bin(k) = k for every code k < d.size() and there are no
+          // more bins than codes (an implied 0.0 past a one-signed feature's values adds an empty
+          // last bin, and the layouts are sized by the bin count: NB would fall one short)
+          if ((int)d.size() != nt + 1) {
             t_id[w] = 0;
           } else {
             for (size_t j = 0; j + 1 < d.size(); j++)
@@ -3660,8 +3693,15 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       h_pos = h_pos_codes;
     } else {
       S = row_stride(Fmax);
+      // integer labels: only the in-bag rows are binned, by rank (k_bin_ranked; the entries then
+      // carry ranks).  SBAG_BIN_RANKED=0: every row (k_bin_cuts)
+      const bool ranked = !f64 && !bin_lut && (!getenv("SBAG_BIN_RANKED") || atoi(getenv("SBAG_BIN_RANKED")) != 0) &&
+                          bin_ranked_fits(ds->code_bytes, ds->S, S, Fmax, ncp);
+      int64_t capb = 0;
+      for (int r = 0; r < R; r++) capb = std::max<int64_t>(capb, (int64_t)inbag[r]);
+      const int64_t rows_b = ranked ? (capb + 1 + 63) / 64 * 64 : N;  // (room for the zero rows)
       // the bins and their column copy, per replica
-      const double need = (double)R * N * S + (double)R * Fmax * ((N + 63) / 64 * 64);
+      const double need = (double)R * rows_b * S + (double)R * Fmax * ((rows_b + 127) / 128 * 128);
       if (need > bins_budget(c)) {
         if (R > 1) {
           (void)hipEventDestroy(ev_start);
@@ -3671,7 +3711,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
         return fail(SBAG_EUNSUPPORTED, "per-replica bins of one learner exceed the device budget");
       }
       uint8_t* d_b;
-      TRY(ws_typed(c, "bins", (size_t)R * N * S + 256, &d_b));
+      TRY(ws_typed(c, "bins", (size_t)R * rows_b * S + 256, &d_b));
       int ncol_r = 1;
       for (int r = 0; r < R; r++) ncol_r = std::max(ncol_r, (int)h_Fr[r]);
       const int64_t npad_r = (N + 63) / 64 * 64;
@@ -3683,13 +3723,22 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
         TRY(upload_cuts(R, Fmax, [&](int r, int fl) { return fl < h_Fr[r] ? &cuts[(size_t)r * Fmax + fl] : nullptr; },
                         &d_cut, &d_z0));
         uint8_t* d_c;
-        const int64_t npad_c = (N + 127) / 128 * 128;
+        const int64_t npad_c = (rows_b + 127) / 128 * 128;
         TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_c, &d_c));
         // (SBAG_BIN_NO_COLS=1: the column copy by k_transpose afterwards, A/B)
         static const bool no_cols = getenv("SBAG_BIN_NO_COLS") != nullptr;
-        if (launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R, d_cut, ncp,
-                            d_z0, d_b, S, (int64_t)N * S, no_cols ? nullptr : d_c, ncol_r, npad_c,
-                            (int64_t)ncol_r * npad_c)) {
+        if (ranked) {
+          if (!launch_bin_ranked(c->stream, ds->d_codes, ds->code_bytes, ds->S, entA, cap, d_inbag, capb, d_sub, d_Fr,
+                                 Fmax, R, d_cut, ncp, d_z0, d_b, S, rows_b * S, d_c, ncol_r, npad_c,
+                                 (int64_t)ncol_r * npad_c))
+            return fail(SBAG_EDEVICE, "internal: ranked bins geometry");
+          HIP_TRY(hipGetLastError());
+          launch_rank_entries(c->stream, entA, cap, d_inbag, R, capb);
+          cols_direct = d_c;
+          cols_direct_npad = npad_c;
+        } else if (launch_bin_cuts(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R, d_cut,
+                                   ncp, d_z0, d_b, S, (int64_t)N * S, no_cols ? nullptr : d_c, ncol_r, npad_c,
+                                   (int64_t)ncol_r * npad_c)) {
           cols_direct = d_c;
           cols_direct_npad = npad_c;
         }
@@ -3712,9 +3761,9 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
         }
       }
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemsetAsync(d_b + (size_t)R * N * S, 0, 256, c->stream));  // zero slack
+      HIP_TRY(hipMemsetAsync(d_b + (size_t)R * rows_b * S, 0, 256, c->stream));  // zero slack
       d_bins = d_b;
-      bins_rstride = (int64_t)N * S;
+      bins_rstride = rows_b * S;
       for (int r = 0; r < R; r++)
         for (int fl = 0; fl < h_Fr[r]; fl++) h_pos[(size_t)r * Fmax + fl] = (int16_t)fl;
     }

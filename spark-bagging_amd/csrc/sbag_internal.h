@@ -254,6 +254,19 @@ struct SplitFindArgs {
   uint32_t* cut;           // [R * Fmax][tc]
 };
 void launch_find_splits(hipStream_t st, const SplitFindArgs& a);
+// launch_bin_cuts over the in-bag rows only, by rank: out[r][rank][fl], cols[r][fl][rank] for the
+// ranks < inbag[r] of the replica's row-ordered entries ent[r][.] (capb >= every inbag[r]); false:
+// not supported for this geometry (the caller bins every row)
+bool launch_bin_ranked(hipStream_t st, const void* codes, int code_bytes, int32_t S_codes, const uint64_t* ent,
+                       int64_t cap, const unsigned long long* d_inbag, int64_t capb, const int32_t* d_sub,
+                       const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
+                       const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols,
+                       int32_t ncol, int64_t npad, int64_t cols_rstride);
+// whether launch_bin_ranked takes this geometry (decided before the bins are sized)
+bool bin_ranked_fits(int code_bytes, int32_t S_codes, int32_t S_out, int32_t Fmax, int32_t ncp);
+// ent[r][i] row field := i (i < inbag[r])
+void launch_rank_entries(hipStream_t st, uint64_t* ent, int64_t cap, const unsigned long long* d_inbag, int R,
+                         int64_t capb);
 // per-replica bins out[r][n][fl] = #{j : cut[r][fl][j] <= codes[n][sub[r][fl]]} (cut [R][Fmax][ncp]
 // ascending, every cut >= 1, padded with ~0u; ncp a power of two) + z0[r][fl] (leading zero cuts
 // left out of the table; nullptr: none), zero past F_r; with cols the

@@ -4059,6 +4059,267 @@ bool launch_bin_cuts(hipStream_t st, const void* codes, int code_bytes, int64_t 
                              out, S_out, out_rstride, cols, ncol, npad, cols_rstride);
 }
 
+// k_bin_ranked: k_bin_cuts over a replica's in-bag rows only, stored by in-bag rank (the
+// entry's index in the replica's row-ordered list): out[r][rank][S_out], cols[r][fl][rank].
+// Out-of-bag rows' bins were never read; the in-bag list of a Poisson(1) bag is 63 % of the rows,
+// so the searches and the stores shrink by as much.  The entries then carry ranks instead of
+// rows (k_rank_entries).  A workgroup takes one replica and a chunk of ranks; each block of
+// 64 ranks loads its rows' ids two blocks ahead and their code rows one block ahead (gathers of
+// whole code rows, mostly consecutive), then searches and emits as k_bin_cuts does.
+template <typename CT, typename KT, int kPv>
+__global__ __launch_bounds__(256) void k_bin_ranked(const CT* __restrict__ codes, int32_t S_codes,
+                                                    const uint64_t* __restrict__ ent, int64_t cap,
+                                                    const unsigned long long* __restrict__ inbag,
+                                                    const int32_t* __restrict__ sub, const int32_t* __restrict__ Fr,
+                                                    int32_t Fmax, const uint32_t* __restrict__ cut, int32_t ncp,
+                                                    int32_t lg, const uint8_t* __restrict__ z0,
+                                                    uint8_t* __restrict__ out, int32_t S_out, int64_t out_rstride,
+                                                    uint8_t* __restrict__ cols, int32_t ncol, int64_t npad,
+                                                    int64_t cols_rstride, int64_t ranks_per_chunk) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  constexpr int kRows = 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = blockIdx.y;
+  const int64_t nin = (int64_t)inbag[r];
+  const int64_t c0 = (int64_t)blockIdx.x * ranks_per_chunk, c1 = min(nin, c0 + ranks_per_chunk);
+  if (c0 >= c1) return;  // (uniform: before any barrier)
+  const int pc = S_codes * (int)sizeof(CT) + 4;
+  const int pb = ((S_out / 4) & 1) ? S_out : S_out + 4;
+  KT* sk = (KT*)smem;
+  const size_t kbytes = ((size_t)Fmax * ncp * sizeof(KT) + 15) & ~(size_t)15;
+  uint8_t* sz = smem + kbytes;
+  const size_t zbytes = z0 ? ((size_t)Fmax + 15) & ~(size_t)15 : 0;
+  uint8_t* sc = sz + zbytes;
+  uint8_t* sb = sc + (size_t)kRows * pc;
+  for (int64_t k = tid; k < (int64_t)Fmax * ncp; k += 256) {
+    const uint32_t c = cut[(int64_t)r * Fmax * ncp + k];
+    sk[k] = c == 0xffffffffu ? (KT)~(KT)0 : (KT)(c - 1u);
+  }
+  if (z0)
+    for (int k = tid; k < Fmax; k += 256) sz[k] = z0[(int64_t)r * Fmax + k];
+  const uint64_t* er = ent + (int64_t)r * cap;
+  const int ngrp4 = S_out / 4;
+  const int rq = S_codes * (int)sizeof(CT) / 16;  // (kPv 16-byte pieces per thread: rows <= 64 kPv bytes)
+  int soff[kPv], srow[kPv], sw[kPv];
+#pragma unroll
+  for (int v = 0; v < kPv; v++) {
+    const int k = tid + 256 * v;
+    const int kk = min(k, kRows * rq - 1);
+    srow[v] = kk / rq;
+    sw[v] = kk - srow[v] * rq;
+    soff[v] = k < kRows * rq ? srow[v] * pc + 16 * sw[v] : -1;
+  }
+  // the row of rank nb + lane (clamped to the chunk: ranks past it are binned, never stored)
+  auto load_rows = [&](int64_t nb) { return (uint32_t)er[min(nb + lane, c1 - 1)]; };
+  uint4 pv[kPv];
+  auto load_block = [&](uint32_t rowv) {
+#pragma unroll
+    for (int v = 0; v < kPv; v++) {
+      const uint32_t row = (uint32_t)__shfl((int)rowv, srow[v]);
+      pv[v] = ((const uint4*)(codes + (int64_t)row * S_codes))[sw[v]];
+    }
+  };
+  const int fr = __builtin_amdgcn_readfirstlane(Fr[r]);
+  int gv;
+  {
+    const int fl = min(4 * (wave + 4 * (lane >> 2)) + (lane & 3), fr - 1);
+    gv = sub[(int64_t)r * Fmax + fl] * (int)sizeof(CT);
+  }
+  load_block(load_rows(c0));
+  uint32_t rows_next = load_rows(c0 + kRows);
+  for (int64_t n0 = c0; n0 < c1; n0 += kRows) {
+    const int nr = (int)min<int64_t>(kRows, c1 - n0);
+    block_sync();  // (the previous block's tile reads; the keys at the first block)
+#pragma unroll
+    for (int v = 0; v < kPv; v++) {
+      if (soff[v] >= 0) {
+        uint32_t* d = (uint32_t*)(sc + soff[v]);
+        d[0] = pv[v].x;
+        d[1] = pv[v].y;
+        d[2] = pv[v].z;
+        d[3] = pv[v].w;
+      }
+    }
+    load_block(rows_next);  // the next block's code rows in flight
+    rows_next = load_rows(n0 + 2 * kRows);
+    block_sync();
+    for (int q = wave, j = 0; q < ngrp4; q += 4, j++) {
+      if (4 * q >= fr) {
+        *(uint32_t*)(sb + lane * pb + 4 * q) = 0u;
+        continue;
+      }
+      const KT* ks[4];
+      uint32_t cv[4], idx[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int fl = min(4 * q + k, fr - 1);
+        const int gb = __builtin_amdgcn_readlane(gv, 4 * j + k);
+        ks[k] = sk + (size_t)fl * ncp;
+        cv[k] = (uint32_t) * (const CT*)(sc + lane * pc + gb);
+        idx[k] = 0u;
+      }
+      auto step = [&](uint32_t h) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) idx[k] += (uint32_t)ks[k][idx[k] + h - 1u] < cv[k] ? h : 0u;
+      };
+      if (lg == 5) {
+        step(16u);
+        step(8u);
+        step(4u);
+        step(2u);
+        step(1u);
+      } else if (lg == 6) {
+        step(32u);
+        step(16u);
+        step(8u);
+        step(4u);
+        step(2u);
+        step(1u);
+      } else {
+        for (int st = lg - 1; st >= 0; st--) step(1u << st);
+      }
+      uint32_t wv = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t kl = (uint32_t)ks[k][ncp - 1];
+        const uint32_t zk = z0 ? (uint32_t)sz[min(4 * q + k, fr - 1)] : 0u;
+        const uint32_t b = idx[k] + (kl < cv[k] ? 1u : 0u) + zk;
+        if (4 * q + k < fr) wv |= b << (8 * k);
+      }
+      *(uint32_t*)(sb + lane * pb + 4 * q) = lane < nr ? wv : 0u;
+    }
+    block_sync();
+    {
+      // (the replica's last block also stores its zeroed rows past the last rank: the row-lane
+      // histogram's aligned loads may read a few bytes past a row, which must be valid bins;
+      // the caller leaves room for them)
+      const int nst = n0 + kRows >= nin ? kRows : nr;
+      uint8_t* o = out + (int64_t)r * out_rstride + n0 * S_out;
+      if (pb == S_out) {
+        const int nb = nst * S_out;
+        if ((((uintptr_t)o) & 15) == 0) {
+          for (int k = tid; k < nb / 16; k += 256) ((uint4*)o)[k] = ((const uint4*)sb)[k];
+          for (int k = nb / 16 * 4 + tid; k < nb / 4; k += 256) ((uint32_t*)o)[k] = ((const uint32_t*)sb)[k];
+        } else {
+          for (int k = tid; k < nb / 4; k += 256) ((uint32_t*)o)[k] = ((const uint32_t*)sb)[k];
+        }
+      } else {
+        const int wpr = S_out / 4;
+        for (int row = tid >> 5; row < nst; row += 8)
+          for (int w = tid & 31; w < wpr; w += 32)
+            ((uint32_t*)o)[row * wpr + w] = *(const uint32_t*)(sb + row * pb + 4 * w);
+      }
+    }
+    if (cols) {
+      constexpr int kRq = kRows / 4;
+      uint8_t* cr = cols + (int64_t)r * cols_rstride + n0;
+      for (int t = tid; t < (ncol + 3) / 4 * kRq; t += 256) {
+        const int fq = t / kRq, rq4 = t % kRq;
+        uint32_t d[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+          const int row = 4 * rq4 + kk;
+          const uint32_t x = *(const uint32_t*)(sb + row * pb + 4 * fq);
+          d[kk] = row < nr ? x : 0u;
+        }
+        const uint32_t lo01 = __builtin_amdgcn_perm(d[1], d[0], 0x05010400u);
+        const uint32_t hi01 = __builtin_amdgcn_perm(d[1], d[0], 0x07030602u);
+        const uint32_t lo23 = __builtin_amdgcn_perm(d[3], d[2], 0x05010400u);
+        const uint32_t hi23 = __builtin_amdgcn_perm(d[3], d[2], 0x07030602u);
+        const uint32_t f4[4] = {__builtin_amdgcn_perm(lo23, lo01, 0x05040100u),
+                                __builtin_amdgcn_perm(lo23, lo01, 0x07060302u),
+                                __builtin_amdgcn_perm(hi23, hi01, 0x05040100u),
+                                __builtin_amdgcn_perm(hi23, hi01, 0x07060302u)};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (4 * fq + i < ncol) *(uint32_t*)(cr + (int64_t)(4 * fq + i) * npad + 4 * rq4) = f4[i];
+      }
+    }
+  }
+}
+
+static size_t bin_ranked_lds(int code_bytes, int32_t S_codes, int32_t S_out, int32_t Fmax, int32_t ncp) {
+  const int kb = code_bytes <= 2 ? 2 : 4;
+  const int pb = ((S_out / 4) & 1) ? S_out : S_out + 4;
+  return (((size_t)Fmax * ncp * kb + 15) & ~(size_t)15) + (((size_t)Fmax + 15) & ~(size_t)15) +
+         (size_t)64 * (S_codes * code_bytes + 4) + (size_t)64 * pb;
+}
+
+bool bin_ranked_fits(int code_bytes, int32_t S_codes, int32_t S_out, int32_t Fmax, int32_t ncp) {
+  return bin_ranked_lds(code_bytes, S_codes, S_out, Fmax, ncp) <= 150 * 1024 && (ncp & (ncp - 1)) == 0 &&
+         S_out % 4 == 0 && ((int64_t)S_codes * code_bytes) % 16 == 0 && (int64_t)S_codes * code_bytes <= 1024;
+}
+
+template <typename CT, typename KT>
+static bool launch_bin_ranked_t(hipStream_t st, const CT* codes, int32_t S_codes, const uint64_t* ent, int64_t cap,
+                                const unsigned long long* d_inbag, int64_t capb, const int32_t* d_sub,
+                                const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
+                                const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols,
+                                int32_t ncol, int64_t npad, int64_t cols_rstride) {
+  constexpr int kRows = 64;
+  if (!bin_ranked_fits((int)sizeof(CT), S_codes, S_out, Fmax, ncp) || npad % kRows != 0 || !cols) return false;
+  const size_t lds = bin_ranked_lds((int)sizeof(CT), S_codes, S_out, Fmax, ncp);
+  int lg = 0;
+  while ((1 << lg) < ncp) lg++;
+  static const int64_t wgs = getenv("SBAG_BIN_WGS") ? atoll(getenv("SBAG_BIN_WGS")) : 65536;
+  const int64_t nblk = (capb + kRows - 1) / kRows;
+  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(nblk, (wgs + R - 1) / R));
+  const int64_t rpc = (nblk + nch - 1) / nch * kRows;
+  const dim3 g((unsigned)((capb + rpc - 1) / rpc), (unsigned)R);
+  const int64_t rowb = (int64_t)S_codes * sizeof(CT);  // code row bytes: 16-byte pieces per thread
+  auto go = [&](const void* fn) {
+    set_max_lds(fn, (int)lds);
+    void* args[] = {(void*)&codes, (void*)&S_codes, (void*)&ent,   (void*)&cap,         (void*)&d_inbag,
+                    (void*)&d_sub, (void*)&d_Fr,    (void*)&Fmax,  (void*)&d_cut,       (void*)&ncp,
+                    (void*)&lg,    (void*)&d_z0,    (void*)&out,   (void*)&S_out,       (void*)&out_rstride,
+                    (void*)&cols,  (void*)&ncol,    (void*)&npad,  (void*)&cols_rstride, (void*)&rpc};
+    (void)hipLaunchKernel(fn, g, dim3(256), args, lds, st);
+  };
+  if (rowb <= 256)
+    go((const void*)k_bin_ranked<CT, KT, 4>);
+  else if (rowb <= 512)
+    go((const void*)k_bin_ranked<CT, KT, 8>);
+  else
+    go((const void*)k_bin_ranked<CT, KT, 16>);
+  return true;
+}
+
+bool launch_bin_ranked(hipStream_t st, const void* codes, int code_bytes, int32_t S_codes, const uint64_t* ent,
+                       int64_t cap, const unsigned long long* d_inbag, int64_t capb, const int32_t* d_sub,
+                       const int32_t* d_Fr, int32_t Fmax, int R, const uint32_t* d_cut, int32_t ncp,
+                       const uint8_t* d_z0, uint8_t* out, int32_t S_out, int64_t out_rstride, uint8_t* cols,
+                       int32_t ncol, int64_t npad, int64_t cols_rstride) {
+  if (code_bytes == 1)
+    return launch_bin_ranked_t<uint8_t, uint16_t>(st, (const uint8_t*)codes, S_codes, ent, cap, d_inbag, capb, d_sub,
+                                                  d_Fr, Fmax, R, d_cut, ncp, d_z0, out, S_out, out_rstride, cols,
+                                                  ncol, npad, cols_rstride);
+  if (code_bytes == 2)
+    return launch_bin_ranked_t<uint16_t, uint16_t>(st, (const uint16_t*)codes, S_codes, ent, cap, d_inbag, capb,
+                                                   d_sub, d_Fr, Fmax, R, d_cut, ncp, d_z0, out, S_out, out_rstride,
+                                                   cols, ncol, npad, cols_rstride);
+  return launch_bin_ranked_t<uint32_t, uint32_t>(st, (const uint32_t*)codes, S_codes, ent, cap, d_inbag, capb, d_sub,
+                                                 d_Fr, Fmax, R, d_cut, ncp, d_z0, out, S_out, out_rstride, cols,
+                                                 ncol, npad, cols_rstride);
+}
+
+// entries' row field -> their in-bag rank (after k_bin_ranked)
+__global__ __launch_bounds__(256) void k_rank_entries(uint64_t* __restrict__ ent, int64_t cap,
+                                                      const unsigned long long* __restrict__ inbag) {
+  const int r = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)inbag[r]) return;
+  uint64_t* e = ent + (int64_t)r * cap + i;
+  *e = (*e & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
+}
+
+void launch_rank_entries(hipStream_t st, uint64_t* ent, int64_t cap, const unsigned long long* d_inbag, int R,
+                         int64_t capb) {
+  if (capb <= 0 || R <= 0) return;
+  hipLaunchKernelGGL(k_rank_entries, dim3((unsigned)((capb + 255) / 256), (unsigned)R), dim3(256), 0, st, ent, cap,
+                     d_inbag);
+}
+
 // Value counts with global atomics (u16 codes / dictionaries too large for LDS)
 template <typename CT>
 __global__ __launch_bounds__(256) void k_vc_global(const CT* __restrict__ codes, int32_t S,

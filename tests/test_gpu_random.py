@@ -141,6 +141,21 @@ def test_split_sample_gap_buffer_tail(ctx, seed):
     forest.free()
 
 
+# scripts/fuzz_parity.py seed 130242 (round 5, gpurun_out r05k3): one negative-only feature of
+# 9 values with fp64 labels; a short split-finding sample implies a 0.0 above every value, whose
+# threshold adds an empty 10th bin while the 9 codes still map to bins 0..8.  The codes were
+# taken as the bins with the layouts sized for 9, so the fp64 finish summed a 10th bin out of
+# its node's histogram and the screen's guard refused the fit.  Identity now requires as many
+# bins as codes.
+@pytest.mark.parametrize("seed", [130242])
+def test_implied_zero_past_the_values(ctx, seed):
+    X, y, cls, f64, part, p, kind = fuzz_case(seed)
+    assert f64 and X.shape[1] == 1 and (X < 0).all()
+    forest, orf = _fit_fuzz(ctx, seed)
+    assert_forest_equal(forest, orf)
+    forest.free()
+
+
 def test_split_sample_one_more_threshold(ctx):
     """scripts/fuzz_parity.py --big seed 90000 (2.87M rows, 32 learners, subspace ratio 0.3 of
     its own, fp64 labels): a split-finding sample larger than numSamples passes one more
