@@ -1642,7 +1642,6 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
   const int r = blockIdx.x % R;
   const int64_t chunk = blockIdx.x / R;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ int s_wave[4];
   __shared__ unsigned long long s_base;
   __shared__ unsigned long long s_red[4];
   __shared__ unsigned int s_max[4];
@@ -1673,38 +1672,57 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
       lk[it] = make_int4(l4[0], l4[1], l4[2], l4[3]);
     }
   }
+  // one cursor reservation for the workgroup's 8192 rows: the 8 iterations' wave scans first
+  // (no barriers between them), their wave totals through LDS, one atomic, then the stores in
+  // row order (8 reservations, each a round trip between two barriers, paced the kernel)
+  __shared__ int s_it[8][4];
+  int incl[8], nn[8];
 #pragma unroll
   for (int it = 0; it < 8; it++) {
-    const int64_t row0 = chunk * 8192 + (int64_t)it * 1024 + (int64_t)tid * 4;
-    uint32_t c[4];
-    const int32_t kk[4] = {lk[it].x, lk[it].y, lk[it].z, lk[it].w};
     int n = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      c[j] = (cw[it] >> (8 * j)) & 0xffu;
-      n += c[j] ? 1 : 0;
-      mysum += c[j];
-      mymax = max(mymax, c[j]);
+      const uint32_t c = (cw[it] >> (8 * j)) & 0xffu;
+      n += c ? 1 : 0;
+      mysum += c;
+      mymax = max(mymax, c);
     }
-    const int incl = wave_incl_scan(n, lane);
-    if (lane == 63) s_wave[wave] = incl;
-    block_sync();
-    int before = 0, total = 0;
-    for (int w = 0; w < 4; w++) {
-      if (w < wave) before += s_wave[w];
-      total += s_wave[w];
-    }
-    if (tid == 0) s_base = total ? atomicAdd(&cursor[r], (unsigned long long)total) : 0ull;
-    block_sync();
-    unsigned long long pos = s_base + (unsigned long long)(before + incl - n);
+    nn[it] = n;
+    incl[it] = wave_incl_scan(n, lane);
+    if (lane == 63) s_it[it][wave] = incl[it];
+  }
+  block_sync();
+  if (tid == 0) {
+    int total = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (c[j]) {
+    for (int it = 0; it < 8; it++)
+#pragma unroll
+      for (int w = 0; w < 4; w++) total += s_it[it][w];
+    s_base = total ? atomicAdd(&cursor[r], (unsigned long long)total) : 0ull;
+  }
+  block_sync();
+  unsigned long long itbase = s_base;
+#pragma unroll
+  for (int it = 0; it < 8; it++) {
+    const int64_t row0 = chunk * 8192 + (int64_t)it * 1024 + (int64_t)tid * 4;
+    const int32_t kk[4] = {lk[it].x, lk[it].y, lk[it].z, lk[it].w};
+    int before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      before += w < wave ? s_it[it][w] : 0;
+      total += s_it[it][w];
+    }
+    unsigned long long pos = itbase + (unsigned long long)(before + incl[it] - nn[it]);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t c = (cw[it] >> (8 * j)) & 0xffu;
+      if (c) {
         const int32_t k = kk[j];
-        mysq += (unsigned long long)c[j] * (unsigned long long)((int64_t)k * k);
-        er[pos++] = pack_entry((uint32_t)(row0 + j), k, c[j]);
+        mysq += (unsigned long long)c * (unsigned long long)((int64_t)k * k);
+        er[pos++] = pack_entry((uint32_t)(row0 + j), k, c);
       }
-    block_sync();
+    }
+    itbase += (unsigned long long)total;
   }
   __shared__ unsigned long long s_sq[4];
   for (int o = 32; o > 0; o >>= 1) {
