@@ -3195,10 +3195,18 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     } else {
       TRY(launch(g0, gini ? kHistGini : kHistVar, T_HIST, seg, h_par));
     }
-    const int64_t words = (int64_t)R * Fmax * ncmax * NS;
+    // its counts are the value counts of replicas thresholded on their whole subbag (numExamples
+    // <= required); replicas thresholded on their split-finding sample (3b: every C3 / C5
+    // replica) need none, and the copy would wait for the root histogram
+    bool any_whole = false;
+    for (int r = 0; r < R; r++) {
+      const int64_t mpb = std::min<int64_t>(tp.max_bins, nw[r]);
+      any_whole = any_whole || std::max<int64_t>(mpb * mpb, 10000) >= nw[r];
+    }
+    const int64_t words = any_whole ? (int64_t)R * Fmax * ncmax * NS : 0;
     std::vector<uint8_t> tmp((size_t)words * word_bytes);
-    TRY(d2h(c, tmp.data(), (const uint8_t*)hist_cur, tmp.size()));
-    for (int r = 0; r < R; r++)
+    if (any_whole) TRY(d2h(c, tmp.data(), (const uint8_t*)hist_cur, tmp.size()));
+    for (int r = 0; r < R && any_whole; r++)
       for (int fl = 0; fl < h_Fr[r]; fl++) {
         const size_t nc = ds->dict[sub[r][fl]].size();
         for (size_t k = 0; k < nc; k++) {
