@@ -1448,6 +1448,8 @@ static constexpr int kSplitRange = -1000;
 // fit_range_impl's integer engine cannot hold the dyadic labels' sums exactly (the packed
 // LDS word or the 2^53 bound on the sum of squares): fit_range refits on the fp64 engine
 static constexpr int kIntRange = -1001;
+// rows the fp64 engine (real-valued regression labels) accepts: the largest size it is tested at
+static constexpr int64_t kF64MaxRows = (int64_t)1 << 30;
 
 // device bytes per-replica bins may take: SBAG_BINS_BUDGET_MB, else 40 % of the device
 static double bins_budget(sbag_ctx* c) {
@@ -1539,6 +1541,7 @@ static bool overlap_fits(sbag_ctx* c, const sbag_dataset* ds, int learners) {
 }
 
 static int fit_learners_halving(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out);
+static int fit_halves(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out);
 // one context: fit_range, or halves of the learner range when per-replica bins exceed
 // the device budget (learners are independent, so concatenation is exact)
 static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
@@ -1558,11 +1561,16 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
       // the per-replica rows hold the subspace's features (not all of them), and
       // with integer labels only the in-bag rows (k_bin_ranked): 1 - e^-ratio of them for
       // Poisson bags, the ratio for Bernoulli ones (a short estimate falls back to halving)
-      const bool ranked = (fp->tree.impurity == SBAG_IMPURITY_GINI || ds->lab.label_ok) &&
-                          (!getenv("SBAG_BIN_RANKED") || atoi(getenv("SBAG_BIN_RANKED")) != 0);
+      // (fit_range_impl's conditions: not the fp64 engine -- gini, or integer labels without
+      // SBAG_F64=1 --, no LUT binning, and k_bin_ranked's LDS geometry for a cut table of up to
+      // maxBins cuts; ADVICE r05: the estimate had missed the last two)
+      const bool force_f64 = getenv("SBAG_F64") && atoi(getenv("SBAG_F64")) != 0;
+      const bool gini = fp->tree.impurity == SBAG_IMPURITY_GINI;
+      const bool lut_bins = getenv("SBAG_BIN_LUT") && atoi(getenv("SBAG_BIN_LUT")) != 0;
+      bool ranked = (gini || (ds->lab.label_ok && !force_f64)) && !lut_bins &&
+                    (!getenv("SBAG_BIN_RANKED") || atoi(getenv("SBAG_BIN_RANKED")) != 0);
       const double ratio = fp->sampler.sample_ratio;
-      const double frac = ranked ? std::min(1.0, (fp->sampler.replacement ? 1.0 - std::exp(-ratio) : ratio) * 1.02 + 1e-3)
-                                 : 1.0;
+      const double frac = std::min(1.0, (fp->sampler.replacement ? 1.0 - std::exp(-ratio) : ratio) * 1.02 + 1e-3);
       const double sratio = fp->subspace_bug_compat ? fp->sampler.sample_ratio : fp->subspace_ratio;
       int fmax = 0;
       std::vector<int32_t> idx(ds->F);
@@ -1576,7 +1584,12 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
         fmax = std::max(fmax, n);
       }
       fmax = std::max(fmax, 1);
-      const double rows = frac * (double)ds->N + 192.0;
+      {
+        int32_t ncp = 32;
+        while (ncp < fp->tree.max_bins) ncp *= 2;
+        ranked = ranked && bin_ranked_fits(ds->code_bytes, ds->S, row_stride(fmax), fmax, ncp);
+      }
+      const double rows = (ranked ? frac : 1.0) * (double)ds->N + 192.0;
       const double per = rows * row_stride(fmax) + (double)fmax * rows;
       const double budget = bins_budget(c);
       const int fitn = (int)std::max(1.0, std::floor(budget / per));
@@ -1590,8 +1603,8 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
           sbag_forest* f = nullptr;
           {
             const int st = fit_range(c, ds, &h, &f);
-            if (st == kSplitRange) {  // the estimate was short: halve as before
-              TRY(fit_learners_halving(c, ds, &h, &f));
+            if (st == kSplitRange) {  // the estimate was short: halve this part (not refit it whole)
+              TRY(fit_halves(c, ds, &h, &f));
             } else {
               TRY(st);
             }
@@ -1614,6 +1627,11 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
 static int fit_learners_halving(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
   const int st = fit_range(c, ds, fp, out);
   if (st != kSplitRange) return st;
+  return fit_halves(c, ds, fp, out);
+}
+
+// the two halves of a learner range that fit_range refused whole, concatenated in learner order
+static int fit_halves(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_forest** out) {
   const int lb = fp->sampler.learner_begin, le = fp->sampler.learner_end, mid = lb + (le - lb) / 2;
   sbag_fit_params h = *fp;
   h.sampler.learner_end = mid;
@@ -2591,6 +2609,12 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   if (f64) {
     if (!lab.finite) return fail(SBAG_EINVAL, "labels must be finite");
     if (!lab.label_ok && !lab.approx_ok) return fail(SBAG_EINVAL, "labels must be finite");
+    // the largest row count the fp64 engine is tested at (tests/test_gpu_f64.py,
+    // test_fp64_engine_near_the_row_limit: 2^30 - 4096 rows, the 64-bit-addressed scatter);
+    // kernels past it (32-bit entry row field up to 2^32) are untested
+    if (ds->N > kF64MaxRows)
+      return fail(SBAG_EUNSUPPORTED, "real-valued regression labels on more than 2^30 rows (the largest "
+                                     "size the fp64 engine is tested at)");
   }
   // the labels' fixed-point image in the entries: exact for dyadic labels, else (f64 path)
   // the screening approximation k = round(y 2^ashift)

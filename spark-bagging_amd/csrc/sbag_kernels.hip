@@ -4228,6 +4228,10 @@ __global__ __launch_bounds__(256) void k_bin_ranked(const CT* __restrict__ codes
           for (int w = tid & 31; w < wpr; w += 32)
             ((uint32_t*)o)[row * wpr + w] = *(const uint32_t*)(sb + row * pb + 4 * w);
       }
+      // a full last block (nin a multiple of 64) leaves the row at rank nin to zero here
+      // (it stayed stale workspace memory)
+      if (n0 + nr == nin && nr == kRows)
+        for (int w = tid; w < S_out / 4; w += 256) ((uint32_t*)(o + (int64_t)kRows * S_out))[w] = 0u;
     }
     if (cols) {
       constexpr int kRq = kRows / 4;

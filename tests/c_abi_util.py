@@ -76,3 +76,24 @@ def run_gbm_driver(tmp_path, X, y, subspaces, *, L, lr, replacement, ratio, seed
         trees.append(np.frombuffer(raw, np.float64, nn * 8, pos).reshape(nn, 8))
         pos += nn * 64
     return p, 0, trees, np.frombuffer(raw, np.float64, X.shape[0], pos)
+
+
+THREADS = os.path.join(ROOT, "tests", "c", "abi_threads")
+THREADS_ASAN = os.path.join(ROOT, "tests", "c", "abi_threads_asan")
+
+
+def run_threads(tmp_path, X, y, offsets, *, seed, depth, bins, impurity, agg, driver=THREADS,
+                env=None):
+    """tests/c/abi_threads: four jobs fitted + predicted from pthreads (one shared context,
+    then four contexts, then with an induced SBAG_EINVAL), each compared byte for byte with
+    the serial run inside the driver.  Returns the CompletedProcess."""
+    X = np.ascontiguousarray(X, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    off = np.asarray(offsets, np.int64)
+    data = tmp_path / "tdata.bin"
+    with open(data, "wb") as f:
+        f.write(struct.pack("<qqq", X.shape[0], X.shape[1], len(off)))
+        f.write(off.tobytes() + X.tobytes() + y.tobytes())
+    args = [driver, str(data), str(int(seed)), str(depth), str(bins), str(impurity), str(agg)]
+    return subprocess.run(args, capture_output=True, text=True, timeout=600,
+                          env=None if env is None else dict(os.environ, **env))

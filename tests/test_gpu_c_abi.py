@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle
-from c_abi_util import run_driver, run_gbm_driver
+from c_abi_util import run_driver, run_gbm_driver, run_threads
 from conftest import DATA
 
 import spark_bagging_amd as sb
@@ -132,3 +132,44 @@ def test_c_gbm_driver_matches_oracle_gbm(tmp_path):
         for k, f in enumerate(FIELDS):
             assert (ctrees[m][:, k] == nodes[f].astype(np.float64)).all(), f"booster {m} {f}"
     np.testing.assert_array_equal(pred, oracle.gbm_predict(w, subs, trees, const, X))
+
+
+THREAD_CASES = [
+    # (data, label transform, partitions, impurity, agg): the gini engine, the integer
+    # variance engine (integral labels) and the fp64 engine (labels / 10)
+    ("vehicle.svm", None, [0, 300, 846], nat.IMPURITY_GINI, nat.AGG_MODE),
+    ("cpusmall.svm", None, [0, 4000, 8192], nat.IMPURITY_VARIANCE, nat.AGG_MEAN),
+    ("cpusmall.svm", 10.0, [0, 2000, 5000, 8192], nat.IMPURITY_VARIANCE, nat.AGG_MEAN),
+]
+
+
+@pytest.mark.parametrize("case", range(len(THREAD_CASES)))
+def test_c_threads_concurrent_fits_equal_serial(tmp_path, case):
+    """CrossValidator.setParallelism(4) (BaggingRegressorSuite.scala:38-43) from plain C:
+    four pthreads fit + predict at once on one shared context, then on four contexts, then
+    with one thread's SBAG_EINVAL -- every forest and prediction byte-equal to the serial
+    run, the error only in the failing thread's sbag_last_error()."""
+    name, div, part, imp, agg = THREAD_CASES[case]
+    X, y = sb.load_libsvm(os.path.join(DATA, name))
+    if div:
+        y = y / div
+    p = run_threads(tmp_path, X, y, part, seed=7 + case, depth=6, bins=32, impurity=imp, agg=agg)
+    assert p.returncode == 0, p.stdout + p.stderr[-3000:]
+    for mode in ("shared", "separate", "errors-shared", "errors-separate"):
+        assert f"ok {mode}:" in p.stdout, p.stdout
+    assert "java/lang/IllegalArgumentException" in p.stdout
+
+
+def test_c_threads_under_host_asan(tmp_path):
+    """The concurrent driver over the host-ASan/UBSan build of libsbag: the per-context
+    lock, the thread-local error and the worker pools raced by four threads, no reports."""
+    from c_abi_util import THREADS_ASAN
+
+    env = {"ASAN_OPTIONS": "detect_leaks=0:verify_asan_link_order=0:halt_on_error=1",
+           "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
+    X, y = sb.load_libsvm(os.path.join(DATA, "cpusmall.svm"))
+    p = run_threads(tmp_path, X, y / 10.0, [0, 2000, 5000, 8192], seed=3, depth=5, bins=16,
+                    impurity=nat.IMPURITY_VARIANCE, agg=nat.AGG_MEAN, driver=THREADS_ASAN, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr[-3000:]
+    assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr
+    assert p.stdout.count("ok ") == 4, p.stdout

@@ -336,12 +336,13 @@ def test_wide_addressing_equals_buffer_path(ctx, cpusmall, monkeypatch):
     assert_forest_equal(b, oracle_forest(X, y2, counts, subs, 7, 32, False))
 
 
-def test_fp64_engine_past_2_28_rows(ctx, monkeypatch):
-    """fp64 labels are no longer limited to < 2^29 rows: 2^28 + 4096 rows
+def test_fp64_engine_near_the_row_limit(ctx, monkeypatch):
+    """fp64 labels up to the engine's explicit limit of 2^30 rows (ADVICE r04 medium lifted
+    the old 2^29; ADVICE r05 asked for a limit at the largest tested size): 2^30 - 4096 rows
     take the 64-bit-addressed scatter.  The fp64 engine forced on dyadic labels (SBAG_F64=1)
     must give the integer engine's tree byte for byte -- its row-order fp64 sums of dyadic
     labels are exact."""
-    N, F = (1 << 28) + 4096, 2
+    N, F = (1 << 30) - 4096, 2
     ds = nat.DeviceDataset.synthetic(N, F, seed=7, ctx=ctx)
     try:
         part = [round(i * N / 256) for i in range(257)]
@@ -360,3 +361,17 @@ def test_fp64_engine_past_2_28_rows(ctx, monkeypatch):
     assert len(na) > 1
     assert na.tobytes() == nb.tobytes()
     assert sa.tobytes() == sb_.tobytes()
+
+
+def test_fp64_engine_refuses_past_the_row_limit(ctx, monkeypatch):
+    """Past 2^30 rows the fp64 engine refuses (SBAG_EUNSUPPORTED) before any work rather than
+    run kernels at sizes no test covers; the integer engine still fits those rows."""
+    N = (1 << 30) + 64
+    ds = nat.DeviceDataset.synthetic(N, 1, seed=7, ctx=ctx)
+    try:
+        monkeypatch.setenv("SBAG_F64", "1")
+        with pytest.raises(nat.SparkException, match="2\\^30"):
+            nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                    learner_end=1, max_depth=1, max_bins=8, impurity=nat.IMPURITY_VARIANCE)
+    finally:
+        ds.free()

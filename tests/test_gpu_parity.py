@@ -304,6 +304,16 @@ def test_many_classes_c5_shape(ctx):
             oracle.predict(orf, X, classification=True)).all()
 
 
+def test_many_classes_known_tile_cursors_checked(ctx, monkeypatch):
+    """Without-replacement bags (every draw count 1) group class tiles from the split's known
+    class counts (k_tile_scatter_known: atomic (segment, tile) cursors placed by host sizes).
+    SBAG_TILE_CHECK=1 copies every cursor back and fails the fit unless each ends exactly at
+    its tile's end (no test had run the check); trees bit-exact."""
+    monkeypatch.setenv("SBAG_TILE_CHECK", "1")
+    ds, X, forest, orf = _synthetic_cls(ctx, 30000, 100, 64, 3, 12, seed_data=29)
+    assert_forest_equal(forest, orf)
+
+
 @pytest.mark.parametrize("replacement", [False, True])
 def test_tile_resident_entries_opt_in(ctx, monkeypatch, replacement):
     """SBAG_TILE_RESIDENT=1: the root's class-tile grouping kept for the whole fit, the

@@ -225,3 +225,35 @@ def test_per_replica_bins_split_learner_range(ctx, monkeypatch):
     assert_forest_equal(b, orf)
     a.free()
     b.free()
+
+
+def test_ranked_bins_inbag_count_multiple_of_64(ctx):
+    """k_bin_ranked stores per-replica bins by in-bag rank and must leave a zero row at rank
+    nin for the row-lane histogram's aligned over-reads (a replica whose in-bag
+    count is a multiple of 64 left that row stale).  A seed is picked whose bags hold such a
+    replica, the context's bins workspace is first dirtied by a fit with 64 bins (stale codes
+    past an 8-bin fit's range), and the 8-bin fit must equal the oracle's."""
+    rng = np.random.default_rng(64)
+    N, F = 5000, 12
+    X = np.round(rng.normal(size=(N, F)) * 5000) / 8.0  # continuous: per-replica thresholds
+    y = rng.integers(-400, 400, size=N) / 16.0           # dyadic: the integer (ranked) engine
+    part = [0, 2100, N]
+    L = 6
+    for seed in range(1, 5000):
+        counts = oracle.bag(True, 1.0, 0, L, seed, part, N)
+        if ((counts > 0).sum(axis=1) % 64 == 0).any():
+            break
+    else:
+        pytest.skip("no seed with an in-bag count multiple of 64")
+    ds = nat.DeviceDataset.from_numpy(X, y, ctx)
+    try:
+        dirty = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=seed + 1, learner_begin=0,
+                        learner_end=L + 2, partition_offsets=part, max_depth=6, max_bins=64)
+        dirty.free()
+        f = nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=seed, learner_begin=0,
+                    learner_end=L, partition_offsets=part, max_depth=6, max_bins=8)
+    finally:
+        ds.free()
+    subs = [oracle.subspace(1.0, F, seed + i) for i in range(L)]
+    assert_forest_equal(f, oracle_forest(X, y, counts, subs, 6, 8, False, part=part))
+    f.free()
