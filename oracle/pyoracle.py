@@ -327,10 +327,15 @@ def _predict(s, gini):
     return float(best)
 
 
-def fit_tree(X, y, counts, sub, max_depth=5, max_bins=32, min_inst=1, min_gain=0.0, gini=False):
+def fit_tree(X, y, counts, sub, max_depth=5, max_bins=32, min_inst=1, min_gain=0.0, gini=False,
+             part_off=None):
     """One base learner on the replicated subbag; returns the pruned tree as a list of
     NodeData dicts in pre-order (id, prediction, impurity, gain, left, right, feature,
-    threshold, stats)."""
+    threshold, stats).  part_off: the partitions' row offsets -- each partition sums its own
+    rows in row order and the partials are merged in partition order (RandomForest
+    .findBestSplits: mapPartitions + reduceByKey(_ merge _)); None: one partition."""
+    if part_off is None:
+        part_off = [0, len(counts)]
     rows = [r for r in range(len(counts)) if counts[r] > 0]
     n = sum(counts[r] for r in rows)
     if n == 0:
@@ -353,25 +358,38 @@ def fit_tree(X, y, counts, sub, max_depth=5, max_bins=32, min_inst=1, min_gain=0
             break
         agg = {h: [[[0.0] * ns for _ in range(max_bins)] for _ in range(Fr)] for h in active}
         par = {h: [0.0] * ns for h in active}
-        for r in rows:
-            h = where[r]
-            if h not in agg:
-                continue
-            for _ in range(counts[r]):
-                for fl in range(Fr):
-                    st = agg[h][fl][binned[r][fl]]
+        for q in range(len(part_off) - 1):
+            # partition q's DTStatsAggregator per node, then a.merge(b) in partition order
+            pagg = {h: [[[0.0] * ns for _ in range(max_bins)] for _ in range(Fr)] for h in active}
+            ppar = {h: [0.0] * ns for h in active}
+            for r in rows:
+                if not part_off[q] <= r < part_off[q + 1]:
+                    continue
+                h = where[r]
+                if h not in pagg:
+                    continue
+                for _ in range(counts[r]):
+                    for fl in range(Fr):
+                        st = pagg[h][fl][binned[r][fl]]
+                        if gini:
+                            st[int(y[r])] += 1.0
+                        else:
+                            st[0] += 1.0
+                            st[1] += 1.0 * y[r]
+                            st[2] += 1.0 * y[r] * y[r]
                     if gini:
-                        st[int(y[r])] += 1.0
+                        ppar[h][int(y[r])] += 1.0
                     else:
-                        st[0] += 1.0
-                        st[1] += 1.0 * y[r]
-                        st[2] += 1.0 * y[r] * y[r]
-                if gini:
-                    par[h][int(y[r])] += 1.0
-                else:
-                    par[h][0] += 1.0
-                    par[h][1] += 1.0 * y[r]
-                    par[h][2] += 1.0 * y[r] * y[r]
+                        ppar[h][0] += 1.0
+                        ppar[h][1] += 1.0 * y[r]
+                        ppar[h][2] += 1.0 * y[r] * y[r]
+            for h in active:
+                for fl in range(Fr):
+                    for b in range(max_bins):
+                        for i in range(ns):
+                            agg[h][fl][b][i] += pagg[h][fl][b][i]
+                for i in range(ns):
+                    par[h][i] += ppar[h][i]
         for h in active:
             node = nodes[h]
             chain = None if level == 0 else (node["stats"]["calc"], node["stats"]["impurity"])

@@ -831,8 +831,20 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
         }
         free(start);
       }
-      /* DTStatsAggregator.update in row order.  Each (feature, bin) cell is summed in row
-         order whatever the thread split: threads own disjoint feature ranges. */
+      /* RandomForest.findBestSplits: every partition aggregates its own rows
+         (mapPartitions -> binSeqOp -> DTStatsAggregator.update, row order within the
+         partition), and the per-node aggregates of the partitions are merged with
+         reduceByKey((a, b) => a.merge(b)) -- allStats(i) += other.allStats(i).  The merge order
+         is the shuffle's; partition order is one order Spark produces (and the only one at
+         P = 1), so each (node, feature, bin) cell here is: per partition, its rows in row
+         order from 0.0; then the partials added in partition order.  An empty partial adds
+         +0.0, which changes no sum (no sum is ever -0.0), so only touched cells are merged.
+         Gini cells are integer counts (order-free): summed directly.  Threads own disjoint
+         feature ranges; the row order within a node segment ascends, so its partition index
+         only advances. */
+      const int64_t one_off[2] = {0, N};
+      const int64_t* poff = p->part_off ? p->part_off : one_off;
+      const int P = p->part_off ? p->num_partitions : 1;
 #pragma omp parallel num_threads(inner)
       {
         int nth = 1, tid = 0;
@@ -841,34 +853,82 @@ static int fit_one(const void* X, int xkind, const double* y, int64_t N, int F, 
         tid = omp_get_thread_num();
 #endif
         const int f0 = (int)((int64_t)Fr * tid / nth), f1 = (int)((int64_t)Fr * (tid + 1) / nth);
+        /* the open partition's partial of the current node: cells (feature-major as agg) and
+           the node total, with the list of touched cells */
+        double* pa = gini ? NULL : (double*)calloc((size_t)(per_node + ns), sizeof(double));
+        uint8_t* tf = gini ? NULL : (uint8_t*)calloc((size_t)per_node, 1);
+        int64_t* tl = gini ? NULL : (int64_t*)malloc(sizeof(int64_t) * (size_t)(per_node > 0 ? per_node : 1));
+        int64_t ntl = 0;
+        int64_t open_s = -1; /* slot of the open partial, -1: none */
+        int open_q = -1;
+        int q = 0;
         for (int64_t o = 0; o < n_order; o++) {
           const int64_t k = order[o];
           const int64_t s = slot[node_of[k] - first];
           const double lab = y[rows[k]];
           double* a = agg + s * per_node;
           double* pp = par + s * ns;
+          if (!gini) {
+            if (s != open_s) q = 0;
+            while (q + 1 < P && rows[k] >= poff[q + 1]) q++;
+            if (s != open_s || q != open_q) { /* merge the closed partial (a.merge(b)) */
+              if (open_s >= 0) {
+                double* ca = agg + open_s * per_node;
+                for (int64_t t = 0; t < ntl; t++) {
+                  ca[tl[t]] += pa[tl[t]];
+                  pa[tl[t]] = 0.0;
+                  tf[tl[t]] = 0;
+                }
+                if (tid == 0)
+                  for (int i = 0; i < ns; i++) {
+                    par[open_s * ns + i] += pa[per_node + i];
+                    pa[per_node + i] = 0.0;
+                  }
+              }
+              ntl = 0;
+              open_s = s;
+              open_q = q;
+            }
+          }
           for (int c = 0; c < cnt[rows[k]]; c++) {
             for (int fl = f0; fl < f1; fl++) {
-              double* st = a + ((int64_t)fl * nb + bins[k * Fr + fl]) * ns;
+              const int64_t cell = ((int64_t)fl * nb + bins[k * Fr + fl]) * ns;
               if (!gini) {
+                double* st = pa + cell;
+                if (!tf[cell]) {
+                  tf[cell] = 1;
+                  tl[ntl++] = cell;
+                  tl[ntl++] = cell + 1;
+                  tl[ntl++] = cell + 2;
+                }
                 st[0] += 1.0;
                 st[1] += 1.0 * lab;
                 st[2] += 1.0 * lab * lab;
               } else {
-                st[(int)lab] += 1.0;
+                a[cell + (int)lab] += 1.0;
               }
             }
             if (tid == 0) {
               if (!gini) {
-                pp[0] += 1.0;
-                pp[1] += 1.0 * lab;
-                pp[2] += 1.0 * lab * lab;
+                double* pt = pa + per_node;
+                pt[0] += 1.0;
+                pt[1] += 1.0 * lab;
+                pt[2] += 1.0 * lab * lab;
               } else {
                 pp[(int)lab] += 1.0;
               }
             }
           }
         }
+        if (!gini && open_s >= 0) {
+          double* ca = agg + open_s * per_node;
+          for (int64_t t = 0; t < ntl; t++) ca[tl[t]] += pa[tl[t]];
+          if (tid == 0)
+            for (int i = 0; i < ns; i++) par[open_s * ns + i] += pa[per_node + i];
+        }
+        free(pa);
+        free(tf);
+        free(tl);
       }
       /* binsToBestSplit for each node of the group */
       for (int64_t gi = 0; gi < g; gi++) {

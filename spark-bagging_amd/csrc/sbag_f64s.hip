@@ -22,9 +22,12 @@
 //                  feature's bin, fused with the stable two-way partition of
 //                  every split node into its children (left |= bin <= s), which keeps the
 //                  children's entries in row order for the next level
-//   k_fb_chain     one lane per (task, bin): the bucket's rows in row order, each label
-//                  added count times (a row drawn c times is c consecutive rows) --
-//                  Spark's cell sums bit for bit
+//   k_fb_chainx    one partition: one lane per (task, bin), the bucket's rows in row order,
+//                  each label added count times (a row drawn c times is c consecutive
+//                  rows) -- Spark's cell sums bit for bit
+//   k_fb_psum / k_fb_pmerge   several partitions: Spark's per-partition aggregates (row
+//                  order inside a partition, one lane per (task, partition), no buckets),
+//                  merged per (task, bin) in partition order (reduceByKey)
 //   k_fb_finish    binsToBestSplit over the chosen feature's exact bins (prefixes in bin
 //                  order, right = total - left, calculateImpurityStats with the node's
 //                  chained stats): the node's gain, impurity and children calculators
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
   const F64Task t = A.tasks[task];
   __shared__ int64_t s_start[257];
   __shared__ int64_t s_wave[4];
-  if (t.kbase >= 0 && !A.fused) {
+  if (t.kbase >= 0 && !A.psum) {
     int64_t tot = 0;
     if (tid < NB)
       for (int64_t p = t.piece0; p < t.piece1; p++) tot += A.pcnt[p * NB + tid];
@@ -359,8 +362,8 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const F64TPiece pc = A.pieces[pi];
   const F64Task t = A.tasks[pc.task];
   const int NB = A.NB;
-  // (uniform: SGPR resources; fused: k_fb_bchain sums the buckets, this only routes)
-  const bool chain = __builtin_amdgcn_readfirstlane((int)(t.kbase >= 0 && !A.fused)) != 0;
+  // (uniform: SGPR resources; psum: k_fb_psum sums per partition without buckets, this only routes)
+  const bool chain = __builtin_amdgcn_readfirstlane((int)(t.kbase >= 0 && !A.psum)) != 0;
   int64_t* sb = s_base[wv];
   for (int b = lane; b < NB; b += 64) sb[b] = chain ? A.pbase[pi * NB + b] : 0;
   uint32_t* scnt = s_scnt[kStage ? wv : 0];
@@ -528,139 +531,18 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   }
 }
 
-// Spark's row-order fp64 sums of every bucket: one lane per (task, bin), kChC chains per
-// wave.  The chains' labels and counts stream through LDS: the whole wave loads each
-// chain's next kChT labels and counts with contiguous loads two stages ahead and writes
-// them to LDS; then lane l < kChC adds its own slice in order, each label count times
-// (sum += y, sumSq += y*y: instanceWeight 1.0 per draw, DTStatsAggregator.update; a row
-// drawn c times is c consecutive rows).  (kChC * kChT = 1024 entries per stage.)
-template <int kChC>
-__global__ __launch_bounds__(64) void k_fb_chain(F64BucketArgs A, int nchain) {
-  constexpr int kChT = 1024 / kChC;  // entries per chain per stage
-  constexpr int kChPitch = kChT + 1;
-  __shared__ double s_y[kChC * kChPitch];
-  __shared__ uint8_t s_c[kChC * kChPitch];
-  const int NB = A.NB, lane = threadIdx.x;
-  const int64_t nlanes = (int64_t)nchain * NB;
-  const int64_t g = (int64_t)blockIdx.x * kChC + lane;
-  int64_t lo = 0, hi = 0;
-  if (lane < kChC && g < nlanes) {
-    const int64_t task = g / NB;
-    const int b = (int)(g - task * NB);
-    const int64_t* ko = A.kb_off + task * (NB + 1);
-    lo = ko[b];
-    hi = ko[b + 1];
-  }
-  const int64_t len = hi - lo;
-  int64_t maxlen = len;
-  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
-  auto rdl64 = [](int64_t x, int j) -> int64_t {  // lane j's value (j wave-uniform)
-    const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j);
-    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), j);
-    return (int64_t)(((uint64_t)h << 32) | l);
-  };
-  // a stage: chain j's entries [off, off + kChT) -- loads u = kPer j ... kPer j + kPer - 1,
-  // 64 entries each; lanes past a chain's end load its first entry again and store count 0
-  constexpr int kPer = kChT / 64;
-  constexpr int kLd = kChC * kPer;
-  static_assert(kChT % 64 == 0, "whole 64-entry loads per chain slice");
-  int64_t jlo[kChC], jlen[kChC];
-#pragma unroll
-  for (int j = 0; j < kChC; j++) {
-    jlo[j] = rdl64(lo, j);
-    jlen[j] = rdl64(len, j);
-  }
-  auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&cv)[kLd]) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int j = u / kPer;
-      const int64_t x = off + (u % kPer) * 64 + lane;
-      // (past the chain's end: its last entry, or the one before an empty chain -- min/max,
-      // no select on the wave-uniform length, which the compiler turns into branches)
-      const int64_t at = max(min(jlo[j] + x, jlo[j] + jlen[j] - 1), (int64_t)0);
-      yv[u] = A.bky[at];
-      cv[u] = (uint32_t)A.bkc[at];  // (unconditional: a masked load would make the
-    }                               //  compiler wait for every load in flight)
-  };
-  double yA[kLd], yB[kLd];
-  uint32_t cA[kLd], cB[kLd];
-  if (maxlen > 0) {
-    load(0, yA, cA);
-    load(kChT, yB, cB);
-  }
-  double s1 = 0.0, s2 = 0.0;
-  uint64_t cnt = 0;
-  for (int64_t off = 0; off < maxlen; off += kChT) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int j = u / kPer;
-      const int x = (u % kPer) * 64 + lane;
-      s_y[j * kChPitch + x] = yA[u];
-      s_c[j * kChPitch + x] = off + x < jlen[j] ? (uint8_t)cA[u] : (uint8_t)0;
-    }
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      yA[u] = yB[u];
-      cA[u] = cB[u];
-    }
-    if (off + 2 * kChT < maxlen) load(off + 2 * kChT, yB, cB);
-    const int n = (int)min((int64_t)kChT, max((int64_t)0, len - off));
-    if (lane < kChC) {
-      const double* sy = s_y + lane * kChPitch;
-      const uint8_t* sc = s_c + lane * kChPitch;
-      // (4 entries' LDS reads ahead of their adds; every bucket entry is drawn, c >= 1.)
-      // A lane's adds are one dependent chain, so the instructions between two adds pace a
-      // long chain: the second to fourth draws are added branch-free (a draw past c adds
-      // -0.0, which leaves every sum unchanged, -0.0 included), the loop takes only c > 4
-      // (scripts/micro/chain_lat.hip: a per-entry count loop costs 4.5x the adds).
-      const bool multi = A.cmax > 1;
-      auto add = [&](double y, uint32_t c) {
-        const double w = 1.0 * y;  // instanceWeight * label
-        const double wy = w * y;   // instanceWeight * label * label
-        s1 += w;
-        s2 += wy;
-        if (multi) {
-          s1 += c >= 2 ? w : -0.0;
-          s2 += c >= 2 ? wy : -0.0;
-          s1 += c >= 3 ? w : -0.0;
-          s2 += c >= 3 ? wy : -0.0;
-          s1 += c >= 4 ? w : -0.0;
-          s2 += c >= 4 ? wy : -0.0;
-          for (uint32_t k = 4; k < c; k++) {
-            s1 += w;
-            s2 += wy;
-          }
-        }
-        cnt += c;
-      };
-      int x = 0;
-      for (; x + 4 <= n; x += 4) {
-        const double y0 = sy[x], y1 = sy[x + 1], y2 = sy[x + 2], y3 = sy[x + 3];
-        const uint32_t c0 = sc[x], c1 = sc[x + 1], c2 = sc[x + 2], c3 = sc[x + 3];
-        add(y0, c0);
-        add(y1, c1);
-        add(y2, c2);
-        add(y3, c3);
-      }
-      for (; x < n; x++) add(sy[x], sc[x]);
-    }
-  }
-  if (lane < kChC && g < nlanes) {
-    double* o = A.chist + g * 3;
-    o[0] = (double)cnt;  // count += 1.0 per draw
-    o[1] = s1;
-    o[2] = s2;
-  }
-}
-
-// k_fb_chain with the draws exploded in LDS: the same sums, but the serial lanes' loop is
-// one 16-byte LDS read and two adds per draw, with no per-entry count logic.  The whole
-// wave turns a stage of 512 entries (kChT per chain, kChC chains) into draw streams: the
-// (sumSq term) products and the draw positions (a scan of the counts per chain) are
-// computed in parallel, entry e of count c is written c times as (w, w*y), and every chain
-// is padded to the wave's longest stream with (-0.0, -0.0), which leaves a sum unchanged
-// (-0.0 included), so the serial loop runs a uniform trip count.  A stage's draws beyond
-// kDcap per chain go through further windows.  The count is the integer sum of the draws.
+// Spark's row-order fp64 sums of every bucket (one partition): one lane per (task, bin), kChC
+// chains per wave.  A lane's adds are one dependent chain, so what paces a long chain is the
+// instructions between two adds: the draws are exploded in LDS first.  The whole wave turns a
+// stage of 512 entries (kChT per chain, kChC chains) into draw streams: the (sumSq term)
+// products and the draw positions (a scan of the counts per chain) are computed in parallel,
+// entry e of count c is written c times as (w, w*y), and every chain is padded to the wave's
+// longest stream with (-0.0, -0.0), which leaves a sum unchanged (-0.0 included), so the serial
+// loop is one 16-byte LDS read and two adds per draw with a uniform trip count.  A stage's
+// draws beyond kDcap per chain go through further windows.  The count is the integer sum of
+// the draws.  (Round 4: 22 cycles per draw against 100 with a per-entry count loop,
+// scripts/micro/chain_lat.hip; the per-entry kernel and a 64-chains-per-wave variant were
+// measured slower and removed in round 6.)
 template <int kChC>
 __global__ __launch_bounds__(64) void k_fb_chainx(F64BucketArgs A, int nchain) {
   constexpr int kChT = 512 / kChC;     // entries per chain per stage
@@ -826,313 +708,132 @@ __global__ __launch_bounds__(64) void k_fb_chainx(F64BucketArgs A, int nchain) {
   }
 }
 
-// k_fb_chain with every lane a chain (64 per wave): the serial adds are VALU-issue-bound
-// where chains are many (the deep levels), and a wave-instruction then serves 64 chains
-// instead of 16.  A stage is 16 entries per chain; load u covers chains 4u .. 4u + 3, 16
-// lanes each (so the chains' bounds are per lane, fetched once with shuffles).
-__global__ __launch_bounds__(64) void k_fb_chain64(F64BucketArgs A, int nchain) {
-  constexpr int kT = 16;          // entries per chain per stage
-  constexpr int kP = kT + 1;
-  constexpr int kLd = 64 * kT / 64;  // 16 loads per stage
-  __shared__ double s_y[64 * kP];
-  __shared__ uint8_t s_c[64 * kP];
-  const int NB = A.NB, lane = threadIdx.x;
-  const int64_t nlanes = (int64_t)nchain * NB;
-  const int64_t g = (int64_t)blockIdx.x * 64 + lane;
-  int64_t lo = 0, hi = 0;
-  if (g < nlanes) {
-    const int64_t task = g / NB;
-    const int b = (int)(g - task * NB);
-    const int64_t* ko = A.kb_off + task * (NB + 1);
-    lo = ko[b];
-    hi = ko[b + 1];
-  }
-  const int64_t len = hi - lo;
-  int64_t maxlen = len;
-  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
-  const int seg = lane >> 4, x16 = lane & 15;
-  // the chains' bounds in LDS (load u reads chain 4u + seg's: per lane, not per wave)
-  __shared__ int64_t s_lo[64], s_len[64];
-  s_lo[lane] = lo;
-  s_len[lane] = len;
-  auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&cv)[kLd]) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int64_t ul = s_lo[4 * u + seg], un = s_len[4 * u + seg];
-      const int64_t x = off + x16;
-      const int64_t at = max(min(ul + x, ul + un - 1), (int64_t)0);
-      yv[u] = A.bky[at];
-      cv[u] = (uint32_t)A.bkc[at];
-    }
-  };
-  double yA[kLd], yB[kLd];
-  uint32_t cA[kLd], cB[kLd];
-  if (maxlen > 0) {
-    load(0, yA, cA);
-    load(kT, yB, cB);
-  }
-  double s1 = 0.0, s2 = 0.0;
-  uint64_t cnt = 0;
-  const bool multi = A.cmax > 1;
-  for (int64_t off = 0; off < maxlen; off += kT) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int j = 4 * u + seg;
-      s_y[j * kP + x16] = yA[u];
-      s_c[j * kP + x16] = off + x16 < s_len[j] ? (uint8_t)cA[u] : (uint8_t)0;
-    }
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      yA[u] = yB[u];
-      cA[u] = cB[u];
-    }
-    if (off + 2 * kT < maxlen) load(off + 2 * kT, yB, cB);
-    const int n = (int)min((int64_t)kT, max((int64_t)0, len - off));
-    const double* sy = s_y + lane * kP;
-    const uint8_t* sc = s_c + lane * kP;
-    // (as k_fb_chain: the second to fourth draws branch-free, -0.0 for absent ones)
-    auto add = [&](double y, uint32_t c) {
-      const double w = 1.0 * y;  // instanceWeight * label
-      const double wy = w * y;   // instanceWeight * label * label
-      s1 += w;
-      s2 += wy;
-      if (multi) {
-        s1 += c >= 2 ? w : -0.0;
-        s2 += c >= 2 ? wy : -0.0;
-        s1 += c >= 3 ? w : -0.0;
-        s2 += c >= 3 ? wy : -0.0;
-        s1 += c >= 4 ? w : -0.0;
-        s2 += c >= 4 ? wy : -0.0;
-        for (uint32_t k = 4; k < c; k++) {
-          s1 += w;
-          s2 += wy;
-        }
-      }
-      cnt += c;
-    };
-    int x = 0;
-    for (; x + 4 <= n; x += 4) {
-      const double y0 = sy[x], y1 = sy[x + 1], y2 = sy[x + 2], y3 = sy[x + 3];
-      const uint32_t c0 = sc[x], c1 = sc[x + 1], c2 = sc[x + 2], c3 = sc[x + 3];
-      add(y0, c0);
-      add(y1, c1);
-      add(y2, c2);
-      add(y3, c3);
-    }
-    for (; x < n; x++) add(sy[x], sc[x]);
-  }
-  if (g < nlanes) {
-    double* o = A.chist + g * 3;
-    o[0] = (double)cnt;  // count += 1.0 per draw
-    o[1] = s1;
-    o[2] = s2;
-  }
-}
 
-// ---------------------------------------------------------------- fused bucket chains
-// Bucketing and chains fused (round 5, SBAG_F64_FUSED=1; the default stays the global buckets of
-// k_fb_scatter + k_fb_chainx, which measured faster: 260 vs 294 ms per serialized C3-shape fit,
-// profiles/r05logs/r05h/ -- the root's few long tasks expose each block's latency).  One workgroup per chain task walks the task's entries
-// (ent_in / ey_in [t.a, t.b): the node's rows in row order, bins from k_fb_count's ebin) in
-// blocks of kE.  A block is ordered by bin in LDS, stably: each 64-entry round ranks its
-// entries among the same bin's with ballots over the bin bits and counts their draws with
-// ballots over the count bits, a scan over (bin, round) places every round's draws, and each
-// entry's label is written c times (a row drawn c times is c consecutive rows,
-// sql/bfunctions.scala:42-44).  Then thread b adds bin b's records in order -- sum += y,
-// sumSq += y * y (instanceWeight 1.0) -- its sums carried across the blocks: Spark's
-// row-order cell sums (DTStatsAggregator.update) bit for bit, with no bucket written to or
-// read from HBM (the global buckets moved ~176 GB per C3-shape fit, profiles/r04am/).  A bin's
-// records are padded to a multiple of 8 with -0.0 (sum += -0.0 and sumSq += +0.0 leave both
-// unchanged: sumSq >= +0.0), so the serial loop takes 8 records a step.  The round bookkeeping
-// is double-buffered, so the next block's ranking overlaps the bin threads' adds: three
-// barriers per block.  A block whose records exceed kD goes through several windows.
-template <int kE, bool kCarried>
-__global__ __launch_bounds__(256) void k_fb_bchain(F64BucketArgs A, int nchain, int nbits, int cbits) {
-  constexpr int kR = kE / 64;   // rounds
-  constexpr int kRW = kR / 4;   // rounds per wave
-  constexpr int kD = kE * 5 / 2;  // records per window
-  const int task = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int NB = A.NB;
+// ---------------------------------------------------------------- per-partition sums
+// Several partitions (P > 1): RandomForest.findBestSplits aggregates each partition's rows on
+// its own (mapPartitions -> binSeqOp: DTStatsAggregator.update, row order within the
+// partition, sums from 0.0) and merges the partitions' aggregates per node with
+// reduceByKey((a, b) => a.merge(b)), allStats(i) += other.allStats(i).  The merge order is the
+// shuffle's; partition order is one order Spark produces (and the only one at P = 1), and the
+// oracle restates the same (oracle/sbag_oracle.c fit_one).  So a (task, bin) cell is P
+// independent row-order chains plus a P-term merge: no bucketing by bin is needed to keep the
+// order -- one lane per (task, partition) walks that partition's entries of the task (a
+// contiguous run: a node's entries are in row order, partitions are row ranges) and adds each
+// into its own LDS bins; k_fb_pmerge then adds the P partials of every (task, bin) in
+// partition order.
+//
+// k_fb_psum: lane l of workgroup w takes unit g = w lpw + l = (task, partition).  Its run is
+// found by two binary searches of the partition's row bounds in the task's entries.  LDS per
+// lane: NB (sum, sumSq) pairs and NB counts, interleaved across the lanes.  Per entry: its bin (k_fb_count's ebin), draw
+// count and label (carried ey_in, else y[row]) are loaded kPs entries ahead; the add is one
+// LDS read-modify-write per entry (sum += y, sumSq += y*y once per draw; a lane's LDS
+// operations execute in order, so consecutive entries of one bin chain through LDS).
+constexpr int kPs = 8;
+__global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain, int lpw) {
   extern __shared__ __align__(16) uint8_t smem[];
-  double* sd = (double*)smem;                                // [kD] records
-  uint32_t* src = (uint32_t*)(smem + (size_t)kD * 8);        // [2][kR][NB] round draws -> slots
-  uint32_t* sbs = src + 2 * kR * NB;                         // [NB + 1] bin starts (padded)
-  uint32_t* sbn = sbs + NB + 1;                              // [NB] bin draws
-  __shared__ int64_t swave[4];  // (static: a pointer rebuilt from an integer is a flat pointer,
-                                //  whose accesses wait for every global load in flight)
+  const int lane = threadIdx.x, NB = A.NB, P = A.P;
+  const int64_t g = (int64_t)blockIdx.x * lpw + lane;
+  if (lane >= lpw || g >= (int64_t)nchain * P) return;  // (no barriers in this kernel)
+  // bins interleaved across the lanes ([bin][lane]): one bin of 64 lanes is 64 consecutive
+  // 16-byte pairs, so a wave's read-modify-write costs the ds_read_b128 minimum whatever the bins
+  double2* sd = (double2*)smem + lane;
+  uint32_t* sc = (uint32_t*)((double2*)smem + (size_t)lpw * NB) + lane;
+  const int64_t task = g / P;
+  const int q = (int)(g - task * P);
   const F64Task t = A.tasks[task];
-  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const uint64_t above = ~(lt | (1ull << lane));
-  constexpr bool carried = kCarried;  // the labels travel with the entries (ey_in), else y[row]
-  for (int k = tid; k < 2 * kR * NB; k += 256) src[k] = 0u;
-  double s1 = 0.0, s2 = 0.0;  // thread b < NB: bin b's sums, carried across the blocks
-  uint64_t cnt = 0;
-  const int64_t n = t.b - t.a;
-  // (every load unconditional, past the task's end at its last entry -- masked at use: a
-  // select on a loaded value, or a branch around a load, makes the compiler wait for it)
-  auto load = [&](int64_t blk, uint64_t (&e)[kRW], double (&y)[kRW], uint32_t (&bn)[kRW]) {
+  // the run of entries whose rows lie in [poff[q], poff[q + 1])
+  auto lower = [&](int64_t row) {
+    int64_t lo = t.a, hi = t.b;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)(uint32_t)A.ent_in[mid] < row)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return lo;
+  };
+  const int64_t lo = lower(A.poff[q]), hi = lower(A.poff[q + 1]);
+  for (int b = 0; b < NB; b++) {
+    sd[(size_t)b * lpw] = make_double2(0.0, 0.0);
+    sc[(size_t)b * lpw] = 0u;
+  }
+  const bool carried = A.ey_in != nullptr;
+  uint64_t eA[kPs], eB[kPs];
+  uint32_t bA[kPs], bB[kPs];
+  double yA[kPs], yB[kPs];
+  // (loads past the run repeat its last entry, masked at use)
+  auto load = [&](int64_t i0, uint64_t (&e)[kPs], uint32_t (&bn)[kPs], double (&yv)[kPs]) {
 #pragma unroll
-    for (int u = 0; u < kRW; u++) {
-      const int64_t ic = min(blk + 64 * (kRW * wave + u) + lane, n - 1);  // round kRW wave + u
-      e[u] = A.ent_in[t.a + ic];
-      y[u] = carried ? A.ey_in[t.a + ic] : 0.0;
-      bn[u] = (uint32_t)A.ebin[t.ebase + ic];
+    for (int u = 0; u < kPs; u++) {
+      const int64_t x = min(i0 + u, hi - 1);
+      e[u] = A.ent_in[x];
+      bn[u] = (uint32_t)A.ebin[t.ebase + (x - t.a)];
+      yv[u] = carried ? A.ey_in[x] : 0.0;
     }
     if (!carried)
 #pragma unroll
-      for (int u = 0; u < kRW; u++) y[u] = A.y[(uint32_t)e[u]];
+      for (int u = 0; u < kPs; u++) yv[u] = A.y[(uint32_t)e[u]];
   };
-  // two blocks' loads in flight ahead of the one being ordered (a task's blocks follow each
-  // other; with one workgroup per CU -- the root's few long tasks -- a block's work is shorter
-  // than the memory latency)
-  uint64_t eA[kRW], eB[kRW], eC[kRW];
-  double yA[kRW], yB[kRW], yC[kRW];
-  uint32_t bA[kRW], bB[kRW], bC[kRW];
-  if (n > 0) {
-    load(0, eA, yA, bA);
-    load(kE, eB, yB, bB);
-  }
-  block_sync();
-  int buf = 0;
-  // the block body (fixed registers per block: rotating buffers whose loads are in flight
-  // would make the compiler wait for them)
-  auto body = [&](int64_t blk, const uint64_t (&eX)[kRW], const double (&yX)[kRW], const uint32_t (&bX)[kRW]) {
-    uint32_t* rc = src + buf * kR * NB;
-    // A: ranks among the round's entries of the same bin (in draws), the round's draws per bin
-    uint32_t pre[kRW], cc[kRW];
+  auto body = [&](int64_t i0, const uint64_t (&e)[kPs], const uint32_t (&bn)[kPs], const double (&yv)[kPs]) {
 #pragma unroll
-    for (int u = 0; u < kRW; u++) {
-      const int q = kRW * wave + u;
-      const bool valid = blk + 64 * q + lane < n;
-      const uint32_t c = valid ? (uint32_t)(eX[u] >> 32) & 0xffu : 0u;  // past the end: no draws
-      cc[u] = c;
-      const uint32_t bin = bX[u];
-      uint64_t eq = __ballot(c != 0u);
-      for (int k = 0; k < nbits; k++) {
-        const bool bit = (bin >> k) & 1u;
-        const uint64_t m = __ballot(bit);
-        eq &= bit ? m : ~m;
+    for (int u = 0; u < kPs; u++) {
+      if (i0 + u >= hi) break;
+      const uint32_t c = (uint32_t)(e[u] >> 32) & 0xffu;
+      const double w = 1.0 * yv[u];  // instanceWeight * label
+      const double wy = w * yv[u];   // instanceWeight * label * label
+      const size_t at = (size_t)bn[u] * lpw;
+      double2 v = sd[at];
+      for (uint32_t k = 0; k < c; k++) {
+        v.x += w;
+        v.y += wy;
       }
-      uint32_t p = 0, tot = 0;
-      for (int k = 0; k < cbits; k++) {
-        const uint64_t m = __ballot((c >> k) & 1u) & eq;
-        p += (uint32_t)__popcll(m & lt) << k;
-        tot += (uint32_t)__popcll(m) << k;
-      }
-      pre[u] = p;
-      if (c != 0u && (eq & above) == 0ull) rc[q * NB + bin] = tot;  // the bin's last lane
+      sd[at] = v;
+      sc[at] += c;  // count += 1.0 per draw (an integer sum: order-free)
     }
-    block_sync();
-    // B: per bin the rounds' offsets, the padded bin sizes, their scan over the bins
-    uint32_t bd = 0, bp = 0;
-    uint32_t ro[kR];  // (all reads first: a read after a write of the same array waits for it)
-    if (tid < NB) {
-#pragma unroll
-      for (int q = 0; q < kR; q++) ro[q] = rc[q * NB + tid];
-#pragma unroll
-      for (int q = 0; q < kR; q++) {
-        const uint32_t v = ro[q];
-        ro[q] = bd;
-        bd += v;
-      }
-      bp = (bd + 7u) & ~7u;
-    }
-    uint32_t ex, all;
-    if (NB <= 64) {
-      if (wave == 0) {
-        uint32_t incl = bp;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t v = __shfl_up(incl, o);
-          if (lane >= o) incl += v;
-        }
-        ex = incl - bp;
-        all = __shfl(incl, 63);
-      }
-    } else {
-      int64_t a64;
-      ex = (uint32_t)scan256((int64_t)bp, swave, &a64);
-      all = (uint32_t)a64;
-    }
-    if (tid < NB) {
-      sbs[tid] = ex;
-      sbn[tid] = bd;
-#pragma unroll
-      for (int q = 0; q < kR; q++) rc[q * NB + tid] = ro[q] + ex;
-      if (tid == 0) sbs[NB] = all;
-    }
-    block_sync();
-    const uint32_t total = sbs[NB];
-    for (uint32_t wnd = 0; wnd < total; wnd += kD) {
-      // C: the window's records -- every entry's draws, each bin's padding
-#pragma unroll
-      for (int u = 0; u < kRW; u++) {
-        if (cc[u] == 0u) continue;
-        const uint32_t at = rc[(kRW * wave + u) * NB + bX[u]] + pre[u];
-        for (uint32_t k = 0; k < cc[u]; k++) {
-          const uint32_t x = at + k;
-          if (x - wnd < (uint32_t)kD) sd[x - wnd] = yX[u];
-        }
-      }
-      if (tid < NB) {
-        const uint32_t b0 = sbs[tid] + sbn[tid], b1 = sbs[tid + 1];
-        for (uint32_t x = max(b0, wnd); x < min(b1, wnd + (uint32_t)kD); x++) sd[x - wnd] = -0.0;
-      }
-      block_sync();
-      // D: thread b adds bin b's records of the window, 8 a step, the next 8 read ahead
-      if (tid < NB) {
-        const uint32_t lo = max(sbs[tid], wnd), hi = min(sbs[tid + 1], wnd + (uint32_t)kD);
-        const int m = (int)(hi > lo ? hi - lo : 0u);  // a multiple of 8 (bins and windows are)
-        const double* p = sd + (lo - wnd);
-        double a[8];
-        if (m > 0)
-#pragma unroll
-          for (int k = 0; k < 8; k++) a[k] = p[k];
-        for (int x = 0; x < m; x += 8) {
-          double b8[8];
-          if (x + 8 < m)
-#pragma unroll
-            for (int k = 0; k < 8; k++) b8[k] = p[x + 8 + k];
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            s1 += a[k];          // instanceWeight * label
-            s2 += a[k] * a[k];   // instanceWeight * label * label
-          }
-#pragma unroll
-          for (int k = 0; k < 8; k++) a[k] = b8[k];
-        }
-        if (wnd + kD >= total) {  // the block's last window: its rounds' slots are spent
-          cnt += sbn[tid];
-          for (int q = 0; q < kR; q++) rc[q * NB + tid] = 0u;
-        }
-      }
-      if (wnd + kD < total) block_sync();  // (more windows: the records are rewritten)
-    }
-    buf ^= 1;
   };
-  for (int64_t blk = 0; blk < n;) {
-    load(blk + 2 * kE, eC, yC, bC);
-    body(blk, eA, yA, bA);
-    if ((blk += kE) >= n) break;
-    load(blk + 2 * kE, eA, yA, bA);
-    body(blk, eB, yB, bB);
-    if ((blk += kE) >= n) break;
-    load(blk + 2 * kE, eB, yB, bB);
-    body(blk, eC, yC, bC);
-    blk += kE;
+  if (lo < hi) load(lo, eA, bA, yA);
+  for (int64_t i0 = lo; i0 < hi; i0 += 2 * kPs) {
+    if (i0 + kPs < hi) load(i0 + kPs, eB, bB, yB);
+    body(i0, eA, bA, yA);
+    if (i0 + kPs >= hi) break;
+    if (i0 + 2 * kPs < hi) load(i0 + 2 * kPs, eA, bA, yA);
+    body(i0 + kPs, eB, bB, yB);
   }
-  if (task < nchain && tid < NB) {
-    double* o = A.chist + ((int64_t)task * NB + tid) * 3;
-    o[0] = (double)cnt;  // count += 1.0 per draw (an integer sum: order-free)
-    o[1] = s1;
-    o[2] = s2;
+  double* o = A.ppart + (size_t)g * NB * 3;
+  for (int b = 0; b < NB; b++) {
+    const double2 v = sd[(size_t)b * lpw];
+    o[3 * b] = (double)sc[(size_t)b * lpw];
+    o[3 * b + 1] = v.x;
+    o[3 * b + 2] = v.y;
   }
 }
 
-static size_t bchain_lds(int kE, int NB) {
-  return (size_t)kE * 5 / 2 * 8 + ((size_t)2 * (kE / 64) * NB + 2 * NB + 1) * 4;
+// the partitions' partials of every (task, bin), added in partition order from 0.0 (the first
+// partial is then itself: no sum is ever -0.0)
+__global__ __launch_bounds__(256) void k_fb_pmerge(F64BucketArgs A, int nchain) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int NB = A.NB, P = A.P;
+  if (i >= (int64_t)nchain * NB) return;
+  const int64_t task = i / NB;
+  const int b = (int)(i - task * NB);
+  const double* p = A.ppart + ((size_t)task * P * NB + b) * 3;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int q = 0; q < P; q++) {
+    s0 += p[0];
+    s1 += p[1];
+    s2 += p[2];
+    p += (size_t)NB * 3;
+  }
+  double* o = A.chist + (size_t)i * 3;
+  o[0] = s0;
+  o[1] = s1;
+  o[2] = s2;
 }
+
+// lanes per k_fb_psum workgroup: as many as 40 KB of LDS bins hold (64 at NB <= 32)
+static int psum_lanes(int NB) { return std::max(1, std::min(64, 40960 / (NB * 20))); }
+size_t fb_psum_part_bytes(int64_t nchain, int P, int NB) { return (size_t)nchain * P * NB * 3 * sizeof(double); }
 
 // ---------------------------------------------------------------- label column
 // analyze_labels (sbag_host.cpp) on the device: per label, finite / integral and the
@@ -1244,60 +945,28 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
       hipLaunchKernelGGL((scatter_stage ? k_fb_scatter<true, false> : k_fb_scatter<false, false>), g, dim3(256), 0,
                          st, a, npieces, nbits);
   }
-  if (a.fused) {  // the chain tasks' sums by k_fb_bchain (no buckets: k_fb_scatter routed only)
-    int cbits = 1;
-    while (cbits < 8 && (a.cmax >> cbits) != 0) cbits++;
-    // 1024-entry blocks: ~25 KB of LDS at 32 bins, six workgroups per CU (SBAG_F64_BCHAIN_E=512|2048)
-    static const int be = getenv("SBAG_F64_BCHAIN_E") ? atoi(getenv("SBAG_F64_BCHAIN_E")) : 1024;
-    if (nchain > 0 && a.NB <= 256) {
-      const bool cy = a.ey_in != nullptr;
-      auto go = [&](const void* fn, int e) {
-        const size_t lds = bchain_lds(e, a.NB);
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        void* args[] = {(void*)&a, (void*)&nchain, (void*)&nbits, (void*)&cbits};
-        (void)hipLaunchKernel(fn, dim3((unsigned)nchain), dim3(256), args, lds, st);
-      };
-      if (be == 512)
-        go(cy ? (const void*)k_fb_bchain<512, true> : (const void*)k_fb_bchain<512, false>, 512);
-      else if (be == 2048)
-        go(cy ? (const void*)k_fb_bchain<2048, true> : (const void*)k_fb_bchain<2048, false>, 2048);
-      else
-        go(cy ? (const void*)k_fb_bchain<1024, true> : (const void*)k_fb_bchain<1024, false>, 1024);
-    }
+  if (nchain <= 0) return;
+  if (a.psum) {  // P > 1: per-partition runs of each chain task, then the merge in partition order
+    const int lpw = psum_lanes(a.NB);
+    const int64_t units = (int64_t)nchain * a.P;
+    const size_t lds = (size_t)lpw * a.NB * (sizeof(double2) + sizeof(uint32_t));
+    hipLaunchKernelGGL(k_fb_psum, dim3((unsigned)((units + lpw - 1) / lpw)), dim3(64), lds, st, a, nchain, lpw);
+    const int64_t cells = (int64_t)nchain * a.NB;
+    hipLaunchKernelGGL(k_fb_pmerge, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, nchain);
     return;
   }
+  // one partition: the buckets' chains.  The serial lanes are latency-bound, so a wave takes
+  // as few chains as keep >= 2048 waves (two per SIMD: the VGPR budget's occupancy) -- C3
+  // shape, serialized fit, ms: 16 everywhere 331, by this rule 305 (root 37 instead of 51); a
+  // booster's few chains get a wave each (GBM 10M x 100: chains 71 -> 16 ms per booster)
   const int64_t lanes = (int64_t)nchain * a.NB;
-  // k_fb_chainx (the default; SBAG_F64_CHAIN_X=0: the per-entry k_fb_chain): the serial
-  // lanes are latency-bound, so a wave takes as few chains as keep >= 2048 waves (two per
-  // SIMD: the VGPR budget's occupancy) -- C3 shape, serialized fit, ms: 16 everywhere 331,
-  // by this rule 305 (root 37 instead of 51); a booster's few chains get a wave each
-  // (GBM 10M x 100: chains 71 -> 16 ms per booster).  k_fb_chain (per-entry loop) kept for
-  // A/B: 16 per wave wherever there are enough chains, else 4 or 1.
-  // (SBAG_F64_CHAIN_C=1|4|16|64 forces the width, for A/B; 64 is k_fb_chain64)
-  const int cenv = getenv("SBAG_F64_CHAIN_C") ? atoi(getenv("SBAG_F64_CHAIN_C")) : 0;
-  const char* xenv = getenv("SBAG_F64_CHAIN_X");
-  const bool xpl = !(xenv && atoi(xenv) == 0);
-  const int cw = cenv == 1 || cenv == 4 || cenv == 16 || cenv == 64 ? cenv
-                 : xpl ? (lanes >= 16 * 2048 ? 16 : lanes >= 4 * 2048 ? 4 : 1)
-                       : (lanes >= 4096 ? 16 : lanes >= 512 ? 4 : 1);
-  if (lanes <= 0) return;
-  if (xpl && cw != 64) {
-    if (cw == 16)
-      hipLaunchKernelGGL(k_fb_chainx<16>, dim3((unsigned)((lanes + 15) / 16)), dim3(64), 0, st, a, nchain);
-    else if (cw == 4)
-      hipLaunchKernelGGL(k_fb_chainx<4>, dim3((unsigned)((lanes + 3) / 4)), dim3(64), 0, st, a, nchain);
-    else
-      hipLaunchKernelGGL(k_fb_chainx<1>, dim3((unsigned)lanes), dim3(64), 0, st, a, nchain);
-    return;
-  }
-  if (cw == 64)
-    hipLaunchKernelGGL(k_fb_chain64, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st, a, nchain);
-  else if (cw == 16)
-    hipLaunchKernelGGL(k_fb_chain<16>, dim3((unsigned)((lanes + 15) / 16)), dim3(64), 0, st, a, nchain);
+  const int cw = lanes >= 16 * 2048 ? 16 : lanes >= 4 * 2048 ? 4 : 1;
+  if (cw == 16)
+    hipLaunchKernelGGL(k_fb_chainx<16>, dim3((unsigned)((lanes + 15) / 16)), dim3(64), 0, st, a, nchain);
   else if (cw == 4)
-    hipLaunchKernelGGL(k_fb_chain<4>, dim3((unsigned)((lanes + 3) / 4)), dim3(64), 0, st, a, nchain);
+    hipLaunchKernelGGL(k_fb_chainx<4>, dim3((unsigned)((lanes + 3) / 4)), dim3(64), 0, st, a, nchain);
   else
-    hipLaunchKernelGGL(k_fb_chain<1>, dim3((unsigned)lanes), dim3(64), 0, st, a, nchain);
+    hipLaunchKernelGGL(k_fb_chainx<1>, dim3((unsigned)lanes), dim3(64), 0, st, a, nchain);
 }
 
 // ---------------------------------------------------------------- finish

@@ -1861,6 +1861,7 @@ struct F64sGrow {
                     const uint64_t*, void*)> int_hist;
   // SURVEY §8d work bytes of a level's node segments
   std::function<void(const std::vector<std::pair<int64_t, int64_t>>&, const std::vector<int>&)> add_work;
+  const std::vector<int64_t>& poff;  // [P + 1] the partitions' row offsets (one: {0, N})
   int64_t fallbacks = 0;
   int levels = 0;
 };
@@ -1888,6 +1889,13 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       G.ds->lab.d_y64 = p;
     }
     d_y64 = G.ds->lab.d_y64;
+  }
+  // the partitions (RandomForest.findBestSplits aggregates each one apart, §4.7)
+  const int P = (int)G.poff.size() - 1;
+  int64_t* d_poff = nullptr;
+  if (P > 1) {
+    TRY(ws_typed(c, "f64_poff", G.poff.size(), &d_poff));
+    TRY(h2d(c, d_poff, G.poff.data(), G.poff.size()));
   }
   const double u = std::ldexp(1.0, -53);
   const double M1 = G.lab.ymax_abs, M2 = G.lab.ymax_sq, Msq = std::max(M2, M1 * M1);
@@ -2040,14 +2048,14 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       TRY(ws_typed(c, "fb_kboff", (size_t)nt * (NB + 1), &d_kboff));
       uint8_t* d_ebin;
       TRY(ws_typed(c, "fb_ebin", (size_t)std::max<int64_t>(1, ebase), &d_ebin));
-      // SBAG_F64_FUSED=1: bucketing fused into the chains in LDS (k_fb_bchain, no bucket space);
-      // measured slower than the global buckets + k_fb_chainx on the C3 shape (serialized fit
-      // 294 vs 260 ms, profiles/r05logs/r05h/: a task's blocks are ordered one after another by one
-      // workgroup, so the root's 256 long tasks expose each block's latency), kept for A/B.
-      // (read per call: the tests switch it between fits)
-      const bool fused = getenv("SBAG_F64_FUSED") && atoi(getenv("SBAG_F64_FUSED")) != 0 && NB <= 256;
-      TRY(ws_typed(c, "fb_bky", (size_t)std::max<int64_t>(1, fused ? 1 : nlabels), &d_bky));
-      TRY(ws_typed(c, "fb_bkc", (size_t)std::max<int64_t>(1, fused ? 1 : nlabels), &d_bkc));
+      // several partitions: Spark's per-partition aggregates merged in partition order
+      // (k_fb_psum + k_fb_pmerge, no buckets); one partition: the buckets' row-order chains
+      const bool psum = P > 1;
+      TRY(ws_typed(c, "fb_bky", (size_t)std::max<int64_t>(1, psum ? 1 : nlabels), &d_bky));
+      TRY(ws_typed(c, "fb_bkc", (size_t)std::max<int64_t>(1, psum ? 1 : nlabels), &d_bkc));
+      double* d_ppart = nullptr;
+      if (psum && nchain > 0)
+        TRY(ws_typed(c, "fb_ppart", fb_psum_part_bytes(nchain, P, NB) / sizeof(double), &d_ppart));
       TRY(h2d(c, d_tk, tk.data(), (size_t)nt));
       TRY(h2d(c, d_pc, pcs.data(), pcs.size()));
       F64BucketArgs ba{};
@@ -2074,7 +2082,10 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.y = d_y64;
       ba.chist = chist;
       ba.cmax = (int32_t)G.cmax;
-      ba.fused = fused ? 1 : 0;
+      ba.psum = psum ? 1 : 0;
+      ba.P = P;
+      ba.poff = d_poff;
+      ba.ppart = d_ppart;
       // (a task's 8-byte arrays or the label column past 2^31 bytes; SBAG_F64_WIDE=1 forces it)
       ba.wide = (G.N >= ((int64_t)1 << 28) || getenv("SBAG_F64_WIDE")) ? 1 : 0;
       // XCD-aware dispatch of k_fb_count (workgroup w runs on XCD w mod 8, each with its own
@@ -2132,7 +2143,10 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     const bool chain_all = getenv("SBAG_F64_FALLBACK") && !strcmp(getenv("SBAG_F64_FALLBACK"), "chain");
     const int64_t walk_max =
         getenv("SBAG_F64_WALK_MAX") ? atoll(getenv("SBAG_F64_WALK_MAX")) : (int64_t)8192;
+    // (several partitions: the walk sums a node in one row order, so every flagged node takes
+    // the per-partition tasks)
     auto walked = [&](int i) {
+      if (P > 1) return false;
       return walk_all || (!chain_all && cur[i].b - cur[i].a <= walk_max);
     };
     std::vector<int> X, xi(M, -1);
@@ -3950,7 +3964,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
                  ha.hist = hist;
                  return launch(g, kHistVar, T_HIST, segs, par);
                },
-               add_work};
+               add_work, poff};
     std::vector<std::vector<BtNode>> ftrees;
     TRY(grow_f64s(G, ftrees));
     HIP_TRY(hipEventRecord(ev_stop, c->stream));

@@ -495,10 +495,14 @@ struct F64BucketArgs {
   double* ey_out;           // the labels of ent_out's entries
   double* chist;            // [task][NB][3] count, sum, sumSq in Spark's row order
   int32_t cmax;             // largest draw count of an entry (1: no count loop)
-  int32_t fused;            // k_fb_bchain sums the chain tasks (no global buckets)
-  int32_t wide, pad2;       // >= 2^28 rows: k_fb_scatter addresses by 64-bit pointers
+  int32_t psum;             // P > 1: k_fb_psum sums the chain tasks per partition (no buckets)
+  int32_t wide, P;          // >= 2^28 rows: k_fb_scatter addresses by 64-bit pointers; partitions
   const int32_t* porder;    // k_fb_count's piece of each workgroup (null: in order)
+  const int64_t* poff;      // [P + 1] the partitions' row offsets (psum)
+  double* ppart;            // [chain task][P][NB][3] per-partition partials (psum)
 };
+// bytes of k_fb_psum's per-partition partials for nchain tasks
+size_t fb_psum_part_bytes(int64_t nchain, int P, int NB);
 // ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]
 // A label column's analysis on the device (sbag_fit_booster's residuals): acc[6] =
 // {not finite, not integral, largest scale s making a label integral, order key of the

@@ -6,7 +6,9 @@
  * (sbag_host.cpp) serialises calls on a shared context, separate contexts run side by side,
  * and sbag_last_error() is per thread.
  *
- * usage: abi_threads data.bin seed depth bins impurity agg
+ * usage: abi_threads data.bin seed depth bins impurity agg [modes]
+ *   modes: comma-separated subset of shared,separate,errors-shared,errors-separate (default all),
+ *          or setup-only (threads create and destroy a context and a dataset, no fit)
  * data.bin: as tests/c/abi_driver.c (int64 N, F, num_offsets, offsets[], f64 X[N*F], y[N]).
  *
  * Four jobs (learner ranges [4j, 4j + 4) with subspace ratio 0.7 and Poisson bags) are first
@@ -104,6 +106,17 @@ static void run_job(int j, int64_t ctx, int64_t ds, double ratio, result_t* r) {
   sbagb_forest_free(forest);
 }
 
+static void* setup_only_main(void* arg) {
+  job_t* jb = (job_t*)arg;
+  int64_t ctx = 0, ds = 0;
+  pthread_barrier_wait(jb->bar);
+  jb->res.status = sbagb_ctx_create(0, &ctx);
+  if (!jb->res.status) jb->res.status = sbagb_dataset_create(ctx, N, (int32_t)F, X, Y, &ds);
+  if (ds) sbagb_dataset_free(ds);
+  if (ctx) sbagb_ctx_destroy(ctx);
+  return NULL;
+}
+
 static void* thread_main(void* arg) {
   job_t* jb = (job_t*)arg;
   int64_t ctx = jb->ctx, ds = jb->ds;
@@ -188,11 +201,25 @@ static int concurrent(const char* mode, int64_t ctx, int64_t ds, const double* r
   return ok;
 }
 
+/* is `m` one of the comma-separated names in `list`? */
+static int has_mode(const char* list, const char* m) {
+  const size_t n = strlen(m);
+  for (const char* p = list; p && *p;) {
+    const char* e = strchr(p, ',');
+    const size_t k = e ? (size_t)(e - p) : strlen(p);
+    if (k == n && !strncmp(p, m, n)) return 1;
+    p = e ? e + 1 : NULL;
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
-  if (argc != 7) {
-    fprintf(stderr, "usage: %s data.bin seed depth bins impurity agg\n", argv[0]);
+  if (argc != 7 && argc != 8) {
+    fprintf(stderr, "usage: %s data.bin seed depth bins impurity agg [modes]\n", argv[0]);
     return 2;
   }
+  setvbuf(stdout, NULL, _IOLBF, 0); /* (each verdict line out before any teardown) */
+  const char* modes = argc == 8 ? argv[7] : "shared,separate,errors-shared,errors-separate";
   size_t len = 0;
   char* buf = (char*)read_all(argv[1], &len);
   if (!buf || len < 24) return 2;
@@ -226,10 +253,27 @@ int main(int argc, char** argv) {
   const double good[NJOBS] = {0.8, 0.8, 0.8, 0.8};
   const double bad0[NJOBS] = {1.5, 0.8, 0.8, 0.8};
   int ok = 1;
-  ok &= concurrent("shared", ctx, ds, good, serial);
-  ok &= concurrent("separate", 0, 0, good, serial);
-  ok &= concurrent("errors-shared", ctx, ds, bad0, serial);
-  ok &= concurrent("errors-separate", 0, 0, bad0, serial);
+  if (has_mode(modes, "setup-only")) {
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, NJOBS);
+    job_t jobs[NJOBS];
+    pthread_t th[NJOBS];
+    memset(jobs, 0, sizeof(jobs));
+    for (int j = 0; j < NJOBS; j++) {
+      jobs[j].bar = &bar;
+      pthread_create(&th[j], NULL, setup_only_main, &jobs[j]);
+    }
+    for (int j = 0; j < NJOBS; j++) pthread_join(th[j], NULL);
+    pthread_barrier_destroy(&bar);
+    int st = 0;
+    for (int j = 0; j < NJOBS; j++) st |= jobs[j].res.status;
+    printf(st ? "setup-only failed\n" : "ok setup-only: %d threads created and destroyed contexts\n", NJOBS);
+    ok &= !st;
+  }
+  if (has_mode(modes, "shared")) ok &= concurrent("shared", ctx, ds, good, serial);
+  if (has_mode(modes, "separate")) ok &= concurrent("separate", 0, 0, good, serial);
+  if (has_mode(modes, "errors-shared")) ok &= concurrent("errors-shared", ctx, ds, bad0, serial);
+  if (has_mode(modes, "errors-separate")) ok &= concurrent("errors-separate", 0, 0, bad0, serial);
   for (int j = 0; j < NJOBS; j++) free_result(&serial[j]);
   sbagb_dataset_free(ds);
   sbagb_ctx_destroy(ctx);

@@ -83,7 +83,7 @@ THREADS_ASAN = os.path.join(ROOT, "tests", "c", "abi_threads_asan")
 
 
 def run_threads(tmp_path, X, y, offsets, *, seed, depth, bins, impurity, agg, driver=THREADS,
-                env=None):
+                env=None, modes=None):
     """tests/c/abi_threads: four jobs fitted + predicted from pthreads (one shared context,
     then four contexts, then with an induced SBAG_EINVAL), each compared byte for byte with
     the serial run inside the driver.  Returns the CompletedProcess."""
@@ -95,5 +95,7 @@ def run_threads(tmp_path, X, y, offsets, *, seed, depth, bins, impurity, agg, dr
         f.write(struct.pack("<qqq", X.shape[0], X.shape[1], len(off)))
         f.write(off.tobytes() + X.tobytes() + y.tobytes())
     args = [driver, str(data), str(int(seed)), str(depth), str(bins), str(impurity), str(agg)]
+    if modes:
+        args.append(modes)
     return subprocess.run(args, capture_output=True, text=True, timeout=600,
                           env=None if env is None else dict(os.environ, **env))

@@ -69,8 +69,14 @@ def fuzz_case(seed):
         y = rng.integers(-400, 400, size=N) / 16.0 + X[:, 0] * 0.25
         if f64:
             y = y * 1.1 + 0.3
-    P = 1 if f64 else int(rng.integers(1, 7))
-    cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
+    if f64:  # (round 6: fp64 labels over several partitions too -- Spark's per-partition sums;
+        # drawn from a stream of their own, so every other draw of a seed stays put)
+        prng = np.random.default_rng(seed + 4099)
+        P = int(prng.integers(1, 7))
+        cuts = np.sort(prng.integers(0, N + 1, size=P - 1))
+    else:
+        P = int(rng.integers(1, 7))
+        cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
     part = [0] + [int(c) for c in cuts] + [N]
     p = dict(L=int(rng.integers(1, 13)), replacement=bool(rng.integers(0, 2)),
              ratio=float(rng.choice([1.0, 0.9, 0.63, 0.5])), depth=int(rng.integers(0, 15)),
@@ -103,8 +109,14 @@ def fuzz_case_big(seed):
         y = rng.integers(-400, 400, size=N) / 16.0 + X[:, 0] * 0.25
         if f64:
             y = y * 1.1 + 0.3
-    P = 1 if f64 else int(rng.integers(1, 9))
-    cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
+    if f64:  # (round 6: fp64 labels over several partitions too -- Spark's per-partition sums;
+        # drawn from a stream of their own, so every other draw of a seed stays put)
+        prng = np.random.default_rng(seed + 4099)
+        P = int(prng.integers(1, 9))
+        cuts = np.sort(prng.integers(0, N + 1, size=P - 1))
+    else:
+        P = int(rng.integers(1, 9))
+        cuts = np.sort(rng.integers(0, N + 1, size=P - 1))
     part = [0] + [int(c) for c in cuts] + [N]
     p = dict(L=int(rng.choice([16, 24, 32])), replacement=bool(rng.integers(0, 2)),
              ratio=float(rng.choice([1.0, 0.8, 0.5])), depth=int(rng.integers(3, 12)),

@@ -10,7 +10,7 @@ import pytest
 
 import oracle
 from c_abi_util import run_driver, run_gbm_driver, run_threads
-from conftest import DATA
+from conftest import DATA, ROOT
 
 import spark_bagging_amd as sb
 from spark_bagging_amd import _native as nat
@@ -168,8 +168,14 @@ def test_c_threads_under_host_asan(tmp_path):
     env = {"ASAN_OPTIONS": "detect_leaks=0:verify_asan_link_order=0:halt_on_error=1",
            "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
     X, y = sb.load_libsvm(os.path.join(DATA, "cpusmall.svm"))
-    p = run_threads(tmp_path, X, y / 10.0, [0, 2000, 5000, 8192], seed=3, depth=5, bins=16,
-                    impurity=nat.IMPURITY_VARIANCE, agg=nat.AGG_MEAN, driver=THREADS_ASAN, env=env)
-    assert p.returncode == 0, p.stdout + p.stderr[-3000:]
-    assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr
-    assert p.stdout.count("ok ") == 4, p.stdout
+    logdir = os.path.join(ROOT, "gpurun_out", "asan_threads")
+    os.makedirs(logdir, exist_ok=True)
+    for modes in ("setup-only", "shared,errors-shared", "separate", "errors-separate"):
+        p = run_threads(tmp_path, X, y / 10.0, [0, 2000, 5000, 8192], seed=3, depth=5, bins=16,
+                        impurity=nat.IMPURITY_VARIANCE, agg=nat.AGG_MEAN, driver=THREADS_ASAN,
+                        env=env, modes=modes)
+        with open(os.path.join(logdir, modes.replace(",", "+") + ".log"), "w") as f:
+            f.write(f"rc {p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}")
+        assert p.returncode == 0, (modes, p.stdout, p.stderr[:4000], p.stderr[-1500:])
+        assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr
+        assert p.stdout.count("ok ") == modes.count(",") + 1, p.stdout

@@ -3,10 +3,12 @@
 The reference accepts any Double label (ml/regression/BaggingRegressor.scala:146-150 selects
 the label column as is; DecisionTreeRegressor sums count, y, y^2 per exploded row in row
 order, RandomForest's DTStatsAggregator.update).  Labels that are not dyadic fixed point
-take the engine's row-order fp64 path (sbag_f64.hip).  At P = 1 the oracle's sums are
-Spark's, so the trees must be bit-exact in every field; with P > 1 Spark merges the
-partitions' aggregates in shuffle order (not deterministic), and the engine keeps the
-one-partition order -- leaves within 1e-5 relative (north_star's regression tolerance).
+take the engine's row-order fp64 path (sbag_f64s.hip).  Spark sums each partition's rows in
+row order and merges the partitions' aggregates with reduceByKey (RandomForest.findBestSplits);
+the merge order is the shuffle's, and partition order is one order Spark produces.  The
+oracle and the engine both follow it (round 6: k_fb_psum / k_fb_pmerge; before, the engine
+and the oracle summed a node's rows in one row order, which no Spark run with P > 1 does), so
+the trees are bit-exact in every field at every P.
 """
 import os
 
@@ -81,16 +83,55 @@ def test_min_instances_and_gain_nondyadic(ctx, cpusmall):
     assert_forest_equal(forest, orf)
 
 
-def test_partitions_p3_leaves_within_tolerance(ctx):
-    """P = 3 partitions: structure and thresholds equal to the oracle's, leaves within
-    1e-5 relative (Spark's partition merge order is not deterministic)."""
+def test_partitions_p3_bit_exact(ctx):
+    """P = 3 partitions: every partition's rows summed in row order, the partials merged in
+    partition order (one execution of Spark's reduceByKey) -- bit-exact in every field."""
     rng = np.random.default_rng(7)
     N, F = 9000, 6
     X = np.round(rng.normal(size=(N, F)), 2)
     y = rng.normal(size=N) * 3.7 + 0.1
     part = [0, 2500, 6100, N]
     forest, orf = _fit_both(ctx, X, y, 5, depth=6, part=part)
-    assert_forest_equal(forest, orf, rel_tol_pred=1e-5)
+    assert_forest_equal(forest, orf)
+
+
+@pytest.mark.parametrize("part", [[0, 1000, 3000, 5000, 8192], [0, 0, 4000, 4000, 8192],
+                                  [round(i * 8192 / 64) for i in range(65)]],
+                         ids=["p4", "empty-partitions", "p64"])
+@pytest.mark.parametrize("depth", [4, 10])
+def test_cpusmall_nondyadic_partitions_bit_exact(ctx, cpusmall, part, depth):
+    """cpusmall with labels y*pi over several partitions -- uneven, empty ones (their
+    partials add +0.0), and 64 of them (most (node, partition) runs of a deep node are empty
+    or a few entries long): bit-exact against the oracle's per-partition sums, and the
+    predictions equal."""
+    X, y = cpusmall
+    forest, orf = _fit_both(ctx, X, y * np.pi, 6, depth=depth, part=part)
+    assert_forest_equal(forest, orf)
+    assert (nat.predict(ctx, forest, X, nat.AGG_MEAN) == oracle.predict(orf, X)).all()
+
+
+def test_partition_order_is_visible(ctx, cpusmall):
+    """The same bags fitted as 1 and as 4 partitions give different fp64 statistics (the
+    merge order shows in the sums), each bit-exact against its own oracle run."""
+    X, y = cpusmall
+    N = len(y)
+    y2 = y * np.pi * 1e3 + 0.1
+    part = [0, 1000, 3000, 5000, N]
+    ds = nat.DeviceDataset.from_numpy(X, y2, ctx)
+    try:
+        fits = [nat.fit(ctx, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                        learner_end=4, partition_offsets=p, max_depth=8, max_bins=32,
+                        impurity=nat.IMPURITY_VARIANCE) for p in (None, part)]
+    finally:
+        ds.free()
+    # Poisson bags depend on the partitions (seed + i + p): draw the P = 4 bags, fit both ways
+    counts = oracle.bag(True, 1.0, 0, 4, SEED_REG, part, N)
+    subs = [oracle.subspace(1.0, X.shape[1], SEED_REG + i) for i in range(4)]
+    assert_forest_equal(fits[1], oracle_forest(X, y2, counts, subs, 8, 32, False, part=part))
+    one = oracle_forest(X, y2, counts, subs, 8, 32, False)
+    four = oracle_forest(X, y2, counts, subs, 8, 32, False, part=part)
+    assert any(not np.array_equal(one.tree(t)[1], four.tree(t)[1]) or len(one.tree(t)[0]) != len(four.tree(t)[0])
+               for t in range(4))
 
 
 def test_sampled_split_finding_nondyadic(ctx):
@@ -168,7 +209,8 @@ def _fit(ctx, X, y, L, depth, part=None, **kw):
     return f
 
 
-@pytest.mark.parametrize("case", ["cpusmall_pi", "cpusmall_sqrt", "ties", "tiny_spread"])
+@pytest.mark.parametrize("case", ["cpusmall_pi", "cpusmall_sqrt", "ties", "tiny_spread",
+                                  "cpusmall_pi_p4", "ties_p4"])
 def test_screened_engine_equals_unscreened(ctx, cpusmall, monkeypatch, case):
     """The screened fp64 engine (sbag_f64s.hip: splits chosen from the integer histograms
     of the labels' fixed-point image under a rigorous bound, only the chosen feature summed
@@ -176,41 +218,48 @@ def test_screened_engine_equals_unscreened(ctx, cpusmall, monkeypatch, case):
     every node in row order) byte for byte, including datasets built to defeat the screen:
     duplicated columns (exact ties) and labels whose spread is a few ulps."""
     X, y = cpusmall
-    if case == "cpusmall_pi":
+    part = [0, 1000, 3000, 5000, len(y)] if case.endswith("_p4") else None
+    if case.startswith("cpusmall_pi"):
         y2 = y * np.pi
     elif case == "cpusmall_sqrt":
         y2 = np.sqrt(y + 0.5)
-    elif case == "ties":
+    elif case.startswith("ties"):
         X = np.concatenate([X, X[:, :4]], axis=1)  # every split of the first 4 columns ties
         y2 = y / 3.0
     else:
         y2 = 1.0 + (y - y.mean()) * 1e-13  # gains at the rounding level: the screen must defer
-    a = _fit(ctx, X, y2, 6, 9)
+    a = _fit(ctx, X, y2, 6, 9, part)
     ta = a.timing()
     monkeypatch.setenv("SBAG_F64_SCREEN", "0")
-    b = _fit(ctx, X, y2, 6, 9)
+    b = _fit(ctx, X, y2, 6, 9, part)
     tb = b.timing()
-    # the exact fallback both ways: every flagged node walked in row order by one wave per
-    # (node, feature group) (k_f64_hist), and every flagged node bucketed + chained per
-    # (node, feature) (the default splits them by node size, SBAG_F64_WALK_MAX)
+    # the exact fallback both ways (one partition): every flagged node walked in row order by
+    # one wave per (node, feature group) (k_f64_hist), and every flagged node's tasks per
+    # (node, feature) (the default splits them by node size, SBAG_F64_WALK_MAX); several
+    # partitions always take the per-partition tasks
     monkeypatch.setenv("SBAG_F64_FALLBACK", "hist")
-    c = _fit(ctx, X, y2, 6, 9)
+    c = _fit(ctx, X, y2, 6, 9, part)
     monkeypatch.setenv("SBAG_F64_FALLBACK", "chain")
-    d = _fit(ctx, X, y2, 6, 9)
+    d = _fit(ctx, X, y2, 6, 9, part)
     # and the scatter gathering y[row] instead of reading the labels carried with the entries
     monkeypatch.delenv("SBAG_F64_SCREEN")
     monkeypatch.delenv("SBAG_F64_FALLBACK")
     monkeypatch.setenv("SBAG_F64_NO_CARRY", "1")
-    e = _fit(ctx, X, y2, 6, 9)
+    e = _fit(ctx, X, y2, 6, 9, part)
     for t in range(6):
         (na, sa), (nb, sb_), (nc, sc), (nd, sd), (ne, se) = a.tree(t), b.tree(t), c.tree(t), d.tree(t), e.tree(t)
         assert na.tobytes() == nb.tobytes() == nc.tobytes() == nd.tobytes() == ne.tobytes(), f"tree {t}"
         assert sa.tobytes() == sb_.tobytes() == sc.tobytes() == sd.tobytes() == se.tobytes()
     assert tb["exact_fallbacks"] >= ta["exact_fallbacks"]
-    if case in ("cpusmall_pi", "cpusmall_sqrt"):
+    if case in ("cpusmall_pi", "cpusmall_sqrt", "cpusmall_pi_p4"):
         assert ta["exact_fallbacks"] < tb["exact_fallbacks"] / 2  # the screen decides most nodes
-    if case == "ties":
+    if case.startswith("ties"):
         assert ta["exact_fallbacks"] > 0
+    if part is not None:
+        N, F = X.shape
+        counts = oracle.bag(True, 1.0, 0, 6, SEED_REG, part, N)
+        subs = [oracle.subspace(1.0, F, SEED_REG + i) for i in range(6)]
+        assert_forest_equal(a, oracle_forest(X, y2, counts, subs, 9, 32, False, part=part))
 
 
 def test_c3_shape_nondyadic_screened(ctx):
@@ -249,12 +298,11 @@ def test_bucket_budget_chunks_equal_one_launch(ctx, cpusmall, monkeypatch):
 
 def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
     """The bench's real-valued-label fit at full size (10M x 100, 128 learners, depth 8,
-    P = 128), where the oracle cannot follow: the default engine (screen, staged bucket
-    scatter, column-ordered and XCD-dispatched tasks, exploded chains) gives the same trees
-    byte for byte as (a) the same screen with round 4's first bucketing and chain kernels,
-    (a') the bucketing fused into the chains in LDS (SBAG_F64_FUSED=1) and
-    (b) the unscreened engine, every node of every level summed by round 3's row-order walk
-    (k_f64_hist) -- two independent exact paths."""
+    P = 128), where the oracle cannot follow: the default engine (screen, staged routing
+    scatter, column-ordered and XCD-dispatched tasks, per-partition sums) gives the same trees
+    byte for byte as (a) the same screen with the unstaged scatter and tasks in node order and
+    (b) the unscreened engine, every feature of every node summed per partition and merged
+    (k_fb_psum / k_fb_pmerge over every (node, feature))."""
     N, F, L = 10_000_000, 100, 128
     ds = nat.DeviceDataset.synthetic(N, F, seed=20261015, ctx=ctx)
     try:
@@ -267,39 +315,31 @@ def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
                            max_bins=32, impurity=nat.IMPURITY_VARIANCE)
 
         a = fit()
-        for k in ("SBAG_F64_CHAIN_X", "SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER",
-                  "SBAG_F64_XCD_ORDER"):
+        for k in ("SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER", "SBAG_F64_XCD_ORDER"):
             monkeypatch.setenv(k, "0")
         b = fit()
-        for k in ("SBAG_F64_CHAIN_X", "SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER",
-                  "SBAG_F64_XCD_ORDER"):
+        for k in ("SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER", "SBAG_F64_XCD_ORDER"):
             monkeypatch.delenv(k)
-        monkeypatch.setenv("SBAG_F64_FUSED", "1")  # the fused bucket chains
-        d = fit()
-        monkeypatch.delenv("SBAG_F64_FUSED")
         monkeypatch.setenv("SBAG_F64_SCREEN", "0")
-        monkeypatch.setenv("SBAG_F64_FALLBACK", "hist")
         c = fit()
     finally:
         ds.free()
     ta, tc = a.timing(), c.timing()
     assert ta["exact_fallbacks"] < tc["exact_fallbacks"] / 20, (ta["exact_fallbacks"], tc["exact_fallbacks"])
     for t in range(L):
-        (na, sa), (nb, sb_), (nc, sc), (nd, sd) = a.tree(t), b.tree(t), c.tree(t), d.tree(t)
-        assert na.tobytes() == nb.tobytes() == nc.tobytes() == nd.tobytes(), f"tree {t}"
-        assert sa.tobytes() == sb_.tobytes() == sc.tobytes() == sd.tobytes(), f"tree {t} stats"
-    for f in (a, b, c, d):
+        (na, sa), (nb, sb_), (nc, sc) = a.tree(t), b.tree(t), c.tree(t)
+        assert na.tobytes() == nb.tobytes() == nc.tobytes(), f"tree {t}"
+        assert sa.tobytes() == sb_.tobytes() == sc.tobytes(), f"tree {t} stats"
+    for f in (a, b, c):
         f.free()
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_chain_windows_many_bins_large_counts(ctx, monkeypatch, fused):
-    """Spark's row-order sums with every row drawn 9 times (a 1024-entry block holds 9216
-    draw records: k_fb_bchain's several LDS windows), maxBins 255 on features with ~1000
-    distinct values (up to 255 chains per task), fp64 labels -- the booster engine, fused
-    bucket chains (SBAG_F64_FUSED=1, round 5) and the global buckets (the default), bit-exact
-    against the oracle."""
-    monkeypatch.setenv("SBAG_F64_FUSED", fused)
+@pytest.mark.parametrize("part", [None, [0, 7000, 7000, 20_000]], ids=["p1-chains", "p3-psum"])
+def test_chain_windows_many_bins_large_counts(ctx, part):
+    """Spark's row-order sums with every row drawn 9 times (k_fb_chainx's several draw
+    windows per stage at P = 1), maxBins 255 on features with ~1000 distinct values (up to 255
+    chains per task; at P > 1, k_fb_psum's LDS bins hold 8 lanes per wave), fp64 labels, one
+    booster -- bit-exact against the oracle."""
     rng = np.random.default_rng(29)
     n, f = 20_000, 6
     X = np.round(rng.normal(size=(n, f)) * 150) / 7
@@ -309,10 +349,11 @@ def test_chain_windows_many_bins_large_counts(ctx, monkeypatch, fused):
     sub = np.arange(f, dtype=np.int32)
     ds = nat.DeviceDataset.from_numpy(X, np.zeros(n), ctx)
     try:
-        fb = nat.fit_booster(ctx, ds, lab, counts, sub, max_depth=6, max_bins=255)
+        fb = nat.fit_booster(ctx, ds, lab, counts, sub, partition_offsets=part, max_depth=6,
+                             max_bins=255)
     finally:
         ds.free()
-    orf = oracle.fit(X, lab, counts[None, :], [sub], max_depth=6, max_bins=255)
+    orf = oracle.fit(X, lab, counts[None, :], [sub], max_depth=6, max_bins=255, part=part)
     assert_tree_equal(fb, 0, orf, 0)
 
 

@@ -373,3 +373,30 @@ def test_nondyadic_labels_c_vs_python():
         for a, b in zip(nodes, pt):
             for k in ("left", "right", "feature", "threshold", "prediction", "impurity", "gain"):
                 assert a[k] == b[k], (t, k)
+
+
+def test_nondyadic_labels_per_partition_sums_c_vs_python():
+    """Several partitions with real-valued labels: Spark aggregates each partition's rows
+    (mapPartitions, DTStatsAggregator.update in row order) and merges the partials with
+    reduceByKey(_ merge _) -- here in partition order, one order Spark produces.  The C oracle
+    and the pure-Python twin agree on every field, and the fp64 statistics differ from a
+    single-partition fit of the same bags (the merge order is visible in the sums)."""
+    X, y = synthetic.generate(900, 6, seed=12)
+    y = y * np.pi * 1e3 + 0.1
+    part = [0, 250, 611, 900]
+    counts = oracle.bag(True, 1.0, 0, 2, 21, part, 900)
+    subs = [oracle.subspace(1.0, 6, 21 + i) for i in range(2)]
+    f = oracle.fit(X, y, counts, subs, max_depth=6, max_bins=8, part=part)
+    f1 = oracle.fit(X, y, counts, subs, max_depth=6, max_bins=8)
+    differ = False
+    for t in range(2):
+        nodes, stats = f.tree(t)
+        pt = po.fit_tree(X.tolist(), y.tolist(), counts[t].tolist(), list(subs[t]), max_depth=6,
+                         max_bins=8, part_off=part)
+        assert len(pt) == len(nodes)
+        for a, b in zip(nodes, pt):
+            for k in ("left", "right", "feature", "threshold", "prediction", "impurity", "gain"):
+                assert a[k] == b[k], (t, k)
+        n1, s1 = f1.tree(t)
+        differ = differ or len(n1) != len(nodes) or not np.array_equal(stats, s1)
+    assert differ, "per-partition sums should round differently from one row-order sum"
