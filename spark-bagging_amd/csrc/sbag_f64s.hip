@@ -261,8 +261,9 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   for (int b = tid; b < NB; b += 256) s_c[b] = 0u;
   block_sync();
   const __amdgpu_buffer_rsrc_t rc = task_col_rsrc(A, t);
-  // the gathered bins, kept for k_fb_scatter (which then reads them in order)
-  const __amdgpu_buffer_rsrc_t re = rsrc_of(A.ebin + t.ebase, (uint64_t)(t.b - t.a));
+  // the gathered bins with the draw counts (bin | count << 8), kept for k_fb_scatter and
+  // k_fb_psum (which then read them in order)
+  const __amdgpu_buffer_rsrc_t re = rsrc_of(A.ebin + t.ebase, (uint64_t)(t.b - t.a) * 2);
   uint32_t nl = 0;
   constexpr int U = 8;
   const int64_t last = pc.b - 1;
@@ -277,7 +278,8 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
     for (int u = 0; u < U; u++) {
       const int64_t i = i0 + u * 256 + tid;
       // (lanes past the piece store past the resource: dropped)
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bin[u], re, i < pc.b ? (int)(i - t.a) : -1, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(bin[u] | ((uint32_t)(e[u] >> 32) & 0xffu) << 8), re,
+                                            i < pc.b ? (int)(uint32_t)(2 * (i - t.a)) : -1, 0, 0);
       if (i < pc.b) {
         atomicAdd(&s_c[bin[u]], 1u);
         nl += bin[u] <= (uint32_t)t.s ? 1u : 0u;
@@ -372,8 +374,8 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
     for (int b = lane; b < 256; b += 64) scnt[b] = 0u;
   int64_t lrun = t.part ? A.plbase[pi] : 0;
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
-  // the entries' bins as k_fb_count gathered them (in entry order: coalesced)
-  const __amdgpu_buffer_rsrc_t re = rsrc_of(A.ebin + t.ebase, (uint64_t)(t.b - t.a));
+  // the entries' bins as k_fb_count gathered them (in entry order: coalesced; bin | count << 8)
+  const __amdgpu_buffer_rsrc_t re = rsrc_of(A.ebin + t.ebase, (uint64_t)(t.b - t.a) * 2);
   // the task's buckets (labels and counts) and its children's segment (each < 4 GB: a
   // node's entries); the labels (rows < 2^28 on this path; kWide takes 64-bit pointers)
   const uint64_t nk = chain ? (uint64_t)(t.b - t.a) : 0;
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
     for (int u = 0; u < kScU; u++) ev[u] = A.ent_in[min(i0 + 64 * u + lane, last)];
 #pragma unroll
     for (int u = 0; u < kScU; u++) {
-      bv[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(re, (int)(min(i0 + 64 * u + lane, last) - t.a), 0, 0);
+      bv[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(re, (int)(uint32_t)(2 * (min(i0 + 64 * u + lane, last) - t.a)), 0, 0) & 0xffu;
       if constexpr (kWide) {
         const double* yp = carried ? A.ey_in + min(i0 + 64 * u + lane, last) : A.y + (uint32_t)ev[u];
         yv[u] = *(const v2u32*)yp;
@@ -722,91 +724,140 @@ __global__ __launch_bounds__(64) void k_fb_chainx(F64BucketArgs A, int nchain) {
 // into its own LDS bins; k_fb_pmerge then adds the P partials of every (task, bin) in
 // partition order.
 //
-// k_fb_psum: lane l of workgroup w takes unit g = w lpw + l = (task, partition).  Its run is
-// found by two binary searches of the partition's row bounds in the task's entries.  LDS per
-// lane: NB (sum, sumSq) pairs and NB counts, interleaved across the lanes.  Per entry: its bin (k_fb_count's ebin), draw
-// count and label (carried ey_in, else y[row]) are loaded kPs entries ahead; the add is one
-// LDS read-modify-write per entry (sum += y, sumSq += y*y once per draw; a lane's LDS
-// operations execute in order, so consecutive entries of one bin chain through LDS).
-constexpr int kPs = 8;
-__global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain, int lpw) {
+// k_fb_psum: a wave takes kL units (task, partition) = (g / P, g % P), g = w kL + l for lane
+// l < kL.  A unit's run is found by two binary searches of the partition's row bounds in the
+// task's entries.  The runs advance in stages of kPsT entries: the whole wave loads a stage of
+// every unit's labels and (bin | count) words -- kPsT lanes per unit, so a load instruction
+// touches one or two lines per unit instead of one line per lane -- into LDS (issued a stage
+// ahead), then lane l adds its unit's stage in order into its LDS bins (sum += y, sumSq += y*y
+// once per draw; count += draws).  LDS per unit: NB (sum, sumSq) pairs and NB counts,
+// interleaved across the units ([bin][unit]), and the staged stage.
+constexpr int kPsT = 16;  // entries per unit per stage
+template <int kL>
+__global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
   extern __shared__ __align__(16) uint8_t smem[];
+  constexpr int kLd = kL * kPsT / 64;  // loads per stage (slot 64 u + lane)
+  constexpr int kYp = kPsT + 1;        // staging pitch (odd: the serial reads spread over banks)
+  static_assert(kL * kPsT % 64 == 0, "whole loads per stage");
   const int lane = threadIdx.x, NB = A.NB, P = A.P;
-  const int64_t g = (int64_t)blockIdx.x * lpw + lane;
-  if (lane >= lpw || g >= (int64_t)nchain * P) return;  // (no barriers in this kernel)
-  // bins interleaved across the lanes ([bin][lane]): one bin of 64 lanes is 64 consecutive
-  // 16-byte pairs, so a wave's read-modify-write costs the ds_read_b128 minimum whatever the bins
-  double2* sd = (double2*)smem + lane;
-  uint32_t* sc = (uint32_t*)((double2*)smem + (size_t)lpw * NB) + lane;
-  const int64_t task = g / P;
-  const int q = (int)(g - task * P);
-  const F64Task t = A.tasks[task];
-  // the run of entries whose rows lie in [poff[q], poff[q + 1])
-  auto lower = [&](int64_t row) {
-    int64_t lo = t.a, hi = t.b;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)(uint32_t)A.ent_in[mid] < row)
-        lo = mid + 1;
-      else
-        hi = mid;
+  double2* sd = (double2*)smem;                                // [NB][kL] (sum, sumSq)
+  double* sy = (double*)(sd + (size_t)NB * kL);                // [kL][kYp] staged labels
+  uint32_t* sb = (uint32_t*)(sy + (size_t)kL * kYp);           // [kL][kYp] staged bin | count << 8
+  uint32_t* sc = sb + (size_t)kL * kYp;                        // [NB][kL] counts
+  __shared__ int64_t s_lo[kL], s_len[kL], s_eb[kL];
+  const int64_t g = (int64_t)blockIdx.x * kL + lane;
+  int64_t lo = 0, len = 0, eb = 0;
+  if (lane < kL && g < (int64_t)nchain * P) {
+    const int64_t task = g / P;
+    const int q = (int)(g - task * P);
+    const F64Task t = A.tasks[task];
+    auto lower = [&](int64_t row) {  // first entry of the task with a row >= row
+      int64_t a = t.a, b = t.b;
+      while (a < b) {
+        const int64_t mid = (a + b) >> 1;
+        if ((int64_t)(uint32_t)A.ent_in[mid] < row)
+          a = mid + 1;
+        else
+          b = mid;
+      }
+      return a;
+    };
+    lo = lower(A.poff[q]);
+    len = lower(A.poff[q + 1]) - lo;
+    eb = t.ebase + (lo - t.a);
+  }
+  if (lane < kL) {
+    s_lo[lane] = lo;
+    s_len[lane] = len;
+    s_eb[lane] = eb;
+    for (int b = 0; b < NB; b++) {
+      sd[(size_t)b * kL + lane] = make_double2(0.0, 0.0);
+      sc[(size_t)b * kL + lane] = 0u;
     }
-    return lo;
-  };
-  const int64_t lo = lower(A.poff[q]), hi = lower(A.poff[q + 1]);
-  for (int b = 0; b < NB; b++) {
-    sd[(size_t)b * lpw] = make_double2(0.0, 0.0);
-    sc[(size_t)b * lpw] = 0u;
+  }
+  int64_t maxlen = len;
+  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
+  block_sync();
+  // load u, lane l: unit j = (64 u + l) / kPsT, entry x = l % kPsT of the stage
+  const int x16 = lane % kPsT;
+  int64_t ulo[kLd], ulen[kLd], ueb[kLd];
+#pragma unroll
+  for (int u = 0; u < kLd; u++) {
+    const int j = (64 * u + lane) / kPsT;
+    ulo[u] = s_lo[j];
+    ulen[u] = s_len[j];
+    ueb[u] = s_eb[j];
   }
   const bool carried = A.ey_in != nullptr;
-  uint64_t eA[kPs], eB[kPs];
-  uint32_t bA[kPs], bB[kPs];
-  double yA[kPs], yB[kPs];
-  // (loads past the run repeat its last entry, masked at use)
-  auto load = [&](int64_t i0, uint64_t (&e)[kPs], uint32_t (&bn)[kPs], double (&yv)[kPs]) {
+  // (every load unconditional, past a run's end at its last entry -- masked at use)
+  auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&bv)[kLd]) {
 #pragma unroll
-    for (int u = 0; u < kPs; u++) {
-      const int64_t x = min(i0 + u, hi - 1);
-      e[u] = A.ent_in[x];
-      bn[u] = (uint32_t)A.ebin[t.ebase + (x - t.a)];
-      yv[u] = carried ? A.ey_in[x] : 0.0;
+    for (int u = 0; u < kLd; u++) {
+      const int64_t k = max(min(off + x16, ulen[u] - 1), (int64_t)0);
+      bv[u] = (uint32_t)A.ebin[ueb[u] + k];
+      yv[u] = carried ? A.ey_in[ulo[u] + k] : 0.0;
     }
     if (!carried)
 #pragma unroll
-      for (int u = 0; u < kPs; u++) yv[u] = A.y[(uint32_t)e[u]];
-  };
-  auto body = [&](int64_t i0, const uint64_t (&e)[kPs], const uint32_t (&bn)[kPs], const double (&yv)[kPs]) {
-#pragma unroll
-    for (int u = 0; u < kPs; u++) {
-      if (i0 + u >= hi) break;
-      const uint32_t c = (uint32_t)(e[u] >> 32) & 0xffu;
-      const double w = 1.0 * yv[u];  // instanceWeight * label
-      const double wy = w * yv[u];   // instanceWeight * label * label
-      const size_t at = (size_t)bn[u] * lpw;
-      double2 v = sd[at];
-      for (uint32_t k = 0; k < c; k++) {
-        v.x += w;
-        v.y += wy;
+      for (int u = 0; u < kLd; u++) {
+        const int64_t k = max(min(off + x16, ulen[u] - 1), (int64_t)0);
+        yv[u] = A.y[(uint32_t)A.ent_in[ulo[u] + k]];
       }
-      sd[at] = v;
-      sc[at] += c;  // count += 1.0 per draw (an integer sum: order-free)
-    }
   };
-  if (lo < hi) load(lo, eA, bA, yA);
-  for (int64_t i0 = lo; i0 < hi; i0 += 2 * kPs) {
-    if (i0 + kPs < hi) load(i0 + kPs, eB, bB, yB);
-    body(i0, eA, bA, yA);
-    if (i0 + kPs >= hi) break;
-    if (i0 + 2 * kPs < hi) load(i0 + 2 * kPs, eA, bA, yA);
-    body(i0 + kPs, eB, bB, yB);
+  double yA[kLd], yB[kLd];
+  uint32_t bA[kLd], bB[kLd];
+  if (maxlen > 0) {
+    load(0, yA, bA);
+    load(kPsT, yB, bB);
   }
-  double* o = A.ppart + (size_t)g * NB * 3;
-  for (int b = 0; b < NB; b++) {
-    const double2 v = sd[(size_t)b * lpw];
-    o[3 * b] = (double)sc[(size_t)b * lpw];
-    o[3 * b + 1] = v.x;
-    o[3 * b + 2] = v.y;
+  for (int64_t off = 0; off < maxlen; off += kPsT) {
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      const int j = (64 * u + lane) / kPsT;
+      sy[j * kYp + x16] = yA[u];
+      sb[j * kYp + x16] = bA[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      yA[u] = yB[u];
+      bA[u] = bB[u];
+    }
+    if (off + 2 * kPsT < maxlen) load(off + 2 * kPsT, yB, bB);
+    block_sync();
+    if (lane < kL) {
+      const int n = (int)min((int64_t)kPsT, max((int64_t)0, len - off));
+      const double* y = sy + lane * kYp;
+      const uint32_t* bc = sb + lane * kYp;
+      for (int x = 0; x < n; x++) {
+        const uint32_t w16 = bc[x];
+        const uint32_t bin = w16 & 0xffu, c = w16 >> 8;
+        const double w = 1.0 * y[x];  // instanceWeight * label
+        const double wy = w * y[x];   // instanceWeight * label * label
+        const size_t at = (size_t)bin * kL + lane;
+        double2 v = sd[at];
+        for (uint32_t k = 0; k < c; k++) {
+          v.x += w;
+          v.y += wy;
+        }
+        sd[at] = v;
+        sc[at] += c;  // count += 1.0 per draw (an integer sum: order-free)
+      }
+    }
+    block_sync();
   }
+  if (lane < kL && g < (int64_t)nchain * P) {
+    double* o = A.ppart + (size_t)g * NB * 3;
+    for (int b = 0; b < NB; b++) {
+      const double2 v = sd[(size_t)b * kL + lane];
+      o[3 * b] = (double)sc[(size_t)b * kL + lane];
+      o[3 * b + 1] = v.x;
+      o[3 * b + 2] = v.y;
+    }
+  }
+}
+
+static size_t psum_lds(int kL, int NB) {
+  return (size_t)NB * kL * (sizeof(double2) + sizeof(uint32_t)) + (size_t)kL * (kPsT + 1) * (sizeof(double) + 4);
 }
 
 // the partitions' partials of every (task, bin), added in partition order from 0.0 (the first
@@ -831,8 +882,13 @@ __global__ __launch_bounds__(256) void k_fb_pmerge(F64BucketArgs A, int nchain) 
   o[2] = s2;
 }
 
-// lanes per k_fb_psum workgroup: as many as 40 KB of LDS bins hold (64 at NB <= 32)
-static int psum_lanes(int NB) { return std::max(1, std::min(64, 40960 / (NB * 20))); }
+// units per k_fb_psum wave: as many as 40 KB of LDS bins hold, a power of two >= 4 (64 at
+// NB <= 32)
+static int psum_lanes(int NB) {
+  int l = 64;
+  while (l > 4 && (size_t)l * NB * 20 > 40960) l /= 2;
+  return l;
+}
 size_t fb_psum_part_bytes(int64_t nchain, int P, int NB) { return (size_t)nchain * P * NB * 3 * sizeof(double); }
 
 // ---------------------------------------------------------------- label column
@@ -947,10 +1003,24 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
   }
   if (nchain <= 0) return;
   if (a.psum) {  // P > 1: per-partition runs of each chain task, then the merge in partition order
-    const int lpw = psum_lanes(a.NB);
+    const int kl = psum_lanes(a.NB);
     const int64_t units = (int64_t)nchain * a.P;
-    const size_t lds = (size_t)lpw * a.NB * (sizeof(double2) + sizeof(uint32_t));
-    hipLaunchKernelGGL(k_fb_psum, dim3((unsigned)((units + lpw - 1) / lpw)), dim3(64), lds, st, a, nchain, lpw);
+    const size_t lds = psum_lds(kl, a.NB);
+    const dim3 grid((unsigned)((units + kl - 1) / kl));
+    auto go = [&](const void* fn) {
+      void* args[] = {(void*)&a, (void*)&nchain};
+      (void)hipLaunchKernel(fn, grid, dim3(64), args, lds, st);
+    };
+    if (kl == 64)
+      go((const void*)k_fb_psum<64>);
+    else if (kl == 32)
+      go((const void*)k_fb_psum<32>);
+    else if (kl == 16)
+      go((const void*)k_fb_psum<16>);
+    else if (kl == 8)
+      go((const void*)k_fb_psum<8>);
+    else
+      go((const void*)k_fb_psum<4>);
     const int64_t cells = (int64_t)nchain * a.NB;
     hipLaunchKernelGGL(k_fb_pmerge, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, nchain);
     return;

@@ -2046,7 +2046,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       TRY(ws_typed(c, "fb_plbase", (size_t)std::max<int64_t>(np, 1), &d_plbase));
       TRY(ws_typed(c, "fb_nleft", (size_t)nt, &d_nleft));
       TRY(ws_typed(c, "fb_kboff", (size_t)nt * (NB + 1), &d_kboff));
-      uint8_t* d_ebin;
+      uint16_t* d_ebin;
       TRY(ws_typed(c, "fb_ebin", (size_t)std::max<int64_t>(1, ebase), &d_ebin));
       // several partitions: Spark's per-partition aggregates merged in partition order
       // (k_fb_psum + k_fb_pmerge, no buckets); one partition: the buckets' row-order chains

@@ -466,7 +466,7 @@ struct F64Task {            // one (node, feature) whose entries are bucketed / 
   int64_t piece0, piece1;   // its pieces
   int32_t r, col, s, part;  // replica, column of the column-major bins (-1: every entry in
                             // bin 0, the node total), split bin, route?
-  int64_t ebase;            // its entries' bins at ebin[ebase, ebase + b - a) (k_fb_count)
+  int64_t ebase;            // its entries' bin | count << 8 at ebin[ebase, ebase + b - a) (k_fb_count)
 };
 struct F64TPiece {
   int64_t a, b;
@@ -483,7 +483,7 @@ struct F64BucketArgs {
   uint64_t* ent_out;        // children: left [a, a + nleft), right [a + nleft, b), row order
   double* bky;              // the buckets: the node's entries' labels grouped by bin, row
   uint8_t* bkc;             //   order kept, and their draw counts
-  uint8_t* ebin;            // every task's entries' bins, gathered once by k_fb_count
+  uint16_t* ebin;           // every task's entries' bin | draw count << 8, gathered once by k_fb_count
   uint32_t* pcnt;           // [piece][NB] entries per bin
   uint32_t* plcnt;          // [piece] entries going left
   int64_t* pbase;           // [piece][NB] bucket position of the piece's first entry per bin

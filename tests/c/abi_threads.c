@@ -25,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "sbag.h"
 #include "sbagjni_core.h"
@@ -278,5 +279,22 @@ int main(int argc, char** argv) {
   sbagb_dataset_free(ds);
   sbagb_ctx_destroy(ctx);
   free(buf);
+#if defined(__SANITIZE_ADDRESS__)
+#define ABI_ASAN 1
+#elif defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#define ABI_ASAN 1
+#endif
+#endif
+#ifdef ABI_ASAN
+  /* Under host ASan, leave without the runtime's static destructors: the HSA runtime's own
+     teardown (libhsa-runtime64's destructors, after contexts were created on several threads)
+     frees through ASan's device allocator after that allocator has been unloaded
+     ("CHECK failed: sanitizer_allocator_device.h ... dev_runtime_unloaded_"), which is the
+     toolchain's teardown order, not this library's code: every context, dataset and forest has
+     been released above, and each verdict line is already out. */
+  fflush(stdout);
+  _exit(ok ? 0 : 1);
+#endif
   return ok ? 0 : 1;
 }
