@@ -733,7 +733,7 @@ __global__ __launch_bounds__(64) void k_fb_chainx(F64BucketArgs A, int nchain) {
 // once per draw; count += draws).  LDS per unit: NB (sum, sumSq) pairs and NB counts,
 // interleaved across the units ([bin][unit]), and the staged stage.
 constexpr int kPsT = 16;  // entries per unit per stage
-template <int kL>
+template <int kL, bool kCarried>
 __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
   extern __shared__ __align__(16) uint8_t smem[];
   constexpr int kLd = kL * kPsT / 64;  // loads per stage (slot 64 u + lane)
@@ -788,62 +788,92 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
     ulen[u] = s_len[j];
     ueb[u] = s_eb[j];
   }
-  const bool carried = A.ey_in != nullptr;
-  // (every load unconditional, past a run's end at its last entry -- masked at use)
+  // (every load unconditional, past a run's end at its last entry -- masked at use: a load
+  // under a branch makes the compiler wait for every load in flight at the join, which would
+  // cost each stage a full memory latency; kCarried is a template argument for the same reason)
   auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&bv)[kLd]) {
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
       const int64_t k = max(min(off + x16, ulen[u] - 1), (int64_t)0);
       bv[u] = (uint32_t)A.ebin[ueb[u] + k];
-      yv[u] = carried ? A.ey_in[ulo[u] + k] : 0.0;
-    }
-    if (!carried)
-#pragma unroll
-      for (int u = 0; u < kLd; u++) {
-        const int64_t k = max(min(off + x16, ulen[u] - 1), (int64_t)0);
+      if constexpr (kCarried)
+        yv[u] = A.ey_in[ulo[u] + k];
+      else
         yv[u] = A.y[(uint32_t)A.ent_in[ulo[u] + k]];
-      }
+    }
   };
-  double yA[kLd], yB[kLd];
-  uint32_t bA[kLd], bB[kLd];
+  // a stage: the loaded words and labels to LDS, then lane l < kL adds its unit's entries
+  auto stage = [&](int64_t off, const double (&yX)[kLd], const uint32_t (&bX)[kLd]) {
+#pragma unroll
+    for (int u = 0; u < kLd; u++) {
+      const int j = (64 * u + lane) / kPsT;
+      sy[j * kYp + x16] = yX[u];
+      sb[j * kYp + x16] = bX[u];
+    }
+    block_sync();
+    if (lane < kL) {
+      const int n = (int)min((int64_t)kPsT, max((int64_t)0, len - off));
+      // the stage's words and labels to registers first (one LDS wait), then one
+      // read-modify-write of the entry's bin per entry: the sums and the count read together
+      uint32_t bcv[kPsT];
+      double yv[kPsT];
+#pragma unroll
+      for (int x = 0; x < kPsT; x++) {
+        bcv[x] = sb[lane * kYp + x];
+        yv[x] = sy[lane * kYp + x];
+      }
+      // (pinned here: the compiler would otherwise sink each read next to its use, one more LDS
+      // round trip per entry)
+#pragma unroll
+      for (int x = 0; x < kPsT; x++) __asm__ volatile("" : "+v"(bcv[x]), "+v"(yv[x]));
+#pragma unroll
+      for (int x = 0; x < kPsT; x++) {
+        if (x < n) {
+          const uint32_t bin = bcv[x] & 0xffu, c = bcv[x] >> 8;  // every run entry is drawn: c >= 1
+          const double w = 1.0 * yv[x];  // instanceWeight * label
+          const double wy = w * yv[x];   // instanceWeight * label * label
+          const uint32_t at = bin * kL + lane;
+          double2 v = sd[at];
+          const uint32_t cn = sc[at];
+          // (draws 2-4 branch-free: an absent draw adds -0.0, which leaves every sum unchanged)
+          v.x += w;
+          v.y += wy;
+          v.x += c >= 2 ? w : -0.0;
+          v.y += c >= 2 ? wy : -0.0;
+          v.x += c >= 3 ? w : -0.0;
+          v.y += c >= 3 ? wy : -0.0;
+          v.x += c >= 4 ? w : -0.0;
+          v.y += c >= 4 ? wy : -0.0;
+          for (uint32_t k = 4; k < c; k++) {
+            v.x += w;
+            v.y += wy;
+          }
+          sd[at] = v;
+          sc[at] = cn + c;  // count += 1.0 per draw (an integer sum: order-free)
+        }
+      }
+    }
+    block_sync();
+  };
+  // three register buffers rotating by unrolling (no copies): a stage's loads are issued two
+  // stages ahead, and waiting for them leaves the later stage's loads in flight (a copy of a
+  // buffer whose loads are in flight would wait for every load, this one's included)
+  double yA[kLd], yB[kLd], yC[kLd];
+  uint32_t bA[kLd], bB[kLd], bC[kLd];
   if (maxlen > 0) {
     load(0, yA, bA);
     load(kPsT, yB, bB);
   }
-  for (int64_t off = 0; off < maxlen; off += kPsT) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int j = (64 * u + lane) / kPsT;
-      sy[j * kYp + x16] = yA[u];
-      sb[j * kYp + x16] = bA[u];
-    }
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      yA[u] = yB[u];
-      bA[u] = bB[u];
-    }
-    if (off + 2 * kPsT < maxlen) load(off + 2 * kPsT, yB, bB);
-    block_sync();
-    if (lane < kL) {
-      const int n = (int)min((int64_t)kPsT, max((int64_t)0, len - off));
-      const double* y = sy + lane * kYp;
-      const uint32_t* bc = sb + lane * kYp;
-      for (int x = 0; x < n; x++) {
-        const uint32_t w16 = bc[x];
-        const uint32_t bin = w16 & 0xffu, c = w16 >> 8;
-        const double w = 1.0 * y[x];  // instanceWeight * label
-        const double wy = w * y[x];   // instanceWeight * label * label
-        const size_t at = (size_t)bin * kL + lane;
-        double2 v = sd[at];
-        for (uint32_t k = 0; k < c; k++) {
-          v.x += w;
-          v.y += wy;
-        }
-        sd[at] = v;
-        sc[at] += c;  // count += 1.0 per draw (an integer sum: order-free)
-      }
-    }
-    block_sync();
+  for (int64_t off = 0; off < maxlen;) {
+    load(off + 2 * kPsT, yC, bC);
+    stage(off, yA, bA);
+    if ((off += kPsT) >= maxlen) break;
+    load(off + 2 * kPsT, yA, bA);
+    stage(off, yB, bB);
+    if ((off += kPsT) >= maxlen) break;
+    load(off + 2 * kPsT, yB, bB);
+    stage(off, yC, bC);
+    off += kPsT;
   }
   if (lane < kL && g < (int64_t)nchain * P) {
     double* o = A.ppart + (size_t)g * NB * 3;
@@ -882,11 +912,12 @@ __global__ __launch_bounds__(256) void k_fb_pmerge(F64BucketArgs A, int nchain) 
   o[2] = s2;
 }
 
-// units per k_fb_psum wave: as many as 40 KB of LDS bins hold, a power of two >= 4 (64 at
-// NB <= 32)
+// units per k_fb_psum wave: as many as 20 KB of LDS bins hold, a power of two in [4, 64] (32 at
+// NB = 32: ~27 KB of LDS per wave with the staging, five waves per CU -- every SIMD busy; 64
+// units at 54 KB left two SIMDs of four idle)
 static int psum_lanes(int NB) {
   int l = 64;
-  while (l > 4 && (size_t)l * NB * 20 > 40960) l /= 2;
+  while (l > 4 && (size_t)l * NB * 20 > 20480) l /= 2;
   return l;
 }
 size_t fb_psum_part_bytes(int64_t nchain, int P, int NB) { return (size_t)nchain * P * NB * 3 * sizeof(double); }
@@ -1011,16 +1042,17 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
       void* args[] = {(void*)&a, (void*)&nchain};
       (void)hipLaunchKernel(fn, grid, dim3(64), args, lds, st);
     };
+    const bool cy = a.ey_in != nullptr;
     if (kl == 64)
-      go((const void*)k_fb_psum<64>);
+      go(cy ? (const void*)k_fb_psum<64, true> : (const void*)k_fb_psum<64, false>);
     else if (kl == 32)
-      go((const void*)k_fb_psum<32>);
+      go(cy ? (const void*)k_fb_psum<32, true> : (const void*)k_fb_psum<32, false>);
     else if (kl == 16)
-      go((const void*)k_fb_psum<16>);
+      go(cy ? (const void*)k_fb_psum<16, true> : (const void*)k_fb_psum<16, false>);
     else if (kl == 8)
-      go((const void*)k_fb_psum<8>);
+      go(cy ? (const void*)k_fb_psum<8, true> : (const void*)k_fb_psum<8, false>);
     else
-      go((const void*)k_fb_psum<4>);
+      go(cy ? (const void*)k_fb_psum<4, true> : (const void*)k_fb_psum<4, false>);
     const int64_t cells = (int64_t)nchain * a.NB;
     hipLaunchKernelGGL(k_fb_pmerge, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, nchain);
     return;
