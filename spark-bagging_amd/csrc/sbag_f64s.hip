@@ -256,6 +256,7 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   const F64TPiece pc = A.pieces[pix];
   const F64Task t = A.tasks[pc.task];
   const int NB = A.NB, tid = threadIdx.x;
+  const bool counting = !A.psum;  // (the per-bin counts place buckets; psum has none)
   __shared__ uint32_t s_c[256];
   __shared__ uint32_t s_l[4];
   for (int b = tid; b < NB; b += 256) s_c[b] = 0u;
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(bin[u] | ((uint32_t)(e[u] >> 32) & 0xffu) << 8), re,
                                             i < pc.b ? (int)(uint32_t)(2 * (i - t.a)) : -1, 0, 0);
       if (i < pc.b) {
-        atomicAdd(&s_c[bin[u]], 1u);
+        if (counting) atomicAdd(&s_c[bin[u]], 1u);
         nl += bin[u] <= (uint32_t)t.s ? 1u : 0u;
       }
     }
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(256) void k_fb_count(F64BucketArgs A) {
   for (int o = 32; o > 0; o >>= 1) nl += __shfl_down(nl, o);
   if ((tid & 63) == 0) s_l[tid >> 6] = nl;
   block_sync();
-  for (int b = tid; b < NB; b += 256) A.pcnt[pix * NB + b] = s_c[b];
+  if (counting)
+    for (int b = tid; b < NB; b += 256) A.pcnt[pix * NB + b] = s_c[b];
   if (tid == 0) A.plcnt[pix] = s_l[0] + s_l[1] + s_l[2] + s_l[3];
 }
 
@@ -422,7 +424,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
       // every store every round, whatever the task does (a task without buckets or
       // without children has zero-size resources: the stores are dropped) -- no branch
       uint64_t eq = __ballot(valid);
-      for (int k = 0; k < nbits; k++) {
+      for (int k = 0; k < (chain ? nbits : 0); k++) {  // (ranks by bin: only for the buckets)
         const bool bit = (bin >> k) & 1u;
         const uint64_t m = __ballot(bit);
         eq &= bit ? m : ~m;
@@ -728,11 +730,12 @@ __global__ __launch_bounds__(64) void k_fb_chainx(F64BucketArgs A, int nchain) {
 // l < kL.  A unit's run is found by two binary searches of the partition's row bounds in the
 // task's entries.  The runs advance in stages of kPsT entries: the whole wave loads a stage of
 // every unit's labels and (bin | count) words -- kPsT lanes per unit, so a load instruction
-// touches one or two lines per unit instead of one line per lane -- into LDS (issued a stage
+// touches a line or two per unit instead of a line per lane -- into LDS (issued two stages
 // ahead), then lane l adds its unit's stage in order into its LDS bins (sum += y, sumSq += y*y
-// once per draw; count += draws).  LDS per unit: NB (sum, sumSq) pairs and NB counts,
-// interleaved across the units ([bin][unit]), and the staged stage.
-constexpr int kPsT = 16;  // entries per unit per stage
+// once per draw).  LDS per unit: NB (sum, sumSq) pairs interleaved across the units
+// ([bin][unit]) and the staged stage.  The draw counts are not summed here: a (task, bin)'s
+// count is its cell of the level's integer histogram (k_fb_pmerge reads it there).
+constexpr int kPsT = 8;  // entries per unit per stage
 template <int kL, bool kCarried>
 __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
   extern __shared__ __align__(16) uint8_t smem[];
@@ -740,10 +743,9 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
   constexpr int kYp = kPsT + 1;        // staging pitch (odd: the serial reads spread over banks)
   static_assert(kL * kPsT % 64 == 0, "whole loads per stage");
   const int lane = threadIdx.x, NB = A.NB, P = A.P;
-  double2* sd = (double2*)smem;                                // [NB][kL] (sum, sumSq)
-  double* sy = (double*)(sd + (size_t)NB * kL);                // [kL][kYp] staged labels
-  uint32_t* sb = (uint32_t*)(sy + (size_t)kL * kYp);           // [kL][kYp] staged bin | count << 8
-  uint32_t* sc = sb + (size_t)kL * kYp;                        // [NB][kL] counts
+  double2* sd = (double2*)smem;                      // [NB][kL] (sum, sumSq)
+  double* sy = (double*)(sd + (size_t)NB * kL);      // [kL][kYp] staged labels
+  uint32_t* sb = (uint32_t*)(sy + (size_t)kL * kYp); // [kL][kYp] staged bin | count << 8
   __shared__ int64_t s_lo[kL], s_len[kL], s_eb[kL];
   const int64_t g = (int64_t)blockIdx.x * kL + lane;
   int64_t lo = 0, len = 0, eb = 0;
@@ -770,16 +772,13 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
     s_lo[lane] = lo;
     s_len[lane] = len;
     s_eb[lane] = eb;
-    for (int b = 0; b < NB; b++) {
-      sd[(size_t)b * kL + lane] = make_double2(0.0, 0.0);
-      sc[(size_t)b * kL + lane] = 0u;
-    }
+    for (int b = 0; b < NB; b++) sd[(size_t)b * kL + lane] = make_double2(0.0, 0.0);
   }
   int64_t maxlen = len;
   for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
   block_sync();
   // load u, lane l: unit j = (64 u + l) / kPsT, entry x = l % kPsT of the stage
-  const int x16 = lane % kPsT;
+  const int xs = lane % kPsT;
   int64_t ulo[kLd], ulen[kLd], ueb[kLd];
 #pragma unroll
   for (int u = 0; u < kLd; u++) {
@@ -794,7 +793,7 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
   auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&bv)[kLd]) {
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
-      const int64_t k = max(min(off + x16, ulen[u] - 1), (int64_t)0);
+      const int64_t k = max(min(off + xs, ulen[u] - 1), (int64_t)0);
       bv[u] = (uint32_t)A.ebin[ueb[u] + k];
       if constexpr (kCarried)
         yv[u] = A.ey_in[ulo[u] + k];
@@ -803,18 +802,19 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
     }
   };
   // a stage: the loaded words and labels to LDS, then lane l < kL adds its unit's entries
+  const uint32_t lbase = (uint32_t)lane;
   auto stage = [&](int64_t off, const double (&yX)[kLd], const uint32_t (&bX)[kLd]) {
 #pragma unroll
     for (int u = 0; u < kLd; u++) {
       const int j = (64 * u + lane) / kPsT;
-      sy[j * kYp + x16] = yX[u];
-      sb[j * kYp + x16] = bX[u];
+      sy[j * kYp + xs] = yX[u];
+      sb[j * kYp + xs] = bX[u];
     }
     block_sync();
     if (lane < kL) {
       const int n = (int)min((int64_t)kPsT, max((int64_t)0, len - off));
       // the stage's words and labels to registers first (one LDS wait), then one
-      // read-modify-write of the entry's bin per entry: the sums and the count read together
+      // read-modify-write of the entry's bin per entry
       uint32_t bcv[kPsT];
       double yv[kPsT];
 #pragma unroll
@@ -829,12 +829,11 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
 #pragma unroll
       for (int x = 0; x < kPsT; x++) {
         if (x < n) {
-          const uint32_t bin = bcv[x] & 0xffu, c = bcv[x] >> 8;  // every run entry is drawn: c >= 1
-          const double w = 1.0 * yv[x];  // instanceWeight * label
-          const double wy = w * yv[x];   // instanceWeight * label * label
-          const uint32_t at = bin * kL + lane;
-          double2 v = sd[at];
-          const uint32_t cn = sc[at];
+          const uint32_t c = bcv[x] >> 8;  // every run entry is drawn: c >= 1
+          const double w = 1.0 * yv[x];    // instanceWeight * label
+          const double wy = w * yv[x];     // instanceWeight * label * label
+          double2* p = sd + ((bcv[x] & 0xffu) * kL + lbase);
+          double2 v = *p;
           // (draws 2-4 branch-free: an absent draw adds -0.0, which leaves every sum unchanged)
           v.x += w;
           v.y += wy;
@@ -848,8 +847,7 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
             v.x += w;
             v.y += wy;
           }
-          sd[at] = v;
-          sc[at] = cn + c;  // count += 1.0 per draw (an integer sum: order-free)
+          *p = v;
         }
       }
     }
@@ -876,51 +874,56 @@ __global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
     off += kPsT;
   }
   if (lane < kL && g < (int64_t)nchain * P) {
-    double* o = A.ppart + (size_t)g * NB * 3;
-    for (int b = 0; b < NB; b++) {
-      const double2 v = sd[(size_t)b * kL + lane];
-      o[3 * b] = (double)sc[(size_t)b * kL + lane];
-      o[3 * b + 1] = v.x;
-      o[3 * b + 2] = v.y;
-    }
+    double2* o = (double2*)A.ppart + (size_t)g * NB;
+    for (int b = 0; b < NB; b++) o[b] = sd[(size_t)b * kL + lane];
   }
 }
 
 static size_t psum_lds(int kL, int NB) {
-  return (size_t)NB * kL * (sizeof(double2) + sizeof(uint32_t)) + (size_t)kL * (kPsT + 1) * (sizeof(double) + 4);
+  return (size_t)NB * kL * sizeof(double2) + (size_t)kL * (kPsT + 1) * (sizeof(double) + 4);
 }
 
 // the partitions' partials of every (task, bin), added in partition order from 0.0 (the first
-// partial is then itself: no sum is ever -0.0)
+// partial is then itself: no sum is ever -0.0); the count is the (task, bin) cell of the
+// level's integer histogram -- Spark's count += 1.0 per draw is the exact integer number of
+// draws, which the integer engine counted (the node total for a task without a feature)
 __global__ __launch_bounds__(256) void k_fb_pmerge(F64BucketArgs A, int nchain) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int NB = A.NB, P = A.P;
   if (i >= (int64_t)nchain * NB) return;
   const int64_t task = i / NB;
   const int b = (int)(i - task * NB);
-  const double* p = A.ppart + ((size_t)task * P * NB + b) * 3;
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  const double2* p = (const double2*)A.ppart + (size_t)task * P * NB + b;
+  double s1 = 0.0, s2 = 0.0;
   for (int q = 0; q < P; q++) {
-    s0 += p[0];
-    s1 += p[1];
-    s2 += p[2];
-    p += (size_t)NB * 3;
+    const double2 v = p[(size_t)q * NB];
+    s1 += v.x;
+    s2 += v.y;
   }
+  const F64Task t = A.tasks[task];
+  const uint64_t* h = A.hist + ((size_t)t.slot * A.Fmax + (t.fl >= 0 ? t.fl : 0)) * NB * 3;
+  uint64_t cnt = 0;
+  if (t.a == t.b)
+    cnt = 0;
+  else if (t.fl >= 0)
+    cnt = h[(size_t)b * 3];
+  else if (b == 0)  // the node total: every entry in bin 0
+    for (int k = 0; k < NB; k++) cnt += h[(size_t)k * 3];
   double* o = A.chist + (size_t)i * 3;
-  o[0] = s0;
+  o[0] = (double)cnt;
   o[1] = s1;
   o[2] = s2;
 }
 
-// units per k_fb_psum wave: as many as 20 KB of LDS bins hold, a power of two in [4, 64] (32 at
-// NB = 32: ~27 KB of LDS per wave with the staging, five waves per CU -- every SIMD busy; 64
-// units at 54 KB left two SIMDs of four idle)
+// units per k_fb_psum wave: as many as 32 KB of LDS bins hold, a power of two in [8, 64] (64 at
+// NB <= 32: ~39 KB of LDS per wave with the staging, four waves per CU -- every SIMD busy with
+// every lane adding)
 static int psum_lanes(int NB) {
   int l = 64;
-  while (l > 4 && (size_t)l * NB * 20 > 20480) l /= 2;
+  while (l > 8 && (size_t)l * NB * 16 > 32768) l /= 2;
   return l;
 }
-size_t fb_psum_part_bytes(int64_t nchain, int P, int NB) { return (size_t)nchain * P * NB * 3 * sizeof(double); }
+size_t fb_psum_part_bytes(int64_t nchain, int P, int NB) { return (size_t)nchain * P * NB * 2 * sizeof(double); }
 
 // ---------------------------------------------------------------- label column
 // analyze_labels (sbag_host.cpp) on the device: per label, finite / integral and the
@@ -1049,10 +1052,8 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
       go(cy ? (const void*)k_fb_psum<32, true> : (const void*)k_fb_psum<32, false>);
     else if (kl == 16)
       go(cy ? (const void*)k_fb_psum<16, true> : (const void*)k_fb_psum<16, false>);
-    else if (kl == 8)
-      go(cy ? (const void*)k_fb_psum<8, true> : (const void*)k_fb_psum<8, false>);
     else
-      go(cy ? (const void*)k_fb_psum<4, true> : (const void*)k_fb_psum<4, false>);
+      go(cy ? (const void*)k_fb_psum<8, true> : (const void*)k_fb_psum<8, false>);
     const int64_t cells = (int64_t)nchain * a.NB;
     hipLaunchKernelGGL(k_fb_pmerge, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, nchain);
     return;

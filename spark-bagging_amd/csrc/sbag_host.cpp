@@ -2086,6 +2086,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.P = P;
       ba.poff = d_poff;
       ba.ppart = d_ppart;
+      ba.hist = (const uint64_t*)hist_cur;
+      ba.Fmax = Fmax;
       // (a task's 8-byte arrays or the label column past 2^31 bytes; SBAG_F64_WIDE=1 forces it)
       ba.wide = (G.N >= ((int64_t)1 << 28) || getenv("SBAG_F64_WIDE")) ? 1 : 0;
       // XCD-aware dispatch of k_fb_count (workgroup w runs on XCD w mod 8, each with its own
@@ -2248,6 +2250,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
             t.r = q.r;
             t.s = -1;
             t.part = 0;
+            t.slot = X[k0 + k];
+            t.fl = fl < G.h_Fr[q.r] ? fl : -1;
             const bool real = (fl < G.h_Fr[q.r] && cmask[(size_t)X[k0 + k] * Fmax + fl]) ||
                               (fl == G.h_Fr[q.r] && f0[q.r] < 0);
             if (real) {
@@ -2309,8 +2313,11 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     std::vector<F64FinishNode> fin;
     std::vector<int> part_task(M, -1), fin_of(M, -1);
     int64_t kb[2] = {0, 0};
-    auto add_task = [&](int pass, const LNode& q, int fl, int s, bool part, bool chain) {
+    auto add_task = [&](int pass, int node, int fl, int s, bool part, bool chain) {
+      const LNode& q = cur[node];
       F64Task t{};
+      t.slot = node;
+      t.fl = fl;
       t.a = q.a;
       t.b = q.b;
       t.kbase = chain ? kb[pass] : -1;
@@ -2343,7 +2350,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       const int f = so[i].f, s = so[i].s;
       F64FinishNode fn{};
       // (children at maxDepth are leaves: nothing to route at the last split level)
-      fn.t = add_task(0, q, f, s, level + 1 < D, true);
+      fn.t = add_task(0, i, f, s, level + 1 < D, true);
       part_task[i] = fn.t;
       fn.f = f;
       fn.s = s;
@@ -2352,7 +2359,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       if (level == 0) {
         fn.ch.set = 0;
         fn.nsp0 = G.h_nbins[(size_t)q.r * Fmax + f0[q.r]] - 1;
-        fn.t0 = f0[q.r] == f ? fn.t : -2 - add_task(1, q, f0[q.r], -1, false, true);  // pass 1: fixed below
+        fn.t0 = f0[q.r] == f ? fn.t : -2 - add_task(1, i, f0[q.r], -1, false, true);  // pass 1: fixed below
       } else {
         const BtNode& n = trees[q.r][q.node];
         for (int j = 0; j < 3; j++) fn.ch.calc[j] = n.calc[j];
@@ -2370,7 +2377,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       const double li = bt_impurity(o.left), ri = bt_impurity(o.right);
       const bool child_leaf = (level + 1) == D;
       if ((child_leaf || li == 0.0) && (child_leaf || ri == 0.0)) continue;
-      part_task[i] = add_task(0, cur[i], o.f, o.s, true, false);
+      part_task[i] = add_task(0, i, o.f, o.s, true, false);
     }
     for (F64FinishNode& fn : fin)
       if (fn.t0 <= -2) fn.t0 = nchain0 + (-2 - fn.t0);  // pass-1 chain sums follow pass 0's

@@ -467,6 +467,8 @@ struct F64Task {            // one (node, feature) whose entries are bucketed / 
   int32_t r, col, s, part;  // replica, column of the column-major bins (-1: every entry in
                             // bin 0, the node total), split bin, route?
   int64_t ebase;            // its entries' bin | count << 8 at ebin[ebase, ebase + b - a) (k_fb_count)
+  int32_t slot, fl;         // its node's slot in the level's integer histograms and the local
+                            // feature (-1: the node total): k_fb_pmerge takes the draw counts there
 };
 struct F64TPiece {
   int64_t a, b;
@@ -499,7 +501,9 @@ struct F64BucketArgs {
   int32_t wide, P;          // >= 2^28 rows: k_fb_scatter addresses by 64-bit pointers; partitions
   const int32_t* porder;    // k_fb_count's piece of each workgroup (null: in order)
   const int64_t* poff;      // [P + 1] the partitions' row offsets (psum)
-  double* ppart;            // [chain task][P][NB][3] per-partition partials (psum)
+  double* ppart;            // [chain task][P][NB][2] per-partition partials (psum): sum, sumSq
+  const uint64_t* hist;     // (psum) the level's integer histograms [slot][Fmax][NB][3]: the
+  int32_t Fmax, pad3;       //   draw counts per (task, bin) (count += 1.0 per draw: exact)
 };
 // bytes of k_fb_psum's per-partition partials for nchain tasks
 size_t fb_psum_part_bytes(int64_t nchain, int P, int NB);
