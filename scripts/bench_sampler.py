@@ -1,5 +1,5 @@
 """Time the Poisson bag sampler alone (sbag_sample) on C3's shape: 10M rows, 128
-learners, P partitions of equal size.  For rocprofv3 / PMC passes over k_poisson3.
+learners, P partitions of equal size.  For rocprofv3 / PMC passes over k_poisson4.
 
 usage: python3 scripts/bench_sampler.py [--partitions P] [--reps K]
 """

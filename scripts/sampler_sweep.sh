@@ -1,6 +1,6 @@
 #!/bin/bash
 # Poisson sampler kernel time (rocprofv3 kernel trace) per variant and partition count,
-# C3 shape (10M rows, 128 learners).  A variant is V:LANES[:EXP] (SBAG_POISSON_V,
+# C3 shape (10M rows, 128 learners).  A variant is V:LANES[:EXP] (V ignored since round 6: k_poisson4 only;
 # SBAG_POISSON_LANES, SBAG_POISSON_EXP).  Box-to-box clocks differ by up to ~10 %: compare
 # variants within one call.  usage: scripts/sampler_sweep.sh <tag> "<variants...>" "<P...>"
 set -u

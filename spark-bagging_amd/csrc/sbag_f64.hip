@@ -19,9 +19,7 @@
 //   k_f64_split       RandomForest.binsToBestSplit in Spark's operation order, one wave
 //                     per node, lane = feature (mergeForFeature prefixes, right = total -
 //                     left, calculateImpurityStats, first max over splits then features)
-//   k_sp_count / k_sp_scan / k_sp_scatter   stable partition of every split node's
-//                     entries into its children (row order kept), reading the split
-//                     column from the column-major bins copy
+//   (the stable partition of a split node's entries is k_fb_scatter's, sbag_f64s.hip)
 //
 // Reference call sites: ml/ensemble/ensembleParams.scala:113-115 (fitBaseLearner ->
 // DecisionTreeRegressor.train), ml/regression/BaggingRegressor.scala:146-150,179-185.
@@ -567,80 +565,6 @@ __global__ __launch_bounds__(64) void k_f64_split(F64SplitArgs A) {
 
 void launch_f64_split(hipStream_t st, const F64SplitArgs& a, int nnodes) {
   hipLaunchKernelGGL(k_f64_split, dim3(nnodes), dim3(64), 0, st, a);
-}
-
-// ---------------------------------------------------------------- stable partition
-// pieces of kSpPiece entries of every split node; left iff bin <= s (shouldGoLeft)
-namespace {
-__device__ __forceinline__ bool sp_left(const F64PartArgs& A, const F64PartNode& p, uint64_t e) {
-  const uint32_t row = (uint32_t)e;
-  const uint8_t bin = A.cols[(int64_t)p.r * A.cols_rstride + (int64_t)p.col * A.npad + row];
-  return bin <= p.s;
-}
-}  // namespace
-
-__global__ __launch_bounds__(256) void k_sp_count(F64PartArgs A) {
-  const F64PartPiece pc = A.pieces[blockIdx.x];
-  const F64PartNode p = A.nodes[pc.node];
-  int n = 0;
-  for (int64_t i = pc.a + threadIdx.x; i < pc.b; i += 256) n += sp_left(A, p, A.ent_in[i]) ? 1 : 0;
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
-  __shared__ int s_n[4];
-  if ((threadIdx.x & 63) == 0) s_n[threadIdx.x >> 6] = n;
-  block_sync();
-  if (threadIdx.x == 0) A.piece_left[blockIdx.x] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
-}
-
-// per split node (one wave each): left entries before each of its pieces, and the node's
-// left total -- 64 pieces per step with a wave prefix scan
-__global__ __launch_bounds__(64) void k_sp_scan(F64PartArgs A, int nnodes) {
-  const int q = blockIdx.x;
-  const int lane = threadIdx.x;
-  const F64PartNode p = A.nodes[q];
-  int64_t acc = 0;
-  for (int64_t k0 = p.piece0; k0 < p.piece1; k0 += 64) {
-    const int64_t k = k0 + lane;
-    const int v = k < p.piece1 ? A.piece_left[k] : 0;
-    const int incl = f64_wave_incl_scan(v, lane);
-    if (k < p.piece1) A.piece_base[k] = acc + (int64_t)(incl - v);
-    acc += (int64_t)__shfl(incl, 63);
-  }
-  if (lane == 0) A.nleft[q] = acc;
-}
-
-__global__ __launch_bounds__(256) void k_sp_scatter(F64PartArgs A) {
-  __shared__ int s_wave[4];
-  const F64PartPiece pc = A.pieces[blockIdx.x];
-  const F64PartNode p = A.nodes[pc.node];
-  const int64_t nl = A.nleft[pc.node];
-  int64_t lpos = p.a + A.piece_base[blockIdx.x];
-  // right entries before this piece = entries before it - left entries before it
-  int64_t rpos = p.a + nl + (pc.a - p.a) - A.piece_base[blockIdx.x];
-  for (int64_t i0 = pc.a; i0 < pc.b; i0 += 256) {
-    const int64_t i = i0 + threadIdx.x;
-    const bool valid = i < pc.b;
-    uint64_t e = 0;
-    bool left = false;
-    if (valid) {
-      e = A.ent_in[i];
-      left = sp_left(A, p, e);
-    }
-    int ltot;
-    const int lex = block_excl_scan256(valid && left ? 1 : 0, s_wave, &ltot);
-    const int nvalid = (int)min((int64_t)256, pc.b - i0);
-    // right rank = entries before me in this round - left entries before me
-    const int rex = (int)threadIdx.x - lex;
-    if (valid) A.ent_out[left ? lpos + lex : rpos + rex] = e;
-    lpos += ltot;
-    rpos += nvalid - ltot;
-  }
-}
-
-void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int64_t npieces) {
-  if (npieces <= 0) return;
-  hipLaunchKernelGGL(k_sp_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_sp_scan, dim3(nnodes), dim3(64), 0, st, a, nnodes);
-  hipLaunchKernelGGL(k_sp_scatter, dim3((unsigned)npieces), dim3(256), 0, st, a);
 }
 
 // ---------------------------------------------------------------- imported codes

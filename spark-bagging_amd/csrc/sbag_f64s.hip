@@ -342,26 +342,26 @@ __global__ __launch_bounds__(256) void k_fb_scan(F64BucketArgs A) {
 // so the compiler's vmcnt waits stay counted.  (The wave's LDS operations execute in
 // order, and the compiler keeps a store to sb[x] before a later load of sb[y] it cannot
 // prove distinct: no fence, which would drain the vector memory counter too.)
-// kStage (the default): a step's 512 entries are first ordered by bin in LDS, so the
-// bucket stores leave as runs of consecutive positions (a 64-entry round spreads over up to
-// NB buckets: 2-entry runs of 8-byte labels and 1-byte counts, written back ~1.7x their
-// bytes as measured by WRITE_SIZE).
+// A step's 512 entries are first ordered by bin in LDS, so the bucket stores leave as runs of
+// consecutive positions (stored straight from the rounds, a 64-entry round spread over up to
+// NB buckets: 2-entry runs of 8-byte labels and 1-byte counts, written back ~1.7x their bytes
+// as measured by WRITE_SIZE; that variant was removed in round 6).
 constexpr int kScU = 8;  // rounds of 64 entries per step
 // kWide (datasets of >= 2^28 rows): the 8-byte labels, buckets and children are addressed by
 // 64-bit pointers with predicated stores -- a buffer resource spans at most 4 GB, and a task's
 // segment (up to a replica's every in-bag row) or the label column (8 N bytes) may not
-template <bool kStage, bool kWide>
+template <bool kWide>
 __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npieces, int nbits) {
   // (the wave index in an SGPR: the piece, its task and the buffer resources built from them
   // are then wave-uniform, with no per-lane waterfall loop around the buffer operations)
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t pi = (int64_t)blockIdx.x * 4 + wv;
   __shared__ int64_t s_base[4][256];
-  // staging (kStage): per wave the step's bin counts and offsets, and its entries by bin
-  __shared__ uint32_t s_scnt[kStage ? 4 : 1][256], s_soff[kStage ? 4 : 1][256];
-  __shared__ v2u32 s_sy[kStage ? 4 : 1][64 * kScU];
-  __shared__ uint32_t s_skp[kStage ? 4 : 1][64 * kScU];
-  __shared__ uint8_t s_sc[kStage ? 4 : 1][64 * kScU];
+  // staging: per wave the step's bin counts and offsets, and its entries by bin
+  __shared__ uint32_t s_scnt[4][256], s_soff[4][256];
+  __shared__ v2u32 s_sy[4][64 * kScU];
+  __shared__ uint32_t s_skp[4][64 * kScU];
+  __shared__ uint8_t s_sc[4][64 * kScU];
   if (pi >= npieces) return;  // whole waves only; no block-wide barrier below
   const F64TPiece pc = A.pieces[pi];
   const F64Task t = A.tasks[pc.task];
@@ -370,10 +370,9 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   const bool chain = __builtin_amdgcn_readfirstlane((int)(t.kbase >= 0 && !A.psum)) != 0;
   int64_t* sb = s_base[wv];
   for (int b = lane; b < NB; b += 64) sb[b] = chain ? A.pbase[pi * NB + b] : 0;
-  uint32_t* scnt = s_scnt[kStage ? wv : 0];
-  uint32_t* soff = s_soff[kStage ? wv : 0];
-  if (kStage)
-    for (int b = lane; b < 256; b += 64) scnt[b] = 0u;
+  uint32_t* scnt = s_scnt[wv];
+  uint32_t* soff = s_soff[wv];
+  for (int b = lane; b < 256; b += 64) scnt[b] = 0u;
   int64_t lrun = t.part ? A.plbase[pi] : 0;
   const int64_t nl = t.part ? A.nleft[pc.task] : 0;
   // the entries' bins as k_fb_count gathered them (in entry order: coalesced; bin | count << 8)
@@ -401,7 +400,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
     uint64_t ev[kScU];
     uint32_t bv[kScU];
     v2u32 yv[kScU];
-    uint32_t rs[kScU];  // (kStage) rank among the step's entries of the same bin
+    uint32_t rs[kScU];  // rank among the step's entries of the same bin
 #pragma unroll
     for (int u = 0; u < kScU; u++) ev[u] = A.ent_in[min(i0 + 64 * u + lane, last)];
 #pragma unroll
@@ -430,24 +429,10 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
         eq &= bit ? m : ~m;
       }
       const int rank = __popcll(eq & lt), cnt = __popcll(eq);
-      if constexpr (kStage) {
+      {
         const uint32_t so = scnt[bin];
         rs[u] = so + (uint32_t)rank;
         if (valid && rank == cnt - 1) scnt[bin] = so + (uint32_t)cnt;
-      } else {
-        const int64_t base = sb[bin];
-        // (positions relative to the task's buckets; invalid lanes store past the end: dropped)
-        const uint32_t kp = valid ? (uint32_t)(base - t.kbase + rank) : 0x1FFFFFFEu;
-        if constexpr (kWide) {
-          if (valid && chain) {
-            *(v2u32*)(A.bky + t.kbase + kp) = yv[u];
-            A.bkc[t.kbase + kp] = (uint8_t)(e >> 32);
-          }
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b64(yv[u], rk, (int)(kp * 8u), 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(e >> 32), rkc, (int)kp, 0, 0);
-        }
-        if (valid && rank == cnt - 1) sb[bin] = base + cnt;
       }
       const bool left = valid && bin <= (uint32_t)t.s;
       const uint64_t lm = __ballot(left);
@@ -464,7 +449,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
       }
       lrun += __popcll(lm);
     }
-    if constexpr (kStage) {
+    {
       if (chain) {
         // step offsets per bin (exclusive scan over the bins, 4 per lane), then every entry
         // to its slot: bins in order, row order inside a bin
@@ -1019,9 +1004,6 @@ void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, d
 void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain) {
   int nbits = 0;
   while ((1 << nbits) < a.NB) nbits++;
-  // SBAG_F64_SCATTER_STAGE=0: the bucket stores straight from the rounds (A/B)
-  const char* senv = getenv("SBAG_F64_SCATTER_STAGE");
-  const bool scatter_stage = !(senv && atoi(senv) == 0);
   if (npieces > 0)
     hipLaunchKernelGGL(k_fb_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
   if (a.ntasks > 0)  // (tasks without pieces still get their bucket bounds)
@@ -1029,11 +1011,9 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
   if (npieces > 0) {
     const dim3 g((unsigned)((npieces + 3) / 4));
     if (a.wide)
-      hipLaunchKernelGGL((scatter_stage ? k_fb_scatter<true, true> : k_fb_scatter<false, true>), g, dim3(256), 0,
-                         st, a, npieces, nbits);
+      hipLaunchKernelGGL(k_fb_scatter<true>, g, dim3(256), 0, st, a, npieces, nbits);
     else
-      hipLaunchKernelGGL((scatter_stage ? k_fb_scatter<true, false> : k_fb_scatter<false, false>), g, dim3(256), 0,
-                         st, a, npieces, nbits);
+      hipLaunchKernelGGL(k_fb_scatter<false>, g, dim3(256), 0, st, a, npieces, nbits);
   }
   if (nchain <= 0) return;
   if (a.psum) {  // P > 1: per-partition runs of each chain task, then the merge in partition order

@@ -1562,12 +1562,11 @@ static int fit_learners(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp
       // with integer labels only the in-bag rows (k_bin_ranked): 1 - e^-ratio of them for
       // Poisson bags, the ratio for Bernoulli ones (a short estimate falls back to halving)
       // (fit_range_impl's conditions: not the fp64 engine -- gini, or integer labels without
-      // SBAG_F64=1 --, no LUT binning, and k_bin_ranked's LDS geometry for a cut table of up to
-      // maxBins cuts; ADVICE r05: the estimate had missed the last two)
+      // SBAG_F64=1 --, and k_bin_ranked's LDS geometry for a cut table of up to maxBins cuts;
+      // the estimate had missed the last one)
       const bool force_f64 = getenv("SBAG_F64") && atoi(getenv("SBAG_F64")) != 0;
       const bool gini = fp->tree.impurity == SBAG_IMPURITY_GINI;
-      const bool lut_bins = getenv("SBAG_BIN_LUT") && atoi(getenv("SBAG_BIN_LUT")) != 0;
-      bool ranked = (gini || (ds->lab.label_ok && !force_f64)) && !lut_bins &&
+      bool ranked = (gini || (ds->lab.label_ok && !force_f64)) &&
                     (!getenv("SBAG_BIN_RANKED") || atoi(getenv("SBAG_BIN_RANKED")) != 0);
       const double ratio = fp->sampler.sample_ratio;
       const double frac = std::min(1.0, (fp->sampler.replacement ? 1.0 - std::exp(-ratio) : ratio) * 1.02 + 1e-3);
@@ -3330,7 +3329,6 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   std::vector<uint32_t> vcs;
   // the sampled replicas' thresholds and cuts from k_find_splits (dev_tc per (replica, feature));
   // SBAG_SPLITS_HOST=1: the host walk over the value counts copied back (A/B)
-  static const bool bin_lut = getenv("SBAG_BIN_LUT") && atoi(getenv("SBAG_BIN_LUT")) != 0;
   bool dev_splits = false;
   const int dev_tc = std::min(520, tp.max_bins + 64);
   std::vector<int32_t> dev_nt;
@@ -3409,7 +3407,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       HIP_TRY(hipGetLastError());
       tm.end(h);
       const bool splits_host = getenv("SBAG_SPLITS_HOST") && atoi(getenv("SBAG_SPLITS_HOST")) != 0;
-      if (!wide && !bin_lut && !splits_host && !getenv("SBAG_DEBUG_SAMPLE") && ds->d_dict) {
+      if (!wide && !splits_host && !getenv("SBAG_DEBUG_SAMPLE") && ds->d_dict) {
         std::vector<int64_t> knw(reps.size()), kns(reps.size());
         for (size_t k = 0; k < reps.size(); k++) {
           const int r = reps[k];
@@ -3493,11 +3491,10 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   }
 
   // ---- 4. thresholds, code cuts (bin(code) = #{j : cut_j <= code}), numSplits per (replica,
-  // feature).  SBAG_BIN_LUT=1: the round-4 per-code LUTs and their gather kernel (A/B only)
+  // feature)
   std::vector<std::vector<double>> thr((size_t)R * Fmax);
   std::vector<std::vector<uint32_t>> cuts((size_t)R * Fmax);
   std::vector<int32_t> h_nbins((size_t)R * Fmax, 1);
-  std::vector<uint8_t> lut(bin_lut ? (size_t)std::max<int64_t>(vc_total, 1) : 0, 0);
   std::vector<int32_t> exact(R, 1);
   bool identity = ds->code_bytes == 1;
   int NB = 1;
@@ -3591,9 +3588,6 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
                 break;
               }
           }
-          if (bin_lut)
-            for (size_t k = 0; k < d.size(); k++)
-              lut[o + k] = (uint8_t)(std::lower_bound(t.begin(), t.end(), d[k]) - t.begin());  // #{t < v}
         }
       }
     };
@@ -3684,13 +3678,11 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   int64_t cols_direct_npad = 0;    // (its row padding)
   {
     int h = tm.begin(T_BIN);
-    uint8_t* d_lut;
-    int64_t* d_lutoff;
     if (identity) {
       d_bins = (const uint8_t*)ds->d_codes;
       S = ds->S;
       h_pos = h_pos_codes;
-    } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30) && !bin_lut) {
+    } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30)) {
       // one bins matrix in global feature coordinates
       S = row_stride(F);
       std::vector<int32_t> gsub(F), gF(1, F);
@@ -3712,43 +3704,11 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       HIP_TRY(hipMemsetAsync(d_b + (size_t)N * S, 0, 256, c->stream));  // zero slack
       d_bins = d_b;
       h_pos = h_pos_codes;
-    } else if (shared && (int64_t)N * row_stride(F) <= ((int64_t)64 << 30)) {
-      // (SBAG_BIN_LUT=1) the same through per-code LUTs
-      S = row_stride(F);
-      std::vector<int32_t> gsub(F), gF(1, F);
-      for (int g = 0; g < F; g++) gsub[g] = g;
-      std::vector<int64_t> gl(F + 1, 0);
-      for (int g = 0; g < F; g++) gl[g + 1] = gl[g] + (int64_t)ds->dict[g].size();
-      std::vector<uint8_t> glut((size_t)std::max<int64_t>(gl[F], 1), 0);
-      for (int r = 0; r < R; r++)
-        for (int fl = 0; fl < h_Fr[r]; fl++) {
-          const int g = sub[r][fl];
-          std::copy(lut.begin() + vcoff[(size_t)r * Fmax + fl],
-                    lut.begin() + vcoff[(size_t)r * Fmax + fl] + (int64_t)ds->dict[g].size(),
-                    glut.begin() + gl[g]);
-        }
-      int32_t *d_gsub, *d_gF;
-      TRY(ws_typed(c, "gsub", (size_t)F, &d_gsub));
-      TRY(ws_typed(c, "gF", 1, &d_gF));
-      TRY(ws_typed(c, "lut", glut.size(), &d_lut));
-      TRY(ws_typed(c, "lutoff", (size_t)F + 1, &d_lutoff));
-      TRY(h2d(c, d_gsub, gsub.data(), (size_t)F));
-      TRY(h2d(c, d_gF, gF.data(), 1));
-      TRY(h2d(c, d_lut, glut.data(), glut.size()));
-      TRY(h2d(c, d_lutoff, gl.data(), (size_t)F + 1));
-      uint8_t* d_b;
-      TRY(ws_typed(c, "bins", (size_t)N * S, &d_b));
-      launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_gsub, d_gF, F, 1, d_lut,
-                         d_lutoff, d_b, S);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemsetAsync(d_b + (size_t)N * S, 0, 256, c->stream));  // zero slack
-      d_bins = d_b;
-      h_pos = h_pos_codes;
     } else {
       S = row_stride(Fmax);
       // integer labels: only the in-bag rows are binned, by rank (k_bin_ranked; the entries then
       // carry ranks).  SBAG_BIN_RANKED=0: every row (k_bin_cuts)
-      const bool ranked = !f64 && !bin_lut && (!getenv("SBAG_BIN_RANKED") || atoi(getenv("SBAG_BIN_RANKED")) != 0) &&
+      const bool ranked = !f64 && (!getenv("SBAG_BIN_RANKED") || atoi(getenv("SBAG_BIN_RANKED")) != 0) &&
                           bin_ranked_fits(ds->code_bytes, ds->S, S, Fmax, ncp);
       int64_t capb = 0;
       for (int r = 0; r < R; r++) capb = std::max<int64_t>(capb, (int64_t)inbag[r]);
@@ -3767,8 +3727,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       TRY(ws_typed(c, "bins", (size_t)R * rows_b * S + 256, &d_b));
       int ncol_r = 1;
       for (int r = 0; r < R; r++) ncol_r = std::max(ncol_r, (int)h_Fr[r]);
-      const int64_t npad_r = (N + 63) / 64 * 64;
-      if (!bin_lut) {
+      {
         // bin(code) = #{t < dict[code]} = #{j : cut_j <= code} by VALU compares (k_bin_cuts),
         // the partition's column copy written by the same pass
         uint32_t* d_cut;
@@ -3794,23 +3753,6 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
                                    (int64_t)ncol_r * npad_c)) {
           cols_direct = d_c;
           cols_direct_npad = npad_c;
-        }
-      } else if (wide) {
-        return fail(SBAG_EUNSUPPORTED, "SBAG_BIN_LUT: wide codes have no LUT form");
-      } else {
-        TRY(ws_typed(c, "lut", lut.size(), &d_lut));
-        TRY(ws_typed(c, "lutoff", vcoff.size(), &d_lutoff));
-        TRY(h2d(c, d_lut, lut.data(), lut.size()));
-        TRY(h2d(c, d_lutoff, vcoff.data(), vcoff.size()));
-        // the column copy for k_partition written by the same pass (no transpose re-reading
-        // the bins: 46 ms per 43-replica part of a C3-sized continuous fit)
-        uint8_t* d_c;
-        TRY(ws_typed(c, "cols", (size_t)R * ncol_r * npad_r, &d_c));
-        if (launch_materialize(c->stream, ds->d_codes, ds->code_bytes, N, ds->S, d_sub, d_Fr, Fmax, R,
-                               d_lut, d_lutoff, d_b, S, getenv("SBAG_MATERIALIZE_NO_COLS") ? nullptr : d_c,
-                               ncol_r, npad_r)) {
-          cols_direct = d_c;
-          cols_direct_npad = npad_r;
         }
       }
       HIP_TRY(hipGetLastError());
@@ -3883,45 +3825,14 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   TRY(h2d(c, d_pos, h_pos.data(), h_pos.size()));
   TRY(h2d(c, d_nbins, h_nbins.data(), h_nbins.size()));
 
-  // Packed rows for the histograms (identity bins under feature subspaces, C5): each entry's
-  // row gather then pulls a row of roundup(F_r) bytes instead of the whole code row, most of
-  // it other replicas' features (C5: 64 of 128 bytes).  Built per fit: R N S_p bytes.  The
-  // partition keeps the shared column copy in global feature coordinates (h_pos).  Opt-in
-  // (SBAG_PACK_ROWS=1): measured on the C5 shard it does not pay -- hist 71.8 -> 69.8 ms per
-  // fit (k_hist is bound by its per-entry instructions, not by the row bytes), k_pack_rows
-  // 46 ms for 51 GB (profiles/r04m/).
+  // (the histograms read the bins rows in place: per-replica packed subspace rows were measured
+  // on the C5 shard in round 4 -- hist 71.8 -> 69.8 ms per fit for 46 ms of packing, k_hist being
+  // bound by its per-entry instructions, not the row bytes -- and removed in round 6)
   const uint8_t* hbins = d_bins;
-  int64_t hb_rstride = bins_rstride;
-  int32_t hS = S;
-  int16_t* hpos = d_pos;
-  std::vector<int16_t> h_hpos = h_pos;
-  {
-    const int Sp = row_stride(Fmax);
-    bool sub_any = false;
-    for (int r = 0; r < R && !sub_any; r++)
-      for (int fl = 0; fl < h_Fr[r]; fl++)
-        if (h_pos[(size_t)r * Fmax + fl] != fl) sub_any = true;
-    const int pack_env = getenv("SBAG_PACK_ROWS") ? atoi(getenv("SBAG_PACK_ROWS")) : -1;
-    const bool can = identity && bins_rstride == 0 && sub_any && Sp < S && ds->code_bytes == 1 &&
-                     S % 4 == 0 && (double)R * N * Sp <= bins_budget(c);
-    const bool pack = can && pack_env == 1;
-    if (pack) {
-      int h = tm.begin(T_BIN);
-      uint8_t* d_pk;
-      TRY(ws_typed(c, "packed_rows", (size_t)R * N * Sp + 256, &d_pk));
-      launch_pack_rows(c->stream, (const uint8_t*)ds->d_codes, N, S, d_sub, d_Fr, Fmax, R, d_pk, Sp);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemsetAsync(d_pk + (size_t)R * N * Sp, 0, 256, c->stream));  // zero slack
-      for (int r = 0; r < R; r++)
-        for (int fl = 0; fl < Fmax; fl++) h_hpos[(size_t)r * Fmax + fl] = (int16_t)(fl < h_Fr[r] ? fl : 0);
-      TRY(ws_typed(c, "pos_hist", h_hpos.size(), &hpos));
-      TRY(h2d(c, hpos, h_hpos.data(), h_hpos.size()));
-      tm.end(h);
-      hbins = d_pk;
-      hb_rstride = (int64_t)N * Sp;
-      hS = Sp;
-    }
-  }
+  const int64_t hb_rstride = bins_rstride;
+  const int32_t hS = S;
+  const int16_t* hpos = d_pos;
+  const std::vector<int16_t>& h_hpos = h_pos;
 
   hmark(12);
   // ---- 6. level-wise growth
@@ -5155,101 +5066,11 @@ int sbag_aggregate_device(sbag_ctx* c, const void* d_in, int32_t in_bytes, int32
 // GBMRegressor's base-learner fit (ml/regression/GBMRegressor.scala:302-319): the subbag
 // of learner m (extractSubBag of withBag's column m, HasSubBag.scala:108-126) sliced to
 // the booster's subspace, labels = the pseudo-residuals -grad(y, F(x)) in fp64, through
-// DecisionTreeRegressor.fit (HasBaseLearner.fitBaseLearner, ensembleParams.scala:99-117).
-// The labels are arbitrary doubles, so the bagging engine's exact integer histograms do
-// not apply: Spark's fp64 sums depend on their order.  Every (node, feature, bin) cell is
-// summed on the device by one lane in row order (k_bt_hist over stably partitioned row
-// lists, k_bt_partition); split selection (binsToBestSplit / calculateImpurityStats) runs
-// on the host in Spark's operation order.  Thresholds are Spark's findSplits of the
-// subbag, with the split-finding sample (k_split_sample) above max(maxBins^2, 1e4) rows.
-namespace {
-// RandomForest.binsToBestSplit for one node over its fp64 histogram [Fr+1][NB][3]
-// (in place: mergeForFeature turns each feature's bins into prefixes).  `level > 0`:
-// the chain starts from the node's stats (set when its parent split); at the root from
-// the first candidate's left + right (calculateImpurityStats with stats == null).
-void bt_best_split(BtNode& node, int level, double* h, int Fr, int NB,
-                   const std::vector<int>& nsplits, const sbag_tree_params& tp, double left_out[3],
-                   double right_out[3], int* best_f_out, int* best_s_out) {
-  bool chain_set = level > 0;
-  double chain_calc[3] = {node.calc[0], node.calc[1], node.calc[2]};
-  double chain_imp = node.impurity;
-  int best_f = -1, best_s = -1;
-  bool best_valid = false;
-  double best_gain = 0.0;
-  for (int fl = 0; fl < Fr; fl++) {
-    const int nsp = nsplits[fl];
-    if (nsp == 0) continue;  // validFeatureSplits: features with splits only
-    double* fa = h + (size_t)fl * NB * 3;
-    for (int s = 0; s < nsp; s++)  // mergeForFeature(offset, s + 1, s)
-      for (int i = 0; i < 3; i++) fa[(s + 1) * 3 + i] += fa[s * 3 + i];
-    int fbest_s = -1;
-    bool fbest_valid = false;
-    double fbest_gain = 0.0;
-    for (int s = 0; s < nsp; s++) {
-      double left[3], right[3];
-      for (int i = 0; i < 3; i++) {
-        left[i] = fa[s * 3 + i];
-        right[i] = fa[nsp * 3 + i];
-      }
-      for (int i = 0; i < 3; i++) right[i] -= left[i];  // rightChildStats.subtract(left)
-      // calculateImpurityStats
-      if (!chain_set) {
-        for (int i = 0; i < 3; i++) chain_calc[i] = left[i] + right[i];
-        chain_imp = bt_impurity(chain_calc);
-        chain_set = true;
-      }
-      const int64_t lc = (int64_t)bt_count(left), rc = (int64_t)bt_count(right);
-      const int64_t total = lc + rc;
-      double gain;
-      bool valid;
-      if (lc < tp.min_instances_per_node || rc < tp.min_instances_per_node) {
-        gain = kDoubleMinValue;
-        valid = false;
-      } else {
-        const double li = bt_impurity(left), ri = bt_impurity(right);
-        const double lw = (double)lc / (double)total, rw = (double)rc / (double)total;
-        gain = chain_imp - lw * li - rw * ri;
-        valid = true;
-        if (gain < tp.min_info_gain) {
-          gain = kDoubleMinValue;
-          valid = false;
-        }
-      }
-      if (fbest_s < 0 || gain > fbest_gain) {  // maxBy: the first maximum
-        fbest_gain = gain;
-        fbest_s = s;
-        fbest_valid = valid;
-      }
-    }
-    if (best_f < 0 || fbest_gain > best_gain) {
-      best_gain = fbest_gain;
-      best_f = fl;
-      best_s = fbest_s;
-      best_valid = fbest_valid;
-    }
-  }
-  *best_f_out = best_f;
-  *best_s_out = best_s;
-  if (best_f < 0) {  // no feature has a split: invalid stats on the parent aggregate
-    const double* par = h + (size_t)Fr * NB * 3;
-    for (int i = 0; i < 3; i++) node.calc[i] = par[i];
-    node.gain = kDoubleMinValue;
-    node.impurity = bt_impurity(node.calc);
-    node.valid = false;
-    return;
-  }
-  for (int i = 0; i < 3; i++) node.calc[i] = chain_calc[i];
-  node.gain = best_gain;
-  node.impurity = chain_imp;
-  node.valid = best_valid;
-  const double* fa = h + (size_t)best_f * NB * 3;
-  const int nsp = nsplits[best_f];
-  for (int i = 0; i < 3; i++) {
-    left_out[i] = fa[best_s * 3 + i];
-    right_out[i] = fa[nsp * 3 + i] - fa[best_s * 3 + i];
-  }
-}
-}  // namespace
+// DecisionTreeRegressor.fit (HasBaseLearner.fitBaseLearner, ensembleParams.scala:99-117):
+// the bagging engine with one learner (fit_range) -- screened fp64 splits and Spark's
+// per-partition row-order sums (sbag_f64s.hip) for real-valued residuals, the integer
+// engine for dyadic ones.  (Round 3's engine, one lane per (node, feature) walking a node's
+// rows with host split selection, was removed in round 6.)
 
 extern "C" {
 
@@ -5331,260 +5152,46 @@ int sbag_fit_booster(sbag_ctx* c, const sbag_dataset* ds, const double* labels,
   std::vector<int64_t> poff;
   TRY(check_partitions(bp->num_partitions, bp->partition_offsets, N, poff));
   HIP_TRY(hipSetDevice(c->device));
-  static const bool bt_engine = getenv("SBAG_BOOSTER_ENGINE") && !strcmp(getenv("SBAG_BOOSTER_ENGINE"), "bt");
-  if (!bt_engine) {
-    // the bagging engine with one learner (fit_range): the iteration's bag column and
-    // subspace, its residuals as labels -- screened fp64 splits and row-order sums
-    // (sbag_f64s.hip) for real-valued residuals, the integer engine for dyadic ones
-    {
-      int64_t n_items = 0;
-      for (int64_t r = 0; r < N; r++) n_items += bp->counts[r];
-      if (n_items == 0)
-        return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
-                                 "empty one.");
-    }
-    bmark(1);  // items
-    TRY(ws_typed(c, "bt_labk", (size_t)N, &lab.d_labk));
-    if (lab.label_ok || lab.approx_ok)
-      launch_label_image(c->stream, lab.d_y64, N, lab.label_ok ? lab.shift : lab.ashift, lab.label_ok,
-                         lab.d_labk);
-    else
-      HIP_TRY(hipMemsetAsync(lab.d_labk, 0, (size_t)N * 4, c->stream));
-    HIP_TRY(hipGetLastError());
-    bmark(2);  // fixed-point image
-    FitExt ext{bp->counts, sub, &lab};
-    sbag_fit_params fp{};
-    fp.sampler.replacement = 1;
-    fp.sampler.sample_ratio = 1.0;
-    fp.sampler.seed = 0;
-    fp.sampler.learner_begin = 0;
-    fp.sampler.learner_end = 1;
-    fp.subspace_ratio = 1.0;
-    fp.subspace_bug_compat = 0;
-    fp.num_partitions = bp->num_partitions;
-    fp.partition_offsets = bp->partition_offsets;
-    fp.tree = tp;
-    sbag_forest* f = nullptr;
-    const int rc = fit_range(c, const_cast<sbag_dataset*>(ds), &fp, &f, &ext);
-    if (rc == kSplitRange) return fail(SBAG_EUNSUPPORTED, "the booster's bins exceed the device budget");
-    TRY(rc);
-    bmark(4);  // fit
-    if (bprof)
-      fprintf(stderr, "[sbag] booster host ms: upload+analysis %.2f items %.2f image %.2f fit %.2f\n",
-              bt[0], bt[1], bt[2], bt[4]);
-    *out = f;
-    return SBAG_OK;
+  // the bagging engine with one learner (fit_range): the iteration's bag column and
+  // subspace, its residuals as labels -- screened fp64 splits and row-order sums
+  // (sbag_f64s.hip) for real-valued residuals, the integer engine for dyadic ones
+  {
+    int64_t n_items = 0;
+    for (int64_t r = 0; r < N; r++) n_items += bp->counts[r];
+    if (n_items == 0)
+      return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
+                               "empty one.");
   }
-  // SBAG_BOOSTER_ENGINE=bt: the round-3 booster engine (one lane per (node, feature) walking
-  // the node's rows in order), kept for A/B
-  if (ds->code_bytes == 4)
-    return fail(SBAG_EUNSUPPORTED, "booster fit on features with more than 65536 distinct values");
-  const int D = tp.max_depth;
-  // in-bag rows in row order; numExamples of the subbag = sum of the counts
-  std::vector<uint32_t> rows;
-  int64_t n_items = 0;
-  for (int64_t r = 0; r < N; r++)
-    if (bp->counts[r]) {
-      rows.push_back((uint32_t)r);
-      n_items += bp->counts[r];
-    }
-  if (n_items == 0)
-    return fail(SBAG_EEMPTY, "DecisionTree requires size of input RDD > 0, but was given by "
-                             "empty one.");
-  const int64_t nrows = (int64_t)rows.size();
-  uint32_t *d_rowsA, *d_rowsB;
-  uint8_t* d_cnt;
-  double* d_y;
-  int32_t* d_sub;
-  TRY(ws_typed(c, "bt_rowsA", (size_t)nrows, &d_rowsA));
-  TRY(ws_typed(c, "bt_rowsB", (size_t)nrows, &d_rowsB));
-  TRY(ws_typed(c, "bt_cnt", (size_t)N, &d_cnt));
-  TRY(ws_typed(c, "bt_y", (size_t)N, &d_y));
-  TRY(ws_typed(c, "bt_sub", (size_t)Fr, &d_sub));
-  TRY(h2d(c, d_rowsA, rows.data(), rows.size()));
-  TRY(h2d(c, d_cnt, bp->counts, (size_t)N));
-  TRY(h2d(c, d_y, labels, (size_t)N));
-  TRY(h2d(c, d_sub, sub.data(), sub.size()));
-
-  // ---- findSplits: value counts of the subbag or of its split-finding sample
-  std::vector<int64_t> vcoff(Fr + 1, 0);
-  for (int fl = 0; fl < Fr; fl++) vcoff[fl + 1] = vcoff[fl] + (int64_t)ds->dict[sub[fl]].size();
-  const int64_t vc_total = vcoff[Fr];
-  int64_t* d_vcoff;
-  uint32_t* d_vc;
-  TRY(ws_typed(c, "bt_vcoff", vcoff.size(), &d_vcoff));
-  TRY(ws_typed(c, "bt_vc", (size_t)std::max<int64_t>(vc_total, 1), &d_vc));
-  TRY(h2d(c, d_vcoff, vcoff.data(), vcoff.size()));
-  HIP_TRY(hipMemsetAsync(d_vc, 0, (size_t)std::max<int64_t>(vc_total, 1) * 4, c->stream));
-  const int64_t mpb = std::min<int64_t>(tp.max_bins, n_items);
-  const int64_t required = std::max<int64_t>(mpb * mpb, 10000);
-  int64_t nsamp = n_items;
-  if (required < n_items) {
-    // RDD.sample(false, required / n, XORShiftRandom(seed).nextInt()) over the subbag
-    const double frac = (double)required / (double)n_items;
-    const int P = (int)poff.size() - 1;
-    uint64_t js = ((uint64_t)(int64_t)HostXS(tp.seed).next(32) ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1);
-    auto jnext = [&]() {
-      js = (js * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
-      return (int64_t)(int32_t)(uint32_t)(js >> 16);
-    };
-    std::vector<uint64_t> pst(P);
-    for (int q = 0; q < P; q++) {
-      const int64_t hi = jnext(), lo = jnext();
-      pst[q] = h_hash_seed((int64_t)((uint64_t)hi << 32) + lo);
-    }
-    const int32_t rep0 = 0, frs = Fr;
-    const double fl2[2] = {frac, std::log1p(-frac)};
-    int32_t *d_reps, *d_Fr;
-    double* d_frac;
-    uint64_t* d_pst;
-    int64_t* d_spoff;
-    TRY(ws_typed(c, "ss_reps", 1, &d_reps));
-    TRY(ws_typed(c, "bt_Fr", 1, &d_Fr));
-    TRY(ws_typed(c, "ss_frac", 2, &d_frac));
-    TRY(ws_typed(c, "ss_pst", pst.size(), &d_pst));
-    TRY(ws_typed(c, "ss_poff", poff.size(), &d_spoff));
-    TRY(h2d(c, d_reps, &rep0, 1));
-    TRY(h2d(c, d_Fr, &frs, 1));
-    TRY(h2d(c, d_frac, fl2, 2));
-    TRY(h2d(c, d_pst, pst.data(), pst.size()));
-    TRY(h2d(c, d_spoff, poff.data(), poff.size()));
-    const int64_t cap = required + 8 * (int64_t)std::ceil(std::sqrt((double)required)) + 1024;
-    uint32_t *d_srows, *d_snr;
-    uint16_t* d_gsums;
-    TRY(ws_typed(c, "ss_rows", (size_t)cap, &d_srows));
-    TRY(ws_typed(c, "ss_nrows", 1, &d_snr));
-    TRY(ws_typed(c, "ss_gsums", (size_t)split_sample_groups(N), &d_gsums));
-    HIP_TRY(hipMemsetAsync(d_snr, 0, 4, c->stream));
-    launch_split_sample(c->stream, d_cnt, N, 1, d_spoff, P, d_reps, 1, d_pst, d_frac, d_gsums,
-                        d_srows, cap, d_snr, frac <= 0.4);
-    HIP_TRY(hipGetLastError());
-    launch_split_sample_vc(c->stream, d_srows, cap, d_snr, d_reps, 1, ds->d_codes, ds->code_bytes,
-                           ds->S, d_sub, d_Fr, Fr, d_vcoff, d_vc,
-                           vc_total <= 16384 ? (int)vc_total : 0);
-    HIP_TRY(hipGetLastError());
-    uint32_t snr = 0;
-    TRY(d2h(c, &snr, d_snr, 1));
-    if ((int64_t)snr > cap) return fail(SBAG_EDEVICE, "split-finding sample exceeds its capacity");
-    nsamp = (int64_t)(int32_t)(frac * (double)n_items);  // (fraction * numExamples).toInt
-  } else {
-    launch_bt_valuecount(c->stream, d_rowsA, nrows, d_cnt, ds->d_codes, ds->code_bytes, ds->S,
-                         d_sub, Fr, d_vcoff, d_vc);
-    HIP_TRY(hipGetLastError());
-  }
-  std::vector<uint32_t> vc((size_t)std::max<int64_t>(vc_total, 1));
-  TRY(d2h(c, vc.data(), d_vc, vc.size()));
-  std::vector<std::vector<double>> thr(Fr);
-  std::vector<int> nsplits(Fr);
-  std::vector<uint8_t> lut((size_t)std::max<int64_t>(vc_total, 1), 0);
-  int NB = 1;
-  for (int fl = 0; fl < Fr; fl++) {
-    const int g = sub[fl];
-    nsplits[fl] = find_splits(ds->dict[g], vc.data() + vcoff[fl], ds->zero_code[g], n_items, nsamp,
-                              tp.max_bins, thr[fl]);
-    NB = std::max(NB, nsplits[fl] + 1);
-    if (NB > 256)  // u8 bin codes; Spark's count can pass maxBins after a large sample
-      return fail(SBAG_EUNSUPPORTED, "more than 256 bins in a feature (maxBins 256 and a "
-                                     "split-finding sample above numSamples)");
-    // TreePoint.findBin: #thresholds < value
-    for (size_t k = 0; k < ds->dict[g].size(); k++)
-      lut[vcoff[fl] + (int64_t)k] = (uint8_t)(std::lower_bound(thr[fl].begin(), thr[fl].end(),
-                                                               ds->dict[g][k]) -
-                                              thr[fl].begin());
-  }
-  uint8_t* d_lut;
-  TRY(ws_typed(c, "bt_lut", lut.size(), &d_lut));
-  TRY(h2d(c, d_lut, lut.data(), lut.size()));
-
-  // ---- level-wise growth (RandomForest.run, numTrees = 1, featureSubsetStrategy "all")
-  std::vector<BtNode> nodes(1);
-  struct Seg {
-    int node;
-    int64_t a, b;
-  };
-  std::vector<Seg> level_nodes{{0, 0, nrows}};
-  for (int level = 0; level <= D && !level_nodes.empty(); level++) {
-    const int A = (int)level_nodes.size();
-    std::vector<int64_t> seg(2 * (size_t)A);
-    for (int q = 0; q < A; q++) {
-      seg[2 * q] = level_nodes[q].a;
-      seg[2 * q + 1] = level_nodes[q].b;
-    }
-    int64_t* d_seg;
-    double* d_hist;
-    const size_t hw = (size_t)A * (Fr + 1) * NB * 3;
-    TRY(ws_typed(c, "bt_seg", seg.size(), &d_seg));
-    TRY(ws_typed(c, "bt_hist", hw, &d_hist));
-    TRY(h2d(c, d_seg, seg.data(), seg.size()));
-    launch_bt_hist(c->stream, d_rowsA, d_seg, A, d_cnt, d_y, ds->d_codes, ds->code_bytes, ds->S,
-                   d_sub, Fr, d_lut, d_vcoff, NB, d_hist);
-    HIP_TRY(hipGetLastError());
-    std::vector<double> hist(hw);
-    TRY(d2h(c, hist.data(), d_hist, hw));
-    std::vector<BtSplitHost> splits;
-    std::vector<int> split_q;
-    for (int q = 0; q < A; q++) {
-      const int id = level_nodes[q].node;
-      double left[3], right[3];
-      int bf, bs;
-      bt_best_split(nodes[id], level, hist.data() + (size_t)q * (Fr + 1) * NB * 3, Fr, NB,
-                    nsplits, tp, left, right, &bf, &bs);
-      BtNode& node = nodes[id];
-      node.is_leaf = (node.gain <= 0) || (level == D);
-      if (node.is_leaf) continue;
-      node.has_split = true;
-      node.fl = bf;
-      node.s = bs;
-      node.thr = thr[bf][bs];
-      const bool child_leaf = (level + 1) == D;
-      BtNode L, R;
-      for (int i = 0; i < 3; i++) {
-        L.calc[i] = left[i];
-        R.calc[i] = right[i];
-      }
-      // LearningNode(child, isLeaf, ImpurityStats.getEmptyImpurityStats(calculator))
-      L.impurity = bt_impurity(L.calc);
-      R.impurity = bt_impurity(R.calc);
-      L.is_leaf = child_leaf || L.impurity == 0.0;
-      R.is_leaf = child_leaf || R.impurity == 0.0;
-      node.left = (int)nodes.size();
-      node.right = node.left + 1;
-      nodes.push_back(L);
-      nodes.push_back(R);
-      splits.push_back(BtSplitHost{level_nodes[q].a, level_nodes[q].b, vcoff[bf], sub[bf], bs});
-      split_q.push_back(q);
-    }
-    std::vector<Seg> next;
-    if (!splits.empty()) {
-      void* d_splits;
-      int64_t* d_nl;
-      TRY(ws_get(c, "bt_splits", splits.size() * sizeof(BtSplitHost), &d_splits));
-      TRY(ws_typed(c, "bt_nl", splits.size(), &d_nl));
-      TRY(h2d(c, (unsigned char*)d_splits, (const unsigned char*)splits.data(),
-              splits.size() * sizeof(BtSplitHost)));
-      launch_bt_partition(c->stream, d_rowsA, d_rowsB, d_splits, (int)splits.size(), ds->d_codes,
-                          ds->code_bytes, ds->S, d_lut, d_nl);
-      HIP_TRY(hipGetLastError());
-      std::vector<int64_t> nl(splits.size());
-      TRY(d2h(c, nl.data(), d_nl, nl.size()));
-      for (size_t k = 0; k < splits.size(); k++) {
-        const BtNode& pn = nodes[level_nodes[split_q[k]].node];
-        const int64_t a = splits[k].a, b = splits[k].b, m = a + nl[k];
-        if (!nodes[pn.left].is_leaf) next.push_back({pn.left, a, m});
-        if (!nodes[pn.right].is_leaf) next.push_back({pn.right, m, b});
-      }
-      std::swap(d_rowsA, d_rowsB);
-    }
-    level_nodes.swap(next);
-  }
-  auto forest = std::make_unique<sbag_forest>();
-  forest->impurity = SBAG_IMPURITY_VARIANCE;
-  HTree t;
-  t.sub = sub;
-  t.ns = 3;
-  bt_emit(nodes, 0, t);
-  forest->trees.push_back(std::move(t));
-  *out = forest.release();
+  bmark(1);  // items
+  TRY(ws_typed(c, "bt_labk", (size_t)N, &lab.d_labk));
+  if (lab.label_ok || lab.approx_ok)
+    launch_label_image(c->stream, lab.d_y64, N, lab.label_ok ? lab.shift : lab.ashift, lab.label_ok,
+                       lab.d_labk);
+  else
+    HIP_TRY(hipMemsetAsync(lab.d_labk, 0, (size_t)N * 4, c->stream));
+  HIP_TRY(hipGetLastError());
+  bmark(2);  // fixed-point image
+  FitExt ext{bp->counts, sub, &lab};
+  sbag_fit_params fp{};
+  fp.sampler.replacement = 1;
+  fp.sampler.sample_ratio = 1.0;
+  fp.sampler.seed = 0;
+  fp.sampler.learner_begin = 0;
+  fp.sampler.learner_end = 1;
+  fp.subspace_ratio = 1.0;
+  fp.subspace_bug_compat = 0;
+  fp.num_partitions = bp->num_partitions;
+  fp.partition_offsets = bp->partition_offsets;
+  fp.tree = tp;
+  sbag_forest* f = nullptr;
+  const int rc = fit_range(c, const_cast<sbag_dataset*>(ds), &fp, &f, &ext);
+  if (rc == kSplitRange) return fail(SBAG_EUNSUPPORTED, "the booster's bins exceed the device budget");
+  TRY(rc);
+  bmark(4);  // fit
+  if (bprof)
+    fprintf(stderr, "[sbag] booster host ms: upload+analysis %.2f items %.2f image %.2f fit %.2f\n",
+            bt[0], bt[1], bt[2], bt[4]);
+  *out = f;
   return SBAG_OK;
 }
 

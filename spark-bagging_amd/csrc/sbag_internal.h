@@ -300,17 +300,6 @@ void launch_zero_slots(hipStream_t st, void* hist, const int32_t* d_slots, int n
                        int64_t u32_words_per_slot);
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
                      int ntriples, int64_t words_per_slot, bool u32words);
-// per-replica bins out[r][n][fl] = lut[lutoff[r][fl] + codes[n][sub[r][fl]]]; with cols, the
-// column-major copy cols[r][fl < ncol][npad] is written by the same pass when the kernel
-// can (returns true; else the caller transposes)
-bool launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
-                        const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
-                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out,
-                        uint8_t* cols = nullptr, int32_t ncol = 0, int64_t npad = 0);
-// identity bins packed per replica: out[r][n][fl] = codes[n][sub[r][fl]], S_out % 4 == 0,
-// S_codes % 4 == 0
-void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
-                      const int32_t* d_Fr, int32_t Fmax, int R, uint8_t* out, int32_t S_out);
 void launch_synth(hipStream_t st, uint8_t* codes, int32_t S, int64_t N, int32_t F, uint64_t seed,
                   int32_t num_classes, int32_t* labk);
 void launch_predict(hipStream_t st, const double* X, const void* codes, int code_bytes,
@@ -340,24 +329,6 @@ void launch_vc_global(hipStream_t st, const void* codes, int code_bytes, int32_t
                       int64_t cap, const unsigned long long* d_inbag, const int32_t* d_sub,
                       const int32_t* d_Fr, int32_t Fmax, int R, const int64_t* d_off, uint32_t* vc);
 size_t hist_lds_limit();
-
-// ---- booster engine (GBM base-learner fits on fp64 labels, sbag_fit_booster)
-struct BtSplitHost {  // layout of the kernels' BtSplit
-  int64_t a, b;       // the node's rows [a, b) in the level's row list
-  int64_t lutoff;     // the split feature's code -> bin table
-  int32_t g, s;       // code column of the split feature, split bin
-};
-void launch_bt_valuecount(hipStream_t st, const uint32_t* rows, int64_t nrows, const uint8_t* cnt,
-                          const void* codes, int code_bytes, int32_t S, const int32_t* sub,
-                          int32_t Fr, const int64_t* vcoff, uint32_t* vc);
-int bt_lanes(int NB);
-void launch_bt_hist(hipStream_t st, const uint32_t* rows, const int64_t* seg, int nnodes,
-                    const uint8_t* cnt, const double* y, const void* codes, int code_bytes,
-                    int32_t S, const int32_t* sub, int32_t Fr, const uint8_t* lut,
-                    const int64_t* lutoff, int NB, double* hist);
-void launch_bt_partition(hipStream_t st, const uint32_t* in, uint32_t* out, const void* splits,
-                         int nsplit, const void* codes, int code_bytes, int32_t S,
-                         const uint8_t* lut, int64_t* nleft);
 
 // ---- fp64 labels (sbag_f64.hip): bagging regression on labels that are not dyadic,
 // Spark's row-order fp64 histogram sums reproduced bit for bit
@@ -403,26 +374,6 @@ struct F64SplitArgs {
   const uint8_t* fmask;    // [node][Fmax] features to consider (null: all); the others hold
                            // no sums (the screen proved none of their candidates can win)
 };
-struct F64PartNode {  // a split node: entries [a, b), pieces [piece0, piece1)
-  int64_t a, b, piece0, piece1;
-  int32_t r, col, s, pad;  // replica, split column of the column-major bins, split bin
-};
-struct F64PartPiece {
-  int64_t a, b;
-  int32_t node, pad;
-};
-struct F64PartArgs {
-  const uint8_t* cols;     // [R?][C][npad]
-  int64_t cols_rstride, npad;
-  const F64PartNode* nodes;
-  const F64PartPiece* pieces;
-  const uint64_t* ent_in;
-  uint64_t* ent_out;
-  int32_t* piece_left;     // [pieces]
-  int64_t* piece_base;     // [pieces]
-  int64_t* nleft;          // [nodes]
-};
-constexpr int64_t kF64PartPiece = 4096;
 // the stable bootstrap compaction of the fp64 path: in-bag rows per (replica, chunk) and
 // per replica (Σ count, max count), then one entry row | (k << 8 | count) << 32 per in-bag
 // row, in row order (k: the labels' fixed-point image, labk)
@@ -552,7 +503,6 @@ int f64_hist_width(int NB);
 size_t f64_hist_lds_bytes(int NB, int parts);
 void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups);
 void launch_f64_split(hipStream_t st, const F64SplitArgs& a, int nnodes);
-void launch_f64_partition(hipStream_t st, const F64PartArgs& a, int nnodes, int64_t npieces);
 // sbag_dataset_import: *d_bad != 0 when a code is past its dictionary or padding is nonzero
 void launch_check_codes(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S,
                         int32_t F, const int64_t* d_dict_off, int* d_bad);

@@ -15,7 +15,7 @@
 //   k_split       prefix scan over bins + fp64 gain + first-max argmax
 //                 (RandomForest.binsToBestSplit / calculateImpurityStats)
 //   k_subtract    sibling histogram = parent - smaller child
-//   k_materialize per-replica bins from value codes (TreePoint.findBin)
+//   k_bin_cuts / k_bin_ranked   per-replica bins from value codes (TreePoint.findBin)
 //   k_predict     slicer + tree walk + in-order mean / breeze mode
 //                 (BaggingRegressor.scala:248-256, BaggingClassifier.scala:248-257)
 //   k_synth       bench data generator
@@ -53,724 +53,19 @@ static void set_max_lds(const void* fn, int bytes) {
 }
 
 // ======================================================================
-// Poisson sampler: Well19937c state in LDS, one lane per stream, all lanes
-// advance their generators in lockstep so the ring index is wave-uniform and
-// every LDS access is conflict-free ([position][lane] layout).
+// Poisson sampler (withBag with replacement, sql/bfunctions.scala:46-68 -> Poisson.scala:53-56):
+// k_poisson4 (sbag_poisson.hip), the step-parallel Well19937c of DESIGN §4.3.  (Rounds 1-3's
+// k_poisson / k_poisson2 / k_poisson3 were measured slower and removed in round 6.)
 // ======================================================================
-// Well19937c runs its ring index downwards one slot per step.  Within a batch of
-// WB <= 69 consecutive steps starting at index i, every value read (v[i-t+70],
-// v[i-t+179], v[i-t+449], the high bit of v[i-t-1], the low bits of v[i-t-2])
-// was written before the batch, so all 5*WB LDS reads are issued up front; the
-// batch then leaves v[i-t] = z3_t (t < WB), v[i-WB] = z4_{WB-1} and the masked
-// v[i-WB-1] -- the same state the sequential recurrence leaves.
-//
-// 624 = 39 * 16: after one prologue step (index 0) every batch of 16 covers the
-// aligned block [16m, 16m+15] (i = 16m+15).  Its five read windows then wrap
-// around the ring end only for m in {0, 10, 27, 34}; every other batch reads each
-// window from one wave-uniform base with immediate offsets (no per-read wrap).
-constexpr int kWB = 16;
-
-
-struct WellOut {
-  uint32_t o[kWB];  // next(26) of each step
-};
-
-// One batch of kWB steps at ring index i.  FAST: no read window wraps inside the
-// batch (bases wrapped once).  Returns the new ring index.
-template <bool FAST>
-__device__ __forceinline__ int well_batch(uint32_t* __restrict__ st, int lane, int i, uint32_t& v0,
-                                          WellOut& w) {
-  uint32_t m1[kWB], m2[kWB], m3[kWB], hb[kWB], lo[kWB], z3v[kWB];
-  if (FAST) {
-    // lowest address of each window, so every read is a non-negative immediate offset
-    const uint32_t* p1 = st + (wrap624(i + 70) - (kWB - 1)) * 64 + lane;
-    const uint32_t* p2 = st + (wrap624(i + 179) - (kWB - 1)) * 64 + lane;
-    const uint32_t* p3 = st + (wrap624(i - 175) - (kWB - 1)) * 64 + lane;
-    const uint32_t* ph = st + (i - 1 - kWB) * 64 + lane;  // m > 0 here: i - 1 - kWB >= 14
-#pragma unroll
-    for (int t = 0; t < kWB; t++) {
-      m1[t] = p1[(kWB - 1 - t) * 64];
-      m2[t] = p2[(kWB - 1 - t) * 64];
-      m3[t] = p3[(kWB - 1 - t) * 64];
-      hb[t] = ph[(kWB - t) * 64];
-      lo[t] = ph[(kWB - 1 - t) * 64];
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < kWB; t++) {
-      const int j = wrap624(i - t);
-      m1[t] = st[wrap624(j + 70) * 64 + lane];
-      m2[t] = st[wrap624(j + 179) * 64 + lane];
-      m3[t] = st[wrap624(j - 175) * 64 + lane];
-      hb[t] = st[wrap624(j - 1) * 64 + lane];
-      lo[t] = st[wrap624(j - 2) * 64 + lane];
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < kWB; t++) {
-    const uint32_t z0 = (0x80000000u & hb[t]) | (0x7FFFFFFFu & lo[t]);
-    const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1[t] ^ (m1[t] >> 27));
-    const uint32_t z2 = (m2[t] >> 9) ^ (m3[t] ^ (m3[t] >> 1));
-    const uint32_t z3 = z1 ^ z2;
-    // AbstractWell's z4 = z0 ^ (z1 ^ z1<<9) ^ (z2 ^ z2<<21) ^ (z3 ^ z3>>21); z1^z2^z3 == 0
-    uint32_t z4 = z0 ^ (z1 << 9) ^ (z2 << 21) ^ (z3 >> 21);
-    z3v[t] = z3;
-    v0 = z4;
-    z4 ^= (z4 << 7) & 0xe46e1700u;
-    z4 ^= (z4 << 15) & 0x9b868000u;
-    w.o[t] = z4 >> 6;  // next(26)
-  }
-  // the written block [i-15, i] never wraps (aligned batches)
-  uint32_t* pw = st + (i - kWB + 1) * 64 + lane;
-#pragma unroll
-  for (int t = 0; t < kWB; t++) pw[(kWB - 1 - t) * 64] = z3v[t];
-  st[wrap624(i - kWB) * 64 + lane] = v0;
-  st[wrap624(i - kWB - 1) * 64 + lane] = lo[kWB - 1] & 0x80000000u;
-  return wrap624(i - kWB);
-}
-
-__global__ __launch_bounds__(64) void k_poisson(uint8_t* __restrict__ counts, int64_t N,
-                                                const int64_t* __restrict__ part_off, int P, int R,
-                                                int learner0, int64_t seed, double mean,
-                                                double p_exp, int* err) {
-  __shared__ uint32_t st[624 * 64];
-  const int lane = threadIdx.x;
-  const int64_t sid = (int64_t)blockIdx.x * 64 + lane;
-  const bool active = sid < (int64_t)R * P;
-  const int r = active ? (int)(sid / P) : 0;
-  const int p = active ? (int)(sid % P) : 0;
-  // PoissonDistribution.reseedRandomGenerator(seed + i + partitionIndex) -> AbstractWell.setSeed
-  const uint64_t s64 = (uint64_t)seed + (uint64_t)(int64_t)(learner0 + r) + (uint64_t)(int64_t)p;
-  uint32_t vm2 = (uint32_t)(s64 >> 32), vm1 = (uint32_t)s64;
-  st[0 * 64 + lane] = vm2;
-  st[1 * 64 + lane] = vm1;
-  for (int i = 2; i < 624; i++) {
-    const int64_t l = (int64_t)(int32_t)vm2;
-    const uint32_t v = (uint32_t)(1812433253ull * (uint64_t)(l ^ (l >> 30)) + (uint64_t)i);
-    st[i * 64 + lane] = v;
-    vm2 = vm1;
-    vm1 = v;
-  }
-  int64_t row = active ? part_off[p] : 0;
-  const int64_t row_end = active ? part_off[p + 1] : 0;
-  uint8_t* out = counts + (int64_t)r * N;
-  // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean)
-  const int icap = (int)ceil(1000.0 * mean);
-  int n = 0, bad = 0;
-  uint8_t* const sink = (uint8_t*)(err + 1) + lane;  // stores of lanes that finish no row
-  double racc = 1.0;
-  uint32_t v0 = st[lane];
-  // prologue: the single step at index 0, leaving index 623 = 16*38+15
-  uint32_t pending;  // next(26) of the prologue step, first half of the first double
-  {
-    const uint32_t m1 = st[70 * 64 + lane], m2 = st[179 * 64 + lane], m3 = st[449 * 64 + lane];
-    const uint32_t hb = st[623 * 64 + lane], lo = st[622 * 64 + lane];
-    const uint32_t z0 = (0x80000000u & hb) ^ (0x7FFFFFFFu & lo);
-    const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1 ^ (m1 >> 27));
-    const uint32_t z2 = (m2 >> 9) ^ (m3 ^ (m3 >> 1));
-    const uint32_t z3 = z1 ^ z2;
-    uint32_t z4 = z0 ^ (z1 ^ (z1 << 9)) ^ (z2 ^ (z2 << 21)) ^ (z3 ^ (z3 >> 21));
-    st[lane] = z3;
-    st[623 * 64 + lane] = z4;
-    st[622 * 64 + lane] = lo & 0x80000000u;
-    v0 = z4;
-    z4 ^= (z4 << 7) & 0xe46e1700u;
-    z4 ^= (z4 << 15) & 0x9b868000u;
-    pending = z4 >> 6;
-  }
-  int index = 623;
-  WellOut w;
-  while (__any(row < row_end)) {
-    const int m = index >> 4;
-    if (m == 0 || m == 10 || m == 27 || m == 34)
-      index = well_batch<false>(st, lane, index, v0, w);
-    else
-      index = well_batch<true>(st, lane, index, v0, w);
-    // doubles: (pending, o0), (o1, o2), ..., (o13, o14); o15 carries over.
-    // BitsStreamGenerator.nextDouble = (next(26) << 26 | next(26)) * 2^-52, built as
-    // the bits of 1 + m * 2^-52 minus 1 (exact: m < 2^52).  Branch-free row update:
-    // a lane that finishes a row stores its count, the others store to a sink.
-#pragma unroll
-    for (int u = 0; u < kWB / 2; u++) {
-      const uint32_t hi = u == 0 ? pending : w.o[2 * u - 1];
-      const uint32_t lo32 = (hi << 26) | w.o[2 * u];
-      const uint32_t hi32 = 0x3FF00000u | (hi >> 6);
-      const double x = __hiloint2double((int)hi32, (int)lo32) - 1.0;
-      const bool live = row < row_end;
-      racc *= x;
-      const bool ge = racc >= p_exp;
-      n += ge ? 1 : 0;
-      const bool done = live && (!ge || n >= icap);
-      bad |= (done && n > 255) ? 1 : 0;
-      uint8_t* dst = done ? out + row : sink;
-      *dst = (uint8_t)min(n, 255);
-      row += done ? 1 : 0;
-      n = done ? 0 : n;
-      racc = done ? 1.0 : racc;
-    }
-    pending = w.o[kWB - 1];
-  }
-  if (bad) atomicOr(err, 1);
-}
-
-// ---- two-wave pipeline: wave 0 runs the Well19937c recurrence, wave 1 the
-// Poisson parse.  With 64 streams per CU (the state fills the LDS) one wave used
-// one SIMD and ran both chains back to back; split, the two chains overlap on two
-// SIMDs.  Wave 0 writes the untempered z4 of each batch of kPB steps into a
-// double-buffered LDS ring (the last 4 KB of the 160 KB); wave 1 tempers, builds
-// the doubles and draws.  One s_barrier per batch; the parser reports "all rows
-// done" in the ring slot it has just consumed, which the generator reads before
-// refilling it.
-constexpr int kPB = 8;  // 624 = 78 * 8: batches cover aligned blocks after the prologue step
-
-// The state is a ring of z3 words: AbstractWell's writes of z4 (at index - 1) and of
-// the `&= 0x80000000` (at index - 2) are overwritten by z3 one or two steps later and
-// read in between only as v0 (kept in a register) or through their top bit (z0's hb,
-// which the mask leaves alone), so a batch writes only its 8 z3 words.
-// LDS layout: quads of 4 consecutive ring positions per lane, [pos / 4][lane][pos % 4],
-// so a batch reads each of its windows (8 or 9 consecutive positions) with 2-3
-// conflict-free ds_read_b128 and writes its z3 words with 2 ds_write_b128.
-__device__ __forceinline__ int wq(int pos, int lane) { return ((pos >> 2) * 64 + lane) * 4 + (pos & 3); }
-
-// 12 words of positions [p0, p0 + 12), p0 a multiple of 4 inside the ring
-__device__ __forceinline__ void well_read12(const uint32_t* __restrict__ st, int lane, int p0,
-                                            uint32_t (&w)[12]) {
-  const uint4* q = (const uint4*)st + (p0 >> 2) * 64 + lane;
-#pragma unroll
-  for (int u = 0; u < 3; u++) {
-    const uint4 v = q[u * 64];
-    w[4 * u] = v.x;
-    w[4 * u + 1] = v.y;
-    w[4 * u + 2] = v.z;
-    w[4 * u + 3] = v.w;
-  }
-}
-
-// batch of kPB = 8 steps at ring index i (i = 8k + 7): steps j = i, i-1, ..., i-7.
-// FAST: no read window straddles the ring end.  Returns the new index i - 8.
-template <bool FAST>
-__device__ __forceinline__ int well_batch_raw(uint32_t* __restrict__ st, int lane, int i,
-                                              uint32_t& v0, uint32_t (&z4o)[kPB]) {
-  uint32_t m1[kPB], m2[kPB], m3[kPB], hb[kPB], lo[kPB], z3v[kPB];
-  if (FAST) {
-    // windows (start mod 4): m1 [i+63, i+70] (2), m2 [i+172, i+179] (3),
-    // m3 [i-182, i-175] (1), hb/lo [i-9, i-1] (2); word 7-t of a window is step t's
-    uint32_t w1[12], w2[12], w3[12], wh[12];
-    well_read12(st, lane, wrap624(i + 63) - 2, w1);
-    well_read12(st, lane, wrap624(i + 172) - 3, w2);
-    well_read12(st, lane, wrap624(i - 182) - 1, w3);
-    well_read12(st, lane, wrap624(i - 9) - 2, wh);
-#pragma unroll
-    for (int t = 0; t < kPB; t++) {
-      m1[t] = w1[2 + 7 - t];
-      m2[t] = w2[3 + 7 - t];
-      m3[t] = w3[1 + 7 - t];
-      hb[t] = wh[2 + 8 - t];
-      lo[t] = wh[2 + 7 - t];
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < kPB; t++) {
-      const int j = i - t;
-      m1[t] = st[wq(wrap624(j + 70), lane)];
-      m2[t] = st[wq(wrap624(j + 179), lane)];
-      m3[t] = st[wq(wrap624(j - 175), lane)];
-      hb[t] = st[wq(wrap624(j - 1), lane)];
-      lo[t] = st[wq(wrap624(j - 2), lane)];
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < kPB; t++) {
-    const uint32_t z0 = (0x80000000u & hb[t]) | (0x7FFFFFFFu & lo[t]);
-    const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1[t] ^ (m1[t] >> 27));
-    const uint32_t z2 = (m2[t] >> 9) ^ (m3[t] ^ (m3[t] >> 1));
-    const uint32_t z3 = z1 ^ z2;
-    const uint32_t z4 = z0 ^ (z1 << 9) ^ (z2 << 21) ^ (z3 >> 21);  // z1 ^ z2 ^ z3 == 0
-    z3v[t] = z3;
-    z4o[t] = z4;
-    v0 = z4;
-  }
-  // positions [i-7, i] (a multiple of 4 apart from the ring start): step t wrote i - t
-  uint4* q = (uint4*)st + ((i - 7) >> 2) * 64 + lane;
-  q[0] = make_uint4(z3v[7], z3v[6], z3v[5], z3v[4]);
-  q[64] = make_uint4(z3v[3], z3v[2], z3v[1], z3v[0]);
-  return wrap624(i - kPB);
-}
-
-__device__ __forceinline__ bool well_window_ok(int p, int len) {  // [p, p+len) inside the ring
-  const int w = wrap624(p);
-  return w + len <= 624;
-}
-
-__global__ __launch_bounds__(128) void k_poisson2(uint8_t* __restrict__ counts, int64_t N,
-                                                  const int64_t* __restrict__ part_off, int P,
-                                                  int R, int learner0, int64_t seed, double mean,
-                                                  double p_exp, int* err, int dbg) {
-  extern __shared__ __align__(16) uint32_t sm[];
-  uint32_t* st = sm;                    // [624][64] state
-  uint32_t* ring = sm + 624 * 64;       // [2][kPB][64] untempered z4
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t sid = (int64_t)blockIdx.x * 64 + lane;
-  const bool active = sid < (int64_t)R * P;
-  const int r = active ? (int)(sid / P) : 0;
-  const int p = active ? (int)(sid % P) : 0;
-  if (wave == 0) {
-    // PoissonDistribution.reseedRandomGenerator(seed + i + partitionIndex) -> AbstractWell.setSeed
-    const uint64_t s64 = (uint64_t)seed + (uint64_t)(int64_t)(learner0 + r) + (uint64_t)(int64_t)p;
-    uint32_t vm2 = (uint32_t)(s64 >> 32), vm1 = (uint32_t)s64;
-    st[wq(0, lane)] = vm2;
-    st[wq(1, lane)] = vm1;
-    for (int i = 2; i < 624; i++) {
-      const int64_t l = (int64_t)(int32_t)vm2;
-      const uint32_t v = (uint32_t)(1812433253ull * (uint64_t)(l ^ (l >> 30)) + (uint64_t)i);
-      st[wq(i, lane)] = v;
-      vm2 = vm1;
-      vm1 = v;
-    }
-    uint32_t v0 = st[wq(0, lane)];
-    // prologue: the single step at index 0 (leaves index 623 = 8*77 + 7); its output
-    // goes to ring slot 1, step kPB-1, where the parser picks up its pending half
-    {
-      const uint32_t m1 = st[wq(70, lane)], m2 = st[wq(179, lane)], m3 = st[wq(449, lane)];
-      const uint32_t hb = st[wq(623, lane)], lo = st[wq(622, lane)];
-      const uint32_t z0 = (0x80000000u & hb) | (0x7FFFFFFFu & lo);
-      const uint32_t z1 = (v0 ^ (v0 << 25)) ^ (m1 ^ (m1 >> 27));
-      const uint32_t z2 = (m2 >> 9) ^ (m3 ^ (m3 >> 1));
-      const uint32_t z3 = z1 ^ z2;
-      const uint32_t z4 = z0 ^ (z1 << 9) ^ (z2 << 21) ^ (z3 >> 21);
-      st[wq(0, lane)] = z3;
-      v0 = z4;
-      ring[kPB * 64 + lane * 4 + (kPB - 1 - 4) + 256] = z4;  // slot 1, half 1, word 3
-    }
-    block_sync();  // the parser takes the prologue output
-    int index = 623;
-    for (int k = 0;; k++) {
-      // the parser's verdict after batch k-2 (its last barrier matched batch k-1's)
-      if (k >= 2 && ring[((k & 1) * kPB) * 64] != 0u) break;
-      uint32_t z4o[kPB];
-      if (dbg & 2) {  // ablation: no generator work
-        uint32_t* slot = ring + (k & 1) * kPB * 64 + lane * 4;
-#pragma unroll
-        for (int t = 0; t < kPB; t++) slot[(t >> 2) * 256 + (t & 3)] = v0 + t * 77777u;
-        block_sync();
-        continue;
-      }
-      const bool fast = well_window_ok(index + 63 - 2, 12) && well_window_ok(index + 172 - 3, 12) &&
-                        well_window_ok(index - 182 - 1, 12) && well_window_ok(index - 9 - 2, 12);
-      if (fast)
-        index = well_batch_raw<true>(st, lane, index, v0, z4o);
-      else
-        index = well_batch_raw<false>(st, lane, index, v0, z4o);
-      // ring slot: [half][lane][4] words, steps 0-3 then 4-7
-      uint4* slot = (uint4*)(ring + (k & 1) * kPB * 64) + lane;
-      slot[0] = make_uint4(z4o[0], z4o[1], z4o[2], z4o[3]);
-      slot[64] = make_uint4(z4o[4], z4o[5], z4o[6], z4o[7]);
-      block_sync();
-    }
-  } else {
-    int64_t row = active ? part_off[p] : 0;
-    const int64_t row_end = active ? part_off[p + 1] : 0;
-    uint8_t* out = counts + (int64_t)r * N;
-    // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean)
-    const int icap = (int)ceil(1000.0 * mean);
-    uint8_t* const sink = (uint8_t*)(err + 1) + lane;  // stores of lanes that finish no row
-    int n = 0, bad = 0;
-    double racc = 1.0;
-    block_sync();  // the prologue output: first half of the first double
-    uint32_t pending = well_temper26(ring[kPB * 64 + lane * 4 + (kPB - 1 - 4) + 256]);
-    for (int k = 0;; k++) {
-      block_sync();  // batch k is in ring slot k & 1
-      uint32_t* slot = ring + (k & 1) * kPB * 64;
-      uint32_t o[kPB];
-      {
-        const uint4 a0 = ((const uint4*)slot)[lane], a1 = ((const uint4*)slot)[64 + lane];
-        o[0] = well_temper26(a0.x);
-        o[1] = well_temper26(a0.y);
-        o[2] = well_temper26(a0.z);
-        o[3] = well_temper26(a0.w);
-        o[4] = well_temper26(a1.x);
-        o[5] = well_temper26(a1.y);
-        o[6] = well_temper26(a1.z);
-        o[7] = well_temper26(a1.w);
-      }
-      // doubles: (pending, o0), (o1, o2), (o3, o4), (o5, o6); o7 carries over.
-      // BitsStreamGenerator.nextDouble = (next(26) << 26 | next(26)) * 2^-52, built as
-      // the bits of 1 + m * 2^-52 minus 1 (exact: m < 2^52).
-      if (dbg & 1) {  // ablation: no parse, one row per double
-        row = min(row + kPB / 2, row_end);
-        if (lane == 0) slot[0] = !__any(row < row_end) ? 1u : 0u;
-        if (!__any(row < row_end)) {
-          block_sync();
-          break;
-        }
-        continue;
-      }
-#pragma unroll
-      for (int u = 0; u < kPB / 2; u++) {
-        const uint32_t hi = u == 0 ? pending : o[2 * u - 1];
-        const uint32_t lo32 = (hi << 26) | o[2 * u];
-        const uint32_t hi32 = 0x3FF00000u | (hi >> 6);
-        const double x = __hiloint2double((int)hi32, (int)lo32) - 1.0;
-        const bool live = row < row_end;
-        racc *= x;
-        const bool ge = racc >= p_exp;
-        n += ge ? 1 : 0;
-        const bool done = live && (!ge || n >= icap);
-        bad |= (done && n > 255) ? 1 : 0;
-        uint8_t* dst = done ? out + row : sink;
-        *dst = (uint8_t)min(n, 255);
-        row += done ? 1 : 0;
-        n = done ? 0 : n;
-        racc = done ? 1.0 : racc;
-      }
-      pending = o[kPB - 1];
-      const bool all_done = !__any(row < row_end);
-      // report in the consumed slot: the generator reads it before refilling the slot
-      if (lane == 0) slot[0] = all_done ? 1u : 0u;
-      if (all_done) {
-        block_sync();  // matches the generator's next barrier
-        break;
-      }
-    }
-    if (bad) atomicOr(err, 1);
-  }
-}
-
-// ---- k_poisson3: step-parallel Well19937c.  Well19937c's only step-to-step
-// dependency is z4 (AbstractWell's v0 = z4 of the previous step); every other word a
-// step reads was written >= 70 steps earlier.  Expanding AbstractWell.next,
-//   z4[n] = L(z4[n-1]) ^ c[n],  L(x) = x<<9 ^ x>>21 ^ (x & 0x7f)<<4,
-//   c[n]  = S(a) ^ z0 ^ z2<<21 ^ z2>>21,  a = m1 ^ m1>>27,  S(x) = x<<9 ^ x>>21,
-//   z3[n] = z4[n-1] ^ z4[n-1]<<25 ^ a ^ z2,
-// with c[n] a function of older ring words only.  So a batch of B = 16*SPL <= 64 steps
-// of one stream runs on 16 lanes (SPL consecutive steps each): all reads first, the
-// c terms in parallel, then an F2-linear Hillis-Steele scan of z4 across the lanes with
-// the powers L^(SPL*2^k) (3-6 shift/mask terms each, built at compile time).  A wave
-// holds 4 streams, 16 streams per 256-thread block (4 blocks per CU by LDS): 16 waves
-// per CU share the generator work that the two-wave k_poisson2 ran on one SIMD.  The
-// Poisson parse (PoissonDistribution.nextPoisson) stays serial per stream: all 16
-// lanes of a stream run it on doubles broadcast with DPP row_newbcast, lane e keeping
-// the e-th count the batch emits, then the lanes store the batch's counts together.
-// tests/test_sampler_algebra.py replays this schedule on the CPU against the
-// sequential generator.
-
-constexpr int kSpLanes = 16;                             // lanes per stream
-constexpr int kSpStreams = 256 / kSpLanes;               // streams per 256-thread block
-// State pitch per stream: 625 = 1 mod 4 words, so the 4 streams of a wave, whose lanes
-// read 4 words apart (SPL = 4), fall on the 4 residue classes of the 64 banks
-// (a 624 pitch put all four on the same 16 banks: 75 % of LDS cycles were conflicts)
-constexpr int kSpPitch = 625;
-constexpr int kSpReadOff[5] = {70, 179, 449, 623, 622};  // m1, m2, m3, hb (j-1), lo (j-2)
-
-// The five ring words of steps n0 .. n0+SPL-1 of a batch starting at ring index i
-// (step n sits at index j = i - n).  FAST: no read window wraps round the ring in this
-// batch (a wave-uniform test), so each window is one base plus immediate offsets.
-// bit m: a batch of B steps starting at ring index 16m reads no window across the ring end
-constexpr uint64_t sp_fast_mask(int B) {
-  uint64_t m = 0;
-  for (int k = 0; k < 39; k++) {
-    bool fast = true;
-    for (int w = 0; w < 5; w++) {
-      const int x = 16 * k + kSpReadOff[w];
-      fast = fast && (x >= 624 ? x - 624 : x) >= B - 1;
-    }
-    if (fast) m |= 1ull << k;
-  }
-  return m;
-}
-
-template <int SPL, bool FAST>
-__device__ __forceinline__ void sp_read(const uint32_t* __restrict__ st, int i, int n0,
-                                        uint32_t (&w)[5][SPL]) {
-#pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const int b = wrap624(i + kSpReadOff[k]);
-    if (FAST) {
-      const uint32_t* p = st + (b - n0 - (SPL - 1));
-#pragma unroll
-      for (int q = 0; q < SPL; q++) w[k][q] = p[SPL - 1 - q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < SPL; q++) {
-        int pos = b - n0 - q;
-        pos += pos < 0 ? 624 : 0;
-        w[k][q] = st[pos];
-      }
-    }
-  }
-}
-
-template <int SPL, bool CAP, bool PAR>
-__global__ __launch_bounds__(256) void k_poisson3(uint8_t* __restrict__ counts, int64_t N,
-                                                  const int64_t* __restrict__ part_off, int P,
-                                                  int R, int learner0, int64_t seed,
-                                                  double p_exp, int icap, int* err) {
-  static_assert(SPL == 2 || SPL == 4, "a lane holds whole doubles");
-  constexpr int B = kSpLanes * SPL;  // steps per batch (<= 69: reads precede the batch)
-  constexpr int DPL = SPL / 2;       // doubles per lane
-  __shared__ uint32_t sm[kSpStreams * kSpPitch];
-  const int t = threadIdx.x & (kSpLanes - 1);
-  const int slot = threadIdx.x / kSpLanes;
-  uint32_t* st = sm + slot * kSpPitch;
-  const int64_t sid = (int64_t)blockIdx.x * kSpStreams + slot;
-  const bool active = sid < (int64_t)R * P;
-  const int r = active ? (int)(sid / P) : 0;
-  const int p = active ? (int)(sid % P) : 0;
-  // PoissonDistribution.reseedRandomGenerator(seed + i + partitionIndex) ->
-  // AbstractWell.setSeed(int[]{hi, lo}): v[i] = 1812433253 * (v[i-2] ^ v[i-2] >>> 30) + i
-  // (sign-extended long arithmetic; the low word only needs the 32-bit arithmetic shift),
-  // two independent chains (even / odd i) on lanes 0 and 1.
-  if (t < 2) {
-    const uint64_t s64 = (uint64_t)seed + (uint64_t)(int64_t)(learner0 + r) + (uint64_t)(int64_t)p;
-    uint32_t x = t == 0 ? (uint32_t)(s64 >> 32) : (uint32_t)s64;
-    st[t] = x;
-    for (int i = 2 + t; i < 624; i += 2) {
-      x = 1812433253u * (x ^ (uint32_t)((int32_t)x >> 30)) + (uint32_t)i;
-      st[i] = x;
-    }
-  }
-  block_sync();
-  int64_t row = active ? part_off[p] : 0;
-  const int64_t row_end = active ? part_off[p + 1] : 0;
-  uint8_t* out = counts + (int64_t)r * N;
-  uint32_t carry = st[0];  // z4 "before" step 0 is v[0] (lane 0 of each stream uses it)
-  int i = 0, n = 0, bad = 0;
-  double racc = 1.0;      // serial parse: open row's product and count
-  double pr = 1.0;        // relaxation parse: carry in-state of lane 0
-  int pn = 0;
-  const int n0 = SPL * t;
-  while (__any(row < row_end)) {
-    uint32_t w[5][SPL];
-    // batch starts are multiples of 16 (B is): bit i/16 of kFast says no window wraps
-    constexpr uint64_t kFast = sp_fast_mask(B);
-    if ((kFast >> (i >> 4)) & 1u)
-      sp_read<SPL, true>(st, i, n0, w);
-    else
-      sp_read<SPL, false>(st, i, n0, w);
-    uint32_t a[SPL], z2[SPL], c[SPL];
-#pragma unroll
-    for (int q = 0; q < SPL; q++) {
-      a[q] = w[0][q] ^ (w[0][q] >> 27);
-      z2[q] = (w[1][q] >> 9) ^ w[2][q] ^ (w[2][q] >> 1);
-      const uint32_t z0 = (w[3][q] & 0x80000000u) | (w[4][q] & 0x7FFFFFFFu);
-      c[q] = (a[q] << 9) ^ (a[q] >> 21) ^ z0 ^ (z2[q] << 21) ^ (z2[q] >> 21);
-    }
-    // lane transfer: z4 after the lane's last step = L^SPL(z4 before) ^ C
-    uint32_t C = c[0];
-#pragma unroll
-    for (int q = 1; q < SPL; q++) C = wellsp::L1(C) ^ c[q];
-    C ^= t == 0 ? wellsp::lpow<SPL>(carry) : 0u;
-    C ^= wellsp::lpow<SPL>(wellsp::dpp<0x111>(C));      // row_shr:1
-    C ^= wellsp::lpow<2 * SPL>(wellsp::dpp<0x112>(C));  // row_shr:2
-    C ^= wellsp::lpow<4 * SPL>(wellsp::dpp<0x114>(C));  // row_shr:4
-    C ^= wellsp::lpow<8 * SPL>(wellsp::dpp<0x118>(C));  // row_shr:8
-    const uint32_t prevC = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)C, 0x121, 0xF, 0xF,
-                                                                  false);  // row_ror:1
-    uint32_t y = t == 0 ? carry : prevC;  // z4 before the lane's first step
-    carry = prevC;                        // lane 0: z4 of the batch's last step
-    uint32_t o[SPL];
-    uint32_t z3[SPL];
-#pragma unroll
-    for (int q = 0; q < SPL; q++) {
-      z3[q] = y ^ (y << 25) ^ a[q] ^ z2[q];
-      y = wellsp::L1(y) ^ c[q];
-      o[q] = well_temper26(y);
-    }
-    if (i >= B - 1) {  // the written block [i - B + 1, i] does not wrap
-      uint32_t* pw = st + (i - n0 - (SPL - 1));
-#pragma unroll
-      for (int q = 0; q < SPL; q++) pw[SPL - 1 - q] = z3[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < SPL; q++) {
-        int pos = i - n0 - q;
-        pos += pos < 0 ? 624 : 0;
-        st[pos] = z3[q];
-      }
-    }
-    i = wrap624(i - B);
-    // doubles: BitsStreamGenerator.nextDouble = (next(26) << 26 | next(26)) * 2^-52,
-    // built exactly as the bits of 1 + m * 2^-52 minus 1
-    double x[DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; k++) {
-      const uint32_t hi = o[2 * k], lo = o[2 * k + 1];
-      x[k] = __hiloint2double((int)(0x3FF00000u | (hi >> 6)), (int)((hi << 26) | lo)) - 1.0;
-    }
-    // PoissonDistribution.nextPoisson (mean < 40): r *= nextDouble() while r >= exp(-mean),
-    // at most n < 1000 * mean draws counted.
-    if constexpr (PAR) {
-      // Lane-parallel parse by relaxation.  A lane's doubles map an in-state (r, n) (the
-      // running product and count of the row open before its first double) to an
-      // out-state; a lane whose doubles end a row emits counts and its out-state no
-      // longer depends on its in-state past that end.  Every lane re-evaluates its
-      // doubles from the previous lane's out-state (lane 0: the carry from the previous
-      // batch) until no in-state changes: the fixed point of this chain is unique and is
-      // the sequential parse, and since every double < exp(-mean) ends whatever row it
-      // is in, chains of lanes without an end are short (a few rounds).
-      double in_r = t == 0 ? pr : 1.0;
-      int in_n = t == 0 ? pn : 0;
-      int nk[DPL];
-      bool ek[DPL];
-      double out_r;
-      int out_n;
-      for (;;) {
-        double r_in = in_r;
-        int n_in = in_n;
-#pragma unroll
-        for (int k = 0; k < DPL; k++) {
-          const double rr = r_in * x[k];
-          const bool ge = rr >= p_exp;
-          const int nn = n_in + (ge ? 1 : 0);
-          const bool e = !ge || (CAP && nn >= icap);
-          nk[k] = nn;
-          ek[k] = e;
-          r_in = e ? 1.0 : rr;
-          n_in = e ? 0 : nn;
-        }
-        out_r = r_in;
-        out_n = n_in;
-        const int ph = (int)wellsp::dpp<0x111>((uint32_t)__double2hiint(out_r));  // row_shr:1
-        const int pl = (int)wellsp::dpp<0x111>((uint32_t)__double2loint(out_r));
-        const int pnn = (int)wellsp::dpp<0x111>((uint32_t)out_n);
-        // branch-free: bitwise, not short-circuit, so no exec-mask juggling per round
-        const int changed = (t != 0) & ((ph != __double2hiint(in_r)) |
-                                        (pl != __double2loint(in_r)) | (pnn != in_n));
-        if (!__any(changed)) break;
-        in_r = t != 0 ? __hiloint2double(ph, pl) : in_r;
-        in_n = t != 0 ? pnn : in_n;
-      }
-      // carry: lane 15's out-state to lane 0 (row_ror:1)
-      {
-        const int ch = __builtin_amdgcn_update_dpp(0, __double2hiint(out_r), 0x121, 0xF, 0xF, false);
-        const int cl = __builtin_amdgcn_update_dpp(0, __double2loint(out_r), 0x121, 0xF, 0xF, false);
-        pn = __builtin_amdgcn_update_dpp(0, out_n, 0x121, 0xF, 0xF, false);
-        pr = __hiloint2double(ch, cl);
-      }
-      // row of each emitted count: ends at earlier positions of this stream's batch
-      int below = 0, mine = 0;
-#pragma unroll
-      for (int k = 0; k < DPL; k++) {
-        const uint64_t m = __ballot(ek[k]);
-        below += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        mine += ek[k] ? 1 : 0;
-      }
-      const int rowbase = (int)__builtin_amdgcn_update_dpp(0, below, 0x150, 0xF, 0xF, false);
-      const int rowend =
-          (int)__builtin_amdgcn_update_dpp(0, below + mine, 0x15F, 0xF, 0xF, false);
-      int rank = below - rowbase;
-#pragma unroll
-      for (int k = 0; k < DPL; k++) {
-        if (ek[k]) {
-          if (row + rank < row_end) {
-            out[row + rank] = (uint8_t)min(nk[k], 255);
-            bad |= nk[k] > 255 ? 1 : 0;
-          }
-          rank++;
-        }
-      }
-      row += rowend - rowbase;
-      continue;
-    }
-    // serial parse: 16 doubles at a time, all lanes of the stream run it, lane e keeps
-    // the e-th count
-#pragma unroll
-    for (int h = 0; h < DPL; h++) {
-      int ne = 0;
-      int cap = 0;
-#pragma unroll
-      for (int d = 0; d < kSpLanes; d++) {
-        // double 16h + d of the batch, in stream order: lane l holds doubles DPL*l ..
-        // DPL*l + DPL - 1, so half h reads lanes 8h .. 8h+7 when DPL = 2
-        const int dl = (DPL == 1) ? d : (8 * h + (d >> 1));
-        const int dk = (DPL == 1) ? 0 : (d & 1);
-        double xd = 0.0;
-        // compile-time lane index for the DPP broadcast
-        switch (dl) {
-#define SBAG_BC(L) case L: xd = wellsp::row_bcast<L>(x[dk]); break;
-          SBAG_BC(0) SBAG_BC(1) SBAG_BC(2) SBAG_BC(3) SBAG_BC(4) SBAG_BC(5) SBAG_BC(6) SBAG_BC(7)
-          SBAG_BC(8) SBAG_BC(9) SBAG_BC(10) SBAG_BC(11) SBAG_BC(12) SBAG_BC(13) SBAG_BC(14)
-          SBAG_BC(15)
-#undef SBAG_BC
-        }
-        racc *= xd;
-        const bool ge = racc >= p_exp;
-        n += ge ? 1 : 0;
-        const bool done = !ge || (CAP && n >= icap);
-        cap = (done && ne == t) ? n : cap;
-        ne += done ? 1 : 0;
-        n = done ? 0 : n;
-        racc = done ? 1.0 : racc;
-      }
-      if (t < ne && row + t < row_end) {
-        out[row + t] = (uint8_t)min(cap, 255);
-        bad |= cap > 255 ? 1 : 0;
-      }
-      row += ne;
-    }
-  }
-  if (bad) atomicOr(err, 1);
-}
-
 void launch_poisson(hipStream_t st, uint8_t* counts, int64_t N, const int64_t* d_part_off, int P,
                     int R, int learner0, int64_t seed, double mean, double p_exp, int* d_err) {
-  const int64_t streams = (int64_t)R * P;
-  const int blocks = (int)((streams + 63) / 64);
-  // A/B knobs, read per launch so tests can switch them: SBAG_POISSON_V (4 = k_poisson4,
-  // the default; 3 = k_poisson3,
-  // 2 = the two-wave k_poisson2, 1 = one wave), SBAG_POISSON_SPL (steps per lane, 2 or 4),
-  // SBAG_POISSON_PAR (1 = lane-parallel relaxation parse, 0 = serial parse)
-  const char* ev = getenv("SBAG_POISSON_V");
-  const char* es = getenv("SBAG_POISSON_SPL");
-  const int ver = ev ? atoi(ev) : 4;
-  const int spl = es ? atoi(es) : 4;
-  if (ver == 4) {
-    // k_poisson4 (sbag_poisson.hip); SBAG_POISSON_LANES: lanes per stream (8, 16 or 4; default
-    // by stream count)
-    const int icap = (int)std::min(ceil(1000.0 * mean), 1e9);
-    const char* el = getenv("SBAG_POISSON_LANES");
-    launch_poisson4(st, counts, N, d_part_off, P, R, learner0, seed, p_exp, icap, icap <= 255,
-                    el ? atoi(el) : 0, d_err);
-    return;
-  }
-  if (ver == 3) {
-    // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean);
-    // the cap is only checked when it can end a row below the 255 limit
-    const int icap = (int)std::min(ceil(1000.0 * mean), 1e9);
-    const bool cap = icap <= 255;
-    const int sb = (int)((streams + kSpStreams - 1) / kSpStreams);
-    const char* ep = getenv("SBAG_POISSON_PAR");
-    const bool par = ep ? atoi(ep) != 0 : true;
-#define SBAG_P3(S, C, A)                                                                   \
-  hipLaunchKernelGGL((k_poisson3<S, C, A>), dim3(sb), dim3(256), 0, st, counts, N, d_part_off, \
-                     P, R, learner0, seed, p_exp, icap, d_err)
-    if (spl == 2) {
-      if (par) {
-        if (cap) SBAG_P3(2, true, true); else SBAG_P3(2, false, true);
-      } else {
-        if (cap) SBAG_P3(2, true, false); else SBAG_P3(2, false, false);
-      }
-    } else {
-      if (par) {
-        if (cap) SBAG_P3(4, true, true); else SBAG_P3(4, false, true);
-      } else {
-        if (cap) SBAG_P3(4, true, false); else SBAG_P3(4, false, false);
-      }
-    }
-#undef SBAG_P3
-    return;
-  }
-  if (ver == 1) {
-    hipLaunchKernelGGL(k_poisson, dim3(blocks), dim3(64), 0, st, counts, N, d_part_off, P, R,
-                       learner0, seed, mean, p_exp, d_err);
-    return;
-  }
-  const size_t lds = (size_t)(624 + 2 * kPB) * 64 * 4;  // 163840 = the whole LDS
-  set_max_lds((const void*)k_poisson2, (int)lds);
-  static const int dbg = getenv("SBAG_POISSON_DBG") ? atoi(getenv("SBAG_POISSON_DBG")) : 0;
-  hipLaunchKernelGGL(k_poisson2, dim3(blocks), dim3(128), lds, st, counts, N, d_part_off, P, R,
-                     learner0, seed, mean, p_exp, d_err, dbg);
+  // PoissonDistribution.nextPoisson's `n < 1000 * mean` for integer n: n < ceil(1000 * mean);
+  // the cap is only checked when it can end a row below the 255 limit.  SBAG_POISSON_LANES:
+  // lanes per stream (8, 16 or 4; default by stream count -- read per launch, the tests switch it)
+  const int icap = (int)std::min(ceil(1000.0 * mean), 1e9);
+  const char* el = getenv("SBAG_POISSON_LANES");
+  launch_poisson4(st, counts, N, d_part_off, P, R, learner0, seed, p_exp, icap, icap <= 255, el ? atoi(el) : 0,
+                  d_err);
 }
 
 // ======================================================================
@@ -3578,165 +2873,6 @@ void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, co
                        (const uint64_t*)parent_hist, d_triples, words_per_slot);
 }
 
-// ======================================================================
-// Per-replica bins from value codes: bin = lut[r][fl][code] (TreePoint.findBin
-// = Arrays.binarySearch over the replica's thresholds, precomputed per code).
-// ======================================================================
-template <typename CT>
-__global__ __launch_bounds__(256) void k_materialize(const CT* __restrict__ codes, int64_t N,
-                                                     int32_t S_codes, const int32_t* __restrict__ sub,
-                                                     const int32_t* __restrict__ Fr, int32_t Fmax,
-                                                     const uint8_t* __restrict__ lut,
-                                                     const int64_t* __restrict__ lutoff,
-                                                     uint8_t* __restrict__ out, int32_t S_out) {
-  const int r = blockIdx.y;
-  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (row >= N) return;
-  const int fr = Fr[r];
-  uint8_t* o = out + ((int64_t)r * N + row) * S_out;
-  const CT* c = codes + row * S_codes;
-  for (int fl = 0; fl < S_out; fl++) {
-    uint8_t b = 0;
-    if (fl < fr) {
-      const int g = sub[(int64_t)r * Fmax + fl];
-      b = lut[lutoff[(int64_t)r * Fmax + fl] + (int64_t)c[g]];
-    }
-    o[fl] = b;
-  }
-}
-
-// The same bins, a workgroup per (64 rows, replica): the rows' codes into LDS with coalesced
-// loads, then each thread assembles output words of 4 bins (LUT lookups; a replica's LUTs stay
-// in L2 while its rows stream: the replicas are the grid's slow dimension) and stores them
-// coalesced.  (k_materialize's thread per row stored one byte per feature S_out bytes apart:
-// 3.8 s for 128 replicas of 10M x 100.)
-constexpr int kMatRows = 64;
-template <typename CT>
-__global__ __launch_bounds__(256) void k_materialize_rows(const CT* __restrict__ codes, int64_t N,
-                                                          int32_t S_codes, const int32_t* __restrict__ sub,
-                                                          const int32_t* __restrict__ Fr, int32_t Fmax,
-                                                          const uint8_t* __restrict__ lut,
-                                                          const int64_t* __restrict__ lutoff,
-                                                          uint8_t* __restrict__ out, int32_t S_out,
-                                                          uint8_t* __restrict__ cols, int32_t ncol,
-                                                          int64_t npad, int R, int rb) {
-  // [kMatRows][S_codes] CT codes, then (cols) [kMatRows][S_out] bins
-  extern __shared__ __align__(16) uint8_t s_codes[];
-  const int tid = threadIdx.x;
-  const int64_t n0 = (int64_t)blockIdx.x * kMatRows;
-  const int nr = (int)min<int64_t>(kMatRows, N - n0);
-  const int rw = S_codes * (int)sizeof(CT) / 4;  // 4-byte words per code row (S_codes % 4 == 0)
-  const uint32_t* src = (const uint32_t*)(codes + n0 * S_codes);
-  for (int k = tid; k < nr * rw; k += 256) ((uint32_t*)s_codes)[k] = src[k];
-  block_sync();
-  const CT* sc = (const CT*)s_codes;
-  // rb replicas per workgroup share the staged code rows
-  for (int r = blockIdx.y * rb; r < min(R, (int)(blockIdx.y + 1) * rb); r++) {
-  if (cols) block_sync();  // (the previous replica's column pass read the bins tile)
-  const int fr = Fr[r];
-  const int32_t* sr = sub + (int64_t)r * Fmax;
-  const int64_t* lo = lutoff + (int64_t)r * Fmax;
-  const int wpr = S_out / 4;  // output words per row
-  uint32_t* o = (uint32_t*)(out + ((int64_t)r * N + n0) * S_out);
-  for (int q = tid; q < nr * wpr; q += 256) {
-    const int row = q / wpr, w = q - row * wpr;
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int fl = 4 * w + k;
-      if (fl < fr) v |= (uint32_t)lut[lo[fl] + (int64_t)sc[row * S_codes + sr[fl]]] << (8 * k);
-    }
-    o[q] = v;
-    if (cols) ((uint32_t*)(s_codes + (size_t)kMatRows * S_codes * sizeof(CT)))[q] = v;
-  }
-  if (!cols) continue;
-  // the column-major copy (k_partition's gathers): per feature the block's 64 rows are 64
-  // consecutive bytes (rows past N: 0)
-  block_sync();
-  const uint8_t* sb = s_codes + (size_t)kMatRows * S_codes * sizeof(CT);
-  uint8_t* cr = cols + (int64_t)r * ncol * npad + n0;
-  for (int q = tid; q < ncol * (kMatRows / 4); q += 256) {
-    const int fl = q / (kMatRows / 4), wd = q - fl * (kMatRows / 4);
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int row = 4 * wd + k;
-      if (row < nr) v |= (uint32_t)sb[row * S_out + fl] << (8 * k);
-    }
-    ((uint32_t*)(cr + (int64_t)fl * npad))[wd] = v;
-  }
-  }
-}
-
-bool launch_materialize(hipStream_t st, const void* codes, int code_bytes, int64_t N, int32_t S_codes,
-                        const int32_t* d_sub, const int32_t* d_Fr, int32_t Fmax, int R,
-                        const uint8_t* d_lut, const int64_t* d_lutoff, uint8_t* out, int32_t S_out,
-                        uint8_t* cols, int32_t ncol, int64_t npad) {
-  const size_t lds = (size_t)kMatRows * S_codes * code_bytes + (cols ? (size_t)kMatRows * S_out : 0);
-  if (S_out % 4 == 0 && (S_codes * code_bytes) % 4 == 0 && lds <= 64 * 1024 && npad % kMatRows == 0 &&
-      !getenv("SBAG_MATERIALIZE_ROWWISE")) {
-    // four replicas per workgroup share the staged code rows (C3-sized continuous fit:
-    // 927 / 894 / 890 ms at 1 / 2 / 4; SBAG_MATERIALIZE_RB overrides)
-    const int rb = std::max(1, std::min(R, getenv("SBAG_MATERIALIZE_RB") ? atoi(getenv("SBAG_MATERIALIZE_RB")) : 4));
-    const dim3 g((unsigned)((N + kMatRows - 1) / kMatRows), (unsigned)((R + rb - 1) / rb));
-    set_max_lds(code_bytes == 1 ? (const void*)k_materialize_rows<uint8_t> : (const void*)k_materialize_rows<uint16_t>,
-                (int)lds);
-    if (code_bytes == 1)
-      hipLaunchKernelGGL(k_materialize_rows<uint8_t>, g, dim3(256), lds, st, (const uint8_t*)codes, N, S_codes,
-                         d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad, R, rb);
-    else
-      hipLaunchKernelGGL(k_materialize_rows<uint16_t>, g, dim3(256), lds, st, (const uint16_t*)codes, N,
-                         S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out, cols, ncol, npad, R, rb);
-    return cols != nullptr;
-  }
-  dim3 grid((unsigned)((N + 255) / 256), (unsigned)R);
-  if (code_bytes == 1)
-    hipLaunchKernelGGL(k_materialize<uint8_t>, grid, dim3(256), 0, st, (const uint8_t*)codes, N,
-                       S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
-  else
-    hipLaunchKernelGGL(k_materialize<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)codes, N,
-                       S_codes, d_sub, d_Fr, Fmax, d_lut, d_lutoff, out, S_out);
-  return false;
-}
-
-// Per-replica packed rows of identity bins: out[r][n][fl] = codes[n][sub[r][fl]] (0 past the
-// replica's F_r), S_out bytes per row.  A workgroup takes 16 rows: their code rows into LDS
-// (coalesced), then per replica one 4-byte word of the 16 x S_out output bytes per thread
-// (coalesced stores).
-__global__ __launch_bounds__(256) void k_pack_rows(const uint8_t* __restrict__ codes, int64_t N,
-                                                   int32_t S_codes, const int32_t* __restrict__ sub,
-                                                   const int32_t* __restrict__ Fr, int32_t Fmax, int R,
-                                                   uint8_t* __restrict__ out, int32_t S_out) {
-  extern __shared__ __align__(16) uint8_t s_rows[];  // [16][S_codes]
-  const int tid = threadIdx.x;
-  const int64_t n0 = (int64_t)blockIdx.x * 16;
-  const int nr = (int)min<int64_t>(16, N - n0);
-  for (int k = tid; k < nr * S_codes / 4; k += 256)
-    ((uint32_t*)s_rows)[k] = ((const uint32_t*)(codes + n0 * S_codes))[k];
-  block_sync();
-  const int wpr = S_out / 4;  // output words per row
-  for (int r = 0; r < R; r++) {
-    const int fr = Fr[r];
-    const int32_t* sr = sub + (int64_t)r * Fmax;
-    for (int q = tid; q < nr * wpr; q += 256) {
-      const int row = q / wpr, w = q - row * wpr;
-      uint32_t v = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int fl = 4 * w + k;
-        if (fl < fr) v |= (uint32_t)s_rows[row * S_codes + sr[fl]] << (8 * k);
-      }
-      ((uint32_t*)(out + ((int64_t)r * N + n0) * S_out))[q] = v;
-    }
-  }
-}
-
-void launch_pack_rows(hipStream_t st, const uint8_t* codes, int64_t N, int32_t S_codes, const int32_t* d_sub,
-                      const int32_t* d_Fr, int32_t Fmax, int R, uint8_t* out, int32_t S_out) {
-  const unsigned blocks = (unsigned)((N + 15) / 16);
-  hipLaunchKernelGGL(k_pack_rows, dim3(blocks), dim3(256), (size_t)16 * S_codes, st, codes, N, S_codes,
-                     d_sub, d_Fr, Fmax, R, out, S_out);
-}
 
 // Per-replica bins by counting code cuts: bin(code) = #{j : cut_j <= code}, cut_j = #{dictionary
 // values <= t_j} of the (replica, feature)'s thresholds t_j -- TreePoint.findBin's binary search
@@ -4729,272 +3865,6 @@ void launch_aggregate(hipStream_t st, const void* votes, int vote_bytes, int K, 
   else
     launch_aggregate_t(st, (const double*)votes, K, N, agg, nclasses, num_learners, out, gcnt,
                        gcnt_rows);
-}
-
-// ======================================================================
-// Booster engine (GBMRegressor's base-learner fits, ml/regression/GBMRegressor.scala:
-// 302-319): one DecisionTreeRegressor per boosting iteration on fp64 pseudo-residual
-// labels.  Spark sums a node's (feature, bin) statistics in fp64, one row at a time in
-// row order (DTStatsAggregator.update, each exploded copy of a row separately), so the
-// sums depend on that order: these kernels keep every node's rows in row order (a
-// stable partition) and give every (node, feature) cell chain to one lane.
-// ======================================================================
-__device__ __forceinline__ uint32_t bt_code(const void* codes, int code_bytes, int64_t at) {
-  return code_bytes == 1 ? (uint32_t)((const uint8_t*)codes)[at]
-                         : (code_bytes == 2 ? (uint32_t)((const uint16_t*)codes)[at]
-                                            : ((const uint32_t*)codes)[at]);
-}
-
-// value counts of the subbag: vc[vcoff[fl] + code] += count for every in-bag row
-__global__ void k_bt_valuecount(const uint32_t* __restrict__ rows, int64_t nrows,
-                                const uint8_t* __restrict__ cnt, const void* __restrict__ codes,
-                                int code_bytes, int32_t S, const int32_t* __restrict__ sub,
-                                int32_t Fr, const int64_t* __restrict__ vcoff,
-                                uint32_t* __restrict__ vc) {
-  const int64_t total = nrows * Fr;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = i / Fr;
-    const int fl = (int)(i - k * Fr);
-    const uint32_t r = rows[k];
-    const uint32_t code = bt_code(codes, code_bytes, (int64_t)r * S + sub[fl]);
-    atomicAdd(&vc[vcoff[fl] + code], (uint32_t)cnt[r]);
-  }
-}
-
-// Histogram of one level: workgroup (node q, feature chunk), lane = feature fl.  The
-// lane walks the node's rows in row order and adds count, label, label^2 to its bin in
-// LDS (count times: the reference's explode), exactly DTStatsAggregator.update's fp64
-// sequence for that (feature, bin).  fl == Fr is the node's total (its parent stats,
-// one bin).  hist: [q][Fr + 1][NB][3] fp64.
-// One wave per (node, feature chunk); lane = feature (lane Fr: the node total).  Rows are
-// taken 64 at a time: lane j loads row i0 + j's id, count and label (coalesced), the wave
-// then walks the batch in row order, each row broadcast by readlane, and every lane adds
-// the row into its feature's bin with LDS fp64 atomics.  One lane's adds to one cell are
-// executed in issue order, so each cell is the sequential fp64 sum over the node's rows
-// in row order, `count` times per row -- DTStatsAggregator.update on the exploded rows.
-// The bin of row t + 8 is gathered while row t is added (the code, then the LUT lookup
-// one group later), so the walk is not paced by two dependent global loads per row.
-constexpr int kBtG = 8;  // rows per gather group
-// CB: code bytes (1, 2, 4) as a template parameter, and every lane loads (lanes without a
-// feature read local feature 0's code and LUT and discard the bin): with bt_code's width
-// branches under a per-lane condition each load sat in its own exec-masked block behind a
-// vmcnt(0), and the walk ran ~650 cycles per row
-template <int CB>
-__global__ __launch_bounds__(64) void k_bt_hist(const uint32_t* __restrict__ rows,
-                                                const int64_t* __restrict__ seg, /*[q][2]*/
-                                                const uint8_t* __restrict__ cnt,
-                                                const double* __restrict__ y,
-                                                const void* __restrict__ codes, int code_bytes,
-                                                int32_t S, const int32_t* __restrict__ sub,
-                                                int32_t Fr, const uint8_t* __restrict__ lut,
-                                                const int64_t* __restrict__ lutoff, int NB, int FL,
-                                                double* __restrict__ hist) {
-  extern __shared__ double acc[];  // [NB * 3][FL]
-  const int lane = threadIdx.x;
-  const int q = blockIdx.x;
-  const int fl = blockIdx.y * FL + lane;
-  const bool on = lane < FL && fl <= Fr;
-  for (int k = lane; k < NB * 3 * FL; k += 64) acc[k] = 0.0;
-  block_sync();
-  const int64_t a = seg[2 * q], b = seg[2 * q + 1];
-  const bool total = fl == Fr;
-  const bool gat = on && !total;  // lanes whose code decides the bin (the total lane: bin 0)
-  const int fg = gat ? fl : 0;
-  const int g = sub[fg];
-  const uint8_t* lt = lut + lutoff[fg];
-  double* const cell0 = acc + lane;
-  for (int64_t i0 = a; i0 < b; i0 += 64) {
-    const int n = (int)min((int64_t)64, b - i0);
-    // lane j: row i0 + j (rows past the node: count 0, label +0.0)
-    const uint32_t rj = lane < n ? rows[i0 + lane] : 0u;
-    const uint32_t cj = lane < n ? (uint32_t)cnt[rj] : 0u;
-    const double vj = lane < n ? y[rj] : 0.0;
-    const int vhi = __double2hiint(vj), vlo = __double2loint(vj);
-    // codes of a group of rows (lane = feature), then their bins through the LUT
-    auto codes_of = [&](int t0, uint32_t (&cd)[kBtG]) {
-#pragma unroll
-      for (int u = 0; u < kBtG; u++) {
-        // groups past the batch read lane 63's row (valid; their bins are never added)
-        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rj, min(t0 + u, 63));
-        const int64_t at = (int64_t)r * S + g;
-        cd[u] = CB == 1 ? (uint32_t)((const uint8_t*)codes)[at]
-                        : (CB == 2 ? (uint32_t)((const uint16_t*)codes)[at] : ((const uint32_t*)codes)[at]);
-      }
-    };
-    auto bins_of = [&](const uint32_t (&cd)[kBtG], uint32_t (&bn)[kBtG]) {
-#pragma unroll
-      for (int u = 0; u < kBtG; u++) {
-        const uint32_t v = lt[cd[u]];
-        bn[u] = gat ? v : 0u;
-      }
-    };
-    // three-stage pipeline over groups of rows: codes of group g + 2, bins (LUT) of group
-    // g + 1, adds of group g
-    uint32_t cA[kBtG], cB[kBtG], bA[kBtG], bB[kBtG];
-    // loads issued unconditionally (no branch between issue and use, so the compiler's
-    // vmcnt counts stay exact and the stages overlap)
-    codes_of(0, cA);
-    codes_of(kBtG, cB);
-    bins_of(cA, bA);
-    for (int t0 = 0; t0 < n; t0 += kBtG) {
-      codes_of(t0 + 2 * kBtG, cA);
-      bins_of(cB, bB);
-      const uint32_t (&bn)[kBtG] = bA;
-#pragma unroll
-      for (int u = 0; u < kBtG; u++) {
-        const int t = t0 + u;
-        if (t >= n) break;  // wave-uniform
-        const int c = __builtin_amdgcn_readlane((int)cj, t);
-        const double v = __hiloint2double(__builtin_amdgcn_readlane(vhi, t),
-                                          __builtin_amdgcn_readlane(vlo, t));
-        const double w = 1.0 * v;  // instanceWeight * label
-        const double w2 = w * v;   // instanceWeight * label * label
-        if (on) {
-          double* cell = cell0 + (size_t)bn[u] * 3 * FL;
-          for (int k = 0; k < c; k++) {  // the row's c exploded copies, in order
-            atomicAdd(cell, 1.0);
-            atomicAdd(cell + FL, w);
-            atomicAdd(cell + 2 * FL, w2);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kBtG; u++) {
-        bA[u] = bB[u];
-        const uint32_t t = cA[u];  // codes of group g + 2 move to the middle stage
-        cA[u] = cB[u];
-        cB[u] = t;
-      }
-    }
-  }
-  block_sync();
-  if (on) {
-    double* out = hist + ((int64_t)q * (Fr + 1) + fl) * NB * 3;
-    const int nb = total ? 1 : NB;
-    for (int k = 0; k < nb; k++) {
-      out[3 * k] = acc[(size_t)k * 3 * FL + lane];
-      out[3 * k + 1] = acc[(size_t)k * 3 * FL + FL + lane];
-      out[3 * k + 2] = acc[(size_t)k * 3 * FL + 2 * FL + lane];
-    }
-  }
-}
-
-// Stable partition of split nodes' rows: one wave per node; left rows (bin <= s, Spark's
-// ContinuousSplit.shouldGoLeft on the binned feature) keep their row order at the front
-// of the node's range, right rows after them.  nleft[q] receives the left row count.
-struct BtSplit {
-  int64_t a, b;
-  int64_t lutoff;
-  int32_t g, s;
-};
-// A workgroup of kBtPartT threads per split node: each pass takes kBtPartT consecutive
-// rows, ranks the left and the right rows of every wave with ballots and the waves with an
-// LDS prefix, so both children keep the node's row order (one wave per node walked the
-// root's 10^6 rows 64 at a time, each step behind two dependent loads).
-constexpr int kBtPartT = 512;
-__global__ __launch_bounds__(kBtPartT) void k_bt_partition(const uint32_t* __restrict__ in,
-                                                           uint32_t* __restrict__ out,
-                                                           const BtSplit* __restrict__ sp,
-                                                           const void* __restrict__ codes,
-                                                           int code_bytes, int32_t S,
-                                                           const uint8_t* __restrict__ lut,
-                                                           int64_t* __restrict__ nleft) {
-  constexpr int W = kBtPartT / 64;
-  __shared__ int s_l[W], s_r[W];
-  __shared__ unsigned long long s_tot;
-  const BtSplit p = sp[blockIdx.x];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint8_t* lt = lut + p.lutoff;
-  auto goes_left = [&](uint32_t r) {
-    return lt[bt_code(codes, code_bytes, (int64_t)r * S + p.g)] <= p.s;
-  };
-  if (tid == 0) s_tot = 0;
-  block_sync();
-  int nl_mine = 0;  // this thread's left rows (pass 1)
-  for (int64_t i = p.a + tid; i < p.b; i += kBtPartT) nl_mine += goes_left(in[i]) ? 1 : 0;
-  // wave sum then one atomic per wave
-  for (int o = 32; o > 0; o >>= 1) nl_mine += __shfl_xor(nl_mine, o);
-  if (lane == 0) atomicAdd(&s_tot, (unsigned long long)nl_mine);
-  block_sync();
-  const int64_t nl = (int64_t)s_tot;
-  int64_t lpos = p.a, rpos = p.a + nl;
-  for (int64_t i0 = p.a; i0 < p.b; i0 += kBtPartT) {
-    const int64_t i = i0 + tid;
-    const bool valid = i < p.b;
-    uint32_t r = 0;
-    bool left = false;
-    if (valid) {
-      r = in[i];
-      left = goes_left(r);
-    }
-    const uint64_t ml = __ballot(valid && left), mr = __ballot(valid && !left);
-    if (lane == 0) {
-      s_l[wave] = __popcll(ml);
-      s_r[wave] = __popcll(mr);
-    }
-    block_sync();
-    int bl = 0, br = 0, tl = 0, tr = 0;  // rows of the waves before this one; pass totals
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      const int cl = s_l[w], cr = s_r[w];
-      bl += w < wave ? cl : 0;
-      br += w < wave ? cr : 0;
-      tl += cl;
-      tr += cr;
-    }
-    const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
-    const uint32_t rank_r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mr >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mr, 0u));
-    if (valid) out[left ? lpos + bl + rank_l : rpos + br + rank_r] = r;
-    lpos += tl;
-    rpos += tr;
-    block_sync();  // s_l / s_r are rewritten by the next pass
-  }
-  if (tid == 0) nleft[blockIdx.x] = nl;
-}
-
-void launch_bt_valuecount(hipStream_t st, const uint32_t* rows, int64_t nrows, const uint8_t* cnt,
-                          const void* codes, int code_bytes, int32_t S, const int32_t* sub,
-                          int32_t Fr, const int64_t* vcoff, uint32_t* vc) {
-  const int64_t total = nrows * Fr;
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
-  if (blocks > 0)
-    hipLaunchKernelGGL(k_bt_valuecount, dim3(blocks), dim3(256), 0, st, rows, nrows, cnt, codes,
-                       code_bytes, S, sub, Fr, vcoff, vc);
-}
-
-int bt_lanes(int NB) {  // features per workgroup: NB * 3 * FL doubles in 64 KB of LDS
-  return std::max(1, std::min(64, (int)(65536 / ((size_t)NB * 3 * 8))));
-}
-
-void launch_bt_hist(hipStream_t st, const uint32_t* rows, const int64_t* seg, int nnodes,
-                    const uint8_t* cnt, const double* y, const void* codes, int code_bytes,
-                    int32_t S, const int32_t* sub, int32_t Fr, const uint8_t* lut,
-                    const int64_t* lutoff, int NB, double* hist) {
-  const int FL = bt_lanes(NB);
-  const size_t lds = (size_t)NB * 3 * FL * 8;
-  const dim3 grid(nnodes, (Fr + 1 + FL - 1) / FL);
-#define SBAG_BTH(CB)                                                                      \
-  set_max_lds((const void*)k_bt_hist<CB>, 64 * 1024);                                     \
-  hipLaunchKernelGGL(k_bt_hist<CB>, grid, dim3(64), lds, st, rows, seg, cnt, y, codes, code_bytes, \
-                     S, sub, Fr, lut, lutoff, NB, FL, hist)
-  if (code_bytes == 1) {
-    SBAG_BTH(1);
-  } else if (code_bytes == 2) {
-    SBAG_BTH(2);
-  } else {
-    SBAG_BTH(4);
-  }
-#undef SBAG_BTH
-}
-
-void launch_bt_partition(hipStream_t st, const uint32_t* in, uint32_t* out, const void* splits,
-                         int nsplit, const void* codes, int code_bytes, int32_t S,
-                         const uint8_t* lut, int64_t* nleft) {
-  hipLaunchKernelGGL(k_bt_partition, dim3(nsplit), dim3(kBtPartT), 0, st, in, out,
-                     (const BtSplit*)splits, codes, code_bytes, S, lut, nleft);
 }
 
 }  // namespace sbag

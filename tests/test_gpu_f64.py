@@ -298,9 +298,9 @@ def test_bucket_budget_chunks_equal_one_launch(ctx, cpusmall, monkeypatch):
 
 def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
     """The bench's real-valued-label fit at full size (10M x 100, 128 learners, depth 8,
-    P = 128), where the oracle cannot follow: the default engine (screen, staged routing
-    scatter, column-ordered and XCD-dispatched tasks, per-partition sums) gives the same trees
-    byte for byte as (a) the same screen with the unstaged scatter and tasks in node order and
+    P = 128), where the oracle cannot follow: the default engine (screen, routing scatter,
+    column-ordered and XCD-dispatched tasks, per-partition sums) gives the same trees byte for
+    byte as (a) the same screen with tasks in node order and pieces in order and
     (b) the unscreened engine, every feature of every node summed per partition and merged
     (k_fb_psum / k_fb_pmerge over every (node, feature))."""
     N, F, L = 10_000_000, 100, 128
@@ -315,10 +315,10 @@ def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
                            max_bins=32, impurity=nat.IMPURITY_VARIANCE)
 
         a = fit()
-        for k in ("SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER", "SBAG_F64_XCD_ORDER"):
+        for k in ("SBAG_F64_TASK_ORDER", "SBAG_F64_XCD_ORDER"):
             monkeypatch.setenv(k, "0")
         b = fit()
-        for k in ("SBAG_F64_SCATTER_STAGE", "SBAG_F64_TASK_ORDER", "SBAG_F64_XCD_ORDER"):
+        for k in ("SBAG_F64_TASK_ORDER", "SBAG_F64_XCD_ORDER"):
             monkeypatch.delenv(k)
         monkeypatch.setenv("SBAG_F64_SCREEN", "0")
         c = fit()

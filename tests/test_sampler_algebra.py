@@ -1,7 +1,7 @@
-"""CPU check of the algebra behind k_poisson3 (the step-parallel Well19937c sampler).
+"""CPU check of the algebra behind k_poisson4 (the step-parallel Well19937c sampler).
 
-k_poisson3 (spark-bagging_amd/csrc/sbag_kernels.hip) does not run a Well19937c stream
-one step at a time.  A batch of B = 16 * SPL consecutive steps is spread over 16 lanes
+k_poisson4 (spark-bagging_amd/csrc/sbag_poisson.hip) does not run a Well19937c stream
+one step at a time.  A batch of B = LANES * SPL consecutive steps is spread over LANES lanes
 (SPL steps per lane): every value a step reads from the state ring was written at least
 70 steps earlier, except z4 of the previous step (AbstractWell's v0), and
 
@@ -55,7 +55,7 @@ def temper26(z4):
 
 def step_parallel_outputs(seed, nsteps, spl, lanes=16):
     """next(26) outputs of the stream seeded `seed`, batch by batch as the kernel does
-    (k_poisson3: 16 lanes; k_poisson4: 8 lanes x 8 steps, 16 x 4, 4 x 16)."""
+    (k_poisson4: 8 lanes x 8 steps, 16 x 4, 4 x 16; smaller batches check the algebra too)."""
     g = pyoracle.Well19937c(seed)  # only for the seeded initial ring
     st = list(g.v)
     B = lanes * spl
