@@ -2,8 +2,8 @@
 
 GBMRegressor (ml/regression/GBMRegressor.scala:196-456) draws its bags with the bagging
 sampler and fits one DecisionTreeRegressor per iteration on fp64 pseudo-residuals.  The
-booster engine (sbag_fit_booster: k_bt_hist / k_bt_partition, fp64 sums in Spark's row
-order) must give the oracle's trees bit for bit -- structure, thresholds, impurities,
+booster fit (sbag_fit_booster: the bagging engine with one learner -- screened fp64 splits,
+Spark's per-partition row-order sums) must give the oracle's trees bit for bit -- structure, thresholds, impurities,
 gains, stats and leaf values -- and the boosted model the oracle's weights, subspaces and
 predictions, also bit for bit.  Workload: data/cpusmall (GBMRegressorSuite.scala reads
 the same file).
