@@ -119,6 +119,7 @@ def parse():
     ap.add_argument("--nondyadic-steps", type=int, default=2)
     ap.add_argument("--no-continuous", action="store_true",
                     help="skip the extra timing of the C3 shape on continuous features")
+    ap.add_argument("--continuous-steps", type=int, default=3)
     a = ap.parse_args()
     w = WORKLOADS[a.workload]
     for k in ("rows", "features", "learners", "depth"):
@@ -194,6 +195,7 @@ def continuous_fit(nat, ctx, N, F, L, depth, bins, part, steps=1):
         f.free()
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
+    tser = serialized_timing(lambda: fit(L))
     ds.free()
     return {"data": "continuous: ~2400-38000 distinct values per feature (host fp64 rows), dyadic "
                     "labels; per-replica thresholds from each replica's split-finding sample, "
@@ -201,7 +203,10 @@ def continuous_fit(nat, ctx, N, F, L, depth, bins, part, steps=1):
             "rows": N, "features": F, "learners": L, "steps": steps,
             "ms_per_step": round(1000.0 * el / steps, 3), "value": round(L * N * steps / el, 1),
             "unit": "estimator*rows/s", "ingest_s_untimed": round(t_ingest, 2),
-            "breakdown_ms": {k: round(v, 3) for k, v in tm.items() if k.endswith("_ms")}}
+            "breakdown_ms": breakdown_of(tser),
+            "breakdown_def": "a fit with the learner parts serialized (SBAG_OVERLAP=0, after one "
+                             "such warm fit), HIP events per stage; the timed steps overlap the parts",
+            "step_total_ms_overlapped": round(tm["total_ms"], 3)}
 
 
 def nproc():
@@ -209,6 +214,76 @@ def nproc():
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 1
+
+
+STAGES = ("sample_ms", "valuecount_ms", "bin_ms", "compact_ms", "hist_ms", "split_ms", "subtract_ms",
+          "partition_ms", "fix_ms", "group_ms", "chain_ms", "root_ms")
+
+
+def serialized_timing(fit):
+    """Per-stage HIP-event times of one fit with the learner parts serialized (SBAG_OVERLAP=0):
+    each launch runs alone, on the stream it is launched on.  The serialized fit runs twice and
+    the second is reported: a single-part fit of all the learners needs bigger per-fit buffers
+    than the timed steps' parts, and the first such fit allocates them inside its event window
+    (the C4 shard: 2.8 s of total_ms against a 1.06 s step before round 6)."""
+    prev = os.environ.get("SBAG_OVERLAP")
+    os.environ["SBAG_OVERLAP"] = "0"
+    try:
+        fit().free()
+        f = fit()
+        tm = f.timing()
+        f.free()
+    finally:
+        if prev is None:
+            os.environ.pop("SBAG_OVERLAP", None)
+        else:
+            os.environ["SBAG_OVERLAP"] = prev
+    return tm
+
+
+def breakdown_of(tm):
+    """breakdown_ms of a timing dict, with the stage sum against total_ms: what the stages do
+    not cover is host time between kernels on the fit's stream (each level's split results and
+    partition cursors go to the host and the next level's work lists come back)."""
+    b = {k: round(v, 3) for k, v in tm.items() if k.endswith("_ms")}
+    ssum = sum(tm.get(k, 0.0) for k in STAGES)
+    tot = tm.get("total_ms", 0.0)
+    b["stage_sum_ms"] = round(ssum, 3)
+    b["unattributed_ms"] = round(tot - ssum, 3)
+    b["unattributed_is"] = ("host time between kernels on the fit's stream (per-level results to "
+                            "the host, work lists back), not a kernel")
+    return b
+
+
+def build_record():
+    """Whether the shipped libsbag.so is newer than every source it is built from (the driver
+    runs __graft_entry__.build() in the build container; the GPU box runs the shipped .so)."""
+    import datetime
+    import glob
+
+    csrc = os.path.join(ROOT, "spark-bagging_amd", "csrc")
+    so = os.path.join(ROOT, "spark-bagging_amd", "libsbag.so")
+    srcs = glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")) + \
+        glob.glob(os.path.join(csrc, "*.h")) + [os.path.join(ROOT, "include", "sbag.h")]
+    objs = glob.glob(os.path.join(csrc, "build", "*.o"))
+
+    def iso(t):
+        return datetime.datetime.fromtimestamp(t, datetime.timezone.utc).isoformat(timespec="seconds")
+
+    try:
+        so_t = os.path.getmtime(so)
+    except OSError:
+        return {"libsbag_so": None}
+    src_t = max(os.path.getmtime(x) for x in srcs)
+    rec = {"libsbag_so_mtime": iso(so_t), "newest_source_mtime": iso(src_t),
+           "so_newer_than_sources": so_t >= src_t}
+    if objs:
+        rec["objects"] = len(objs)
+        rec["objects_newer_than_sources"] = min(os.path.getmtime(o) for o in objs) >= src_t
+        rec["so_newer_than_objects"] = so_t >= max(os.path.getmtime(o) for o in objs)
+    else:
+        rec["objects"] = 0  # (the object directory is not shipped to the GPU box)
+    return rec
 
 
 def main():
@@ -294,11 +369,7 @@ def main():
     # the other half's, which stretches its HIP-event duration; the serialized fit measures
     # each launch alone, on the stream it runs on.  The rocprofv3 profile uses the same
     # setting.
-    prev = os.environ.get("SBAG_OVERLAP")
-    os.environ["SBAG_OVERLAP"] = "0"
-    f = step()
-    kernel_fit = f.timing()
-    f.free()
+    kernel_fit = serialized_timing(step)
     timings = [kernel_fit]
     hist_ms = sum(t["hist_ms"] for t in timings)
     hist_launches = sum(t["hist_launches"] for t in timings)
@@ -357,7 +428,7 @@ def main():
                                  "ops_def": "2 x 32^3 int8 ops per v_mfma_i32_32x32x32_i8 issued: "
                                             "ceil(N/32) row steps x F x ceil(R/32) replica tiles "
                                             "x (1 + label digit planes)"}
-    breakdown = {k: round(v, 3) for k, v in timings[-1].items() if k.endswith("_ms")}
+    breakdown = breakdown_of(timings[-1])
     # the sampler's cost depends on rows per partition stream (Poisson.scala:53-56 reseeds
     # per partition): one extra fit, outside the timed region, at P = nproc
     sp = args.sampler_partitions or nproc()
@@ -375,10 +446,6 @@ def main():
                      "headline_partitions": args.partitions, "headline_sample_ms": breakdown["sample_ms"]}
     else:
         sampler_p = {"partitions": sp, "sample_ms": breakdown["sample_ms"]}
-    if prev is None:
-        os.environ.pop("SBAG_OVERLAP", None)
-    else:
-        os.environ["SBAG_OVERLAP"] = prev
     # The same fit on real-valued labels: y' = 1.1 y + 0.3 is not dyadic,
     # so sbag_fit takes the screened fp64 path (Spark's DTStatsAggregator row-order sums of the
     # chosen features, sbag_f64s.hip).
@@ -397,39 +464,32 @@ def main():
             f.free()
         torch.cuda.synchronize()
         el = time.perf_counter() - t1
-        # per-stage times from one more fit with the learner halves serialized, as for the
-        # headline's breakdown (the overlapped steps stretch each stage by the other half's)
-        prev_ov = os.environ.get("SBAG_OVERLAP")
-        os.environ["SBAG_OVERLAP"] = "0"
-        f = step()
-        tser = f.timing()
-        f.free()
-        if prev_ov is None:
-            os.environ.pop("SBAG_OVERLAP", None)
-        else:
-            os.environ["SBAG_OVERLAP"] = prev_ov
+        # per-stage times from a serialized fit, as for the headline's breakdown (the
+        # overlapped steps stretch each stage by the other half's)
+        tser = serialized_timing(step)
         ds.set_labels(y0)
         nondyadic = {"labels": "1.1 * y + 0.3 (fp64, not dyadic)", "steps": args.nondyadic_steps,
                      "ms_per_step": round(1000.0 * el / args.nondyadic_steps, 3),
                      "value": round(L * N * args.nondyadic_steps / el, 1),
                      "unit": "estimator*rows/s",
-                     "breakdown_ms": {k: round(v, 3) for k, v in tser.items() if k.endswith("_ms")},
-                     "breakdown_def": "one extra fit with the learner halves serialized "
-                                      "(SBAG_OVERLAP=0), HIP events per stage",
+                     "breakdown_ms": breakdown_of(tser),
+                     "breakdown_def": "a fit with the learner halves serialized (SBAG_OVERLAP=0, "
+                                      "after one such warm fit), HIP events per stage",
                      "exact_fallbacks": int(tl[-1]["exact_fallbacks"]),
                      "engine": "screened fp64 engine: splits chosen from integer histograms of the "
-                               "labels' fixed-point image under a rigorous error bound, the chosen "
-                               "feature's bins summed in Spark's row order (bucketing staged by bin, "
-                               "chains with the draws exploded in LDS), "
-                               "flagged nodes ('exact_fallbacks') summed exactly on every feature "
-                               "(DESIGN.md §4.7)"}
+                               "labels' fixed-point image under a rigorous error bound; the chosen "
+                               "feature's bins summed as Spark's executors do -- each partition's "
+                               "rows in row order, the partials merged in partition order "
+                               "(k_fb_psum / k_fb_pmerge; 'chain_ms' includes the stable routing); "
+                               "flagged nodes ('exact_fallbacks') summed the same way on every "
+                               "contending feature (DESIGN.md §4.7)"}
     # The C3 shape on continuous features: thousands of distinct values per
     # feature, so every replica is thresholded on its own split-finding sample and its bins are
     # materialized per replica.  Reported beside the headline; not `value`.
     continuous = None
     if args.workload == "c3" and world == 1 and not args.no_continuous:
         ds.free()
-        continuous = continuous_fit(nat, ctx, N, F, L, args.depth, args.bins, part, steps=1)
+        continuous = continuous_fit(nat, ctx, N, F, L, args.depth, args.bins, part, steps=args.continuous_steps)
     out = {
         "metric": "estimator×rows trained/sec", "value": round(value, 1),
         "unit": "estimator*rows/s", "n_gpus": world, "backend": args.backend if world > 1 else None,
@@ -447,9 +507,10 @@ def main():
         "nondyadic_labels": nondyadic, "continuous_features": continuous, "replication": replication,
         "value_incl_replication": (round(world * L * N * args.steps / (elapsed + replication["seconds"]), 1)
                                    if replication else None),
-        "kernel_timing": "roofline and breakdown_ms: one extra fit after the timed steps with "
-                         "the learner halves serialized (SBAG_OVERLAP=0), so each launch runs "
-                         "alone; the timed steps overlap the two halves on two streams",
+        "kernel_timing": "roofline and breakdown_ms: a fit after the timed steps with the learner "
+                         "halves serialized (SBAG_OVERLAP=0, after one such warm fit), so each "
+                         "launch runs alone; the timed steps overlap the two halves on two streams",
+        "build": build_record(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
