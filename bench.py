@@ -279,7 +279,7 @@ def build_record():
            "so_newer_than_sources": so_t >= src_t}
     if objs:
         rec["objects"] = len(objs)
-        rec["objects_newer_than_sources"] = min(os.path.getmtime(o) for o in objs) >= src_t
+        rec["newest_object_mtime"] = iso(max(os.path.getmtime(o) for o in objs))
         rec["so_newer_than_objects"] = so_t >= max(os.path.getmtime(o) for o in objs)
     else:
         rec["objects"] = 0  # (the object directory is not shipped to the GPU box)
