@@ -25,9 +25,9 @@
 //   k_fb_chainx    one partition: one lane per (task, bin), the bucket's rows in row order,
 //                  each label added count times (a row drawn c times is c consecutive
 //                  rows) -- Spark's cell sums bit for bit
-//   k_fb_psum / k_fb_pmerge   several partitions: Spark's per-partition aggregates (row
-//                  order inside a partition, one lane per (task, partition), no buckets),
-//                  merged per (task, bin) in partition order (reduceByKey)
+//   k_fb_runs / k_fb_psum / k_fb_pmerge   several partitions: Spark's per-partition
+//                  aggregates (row order inside a partition, a chain per (task, partition,
+//                  bin), no buckets), merged per (task, bin) in partition order (reduceByKey)
 //   k_fb_finish    binsToBestSplit over the chosen feature's exact bins (prefixes in bin
 //                  order, right = total - left, calculateImpurityStats with the node's
 //                  chained stats): the node's gain, impurity and children calculators
@@ -705,167 +705,191 @@ __global__ __launch_bounds__(64) void k_fb_chainx(F64BucketArgs A, int nchain) {
 // reduceByKey((a, b) => a.merge(b)), allStats(i) += other.allStats(i).  The merge order is the
 // shuffle's; partition order is one order Spark produces (and the only one at P = 1), and the
 // oracle restates the same (oracle/sbag_oracle.c fit_one).  So a (task, bin) cell is P
-// independent row-order chains plus a P-term merge: no bucketing by bin is needed to keep the
-// order -- one lane per (task, partition) walks that partition's entries of the task (a
-// contiguous run: a node's entries are in row order, partitions are row ranges) and adds each
-// into its own LDS bins; k_fb_pmerge then adds the P partials of every (task, bin) in
-// partition order.
+// independent row-order chains plus a P-term merge; a run (task, partition) is a contiguous
+// range of the task's entries (a node's entries are in row order, partitions are row ranges).
 //
-// k_fb_psum: a wave takes kL units (task, partition) = (g / P, g % P), g = w kL + l for lane
-// l < kL.  A unit's run is found by two binary searches of the partition's row bounds in the
-// task's entries.  The runs advance in stages of kPsT entries: the whole wave loads a stage of
-// every unit's labels and (bin | count) words -- kPsT lanes per unit, so a load instruction
-// touches a line or two per unit instead of a line per lane -- into LDS (issued two stages
-// ahead), then lane l adds its unit's stage in order into its LDS bins (sum += y, sumSq += y*y
-// once per draw).  LDS per unit: NB (sum, sumSq) pairs interleaved across the units
-// ([bin][unit]) and the staged stage.  The draw counts are not summed here: a (task, bin)'s
-// count is its cell of the level's integer histogram (k_fb_pmerge reads it there).
-constexpr int kPsT = 8;  // entries per unit per stage
-template <int kL, bool kCarried>
-__global__ __launch_bounds__(64) void k_fb_psum(F64BucketArgs A, int nchain) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  constexpr int kLd = kL * kPsT / 64;  // loads per stage (slot 64 u + lane)
-  constexpr int kYp = kPsT + 1;        // staging pitch (odd: the serial reads spread over banks)
-  static_assert(kL * kPsT % 64 == 0, "whole loads per stage");
-  const int lane = threadIdx.x, NB = A.NB, P = A.P;
-  double2* sd = (double2*)smem;                      // [NB][kL] (sum, sumSq)
-  double* sy = (double*)(sd + (size_t)NB * kL);      // [kL][kYp] staged labels
-  uint32_t* sb = (uint32_t*)(sy + (size_t)kL * kYp); // [kL][kYp] staged bin | count << 8
-  __shared__ int64_t s_lo[kL], s_len[kL], s_eb[kL];
-  const int64_t g = (int64_t)blockIdx.x * kL + lane;
-  int64_t lo = 0, len = 0, eb = 0;
-  if (lane < kL && g < (int64_t)nchain * P) {
-    const int64_t task = g / P;
-    const int q = (int)(g - task * P);
-    const F64Task t = A.tasks[task];
-    auto lower = [&](int64_t row) {  // first entry of the task with a row >= row
-      int64_t a = t.a, b = t.b;
-      while (a < b) {
-        const int64_t mid = (a + b) >> 1;
-        if ((int64_t)(uint32_t)A.ent_in[mid] < row)
-          a = mid + 1;
-        else
-          b = mid;
-      }
-      return a;
-    };
-    lo = lower(A.poff[q]);
-    len = lower(A.poff[q + 1]) - lo;
-    eb = t.ebase + (lo - t.a);
-  }
-  if (lane < kL) {
-    s_lo[lane] = lo;
-    s_len[lane] = len;
-    s_eb[lane] = eb;
-    for (int b = 0; b < NB; b++) sd[(size_t)b * kL + lane] = make_double2(0.0, 0.0);
-  }
-  int64_t maxlen = len;
-  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (int64_t)__shfl_xor(maxlen, o));
-  block_sync();
-  // load u, lane l: unit j = (64 u + l) / kPsT, entry x = l % kPsT of the stage
-  const int xs = lane % kPsT;
-  int64_t ulo[kLd], ulen[kLd], ueb[kLd];
-#pragma unroll
-  for (int u = 0; u < kLd; u++) {
-    const int j = (64 * u + lane) / kPsT;
-    ulo[u] = s_lo[j];
-    ulen[u] = s_len[j];
-    ueb[u] = s_eb[j];
-  }
-  // (every load unconditional, past a run's end at its last entry -- masked at use: a load
-  // under a branch makes the compiler wait for every load in flight at the join, which would
-  // cost each stage a full memory latency; kCarried is a template argument for the same reason)
-  auto load = [&](int64_t off, double (&yv)[kLd], uint32_t (&bv)[kLd]) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int64_t k = max(min(off + xs, ulen[u] - 1), (int64_t)0);
-      bv[u] = (uint32_t)A.ebin[ueb[u] + k];
-      if constexpr (kCarried)
-        yv[u] = A.ey_in[ulo[u] + k];
+// k_fb_psum: a wave per R runs with R = 64 / 2^nbits clamped to [1, 8] (C3's 32 bins: 2).  A
+// step of 512 entries (512 / R per run) is loaded coalesced, ordered by key = (run, bin) in LDS
+// (stable: an entry's rank among the step's entries of its key, from ballots over the key's
+// bits, as k_fb_scatter orders its buckets), and then lane l adds the entries of its keys l,
+// l + 64, ... in row order: a chain per (run, bin), ~512 / 64 entries long per step.  The run
+// bounds come from k_fb_runs (one lane per run, two binary searches of the partition's row
+// bounds).  The walk is VALU-issue bound, so every lane is kept busy and an entry's draws past
+// the first are an exec-masked loop.  (Round 6 measured, per C3 fit: one lane per run, 64 runs
+// per wave, 8 entries a stage, all of them walked by the run's lane -- 47.5 ms, the first
+// levels' few long runs leaving most SIMDs idle; the same with 2-8 lanes per run splitting the
+// bins -- 48 ms; one run per wave, 4 predicated draws per entry -- ~4 ms per level; this
+// kernel -- 29 ms.)  k_fb_pmerge then adds the P partials of every (task, bin) in partition
+// order.
+constexpr int kPwU = 8;  // rounds of 64 entries per step
+__global__ __launch_bounds__(256) void k_fb_runs(F64BucketArgs A, int64_t runs) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= runs) return;
+  const int64_t task = g / A.P;
+  const int q = (int)(g - task * A.P);
+  const F64Task t = A.tasks[task];
+  auto lower = [&](int64_t row) {  // first entry of the task with a row >= row
+    int64_t a = t.a, b = t.b;
+    while (a < b) {
+      const int64_t mid = (a + b) >> 1;
+      if ((int64_t)(uint32_t)A.ent_in[mid] < row)
+        a = mid + 1;
       else
-        yv[u] = A.y[(uint32_t)A.ent_in[ulo[u] + k]];
+        b = mid;
     }
+    return a;
   };
-  // a stage: the loaded words and labels to LDS, then lane l < kL adds its unit's entries
-  const uint32_t lbase = (uint32_t)lane;
-  auto stage = [&](int64_t off, const double (&yX)[kLd], const uint32_t (&bX)[kLd]) {
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int j = (64 * u + lane) / kPsT;
-      sy[j * kYp + xs] = yX[u];
-      sb[j * kYp + xs] = bX[u];
-    }
-    block_sync();
-    if (lane < kL) {
-      const int n = (int)min((int64_t)kPsT, max((int64_t)0, len - off));
-      // the stage's words and labels to registers first (one LDS wait), then one
-      // read-modify-write of the entry's bin per entry
-      uint32_t bcv[kPsT];
-      double yv[kPsT];
-#pragma unroll
-      for (int x = 0; x < kPsT; x++) {
-        bcv[x] = sb[lane * kYp + x];
-        yv[x] = sy[lane * kYp + x];
-      }
-      // (pinned here: the compiler would otherwise sink each read next to its use, one more LDS
-      // round trip per entry)
-#pragma unroll
-      for (int x = 0; x < kPsT; x++) __asm__ volatile("" : "+v"(bcv[x]), "+v"(yv[x]));
-#pragma unroll
-      for (int x = 0; x < kPsT; x++) {
-        if (x < n) {
-          const uint32_t c = bcv[x] >> 8;  // every run entry is drawn: c >= 1
-          const double w = 1.0 * yv[x];    // instanceWeight * label
-          const double wy = w * yv[x];     // instanceWeight * label * label
-          double2* p = sd + ((bcv[x] & 0xffu) * kL + lbase);
-          double2 v = *p;
-          // (draws 2-4 branch-free: an absent draw adds -0.0, which leaves every sum unchanged)
-          v.x += w;
-          v.y += wy;
-          v.x += c >= 2 ? w : -0.0;
-          v.y += c >= 2 ? wy : -0.0;
-          v.x += c >= 3 ? w : -0.0;
-          v.y += c >= 3 ? wy : -0.0;
-          v.x += c >= 4 ? w : -0.0;
-          v.y += c >= 4 ? wy : -0.0;
-          for (uint32_t k = 4; k < c; k++) {
-            v.x += w;
-            v.y += wy;
-          }
-          *p = v;
-        }
-      }
-    }
-    block_sync();
-  };
-  // three register buffers rotating by unrolling (no copies): a stage's loads are issued two
-  // stages ahead, and waiting for them leaves the later stage's loads in flight (a copy of a
-  // buffer whose loads are in flight would wait for every load, this one's included)
-  double yA[kLd], yB[kLd], yC[kLd];
-  uint32_t bA[kLd], bB[kLd], bC[kLd];
-  if (maxlen > 0) {
-    load(0, yA, bA);
-    load(kPsT, yB, bB);
-  }
-  for (int64_t off = 0; off < maxlen;) {
-    load(off + 2 * kPsT, yC, bC);
-    stage(off, yA, bA);
-    if ((off += kPsT) >= maxlen) break;
-    load(off + 2 * kPsT, yA, bA);
-    stage(off, yB, bB);
-    if ((off += kPsT) >= maxlen) break;
-    load(off + 2 * kPsT, yB, bB);
-    stage(off, yC, bC);
-    off += kPsT;
-  }
-  if (lane < kL && g < (int64_t)nchain * P) {
-    double2* o = (double2*)A.ppart + (size_t)g * NB;
-    for (int b = 0; b < NB; b++) o[b] = sd[(size_t)b * kL + lane];
-  }
+  const int64_t lo = lower(A.poff[q]);
+  A.prun[2 * g] = lo;
+  A.prun[2 * g + 1] = lower(A.poff[q + 1]) - lo;
 }
 
-static size_t psum_lds(int kL, int NB) {
-  return (size_t)NB * kL * sizeof(double2) + (size_t)kL * (kPsT + 1) * (sizeof(double) + 4);
+template <int R, bool kCarried>
+__global__ __launch_bounds__(256) void k_fb_psum(F64BucketArgs A, int64_t runs, int nbits) {
+  constexpr int kRu = kPwU / R;  // rounds per run per step
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t g0 = ((int64_t)blockIdx.x * 4 + wv) * R;  // the wave's first run
+  __shared__ uint32_t s_cnt[4][256], s_off[4][256];
+  constexpr int kKeys = R == 1 ? 256 : 64;  // keys at most (R = 1: up to 256 bins)
+  __shared__ uint64_t s_eq[4][kKeys + 1];     // per key: the round's lanes of that key (+ invalid)
+  // key k's entries at soff[k] + k + rank: one slot of padding per key, so the walk's lanes
+  // (reading soff[l] + l + j, ~8 entries per key apart) spread over the LDS banks
+  __shared__ double s_y[4][64 * kPwU + kKeys];
+  __shared__ uint8_t s_c[4][64 * kPwU + kKeys];
+  if (g0 >= runs) return;  // whole waves only; no block-wide barrier below
+  const int NB = A.NB;
+  const int nkey = R << nbits;  // keys (run r, bin b) = r 2^nbits + b
+  // per run (wave-uniform): its entries' bins and labels from 32-bit offsets (a run < 2^31)
+  const uint16_t* rb[R];
+  const double* ry[R];
+  const uint64_t* re[R];
+  int32_t len[R], lm1[R];
+  int32_t steps = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int64_t g = g0 + r;
+    int64_t lo = 0, n = 0, eb = 0;
+    if (g < runs) {
+      const int64_t task = g / A.P;
+      lo = A.prun[2 * g];
+      n = A.prun[2 * g + 1];
+      eb = A.tasks[task].ebase - A.tasks[task].a;
+    }
+    rb[r] = A.ebin + eb + lo;
+    ry[r] = kCarried ? A.ey_in + lo : nullptr;
+    re[r] = A.ent_in + lo;
+    len[r] = (int32_t)n;
+    lm1[r] = max((int32_t)n - 1, 0);
+    steps = max(steps, (int32_t)((n + 64 * kRu - 1) / (64 * kRu)));
+  }
+  uint32_t* scnt = s_cnt[wv];
+  uint32_t* soff = s_off[wv];
+  uint64_t* seq = s_eq[wv];
+  double* sy = s_y[wv];
+  uint8_t* sc = s_c[wv];
+  for (int b = lane; b < 256; b += 64) scnt[b] = 0u;
+  double2 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) acc[k] = make_double2(0.0, 0.0);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t me = 1ull << lane;
+  __builtin_amdgcn_wave_barrier();
+  for (int32_t st = 0; st < steps; st++) {
+    uint32_t kv[kPwU], rs[kPwU];
+    double yv[kPwU];
+    // round u: run u / kRu, its entry st 64 kRu + 64 (u % kRu) + lane (loads at clamped
+    // offsets, unconditional: one memory latency per step)
+#pragma unroll
+    for (int u = 0; u < kPwU; u++) {
+      const int r = u / kRu;
+      const int32_t i = min(st * 64 * kRu + 64 * (u % kRu) + lane, lm1[r]);
+      kv[u] = (uint32_t)rb[r][i];
+      if constexpr (kCarried)
+        yv[u] = ry[r][i];
+      else
+        yv[u] = A.y[(uint32_t)re[r][i]];
+    }
+    // ranks: the round's lanes of each key by an atomic OR of the lane bits into the key's
+    // mask (the OR's result does not depend on the lanes' order), then the lanes before this
+    // one in that mask
+#pragma unroll
+    for (int u = 0; u < kPwU; u++) {
+      const int r = u / kRu;
+      const bool valid = st * 64 * kRu + 64 * (u % kRu) + lane < len[r];
+      const uint32_t key = valid ? ((uint32_t)r << nbits | (kv[u] & 0xffu)) : (uint32_t)kKeys;
+      seq[key] = 0ull;
+      __hip_atomic_fetch_or(&seq[key], me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint64_t eq = seq[key];
+      const int rank = __popcll(eq & lt), cnt = __popcll(eq);
+      const uint32_t so = valid ? scnt[key] : 0u;
+      rs[u] = so + (uint32_t)rank;
+      if (valid && rank == cnt - 1) scnt[key] = so + (uint32_t)cnt;
+      kv[u] = valid ? (key | (kv[u] >> 8) << 16) : 0xFFFFFFFFu;  // key | count << 16; invalid
+    }
+    __builtin_amdgcn_wave_barrier();
+    // step offsets per key (exclusive scan, 4 keys per lane)
+    uint32_t c4[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c4[k] = scnt[4 * lane + k];
+      sum += c4[k];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      soff[4 * lane + k] = run + 4 * lane + k;  // (+ key: the padding)
+      run += c4[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < kPwU; u++) {
+      if (kv[u] != 0xFFFFFFFFu) {
+        const uint32_t slot = soff[kv[u] & 0xffffu] + rs[u];
+        sy[slot] = yv[u];
+        sc[slot] = (uint8_t)(kv[u] >> 16);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // lane l: keys l + 64 k, each one chain in row order; an entry's draws past the first in
+    // an exec-masked loop (every entry of a key is drawn: c >= 1)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (64 * k >= nkey) break;  // (uniform)
+      const int key = lane + 64 * k;
+      const uint32_t n = key < nkey ? scnt[key] : 0u, o = key < nkey ? soff[key] : 0u;
+      double2 v = acc[k];
+      for (uint32_t j = 0; j < n; j++) {
+        const double w = 1.0 * sy[o + j];  // instanceWeight * label
+        const double wy = w * sy[o + j];   // instanceWeight * label * label
+        const uint32_t c = sc[o + j];
+        v.x += w;
+        v.y += wy;
+        for (uint32_t d = 1; d < c; d++) {
+          v.x += w;
+          v.y += wy;
+        }
+      }
+      acc[k] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // the counts restart (after every lane's walk read them: in-order LDS operations)
+#pragma unroll
+    for (int k = 0; k < 4; k++) scnt[4 * lane + k] = 0u;
+    __builtin_amdgcn_wave_barrier();
+  }
+  // lane l's keys: run (l + 64 k) >> nbits of the wave, bin (l + 64 k) & (2^nbits - 1)
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int key = lane + 64 * k;
+    const int r = key >> nbits, b = key & ((1 << nbits) - 1);
+    if (key < nkey && b < NB && g0 + r < runs) ((double2*)A.ppart)[(size_t)(g0 + r) * NB + b] = acc[k];
+  }
 }
 
 // the partitions' partials of every (task, bin), added in partition order from 0.0 (the first
@@ -900,15 +924,8 @@ __global__ __launch_bounds__(256) void k_fb_pmerge(F64BucketArgs A, int nchain) 
   o[2] = s2;
 }
 
-// units per k_fb_psum wave: as many as 32 KB of LDS bins hold, a power of two in [8, 64] (64 at
-// NB <= 32: ~39 KB of LDS per wave with the staging, four waves per CU -- every SIMD busy with
-// every lane adding)
-static int psum_lanes(int NB) {
-  int l = 64;
-  while (l > 8 && (size_t)l * NB * 16 > 32768) l /= 2;
-  return l;
-}
-size_t fb_psum_part_bytes(int64_t nchain, int P, int NB) { return (size_t)nchain * P * NB * 2 * sizeof(double); }
+// the partials, then the run bounds (entry offset, length) k_fb_runs finds for k_fb_psum
+size_t fb_psum_part_bytes(int64_t nchain, int P, int NB) { return (size_t)nchain * P * (NB + 1) * 2 * sizeof(double); }
 
 // ---------------------------------------------------------------- label column
 // analyze_labels (sbag_host.cpp) on the device: per label, finite / integral and the
@@ -1017,23 +1034,25 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
   }
   if (nchain <= 0) return;
   if (a.psum) {  // P > 1: per-partition runs of each chain task, then the merge in partition order
-    const int kl = psum_lanes(a.NB);
-    const int64_t units = (int64_t)nchain * a.P;
-    const size_t lds = psum_lds(kl, a.NB);
-    const dim3 grid((unsigned)((units + kl - 1) / kl));
-    auto go = [&](const void* fn) {
-      void* args[] = {(void*)&a, (void*)&nchain};
-      (void)hipLaunchKernel(fn, grid, dim3(64), args, lds, st);
-    };
+    const int64_t runs = (int64_t)nchain * a.P;
+    hipLaunchKernelGGL(k_fb_runs, dim3((unsigned)((runs + 255) / 256)), dim3(256), 0, st, a, runs);
+    const int R = nbits >= 6 ? 1 : nbits == 5 ? 2 : nbits == 4 ? 4 : 8;  // runs per wave
+    const dim3 g((unsigned)((runs + 4 * R - 1) / (4 * R)));
     const bool cy = a.ey_in != nullptr;
-    if (kl == 64)
-      go(cy ? (const void*)k_fb_psum<64, true> : (const void*)k_fb_psum<64, false>);
-    else if (kl == 32)
-      go(cy ? (const void*)k_fb_psum<32, true> : (const void*)k_fb_psum<32, false>);
-    else if (kl == 16)
-      go(cy ? (const void*)k_fb_psum<16, true> : (const void*)k_fb_psum<16, false>);
+#define SBAG_PSUMW(r)                                                                  \
+  if (cy)                                                                              \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fb_psum<r, true>), g, dim3(256), 0, st, a, runs, nbits); \
+  else                                                                                 \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fb_psum<r, false>), g, dim3(256), 0, st, a, runs, nbits)
+    if (R == 1)
+      SBAG_PSUMW(1);
+    else if (R == 2)
+      SBAG_PSUMW(2);
+    else if (R == 4)
+      SBAG_PSUMW(4);
     else
-      go(cy ? (const void*)k_fb_psum<8, true> : (const void*)k_fb_psum<8, false>);
+      SBAG_PSUMW(8);
+#undef SBAG_PSUMW
     const int64_t cells = (int64_t)nchain * a.NB;
     hipLaunchKernelGGL(k_fb_pmerge, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, nchain);
     return;

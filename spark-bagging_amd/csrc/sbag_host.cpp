@@ -2085,6 +2085,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.P = P;
       ba.poff = d_poff;
       ba.ppart = d_ppart;
+      ba.prun = d_ppart ? (int64_t*)(d_ppart + (size_t)nchain * P * NB * 2) : nullptr;
       ba.hist = (const uint64_t*)hist_cur;
       ba.Fmax = Fmax;
       // (a task's 8-byte arrays or the label column past 2^31 bytes; SBAG_F64_WIDE=1 forces it)

@@ -455,6 +455,7 @@ struct F64BucketArgs {
   double* ppart;            // [chain task][P][NB][2] per-partition partials (psum): sum, sumSq
   const uint64_t* hist;     // (psum) the level's integer histograms [slot][Fmax][NB][3]: the
   int32_t Fmax, pad3;       //   draw counts per (task, bin) (count += 1.0 per draw: exact)
+  int64_t* prun;            // [chain task][P][2] the runs' first entry and length (k_fb_psum)
 };
 // bytes of k_fb_psum's per-partition partials for nchain tasks
 size_t fb_psum_part_bytes(int64_t nchain, int P, int NB);
