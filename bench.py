@@ -31,10 +31,10 @@ LDS_ATOMIC_PEAK = 256 * 2.4e9 / 7.16
 LDS_ATOMIC_PEAK_U32 = 256 * 2.4e9 / 5.97
 # committed rocprofv3 PMC summaries of this command per workload (scripts/profile.sh +
 # scripts/pmc_summary.py); the newest one present is used
-PMC_SUMMARIES = {"c3": ["profiles/r05pr/c3/summary.json", "profiles/r04bn/c3/summary.json", "profiles/r04ac/c3/summary.json", "profiles/r04o/c3/summary.json", "profiles/r03y/c3/summary.json", "profiles/r03r/c3/summary.json", "profiles/r03g/c3/summary.json", "profiles/r02g/c3/summary.json", "profiles/r02f/c3/summary.json",
+PMC_SUMMARIES = {"c3": ["profiles/r06/c3/summary.json", "profiles/r05pr/c3/summary.json", "profiles/r04bn/c3/summary.json", "profiles/r04ac/c3/summary.json", "profiles/r04o/c3/summary.json", "profiles/r03y/c3/summary.json", "profiles/r03r/c3/summary.json", "profiles/r03g/c3/summary.json", "profiles/r02g/c3/summary.json", "profiles/r02f/c3/summary.json",
                         "profiles/r02e/c3/summary.json", "profiles/r01g/summary.json"],
-                 "c4": ["profiles/r05pr/c4/summary.json", "profiles/r04o/c4/summary.json", "profiles/r02g/c4/summary.json", "profiles/r02f/c4/summary.json"],
-                 "c5": ["profiles/r05s/c5/summary.json", "profiles/r05a/c5/summary.json", "profiles/r03y/c5/summary.json", "profiles/r02g/c5/summary.json", "profiles/r02f/c5/summary.json",
+                 "c4": ["profiles/r06/c4/summary.json", "profiles/r05pr/c4/summary.json", "profiles/r04o/c4/summary.json", "profiles/r02g/c4/summary.json", "profiles/r02f/c4/summary.json"],
+                 "c5": ["profiles/r06/c5/summary.json", "profiles/r05s/c5/summary.json", "profiles/r05a/c5/summary.json", "profiles/r03y/c5/summary.json", "profiles/r02g/c5/summary.json", "profiles/r02f/c5/summary.json",
                         "profiles/r02e/c5/summary.json", "profiles/r01g_c5/summary.json"]}
 
 
