@@ -220,8 +220,8 @@ typedef struct {
   double hist_lds_atomics; /* LDS atomic wave-instructions issued by the hist launches   */
   double group_ms;         /* gini class tiles: entries regrouped by tile before the
                               histogram (k_tile_count / k_tile_scatter), not in hist_ms   */
-  double chain_ms;         /* fp64 labels: the chosen features' bins summed in Spark's row
-                              order (bucketing + routing + k_fb_chain)        */
+  double chain_ms;         /* fp64 labels: the chosen features' bins summed in Spark's order
+                              (routing + k_fb_chainx or k_fb_psum / k_fb_pmerge) */
   double root_ms;          /* root histogram as an int8 MFMA contraction (k_hist_mfma);
                               0 when the root went through k_hist_rl (then in hist_ms)     */
   double root_mfma_ops;    /* its int8 operations (2 x 32^3 per MFMA)                      */

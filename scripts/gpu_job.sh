@@ -8,6 +8,7 @@
 #     smoke                   __graft_entry__.smoke()
 #     bench                   default `python bench.py` (the driver's line)
 #     c3 | c4 | c5            bench.py --workload <w>, short (env passes through, e.g. SBAG_*)
+#     c4nd                    the C4 shard with real-valued labels (bench.py's nondyadic line)
 #     cont                    scripts/bench_continuous.py (C3 shape on continuous features)
 #     gbm                     scripts/bench_gbm.py
 #     f64probe                scripts/f64_probe.py, serialized, per-level stage times
@@ -55,6 +56,11 @@ run_step() {
       timeout -k 10 400 python3 bench.py --workload $st $extra --no-cpu-baseline --no-nondyadic --no-continuous \
         > "$OUT/bench_$st$tag.log" 2>&1
       rc=$?; [ $rc -ne 0 ] && tail -20 "$OUT/bench_$st$tag.log"; summ "$OUT/bench_$st$tag.log"; return $rc ;;
+    c4nd)
+      # the C4 shard with real-valued labels (bench.py's nondyadic line on the c4 workload)
+      timeout -k 10 500 python3 bench.py --workload c4 --steps 1 --warmup 1 --no-cpu-baseline --no-continuous \
+        --nondyadic-steps 2 > "$OUT/bench_c4nd$tag.log" 2>&1
+      rc=$?; [ $rc -ne 0 ] && tail -20 "$OUT/bench_c4nd$tag.log"; summ "$OUT/bench_c4nd$tag.log"; return $rc ;;
     nondyadic)
       timeout -k 10 400 python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-continuous --nondyadic-steps 3 \
         > "$OUT/bench_nd$tag.log" 2>&1

@@ -80,13 +80,30 @@ __global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__
   const int64_t chunk = blockIdx.x / R;
   const uint8_t* cr = counts + (int64_t)r * N;
   unsigned int s = 0, m = 0, n = 0;
-  for (int it = 0; it < kChunkRows / 256; it++) {
-    const int64_t row = chunk * kChunkRows + it * 256 + threadIdx.x;
-    if (row < N) {
-      const unsigned int c = cr[row];
-      s += c;
-      n += c ? 1u : 0u;
-      m = max(m, c);
+  const uint8_t* cc = cr + chunk * kChunkRows;
+  if ((chunk + 1) * kChunkRows <= N && (((uintptr_t)cc) & 15) == 0) {
+    // 16 counts per load: Σ by v_sad_u8, the nonzero bytes by (b & 0x7f) + 0x7f | b, the max
+    // bytewise
+    for (int k = threadIdx.x; k < kChunkRows / 16; k += 256) {
+      const uint4 v = ((const uint4*)cc)[k];
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t w = w4[q];
+        s = __builtin_amdgcn_sad_u8(w, 0u, s);
+        n += (uint32_t)__builtin_popcount((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u);
+        m = max(m, max(max(w & 0xFFu, (w >> 8) & 0xFFu), max((w >> 16) & 0xFFu, w >> 24)));
+      }
+    }
+  } else {
+    for (int it = 0; it < kChunkRows / 256; it++) {
+      const int64_t row = chunk * kChunkRows + it * 256 + threadIdx.x;
+      if (row < N) {
+        const unsigned int c = cr[row];
+        s += c;
+        n += c ? 1u : 0u;
+        m = max(m, c);
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -109,6 +126,38 @@ __global__ __launch_bounds__(256) void k_chunk_inbag(const uint8_t* __restrict__
     const unsigned int mm = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
     if (mm) atomicMax(&cmax[r], mm);
   }
+}
+
+// per (replica, 8192-row chunk): in-bag rows only (the entry capacity's pre-count on the
+// integer path), 16 counts per load: a byte is nonzero iff (b & 0x7f) + 0x7f or b has bit 7
+__global__ __launch_bounds__(256) void k_chunk_rows(const uint8_t* __restrict__ counts, int64_t N,
+                                                    int R, int64_t chunks, uint32_t* __restrict__ ncnt) {
+  const int r = blockIdx.x % R;
+  const int64_t chunk = blockIdx.x / R;
+  const uint8_t* cr = counts + (int64_t)r * N + chunk * kChunkRows;
+  const int64_t nrow = min((int64_t)kChunkRows, N - chunk * kChunkRows);
+  uint32_t n = 0;
+  auto nz = [](uint32_t w) {
+    return (uint32_t)__builtin_popcount((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u);
+  };
+  if (nrow == kChunkRows && (((uintptr_t)cr) & 15) == 0) {
+    for (int k = threadIdx.x; k < kChunkRows / 16; k += 256) {
+      const uint4 v = ((const uint4*)cr)[k];
+      n += nz(v.x) + nz(v.y) + nz(v.z) + nz(v.w);
+    }
+  } else {
+    for (int64_t k = threadIdx.x; k < nrow; k += 256) n += cr[k] ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
+  __shared__ uint32_t s_n[4];
+  if ((threadIdx.x & 63) == 0) s_n[threadIdx.x >> 6] = n;
+  block_sync();
+  if (threadIdx.x == 0) ncnt[(int64_t)r * chunks + chunk] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+}
+
+void launch_chunk_rows(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint32_t* d_ncnt) {
+  const int64_t chunks = compact_ordered_chunks(N);
+  hipLaunchKernelGGL(k_chunk_rows, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, R, chunks, d_ncnt);
 }
 
 // per replica: exclusive prefix of the chunks' entries; cursor[r] = the total

@@ -1933,13 +1933,34 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   uint64_t* ent_nxt = G.entB;
   // the entries' labels, carried beside them (the scatter reads them in order and writes
   // the children's): gathered once here from the root entries
-  // (skipped past 15 % of the device: the C4 shard's 102 GB; the scatter gathers by row then)
+  // (skipped when the two copies would not leave 5 % of the device plus 12 GB free for the
+  // level's workspaces (C4 shard: ≈10 GB, most of it the (bin, count) words) -- the scatter and k_fb_psum gather y[row] then, ~1.4x
+  // the carried path's routing + sums on C3, profiles/r06logs/r06u2/).  The copies are
+  // compact: replica r's labels at r * capc, capc its largest in-bag count (the entries
+  // keep r * cap, cap = N); the kernels shift by r * (capc - cap).  Round 5 sized them as
+  // the entries and carried only below 15 % of the device, which left the C4 shard on the
+  // gather path (real-label step 2.08 s, profiles/r06logs/r06c4/: 64 x 10^8 x 16 B)
   double *ey_cur = nullptr, *ey_nxt = nullptr;
+  int64_t capc = 0;
+  for (int r = 0; r < R; r++) capc = std::max(capc, (int64_t)G.inbag[r]);
+  capc = std::min<int64_t>(cap, (capc + 63) / 64 * 64);
   size_t dev_free = 0, dev_total = 0;
   (void)hipMemGetInfo(&dev_free, &dev_total);
-  if ((double)R * cap * 16.0 <= 0.15 * (double)dev_total && !getenv("SBAG_F64_NO_CARRY")) {
-    TRY(ws_typed(c, "f64_eyA", (size_t)R * cap, &ey_cur));
-    TRY(ws_typed(c, "f64_eyB", (size_t)R * cap, &ey_nxt));
+  // (the copies' own buffers from an earlier fit count as free; ws_get adds 1/8 slack)
+  const double ey_bytes = (double)R * capc * 16.0 * 1.125;
+  double ey_free = (double)dev_free;
+  for (const char* nm : {"f64_eyA", "f64_eyB"}) {
+    auto it = c->ws.find(nm);
+    if (it != c->ws.end()) ey_free += (double)it->second.cap;
+  }
+  const bool carry = ey_bytes + 0.05 * (double)dev_total + 12e9 <= ey_free && !getenv("SBAG_F64_NO_CARRY");
+  static const bool ey_trace = getenv("SBAG_LEVEL_TRACE") != nullptr;
+  if (ey_trace)
+    fprintf(stderr, "f64 labels %s: %d replicas x %lld entries, %.1f GB of copies, %.1f GB free\n",
+            carry ? "carried" : "gathered by row", R, (long long)capc, ey_bytes / 1e9, ey_free / 1e9);
+  if (carry) {
+    TRY(ws_typed(c, "f64_eyA", (size_t)R * capc, &ey_cur));
+    TRY(ws_typed(c, "f64_eyB", (size_t)R * capc, &ey_nxt));
     std::vector<int64_t> nent(R);
     int64_t mx = 0;
     for (int r = 0; r < R; r++) {
@@ -1950,7 +1971,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
     TRY(ws_typed(c, "f64_nent", (size_t)R, &d_nent));
     TRY(h2d(c, d_nent, nent.data(), (size_t)R));
     int h = G.tm.begin(T_COMPACT);
-    launch_entry_labels(c->stream, ent_cur, d_y64, ey_cur, cap, d_nent, R, mx);
+    launch_entry_labels(c->stream, ent_cur, d_y64, ey_cur, cap, capc, d_nent, R, mx);
     HIP_TRY(hipGetLastError());
     G.tm.end(h);
   }
@@ -2069,6 +2090,7 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.ent_out = ent_nxt;
       ba.ey_in = ey_cur;
       ba.ey_out = ey_nxt;
+      ba.eyd = capc - cap;
       ba.ebin = d_ebin;
       ba.bky = d_bky;
       ba.bkc = d_bkc;
@@ -2710,25 +2732,55 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       TRY(run_sampler(c, &fp->sampler, poff, N, d_counts));
     tm.end(h);
   }
-  // ---- 2. in-bag entry lists (two ping-pong buffers per replica, capacity N)
+  // ---- 2. in-bag entry lists: two ping-pong buffers per replica.  Capacity N, or -- on the
+  // fp64 path, and wherever the two lists pass 10 % of the device -- the largest in-bag count
+  // (+ 4096 entries of slack for the kernels' clamped read-ahead): a Poisson(1) bag holds 63 %
+  // of the rows.  Round 5 always took N, which with two learner halves' contexts left the C4
+  // shard too little HBM to carry its fp64 labels (§4.7).  The counts per (replica, 8192-row
+  // chunk) come first (k_chunk_inbag, also the ordered compaction's offsets; k_chunk_rows on
+  // the integer path), then one copy of them to the host; small fits skip that round trip
   unsigned long long* d_inbag;
   TRY(ws_typed(c, "inbag", (size_t)R * 4, &d_inbag));
   unsigned long long* d_wsum = d_inbag + R;
   unsigned int* d_cmax = (unsigned int*)(d_inbag + 2 * R);
   unsigned long long* d_sqsum = d_inbag + 3 * R;
   HIP_TRY(hipMemsetAsync(d_inbag, 0, (size_t)R * 32, c->stream));
-  const int64_t cap = N;
+  const int64_t nchunk = compact_ordered_chunks(N);
+  uint32_t* d_ncnt = nullptr;
+  int64_t cap = N;
+  size_t dev_free0 = 0, dev_total0 = 0;
+  (void)hipMemGetInfo(&dev_free0, &dev_total0);
+  static const int cap_env = getenv("SBAG_ENT_TIGHT") ? atoi(getenv("SBAG_ENT_TIGHT")) : -1;  // (A/B)
+  const bool tight = cap_env >= 0 ? cap_env != 0 : f64 || (double)R * N * 16.0 > 0.1 * (double)dev_total0;
+  if (tight) {
+    TRY(ws_typed(c, "inbag_ncnt", (size_t)R * nchunk, &d_ncnt));
+    {
+      int h = tm.begin(T_COMPACT);
+      if (f64)
+        launch_chunk_draws(c->stream, d_counts, N, R, d_ncnt, d_wsum, d_cmax);
+      else  // (launch_compact computes Σ count and max count itself)
+        launch_chunk_rows(c->stream, d_counts, N, R, d_ncnt);
+      HIP_TRY(hipGetLastError());
+      tm.end(h);
+    }
+    std::vector<uint32_t> hn((size_t)R * nchunk);
+    TRY(d2h(c, hn.data(), d_ncnt, hn.size()));
+    int64_t mx = 1;
+    for (int r = 0; r < R; r++) {
+      int64_t n = 0;
+      for (int64_t k = 0; k < nchunk; k++) n += hn[(size_t)r * nchunk + k];
+      mx = std::max(mx, n);
+    }
+    cap = std::min<int64_t>(N, (mx + 4096 + 63) / 64 * 64);
+  }
   uint64_t *entA, *entB;
   TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
   TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
   {
     int h = tm.begin(T_COMPACT);
     if (f64) {  // row order inside every replica (Spark's fp64 sums follow it)
-      uint32_t* d_ncnt;
       unsigned long long* d_cbase;
-      TRY(ws_typed(c, "f64_ncnt", (size_t)R * compact_ordered_chunks(N), &d_ncnt));
-      TRY(ws_typed(c, "f64_cbase", (size_t)R * compact_ordered_chunks(N), &d_cbase));
-      launch_chunk_draws(c->stream, d_counts, N, R, d_ncnt, d_wsum, d_cmax);
+      TRY(ws_typed(c, "f64_cbase", (size_t)R * nchunk, &d_cbase));
       launch_compact_ordered(c->stream, d_counts, lab.d_labk, N, R, entA, cap, d_ncnt, d_cbase, d_inbag);
     } else {
       launch_compact(c->stream, d_counts, N, R, lab.d_labk, entA, cap, d_inbag, d_wsum, d_cmax,

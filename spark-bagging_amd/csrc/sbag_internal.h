@@ -456,6 +456,7 @@ struct F64BucketArgs {
   const uint64_t* hist;     // (psum) the level's integer histograms [slot][Fmax][NB][3]: the
   int32_t Fmax, pad3;       //   draw counts per (task, bin) (count += 1.0 per draw: exact)
   int64_t* prun;            // [chain task][P][2] the runs' first entry and length (k_fb_psum)
+  int64_t eyd;              // replica r's carried labels: entry e at ey[e + r * eyd] (compact copies)
 };
 // bytes of k_fb_psum's per-partition partials for nchain tasks
 size_t fb_psum_part_bytes(int64_t nchain, int P, int NB);
@@ -467,7 +468,7 @@ size_t fb_psum_part_bytes(int64_t nchain, int P, int NB);
 // rint(y 2^shift) (the fp64 screen's image).
 void launch_label_stats(hipStream_t st, const double* y, int64_t N, uint64_t* acc);
 void launch_label_image(hipStream_t st, const double* y, int64_t N, int shift, bool dyadic, int32_t* k);
-void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap,
+void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap, int64_t capc,
                          const int64_t* d_nent, int R, int64_t max_nent);
 struct F64FinishNode {
   int32_t t, t0;            // task of the chosen feature; task of the first feature with
@@ -500,6 +501,8 @@ void launch_f64_screen(hipStream_t st, const F64ScreenArgs& a, int M);
 void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain);
 void launch_fb_finish(hipStream_t st, const F64FinishArgs& a);
 int64_t compact_ordered_chunks(int64_t N);
+// in-bag rows per (replica, chunk) only (the entry capacity's pre-count)
+void launch_chunk_rows(hipStream_t st, const uint8_t* counts, int64_t N, int R, uint32_t* d_ncnt);
 int f64_hist_width(int NB);
 size_t f64_hist_lds_bytes(int NB, int parts);
 void launch_f64_hist(hipStream_t st, const F64HistArgs& a, int nnodes, int ngroups);

@@ -338,8 +338,9 @@ def test_c3_full_nondyadic_engines_agree(ctx, monkeypatch):
 def test_chain_windows_many_bins_large_counts(ctx, part):
     """Spark's row-order sums with every row drawn 9 times (k_fb_chainx's several draw
     windows per stage at P = 1), maxBins 255 on features with ~1000 distinct values (up to 255
-    chains per task; at P > 1, k_fb_psum's LDS bins hold 8 lanes per wave), fp64 labels, one
-    booster -- bit-exact against the oracle."""
+    chains per task; at P > 1, k_fb_psum's one run per wave with four (run, bin) keys per lane
+    and 9 draws per entry in its draw loop), fp64 labels, one booster -- bit-exact against the
+    oracle."""
     rng = np.random.default_rng(29)
     n, f = 20_000, 6
     X = np.round(rng.normal(size=(n, f)) * 150) / 7
