@@ -801,6 +801,15 @@ static void ws_release(sbag_ctx* c) {
   c->ws.clear();
 }
 
+// frees one named workspace buffer if it holds more than `keep` bytes (the stream is drained)
+static void ws_trim(sbag_ctx* c, const std::string& name, size_t keep) {
+  auto it = c->ws.find(name);
+  if (it == c->ws.end() || it->second.cap <= keep) return;
+  (void)hipStreamSynchronize(c->stream);
+  if (it->second.p) (void)hipFree(it->second.p);
+  c->ws.erase(it);
+}
+
 int sbag_ctx_destroy(sbag_ctx* c) {
   if (!c) return SBAG_OK;
   { CTX_LOCK(c); }  // no call is in flight on it any more
@@ -2733,12 +2742,15 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     tm.end(h);
   }
   // ---- 2. in-bag entry lists: two ping-pong buffers per replica.  Capacity N, or -- on the
-  // fp64 path, and wherever the two lists pass 10 % of the device -- the largest in-bag count
+  // fp64 path, and wherever the two lists pass 40 % of the device -- the largest in-bag count
   // (+ 4096 entries of slack for the kernels' clamped read-ahead): a Poisson(1) bag holds 63 %
-  // of the rows.  Round 5 always took N, which with two learner halves' contexts left the C4
-  // shard too little HBM to carry its fp64 labels (§4.7).  The counts per (replica, 8192-row
-  // chunk) come first (k_chunk_inbag, also the ordered compaction's offsets; k_chunk_rows on
-  // the integer path), then one copy of them to the host; small fits skip that round trip
+  // of the rows.  The counts per (replica, 8192-row chunk) come first (k_chunk_inbag, also the
+  // ordered compaction's offsets; k_chunk_rows on the integer path), then one copy of them to
+  // the host.  The fp64 path also trims lists an earlier integer fit left at capacity N, so
+  // that its carried labels fit (§4.7: round 5 took N everywhere, and the C4 shard's
+  // real-label fit gathered its labels by row, 2.05 s).  The integer path keeps N below 40 %:
+  // the host round trip before the compaction cost the C4 shard step 1062 -> 1088 ms
+  // (profiles/r06logs/r06cap3/, SBAG_ENT_TIGHT=0/1)
   unsigned long long* d_inbag;
   TRY(ws_typed(c, "inbag", (size_t)R * 4, &d_inbag));
   unsigned long long* d_wsum = d_inbag + R;
@@ -2751,7 +2763,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   size_t dev_free0 = 0, dev_total0 = 0;
   (void)hipMemGetInfo(&dev_free0, &dev_total0);
   static const int cap_env = getenv("SBAG_ENT_TIGHT") ? atoi(getenv("SBAG_ENT_TIGHT")) : -1;  // (A/B)
-  const bool tight = cap_env >= 0 ? cap_env != 0 : f64 || (double)R * N * 16.0 > 0.1 * (double)dev_total0;
+  const bool tight = cap_env >= 0 ? cap_env != 0 : f64 || (double)R * N * 16.0 > 0.4 * (double)dev_total0;
   if (tight) {
     TRY(ws_typed(c, "inbag_ncnt", (size_t)R * nchunk, &d_ncnt));
     {
@@ -2772,6 +2784,11 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       mx = std::max(mx, n);
     }
     cap = std::min<int64_t>(N, (mx + 4096 + 63) / 64 * 64);
+    if (f64) {  // (ws_get's 1/8 slack, and a quarter more before a list is worth trimming)
+      const size_t need = (size_t)R * cap * sizeof(uint64_t);
+      ws_trim(c, "entA", need + need / 8 + need / 4);
+      ws_trim(c, "entB", need + need / 8 + need / 4);
+    }
   }
   uint64_t *entA, *entB;
   TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
