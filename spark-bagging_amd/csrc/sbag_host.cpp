@@ -1955,13 +1955,12 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   capc = std::min<int64_t>(cap, (capc + 63) / 64 * 64);
   size_t dev_free = 0, dev_total = 0;
   (void)hipMemGetInfo(&dev_free, &dev_total);
-  // (the copies' own buffers from an earlier fit count as free; ws_get adds 1/8 slack)
+  // (the copies' and the level workspaces' own buffers from an earlier fit count as free:
+  // the margin below is for the latter; ws_get adds 1/8 slack)
   const double ey_bytes = (double)R * capc * 16.0 * 1.125;
   double ey_free = (double)dev_free;
-  for (const char* nm : {"f64_eyA", "f64_eyB"}) {
-    auto it = c->ws.find(nm);
-    if (it != c->ws.end()) ey_free += (double)it->second.cap;
-  }
+  for (const auto& kv : c->ws)
+    if (kv.first.rfind("f64_ey", 0) == 0 || kv.first.rfind("fb_", 0) == 0) ey_free += (double)kv.second.cap;
   const bool carry = ey_bytes + 0.05 * (double)dev_total + 12e9 <= ey_free && !getenv("SBAG_F64_NO_CARRY");
   static const bool ey_trace = getenv("SBAG_LEVEL_TRACE") != nullptr;
   if (ey_trace)
