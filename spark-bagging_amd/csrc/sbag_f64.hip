@@ -183,12 +183,15 @@ __global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restri
                                                          const int32_t* __restrict__ labk, int64_t N,
                                                          int R, int64_t chunks,
                                                          const unsigned long long* __restrict__ base,
-                                                         uint64_t* __restrict__ ent, int64_t cap) {
+                                                         uint64_t* __restrict__ ent, int64_t cap,
+                                                         const double* __restrict__ y,
+                                                         double* __restrict__ ey) {
   __shared__ int s_wave[4];
   const int r = blockIdx.x % R;
   const int64_t chunk = blockIdx.x / R;
   const uint8_t* cr = counts + (int64_t)r * N;
   uint64_t* er = ent + (int64_t)r * cap;
+  double* eyr = ey ? ey + (int64_t)r * cap : nullptr;  // (the carried fp64 labels, same positions)
   unsigned long long pos0 = base[(int64_t)r * chunks + chunk];
   for (int it = 0; it < kChunkRows / 1024; it++) {
     const int64_t row0 = chunk * kChunkRows + (int64_t)it * 1024 + (int64_t)threadIdx.x * 4;
@@ -204,7 +207,10 @@ __global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restri
     unsigned long long pos = pos0 + (unsigned long long)ex;
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if (c[j]) er[pos++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
+      if (c[j]) {
+        if (eyr) eyr[pos] = y[row0 + j];
+        er[pos++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
+      }
     pos0 += (unsigned long long)tot;
   }
 }
@@ -218,11 +224,12 @@ void launch_chunk_draws(hipStream_t st, const uint8_t* counts, int64_t N, int R,
 
 void launch_compact_ordered(hipStream_t st, const uint8_t* counts, const int32_t* labk, int64_t N,
                             int R, uint64_t* ent, int64_t cap, const uint32_t* d_ncnt,
-                            unsigned long long* d_base, unsigned long long* d_cursor) {
+                            unsigned long long* d_base, unsigned long long* d_cursor, const double* y,
+                            double* ey) {
   const int64_t chunks = compact_ordered_chunks(N);
   hipLaunchKernelGGL(k_chunk_scan, dim3(R), dim3(256), 0, st, d_ncnt, chunks, d_base, d_cursor);
   hipLaunchKernelGGL(k_compact_ordered, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, labk,
-                     N, R, chunks, d_base, ent, cap);
+                     N, R, chunks, d_base, ent, cap, y, ey);
 }
 
 int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunkRows; }

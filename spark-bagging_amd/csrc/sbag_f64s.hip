@@ -386,11 +386,10 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
   // the entries' labels: carried in entry order (coalesced; and the children's written),
   // or, without the carried copy (ey_in null: too big), gathered by row
   const bool carried = A.ey_in != nullptr;
-  const int64_t eyd = (int64_t)t.r * A.eyd;  // (the replica's compact label copies)
   const __amdgpu_buffer_rsrc_t ry =
-      carried ? rsrc_of(A.ey_in + eyd + t.a, (uint64_t)(t.b - t.a) * 8) : rsrc_of(A.y, 0xFFFFFFFFull);
+      carried ? rsrc_of(A.ey_in + t.a, (uint64_t)(t.b - t.a) * 8) : rsrc_of(A.y, 0xFFFFFFFFull);
   const __amdgpu_buffer_rsrc_t roy =
-      rsrc_of(carried ? A.ey_out + eyd + t.a : A.ey_out, carried && t.part ? (uint64_t)(t.b - t.a) * 8 : 0);
+      rsrc_of(carried ? A.ey_out + t.a : A.ey_out, carried && t.part ? (uint64_t)(t.b - t.a) * 8 : 0);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t last = pc.b - 1;
   // kScU rounds of 64 entries per step: all their entry loads, then all their bin and label
@@ -408,7 +407,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
     for (int u = 0; u < kScU; u++) {
       bv[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(re, (int)(uint32_t)(2 * (min(i0 + 64 * u + lane, last) - t.a)), 0, 0) & 0xffu;
       if constexpr (kWide) {
-        const double* yp = carried ? A.ey_in + eyd + min(i0 + 64 * u + lane, last) : A.y + (uint32_t)ev[u];
+        const double* yp = carried ? A.ey_in + min(i0 + 64 * u + lane, last) : A.y + (uint32_t)ev[u];
         yv[u] = *(const v2u32*)yp;
       } else {
         const int yoff = carried ? (int)(min(i0 + 64 * u + lane, last) - t.a) * 8 : (int)((uint32_t)ev[u] * 8u);
@@ -442,7 +441,7 @@ __global__ __launch_bounds__(256) void k_fb_scatter(F64BucketArgs A, int64_t npi
       if constexpr (kWide) {
         if (valid && t.part) {
           A.ent_out[t.a + pos] = e;
-          if (carried) *(v2u32*)(A.ey_out + eyd + t.a + pos) = yv[u];
+          if (carried) *(v2u32*)(A.ey_out + t.a + pos) = yv[u];
         }
       } else {
         rstore64(ro, valid ? (uint32_t)pos * 8u : 0xFFFFFFF0u, e);
@@ -769,16 +768,15 @@ __global__ __launch_bounds__(256) void k_fb_psum(F64BucketArgs A, int64_t runs, 
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const int64_t g = g0 + r;
-    int64_t lo = 0, n = 0, eb = 0, eyd = 0;
+    int64_t lo = 0, n = 0, eb = 0;
     if (g < runs) {
       const int64_t task = g / A.P;
       lo = A.prun[2 * g];
       n = A.prun[2 * g + 1];
       eb = A.tasks[task].ebase - A.tasks[task].a;
-      eyd = (int64_t)A.tasks[task].r * A.eyd;
     }
     rb[r] = A.ebin + eb + lo;
-    ry[r] = kCarried ? A.ey_in + eyd + lo : nullptr;
+    ry[r] = kCarried ? A.ey_in + lo : nullptr;
     re[r] = A.ent_in + lo;
     len[r] = (int32_t)n;
     lm1[r] = max((int32_t)n - 1, 0);
@@ -1001,25 +999,6 @@ void launch_label_image(hipStream_t st, const double* y, int64_t N, int shift, b
   hipLaunchKernelGGL(k_label_image, dim3(bx), dim3(256), 0, st, y, N, shift, dyadic ? 1 : 0, k);
 }
 
-// the labels of the root entries, in entry order: what the scatter reads (and carries to
-// the children) instead of gathering y[row] per entry at every level
-__global__ __launch_bounds__(256) void k_entry_labels(const uint64_t* __restrict__ ent,
-                                                      const double* __restrict__ y,
-                                                      double* __restrict__ ey, int64_t cap, int64_t capc,
-                                                      const int64_t* __restrict__ nent) {
-  const int r = blockIdx.y;
-  const int64_t n = nent[r];
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    ey[r * capc + i] = y[(uint32_t)ent[r * cap + i]];
-}
-
-void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap, int64_t capc,
-                         const int64_t* d_nent, int R, int64_t max_nent) {
-  if (R <= 0 || max_nent <= 0) return;
-  const unsigned bx = (unsigned)std::min<int64_t>((max_nent + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_entry_labels, dim3(bx, (unsigned)R), dim3(256), 0, st, ent, y, ey, cap, capc, d_nent);
-}
-
 void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain) {
   int nbits = 0;
   while ((1 << nbits) < a.NB) nbits++;
@@ -1027,7 +1006,7 @@ void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, in
     hipLaunchKernelGGL(k_fb_count, dim3((unsigned)npieces), dim3(256), 0, st, a);
   if (a.ntasks > 0)  // (tasks without pieces still get their bucket bounds)
     hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)a.ntasks), dim3(256), 0, st, a);
-  if (npieces > 0) {
+  if (npieces > 0 && (a.route || !a.psum)) {
     const dim3 g((unsigned)((npieces + 3) / 4));
     if (a.wide)
       hipLaunchKernelGGL(k_fb_scatter<true>, g, dim3(256), 0, st, a, npieces, nbits);

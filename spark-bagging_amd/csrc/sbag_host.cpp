@@ -1870,34 +1870,41 @@ struct F64sGrow {
   // SURVEY §8d work bytes of a level's node segments
   std::function<void(const std::vector<std::pair<int64_t, int64_t>>&, const std::vector<int>&)> add_work;
   const std::vector<int64_t>& poff;  // [P + 1] the partitions' row offsets (one: {0, N})
+  double* d_y64;                     // the fp64 labels [N + 1]
+  double* eyA;                       // the entries' labels carried beside entA (null: gathered by
+  double* eyB;                       //   row), written by the ordered compaction
   int64_t fallbacks = 0;
   int levels = 0;
 };
+
+// the fp64 labels on the device, once per label set, published only when complete (+ one
+// +0.0 at index N: the label of k_f64_hist's padding entries)
+static int f64_device_labels(sbag_dataset* ds, const LabelSet& lab, int64_t N, double** out) {
+  if (&lab != &ds->lab) {  // a booster's residuals: uploaded by sbag_fit_booster
+    if (!lab.d_y64) return fail(SBAG_EDEVICE, "internal: booster labels not on the device");
+    *out = lab.d_y64;
+    return SBAG_OK;
+  }
+  std::lock_guard<std::mutex> lk(ds->layout_mu);
+  if (!ds->lab.d_y64) {
+    double* p = nullptr;
+    HIP_TRY(hipMalloc(&p, (size_t)(N + 1) * 8));
+    if (hipMemcpy(p, ds->lab.y.data(), (size_t)N * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(p + N, 0, 8) != hipSuccess) {
+      (void)hipFree(p);
+      return fail(SBAG_EDEVICE, "labels could not be copied to the device");
+    }
+    ds->lab.d_y64 = p;
+  }
+  *out = ds->lab.d_y64;
+  return SBAG_OK;
+}
 
 static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   sbag_ctx* c = G.c;
   const int R = G.R, Fmax = G.Fmax, NB = G.NB, D = G.tp.max_depth;
   const int64_t cap = G.cap;
-  // the labels on the device, once per label set, published only when complete (+ one
-  // +0.0 at index N: the label of k_f64_hist's padding entries)
-  double* d_y64 = nullptr;
-  if (&G.lab != &G.ds->lab) {  // a booster's residuals: uploaded by sbag_fit_booster
-    d_y64 = G.lab.d_y64;
-    if (!d_y64) return fail(SBAG_EDEVICE, "internal: booster labels not on the device");
-  } else {
-    std::lock_guard<std::mutex> lk(G.ds->layout_mu);
-    if (!G.ds->lab.d_y64) {
-      double* p = nullptr;
-      HIP_TRY(hipMalloc(&p, (size_t)(G.N + 1) * 8));
-      if (hipMemcpy(p, G.ds->lab.y.data(), (size_t)G.N * 8, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemset(p + G.N, 0, 8) != hipSuccess) {
-        (void)hipFree(p);
-        return fail(SBAG_EDEVICE, "labels could not be copied to the device");
-      }
-      G.ds->lab.d_y64 = p;
-    }
-    d_y64 = G.ds->lab.d_y64;
-  }
+  double* d_y64 = G.d_y64;
   // the partitions (RandomForest.findBestSplits aggregates each one apart, §4.7)
   const int P = (int)G.poff.size() - 1;
   int64_t* d_poff = nullptr;
@@ -1941,48 +1948,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
   uint64_t* ent_cur = G.entA;
   uint64_t* ent_nxt = G.entB;
   // the entries' labels, carried beside them (the scatter reads them in order and writes
-  // the children's): gathered once here from the root entries
-  // (skipped when the two copies would not leave 5 % of the device plus 12 GB free for the
-  // level's workspaces (C4 shard: ≈10 GB, most of it the (bin, count) words) -- the scatter and k_fb_psum gather y[row] then, ~1.4x
-  // the carried path's routing + sums on C3, profiles/r06logs/r06u2/).  The copies are
-  // compact: replica r's labels at r * capc, capc its largest in-bag count (the entries
-  // keep r * cap, cap = N); the kernels shift by r * (capc - cap).  Round 5 sized them as
-  // the entries and carried only below 15 % of the device, which left the C4 shard on the
-  // gather path (real-label step 2.08 s, profiles/r06logs/r06c4/: 64 x 10^8 x 16 B)
-  double *ey_cur = nullptr, *ey_nxt = nullptr;
-  int64_t capc = 0;
-  for (int r = 0; r < R; r++) capc = std::max(capc, (int64_t)G.inbag[r]);
-  capc = std::min<int64_t>(cap, (capc + 63) / 64 * 64);
-  size_t dev_free = 0, dev_total = 0;
-  (void)hipMemGetInfo(&dev_free, &dev_total);
-  // (the copies' and the level workspaces' own buffers from an earlier fit count as free:
-  // the margin below is for the latter; ws_get adds 1/8 slack)
-  const double ey_bytes = (double)R * capc * 16.0 * 1.125;
-  double ey_free = (double)dev_free;
-  for (const auto& kv : c->ws)
-    if (kv.first.rfind("f64_ey", 0) == 0 || kv.first.rfind("fb_", 0) == 0) ey_free += (double)kv.second.cap;
-  const bool carry = ey_bytes + 0.05 * (double)dev_total + 12e9 <= ey_free && !getenv("SBAG_F64_NO_CARRY");
-  static const bool ey_trace = getenv("SBAG_LEVEL_TRACE") != nullptr;
-  if (ey_trace)
-    fprintf(stderr, "f64 labels %s: %d replicas x %lld entries, %.1f GB of copies, %.1f GB free\n",
-            carry ? "carried" : "gathered by row", R, (long long)capc, ey_bytes / 1e9, ey_free / 1e9);
-  if (carry) {
-    TRY(ws_typed(c, "f64_eyA", (size_t)R * capc, &ey_cur));
-    TRY(ws_typed(c, "f64_eyB", (size_t)R * capc, &ey_nxt));
-    std::vector<int64_t> nent(R);
-    int64_t mx = 0;
-    for (int r = 0; r < R; r++) {
-      nent[r] = (int64_t)G.inbag[r];
-      mx = std::max(mx, nent[r]);
-    }
-    int64_t* d_nent;
-    TRY(ws_typed(c, "f64_nent", (size_t)R, &d_nent));
-    TRY(h2d(c, d_nent, nent.data(), (size_t)R));
-    int h = G.tm.begin(T_COMPACT);
-    launch_entry_labels(c->stream, ent_cur, d_y64, ey_cur, cap, capc, d_nent, R, mx);
-    HIP_TRY(hipGetLastError());
-    G.tm.end(h);
-  }
+  // the children's; fit_range_impl decides, and the ordered compaction writes the first copy)
+  double *ey_cur = G.eyA, *ey_nxt = G.eyB;
   const size_t node_words = (size_t)(Fmax + 1) * NB * 3;
   for (int level = 0; level <= D && !cur.empty(); level++) {
     G.levels++;
@@ -2098,7 +2065,6 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
       ba.ent_out = ent_nxt;
       ba.ey_in = ey_cur;
       ba.ey_out = ey_nxt;
-      ba.eyd = capc - cap;
       ba.ebin = d_ebin;
       ba.bky = d_bky;
       ba.bkc = d_bkc;
@@ -2154,6 +2120,8 @@ static int grow_f64s(F64sGrow& G, std::vector<std::vector<BtNode>>& trees) {
           ba.porder = d_ord;
         }
       }
+      ba.route = 0;
+      for (const F64Task& t : tk) ba.route |= t.part;
       launch_fb_route(c->stream, ba, np, nchain);
       HIP_TRY(hipGetLastError());
       if (nleft_out) {
@@ -2789,6 +2757,34 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       ws_trim(c, "entB", need + need / 8 + need / 4);
     }
   }
+  // fp64 path: the entries' labels carried beside them (k_fb_scatter reads them in entry
+  // order and writes the children's; the ordered compaction writes the root copy), when the
+  // two copies leave 5 % of the device plus 12 GB free for the level's buffers (C4 shard:
+  // ≈10 GB, most of it the (bin, count) words) -- else the scatter and k_fb_psum gather
+  // y[row], ~1.4x the carried path's routing + sums on C3 (profiles/r06logs/r06u2/).  Round 5
+  // sized the copies as N-entry lists and carried only below 15 % of the device, which left
+  // the C4 shard on the gather path (real-label step 2.08 s, profiles/r06logs/r06c4/)
+  double *d_y64 = nullptr, *eyA = nullptr, *eyB = nullptr;
+  if (f64) {
+    TRY(f64_device_labels(ds, lab, N, &d_y64));
+    size_t dev_free = 0, dev_total = 0;
+    (void)hipMemGetInfo(&dev_free, &dev_total);
+    // (the copies' and the level buffers' own memory from an earlier fit counts as free:
+    // the margin is for the latter; ws_get adds 1/8 slack)
+    const double ey_bytes = (double)R * cap * 16.0 * 1.125;
+    double ey_free = (double)dev_free;
+    for (const auto& kv : c->ws)
+      if (kv.first.rfind("f64_ey", 0) == 0 || kv.first.rfind("fb_", 0) == 0) ey_free += (double)kv.second.cap;
+    const bool carry = ey_bytes + 0.05 * (double)dev_total + 12e9 <= ey_free && !getenv("SBAG_F64_NO_CARRY");
+    static const bool ey_trace = getenv("SBAG_LEVEL_TRACE") != nullptr;
+    if (ey_trace)
+      fprintf(stderr, "f64 labels %s: %d replicas x %lld entries, %.1f GB of copies, %.1f GB free\n",
+              carry ? "carried" : "gathered by row", R, (long long)cap, ey_bytes / 1e9, ey_free / 1e9);
+    if (carry) {
+      TRY(ws_typed(c, "f64_eyA", (size_t)R * cap, &eyA));
+      TRY(ws_typed(c, "f64_eyB", (size_t)R * cap, &eyB));
+    }
+  }
   uint64_t *entA, *entB;
   TRY(ws_typed(c, "entA", (size_t)R * cap, &entA));
   TRY(ws_typed(c, "entB", (size_t)R * cap, &entB));
@@ -2797,7 +2793,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     if (f64) {  // row order inside every replica (Spark's fp64 sums follow it)
       unsigned long long* d_cbase;
       TRY(ws_typed(c, "f64_cbase", (size_t)R * nchunk, &d_cbase));
-      launch_compact_ordered(c->stream, d_counts, lab.d_labk, N, R, entA, cap, d_ncnt, d_cbase, d_inbag);
+      launch_compact_ordered(c->stream, d_counts, lab.d_labk, N, R, entA, cap, d_ncnt, d_cbase, d_inbag, d_y64, eyA);
     } else {
       launch_compact(c->stream, d_counts, N, R, lab.d_labk, entA, cap, d_inbag, d_wsum, d_cmax,
                      d_sqsum);
@@ -3951,7 +3947,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
                  ha.hist = hist;
                  return launch(g, kHistVar, T_HIST, segs, par);
                },
-               add_work, poff};
+               add_work, poff, d_y64, eyA, eyB};
     std::vector<std::vector<BtNode>> ftrees;
     TRY(grow_f64s(G, ftrees));
     HIP_TRY(hipEventRecord(ev_stop, c->stream));

@@ -382,7 +382,8 @@ void launch_chunk_draws(hipStream_t st, const uint8_t* counts, int64_t N, int R,
                         unsigned int* d_cmax);
 void launch_compact_ordered(hipStream_t st, const uint8_t* counts, const int32_t* labk, int64_t N,
                             int R, uint64_t* ent, int64_t cap, const uint32_t* d_ncnt,
-                            unsigned long long* d_base /*[R][chunks]*/, unsigned long long* d_cursor);
+                            unsigned long long* d_base /*[R][chunks]*/, unsigned long long* d_cursor,
+                            const double* y, double* ey /* null, or the carried fp64 labels [R][cap] */);
 
 // ---- screened fp64 engine (sbag_f64s.hip): the split of a node is chosen from the integer
 // histograms of the labels' fixed-point image with a rigorous bound on Spark's fp64 gain
@@ -456,11 +457,11 @@ struct F64BucketArgs {
   const uint64_t* hist;     // (psum) the level's integer histograms [slot][Fmax][NB][3]: the
   int32_t Fmax, pad3;       //   draw counts per (task, bin) (count += 1.0 per draw: exact)
   int64_t* prun;            // [chain task][P][2] the runs' first entry and length (k_fb_psum)
-  int64_t eyd;              // replica r's carried labels: entry e at ey[e + r * eyd] (compact copies)
+  int32_t route, pad4;      // some task routes its entries to children (else, at P > 1, no
+                            // k_fb_scatter: it only routes there -- the last split level)
 };
 // bytes of k_fb_psum's per-partition partials for nchain tasks
 size_t fb_psum_part_bytes(int64_t nchain, int P, int NB);
-// ey[r cap + i] = y[row of ent[r cap + i]] for i < nent[r]
 // A label column's analysis on the device (sbag_fit_booster's residuals): acc[6] =
 // {not finite, not integral, largest scale s making a label integral, order key of the
 // smallest and of the largest label, bits of the largest |y|}; acc must hold the
@@ -468,8 +469,6 @@ size_t fb_psum_part_bytes(int64_t nchain, int P, int NB);
 // rint(y 2^shift) (the fp64 screen's image).
 void launch_label_stats(hipStream_t st, const double* y, int64_t N, uint64_t* acc);
 void launch_label_image(hipStream_t st, const double* y, int64_t N, int shift, bool dyadic, int32_t* k);
-void launch_entry_labels(hipStream_t st, const uint64_t* ent, const double* y, double* ey, int64_t cap, int64_t capc,
-                         const int64_t* d_nent, int R, int64_t max_nent);
 struct F64FinishNode {
   int32_t t, t0;            // task of the chosen feature; task of the first feature with
                             // splits (root: the parent stats), -1 when not needed
