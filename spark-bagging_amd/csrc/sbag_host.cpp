@@ -3269,11 +3269,24 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       for (int fl = 0; fl < h_Fr[r] && mfma_root; fl++)
         if (h_pos_codes[(size_t)r * Fmax + fl] != fl) mfma_root = false;
     }
-    // 7-bit digit planes of k + K0 (< 2^24: at most 4).  The root needs no squares plane
+    // digit planes of the label image: 7-bit digits of k + K0 >= 0, or -- when fewer -- the
+    // balanced base-256 digits (int8, [-128, 127]) of k - its range's midpoint (round 6: a
+    // non-dyadic label's 23-bit image takes 3 planes instead of 4; |count x digit| <=
+    // 127 x 128 keeps a 65536-row int32 sum exact).  The root needs no squares plane
     // (words [.][2]): the screen decides from (count, Σck), and the exact path's Σck² comes
     // from k_compact / k_partition reductions and kHistSq launches
     int nd1 = 1;
     while (nd1 < 10 && ((uint64_t)(lkmax - lkmin) >> (7 * nd1)) != 0) nd1++;
+    const int64_t kmid = lkmin + (lkmax - lkmin) / 2;
+    int nds = 1;  // balanced base-256 digits of k - kmid: n of them cover [-128 m, 127 m], m = (256^n - 1) / 255
+    for (; nds < 8; nds++) {
+      const int64_t m = (((int64_t)1 << (8 * nds)) - 1) / 255;
+      if (lkmin - kmid >= -128 * m && lkmax - kmid <= 127 * m) break;
+    }
+    const int dig_env = getenv("SBAG_MFMA_DIGITS") ? atoi(getenv("SBAG_MFMA_DIGITS")) : 0;  // 7 / 8: force (tests)
+    const bool signed_digits = dig_env == 8 || (dig_env != 7 && nds < nd1);
+    if (signed_digits) nd1 = nds;
+    const int64_t dK0 = signed_digits ? -kmid : K0;  // the digits are of k + dK0
     const int nd2 = 0;
     if (nd1 + nd2 > 6) mfma_root = false;
     if (mfma_root) {
@@ -3281,7 +3294,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       uint8_t* d_dig;
       TRY(ws_typed(c, "mfma_digits", (size_t)(nd1 + nd2) * N, &d_dig));
       int h = tm.begin(T_ROOT);
-      launch_label_digits(c->stream, lab.d_labk, N, (int32_t)K0, nd1, nd2, d_dig);
+      launch_label_digits(c->stream, lab.d_labk, N, (int32_t)dK0, nd1, nd2, d_dig, signed_digits);
       MfmaHistArgs ma{};
       ma.counts = d_counts;
       ma.cols = ds->d_cols;
@@ -3294,7 +3307,8 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       ma.NB = ncmax;
       ma.ND1 = nd1;
       ma.ND = nd1 + nd2;
-      ma.K0 = (int32_t)K0;
+      ma.K0 = (int32_t)dK0;
+      ma.dbits = signed_digits ? 8 : 7;
       ma.hist = (unsigned long long*)hist_cur;
       if (!launch_hist_mfma(c->stream, ma)) return fail(SBAG_EDEVICE, "internal: MFMA root histogram geometry");
       HIP_TRY(hipGetLastError());

@@ -492,10 +492,12 @@ struct MfmaHistArgs {
   int64_t N, npad;
   int32_t R, F, Fmax, NB, ND1, ND, K0;
   unsigned long long* hist;  // [R][Fmax][NB][3] words: += count, += sum c k, (ND > ND1) += sum c k^2
+  int32_t dbits, pad;        // the k planes' digit base: 7 (unsigned digits of k + K0) or 8
+                             // (balanced int8 digits of k + K0)
 };
 bool launch_hist_mfma(hipStream_t st, const MfmaHistArgs& a);
 void launch_label_digits(hipStream_t st, const int32_t* labk, int64_t N, int32_t K0, int nd1, int nd2,
-                         uint8_t* digits);
+                         uint8_t* digits, bool balanced);
 void launch_f64_screen(hipStream_t st, const F64ScreenArgs& a, int M);
 void launch_fb_route(hipStream_t st, const F64BucketArgs& a, int64_t npieces, int nchain);
 void launch_fb_finish(hipStream_t st, const F64FinishArgs& a);

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kMfWaves * 64, 1) void k_hist_mfma(MfmaHistArgs A) 
       for (int j = 0; j < ND; j++) {
         const int64_t v = acc[m][1 + j][reg];
         if (j < A.ND1)
-          sk += v << (7 * j);
+          sk += v * ((int64_t)1 << (A.dbits * j));  // (v may be negative: balanced digits)
         else
           sq += v << (7 * (j - A.ND1));
       }
@@ -251,24 +251,36 @@ bool launch_hist_mfma(hipStream_t st, const MfmaHistArgs& a) {
   return true;
 }
 
-// the 7-bit digits of k' = k + K0 >= 0, plane j = (k' >> 7j) & 127 (j < nd1), then those of
-// k^2, plane nd1 + j = (k^2 >> 7j) & 127 (j < nd2)
+// the digits of k' = k + K0: unsigned 7-bit, plane j = (k' >> 7j) & 127 (k' >= 0), or
+// balanced base 256 (int8 digits d_j in [-128, 127], k' = Σ d_j 256^j: each digit the low
+// byte read as signed, the rest carried up); then those of k^2, plane nd1 + j =
+// (k^2 >> 7j) & 127 (j < nd2)
 __global__ __launch_bounds__(256) void k_label_digits(const int32_t* __restrict__ labk, int64_t N,
-                                                      int32_t K0, int nd1, int nd2,
+                                                      int32_t K0, int nd1, int nd2, int balanced,
                                                       uint8_t* __restrict__ digits) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256) {
     const int64_t k = labk[i];
     const uint64_t kp = (uint64_t)(k + K0), k2 = (uint64_t)((int64_t)k * k);
-    for (int j = 0; j < nd1; j++) digits[(int64_t)j * N + i] = (uint8_t)((kp >> (7 * j)) & 127u);
+    if (balanced) {
+      int64_t v = k + K0;
+      for (int j = 0; j < nd1; j++) {
+        const int64_t d = (int64_t)(int8_t)(uint8_t)(v & 0xFF);
+        digits[(int64_t)j * N + i] = (uint8_t)d;
+        v = (v - d) / 256;  // (exact)
+      }
+    } else {
+      for (int j = 0; j < nd1; j++) digits[(int64_t)j * N + i] = (uint8_t)((kp >> (7 * j)) & 127u);
+    }
     for (int j = 0; j < nd2; j++) digits[(int64_t)(nd1 + j) * N + i] = (uint8_t)((k2 >> (7 * j)) & 127u);
   }
 }
 
 void launch_label_digits(hipStream_t st, const int32_t* labk, int64_t N, int32_t K0, int nd1, int nd2,
-                         uint8_t* digits) {
+                         uint8_t* digits, bool balanced) {
   if (nd1 + nd2 <= 0 || N <= 0) return;
   const int blocks = (int)std::min<int64_t>((N + 255) / 256, 256 * 8);
-  hipLaunchKernelGGL(k_label_digits, dim3(blocks), dim3(256), 0, st, labk, N, K0, nd1, nd2, digits);
+  hipLaunchKernelGGL(k_label_digits, dim3(blocks), dim3(256), 0, st, labk, N, K0, nd1, nd2, balanced ? 1 : 0,
+                     digits);
 }
 
 }  // namespace sbag

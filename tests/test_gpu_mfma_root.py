@@ -51,12 +51,18 @@ def _fit(ctx, X, y, L, depth, monkeypatch, mfma):
     return f
 
 
+@pytest.mark.parametrize("digits", ["auto", "7"])
 @pytest.mark.parametrize("label", ["dyadic", "f64", "wide"])
 @pytest.mark.parametrize("N,F,L", [(135_184, 13, 3), (70_000, 9, 40), (200_016, 21, 70)])
-def test_mfma_root_equals_lds_root(ctx, monkeypatch, label, N, F, L):
+def test_mfma_root_equals_lds_root(ctx, monkeypatch, label, N, F, L, digits):
     """Trees byte-identical with the MFMA root and with k_hist_rl's: row counts across
     65536-row slices and ragged 256-row chunks, 8-feature groups with idle waves, one to
-    three 32-replica tiles and replica groups split over launches."""
+    three 32-replica tiles and replica groups split over launches -- with the label image's
+    digit planes as the host picks them (balanced int8 base-256 digits of k - midpoint
+    whenever they need fewer planes: every case here) and forced to unsigned 7-bit digits
+    (SBAG_MFMA_DIGITS=7)."""
+    if digits == "7":
+        monkeypatch.setenv("SBAG_MFMA_DIGITS", "7")
     X, y = _data(N, F, label, N + F)
     a = _fit(ctx, X, y, L, 6, monkeypatch, True)
     b = _fit(ctx, X, y, L, 6, monkeypatch, False)
