@@ -116,7 +116,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-nondyadic", action="store_true",
                     help="skip the extra timing of the same fit on real-valued (non-dyadic) labels")
-    ap.add_argument("--nondyadic-steps", type=int, default=2)
+    ap.add_argument("--nondyadic-steps", type=int, default=3)
     ap.add_argument("--no-continuous", action="store_true",
                     help="skip the extra timing of the C3 shape on continuous features")
     ap.add_argument("--continuous-steps", type=int, default=3)
