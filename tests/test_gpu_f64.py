@@ -417,3 +417,42 @@ def test_fp64_engine_refuses_past_the_row_limit(ctx, monkeypatch):
                     learner_end=1, max_depth=1, max_bins=8, impurity=nat.IMPURITY_VARIANCE)
     finally:
         ds.free()
+
+
+def test_fp64_fit_after_integer_fit_on_one_context():
+    """Round 6 sizes the fp64 path's entry lists by the largest in-bag count and trims the
+    N-entry lists an earlier integer fit left in the context's workspace (so the carried
+    labels fit on the C4 shard).  An integer fit, then a real-label fit on the same context,
+    must give the real-label fit of a fresh context byte for byte (and so must the integer
+    fit run again afterwards, on lists the fp64 fit re-sized)."""
+    N, F, L = 100_000, 8, 6
+    part = [0, 30_000, 30_000, 64_000, N]
+
+    def fit(c, labels):
+        ds = nat.DeviceDataset.synthetic(N, F, seed=11, ctx=c)
+        try:
+            if labels == "real":
+                ds.set_labels(ds.labels() * 1.1 + 0.3)
+            return nat.fit(c, ds, replacement=True, sample_ratio=1.0, seed=SEED_REG, learner_begin=0,
+                           learner_end=L, partition_offsets=part, max_depth=7, max_bins=32,
+                           impurity=nat.IMPURITY_VARIANCE)
+        finally:
+            ds.free()
+
+    shared, fresh_r, fresh_i = nat.Context(0), nat.Context(0), nat.Context(0)
+    try:
+        i1 = fit(shared, "int")
+        r1 = fit(shared, "real")
+        i2 = fit(shared, "int")
+        r0 = fit(fresh_r, "real")
+        i0 = fit(fresh_i, "int")
+        for t in range(L):
+            for a, b in ((r1, r0), (i1, i0), (i2, i0)):
+                (na, sa), (nb, sb_) = a.tree(t), b.tree(t)
+                assert na.tobytes() == nb.tobytes(), f"tree {t}"
+                assert sa.tobytes() == sb_.tobytes(), f"tree {t} stats"
+        for f in (i1, r1, i2, r0, i0):
+            f.free()
+    finally:
+        for c in (shared, fresh_r, fresh_i):
+            c.close()
