@@ -850,8 +850,20 @@ static int check_sampler(const sbag_sampler_params* p) {
 }
 
 // counts [R][N] on the device (bfunctions.bag)
+// (check_now = false: the caller reads the Poisson overflow flag later, with its next copy
+// from the device -- sbag_fit does after the compaction -- so the sampler and the compaction
+// queue back to back instead of the host waiting out the sampler in between)
+static int sampler_overflow(sbag_ctx* c) {
+  int* d_err;
+  TRY(ws_typed(c, "err", 1 + 16, &d_err));
+  int err = 0;
+  TRY(d2h(c, &err, d_err, 1));
+  if (err) return fail(SBAG_EUNSUPPORTED, "a Poisson draw exceeded 255");
+  return SBAG_OK;
+}
+
 static int run_sampler(sbag_ctx* c, const sbag_sampler_params* p, const std::vector<int64_t>& poff,
-                       int64_t N, uint8_t* d_counts) {
+                       int64_t N, uint8_t* d_counts, bool check_now = true) {
   const int R = p->learner_end - p->learner_begin;
   const int P = (int)poff.size() - 1;
   int64_t* d_poff;
@@ -867,9 +879,7 @@ static int run_sampler(sbag_ctx* c, const sbag_sampler_params* p, const std::vec
     launch_poisson(c->stream, d_counts, N, d_poff, P, R, p->learner_begin, p->seed, p->sample_ratio,
                    p_exp, d_err);
     HIP_TRY(hipGetLastError());
-    int err = 0;
-    TRY(d2h(c, &err, d_err, 1));
-    if (err) return fail(SBAG_EUNSUPPORTED, "a Poisson draw exceeded 255");
+    if (check_now) TRY(sampler_overflow(c));
   } else if (p->sample_ratio == 1.0) {
     launch_fill(c->stream, d_counts, 1, (int64_t)R * N);
     HIP_TRY(hipGetLastError());
@@ -2705,7 +2715,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     if (ext)  // the booster's bag column
       TRY(h2d(c, d_counts, ext->counts, (size_t)N));
     else
-      TRY(run_sampler(c, &fp->sampler, poff, N, d_counts));
+      TRY(run_sampler(c, &fp->sampler, poff, N, d_counts, false));
     tm.end(h);
   }
   // ---- 2. in-bag entry lists: two ping-pong buffers per replica.  Capacity N, or -- on the
@@ -2775,7 +2785,14 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     double ey_free = (double)dev_free;
     for (const auto& kv : c->ws)
       if (kv.first.rfind("f64_ey", 0) == 0 || kv.first.rfind("fb_", 0) == 0) ey_free += (double)kv.second.cap;
-    const bool carry = ey_bytes + 0.05 * (double)dev_total + 12e9 <= ey_free && !getenv("SBAG_F64_NO_CARRY");
+    // (and the entry lists, allocated below, where the workspace does not hold them yet)
+    double ent_new = 0.0;
+    for (const char* nm : {"entA", "entB"}) {
+      auto it = c->ws.find(nm);
+      const double need = (double)R * cap * 8.0;
+      if (it == c->ws.end() || (double)it->second.cap < need) ent_new += need * 1.125;
+    }
+    const bool carry = ey_bytes + ent_new + 0.05 * (double)dev_total + 12e9 <= ey_free && !getenv("SBAG_F64_NO_CARRY");
     static const bool ey_trace = getenv("SBAG_LEVEL_TRACE") != nullptr;
     if (ey_trace)
       fprintf(stderr, "f64 labels %s: %d replicas x %lld entries, %.1f GB of copies, %.1f GB free\n",
@@ -2804,6 +2821,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   hmark(8);
   std::vector<unsigned long long> inbag(4 * R);
   TRY(d2h(c, inbag.data(), d_inbag, (size_t)4 * R));
+  if (!ext && fp->sampler.replacement) TRY(sampler_overflow(c));  // (run_sampler left it to here)
   hmark(9);
   std::vector<int64_t> nw(R);
   unsigned int cmax = 1;
