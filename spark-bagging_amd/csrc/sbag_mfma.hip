@@ -39,10 +39,13 @@ constexpr int kMfChunk = 256;        // rows per LDS chunk of A
 constexpr int kMfPitch = kMfChunk + 16;  // LDS bytes per replica row (bank spread)
 constexpr int64_t kMfSlice = 65536;  // rows per workgroup (int32 accumulators exact)
 
-// 4 bytes x of a column vs bin b: 0x80 in every byte equal to b
+// 4 bytes x of a column vs bin b: 0x80 in every byte equal to b.  The last step
+// ~(s | t) & 0x80808080 is one gfx950 v_bitop3_b32 (LUT index a << 2 | b << 1 | c; the
+// compiler emitted or, not, and: the B fragments' VALU is what bounds this kernel, §4.8)
 __device__ __forceinline__ uint32_t eq_hi(uint32_t x, uint32_t bb) {
   const uint32_t t = x ^ bb;
-  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+  const uint32_t s = (t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return __builtin_amdgcn_bitop3_b32(s, t, 0x80808080u, 0x02);
 }
 }  // namespace
 
