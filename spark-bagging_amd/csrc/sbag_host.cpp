@@ -26,6 +26,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -138,6 +139,45 @@ struct HostPool {
   }
 };
 
+// Frees a finished fit's host containers on a thread of its own: C5's ~65 000 tree nodes
+// with heap-held class counts (allocated on the pool's workers) took 3-14 ms to destroy
+// on the fit's thread, after its last kernel and before the next fit could launch one
+struct Reaper {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<std::shared_ptr<void>> q;
+  bool stop = false;
+  std::thread th;
+  void post(std::shared_ptr<void> p) {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      if (!th.joinable()) th = std::thread([this] { loop(); });
+      q.push_back(std::move(p));
+    }
+    cv.notify_one();
+  }
+  void loop() {
+    std::unique_lock<std::mutex> lk(m);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || !q.empty(); });
+      if (q.empty()) return;  // stopped and drained
+      std::vector<std::shared_ptr<void>> w;
+      w.swap(q);
+      lk.unlock();
+      w.clear();
+      lk.lock();
+    }
+  }
+  ~Reaper() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stop = true;
+    }
+    cv.notify_all();
+    if (th.joinable()) th.join();
+  }
+};
+
 struct sbag_ctx {
   HostPool pool;
   int device = 0;
@@ -160,6 +200,11 @@ struct sbag_ctx {
   // learner parts fitting concurrently on this device (sbag_fit's overlap): each part's
   // per-replica bins get 1/concurrent_parts of the device budget
   int concurrent_parts = 1;
+  // the split stats planes copied back per level (C5's deep levels: ~50 MB), kept between
+  // fits: a fresh buffer per fit page-faulted on every first copy and was unmapped at its end
+  std::unique_ptr<int64_t[]> h_sst;
+  size_t h_sst_cap = 0;
+  Reaper reaper;  // (last: destroyed first, after its pending frees)
 };
 #define CTX_LOCK(c) std::lock_guard<std::recursive_mutex> ctx_lock_((c)->mu)
 
@@ -1713,6 +1758,7 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
     });
   sts[0] = fit_learners(c, ds, &hp[0], &fs[0]);
   for (auto& t : th) t.join();
+  const auto tj = std::chrono::steady_clock::now();
   c->concurrent_parts = 1;
   for (int k = 1; k < parts; k++) c->twins[k - 1]->concurrent_parts = 1;
   std::vector<std::unique_ptr<sbag_forest>> own;
@@ -1738,6 +1784,9 @@ int sbag_fit(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* fp, sbag_fore
   // the parts ran concurrently: the fit took the wall time, not the sum
   own[0]->timing.total_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (getenv("SBAG_PROFILE_HOST"))
+    fprintf(stderr, "host ms: parts wall %.2f, joined -> merged %.2f\n", own[0]->timing.total_ms,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tj).count());
   *out = own[0].release();
   return SBAG_OK;
 }
@@ -2695,7 +2744,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   HIP_TRY(hipEventRecord(ev_start, c->stream));
   // host-side phase timing (SBAG_PROFILE_HOST=1 prints it): where the GPU waits
   const bool hprof = getenv("SBAG_PROFILE_HOST") != nullptr;
-  double hp[20] = {0};  // [16..19]: inside histogram launches (grouping, work lists, launch)
+  double hp[24] = {0};  // [16..19]: inside histogram launches (grouping, work lists, launch)
   auto hnow = [] {
     return std::chrono::duration<double, std::milli>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -2706,6 +2755,17 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     hp[k] += t - ht;
     ht = t;
   };
+  // (the fit's tail after the forest is built: every workspace-local container's destructor)
+  struct HostTail {
+    bool on;
+    double t15;
+    ~HostTail() {
+      if (on && t15 > 0)
+        fprintf(stderr, "host ms: destructors %.2f\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
+                        .count() - t15);
+    }
+  } htail{hprof, 0.0};
 
   // ---- 1. bag: counts [R][N]
   uint8_t* d_counts;
@@ -4076,8 +4136,8 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   std::vector<uint64_t> slot_sq(R);
   for (int r = 0; r < R; r++) slot_sq[r] = inbag[3 * R + r];
   int64_t fallbacks = 0;
-  std::unique_ptr<int64_t[]> sst_buf;  // split stats planes copied back per level
-  size_t sst_cap = 0;
+  std::unique_ptr<int64_t[]>& sst_buf = c->h_sst;  // split stats planes copied back per level
+  size_t& sst_cap = c->h_sst_cap;
   for (int level = 0; level <= D; level++) {
     const int M = (int)slots.size();
     if (M == 0) break;
@@ -4284,8 +4344,12 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       pseg.insert(pseg.end(), cpseg[w].begin(), cpseg[w].end());
       psplit.insert(psplit.end(), cpsplit[w].begin(), cpsplit[w].end());
     }
+    const double hp2 = hp[2];
     hmark(2);
-    if (par.empty()) break;
+    if (par.empty()) {
+      hp[23] = hp[2] - hp2;  // the last level's node updates
+      break;
+    }
     // tile-resident entries: one partition parent per (split node, non-empty class tile)
     const int NPn = (int)par.size();  // split nodes
     std::vector<int32_t> tq_first, tq_tile;
@@ -4609,6 +4673,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
   }
   HIP_TRY(hipEventRecord(ev_stop, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  hmark(20);
 
   // ---- 7. models (toNode(prune = true)) + subspaces, trees on host threads
   forest->trees.resize(R);
@@ -4636,6 +4701,7 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     };
     c->pool.run(nth, work);
   }
+  hmark(21);
   forest->nclasses = gini ? std::max(nclasses, (int)lab.kmax + 1) : 0;
   double cats[T_NCAT] = {0};
   tm.collect(cats, nullptr, -1);
@@ -4690,6 +4756,17 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
                     " | in hist launches: grouping %.2f (count wait %.2f, prefix %.2f) work lists %.2f\n",
             hp[8], hp[9], hp[10], hp[11], hp[12], hp[0], hp[1], hp[2], hp[13], hp[14], hp[3], hp[4], hp[5],
             hp[6], hp[7], hp[15], hp[16], hp[18], hp[19], hp[17]);
+  if (hprof) {
+    fprintf(stderr, "host ms: tail: last level's nodes %.2f stream sync %.2f emit %.2f collect %.2f\n", hp[23], hp[20],
+            hp[21], hp[15]);
+    htail.t15 = hnow();
+  }
+  // the trees' nodes and the per-replica threshold tables are freed on the context's reaper
+  // thread, not between this fit's last kernel and the next fit's first
+  c->reaper.post(std::make_shared<std::tuple<std::vector<std::vector<HNode>>, std::vector<std::vector<double>>,
+                                             std::vector<std::vector<uint32_t>>,
+                                             std::vector<std::pair<int64_t, int64_t>>>>(
+      std::move(trees), std::move(thr), std::move(cuts), std::move(tseg)));
   *out = forest.release();
   return SBAG_OK;
 }
