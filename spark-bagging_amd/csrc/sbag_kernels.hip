@@ -2581,11 +2581,24 @@ __device__ __forceinline__ void split_stage_prefix(const uint32_t* __restrict__ 
     }
   }
   block_sync();
+  // (16 bins read before any is written back: one LDS round trip per 16 bins -- the plain
+  // read-add-write chain waited out a round trip per bin, 32 per group on C5)
   for (int q = tid; q < g * NS; q += 256) {
     const int fl = q / NS, c = q - fl * NS;
     uint32_t* o = pre + (size_t)fl * FS + c;
     uint32_t acc = 0;
-    for (int b = 0; b < NB; b++) {
+    int b = 0;
+    for (; b + 16 <= NB; b += 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) v[u] = o[(size_t)(b + u) * NSP];
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        acc += v[u];
+        o[(size_t)(b + u) * NSP] = acc;
+      }
+    }
+    for (; b < NB; b++) {
       acc += o[(size_t)b * NSP];
       o[(size_t)b * NSP] = acc;
     }
