@@ -4696,6 +4696,9 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
         t.sub = sub[r];
         t.exact = exact[r];
         t.ns = ns_of[r];
+        // (at most one emitted node per learning node: no regrowth of C5's 4-MB stats arrays)
+        t.nodes.reserve(trees[r].size());
+        t.stats.reserve(trees[r].size() * (size_t)ns_of[r]);
         emit(trees[r], 0, t, NS, gini, lab.shift, ns_of[r]);
       }
     };
