@@ -3163,6 +3163,15 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     return (g.grouped && g.CT < NS && NS % g.CT == 0) ? g.CT : NS;
   };
   std::function<int()> pre_hist;  // queued by launch() right before the histogram kernel
+  // grouped gini launches: per histogram slot, the class tiles whose (node, tile) sub-segment
+  // one workgroup flushes with stores (every cell of its features written, zeros included),
+  // and whether any of the slot's sub-segments is shared between workgroups (then its flushes
+  // add, and the slot must start from zero).  pre_hist then zeros only the shared slots and
+  // the tiles no sub-segment covers (C5: most deep-level slots need no zeroing at all)
+  bool zplan = false;
+  int zplan_ntc = 0;
+  std::vector<uint64_t> zplan_cov;  // [slot] bit t: tile t stored by one workgroup
+  std::vector<uint8_t> zplan_shared;  // [slot]
   auto launch = [&](const HistGeom& g, int mode, int cat,
                     const std::vector<std::pair<int64_t, int64_t>>& segs_in,
                     const std::vector<ParentInfo>& par_in) -> int {
@@ -3202,6 +3211,27 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
     const std::vector<ParentInfo>& par = regrouped ? gpar : par_in;
     build_work(segs, flush_limit, 256 * wpc * (grouped ? 2 : 1), g.T, work);
     TRY(upload_work(par));
+    static const bool zplan_off = getenv("SBAG_ZERO_ALL") && atoi(getenv("SBAG_ZERO_ALL")) != 0;  // (A/B)
+    zplan = regrouped && mode == kHistGini && !zplan_off && ha.hct == g.CT && g.CT < NS && NS % g.CT == 0 &&
+            NS / g.CT <= 64;
+    static const bool ztrace = getenv("SBAG_LEVEL_TRACE") != nullptr;
+    if (ztrace)
+      fprintf(stderr, "[sbag] zero plan %d (CT %d, layout tile %d, pieces %zu)\n", zplan ? 1 : 0, g.CT, ha.hct,
+              work.pieces.size());
+    if (zplan) {
+      zplan_ntc = NS / g.CT;
+      int smax = 0;
+      for (const HistChunk& pc : work.pieces) smax = std::max(smax, pc.slot + 1);
+      zplan_cov.assign((size_t)smax, 0ull);
+      zplan_shared.assign((size_t)smax, 0);
+      for (const HistChunk& pc : work.pieces) {
+        if (pc.slot < 0) continue;
+        if (pc.excl)
+          zplan_cov[pc.slot] |= 1ull << pc.tile;
+        else
+          zplan_shared[pc.slot] = 1;
+      }
+    }
     if (hprof) {
       const double t = hnow();
       hp[17] += t - lt0;
@@ -4627,6 +4657,40 @@ static int fit_range_impl(sbag_ctx* c, sbag_dataset* ds, const sbag_fit_params* 
       for (const ParentInfo& p : hpar)  // (a tile-resident slot's sub-segments are adjacent)
         if (zs.empty() || zs.back() != p.hist_slot) zs.push_back(p.hist_slot);
       const int64_t u32w = slot_words * (int64_t)word_bytes / 4;
+      const int64_t tilew = zplan && zplan_ntc > 0 ? u32w / zplan_ntc : 0;
+      if (zplan && (tilew & 3) == 0 && tilew * zplan_ntc == u32w) {
+        // only shared slots whole, and the uncovered class tiles of the others (as blocks
+        // of one tile's words: block index slot * ntc + tile)
+        std::vector<int32_t> zfull, zblk;
+        for (int32_t sl : zs) {
+          const bool known = sl >= 0 && (size_t)sl < zplan_cov.size();
+          if (!known || zplan_shared[sl]) {
+            zfull.push_back(sl);
+            continue;
+          }
+          for (int t = 0; t < zplan_ntc; t++)
+            if (!((zplan_cov[sl] >> t) & 1ull)) zblk.push_back(sl * zplan_ntc + t);
+        }
+        static const bool ztrace = getenv("SBAG_LEVEL_TRACE") != nullptr;
+        if (ztrace)
+          fprintf(stderr, "[sbag] zeroed: %zu of %zu slots whole, %zu tile blocks\n", zfull.size(), zs.size(),
+                  zblk.size());
+        if (!zfull.empty()) {
+          int32_t* d_zs;
+          TRY(ws_typed(c, "zslots", zfull.size(), &d_zs));
+          TRY(h2d(c, d_zs, zfull.data(), zfull.size()));
+          launch_zero_slots(c->stream, hist_nxt, d_zs, (int)zfull.size(), u32w);
+          HIP_TRY(hipGetLastError());
+        }
+        if (!zblk.empty()) {
+          int32_t* d_zb;
+          TRY(ws_typed(c, "zblocks", zblk.size(), &d_zb));
+          TRY(h2d(c, d_zb, zblk.data(), zblk.size()));
+          launch_zero_slots(c->stream, hist_nxt, d_zb, (int)zblk.size(), tilew);
+          HIP_TRY(hipGetLastError());
+        }
+        return SBAG_OK;
+      }
       if ((u32w & 3) == 0 && !zs.empty()) {
         int32_t* d_zs;
         TRY(ws_typed(c, "zslots", zs.size(), &d_zs));

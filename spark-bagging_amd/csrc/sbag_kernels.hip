@@ -1146,15 +1146,14 @@ __device__ __forceinline__ void hist_flush(const HistArgs& A, const unsigned cha
           v.w = *(const uint32_t*)(src + (size_t)(cl + 3) * plane);
           *(uint4*)(gh + gini_cell(ft0 + f, b, c0 + cl, NB, A.Fmax, hct)) = v;
         }
+      // (a stored flush writes its zeros too: the host then leaves the slot's tile unzeroed)
       for (; cl < nct; cl++) {
         const uint32_t v = *(const uint32_t*)(src + (size_t)cl * plane);
-        if (v) {
-          uint32_t* dst = gh + gini_cell(ft0 + f, b, c0 + cl, NB, A.Fmax, hct);
-          if (store)
-            *dst = v;
-          else
-            atomicAdd(dst, v);
-        }
+        uint32_t* dst = gh + gini_cell(ft0 + f, b, c0 + cl, NB, A.Fmax, hct);
+        if (store)
+          *dst = v;
+        else if (v)
+          atomicAdd(dst, v);
       }
     }
   } else {
@@ -2869,8 +2868,9 @@ void launch_zero_slots(hipStream_t st, void* hist, const int32_t* d_slots, int n
                        int64_t u32_words_per_slot) {
   if (nslots <= 0) return;
   const unsigned gx = (unsigned)std::min<int64_t>((u32_words_per_slot / 4 + 255) / 256, 64);
-  hipLaunchKernelGGL(k_zero_slots, dim3(std::max(gx, 1u), (unsigned)nslots), dim3(256), 0, st,
-                     (uint32_t*)hist, d_slots, u32_words_per_slot);
+  for (int k0 = 0; k0 < nslots; k0 += 65535)  // (grid.y is at most 65535)
+    hipLaunchKernelGGL(k_zero_slots, dim3(std::max(gx, 1u), (unsigned)std::min(65535, nslots - k0)), dim3(256), 0,
+                       st, (uint32_t*)hist, d_slots + k0, u32_words_per_slot);
 }
 
 void launch_subtract(hipStream_t st, void* dst_hist, const void* parent_hist, const int32_t* d_triples,
