@@ -928,6 +928,7 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+template <bool STG>
 __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ counts, int64_t N,
                                                  const int32_t* __restrict__ labk,
                                                  uint64_t* __restrict__ ent, int64_t cap,
@@ -971,6 +972,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
   // (no barriers between them), their wave totals through LDS, one atomic, then the stores in
   // row order (8 reservations, each a round trip between two barriers, paced the kernel)
   __shared__ int s_it[8][4];
+  __shared__ uint64_t s_stage[STG ? 4 : 1][STG ? 256 : 1];
   int incl[8], nn[8];
 #pragma unroll
   for (int it = 0; it < 8; it++) {
@@ -1007,14 +1009,38 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ cou
       before += w < wave ? s_it[it][w] : 0;
       total += s_it[it][w];
     }
-    unsigned long long pos = itbase + (unsigned long long)(before + incl[it] - nn[it]);
+    if (STG) {
+      // the wave's entries (contiguous in the output) go through its LDS run first, then out
+      // as lane-consecutive 8-byte stores: one 512-byte line run per store instead of 64
+      // lanes' entries scattered over the wave's ~1.3 KB (4 predicated stores per iteration)
+      uint64_t* sw = s_stage[wave];
+      int lp = incl[it] - nn[it];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t c = (cw[it] >> (8 * j)) & 0xffu;
-      if (c) {
-        const int32_t k = kk[j];
-        mysq += (unsigned long long)c * (unsigned long long)((int64_t)k * k);
-        er[pos++] = pack_entry((uint32_t)(row0 + j), k, c);
+      for (int j = 0; j < 4; j++) {
+        const uint32_t c = (cw[it] >> (8 * j)) & 0xffu;
+        if (c) {
+          const int32_t k = kk[j];
+          mysq += (unsigned long long)c * (unsigned long long)((int64_t)k * k);
+          sw[lp++] = pack_entry((uint32_t)(row0 + j), k, c);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int wn = s_it[it][wave];
+      uint64_t* dst = er + itbase + (unsigned long long)before;
+      for (int q = lane; q < wn; q += 64) dst[q] = sw[q];
+      __builtin_amdgcn_wave_barrier();  // (the run is rewritten by the next iteration)
+    } else {
+      unsigned long long pos = itbase + (unsigned long long)(before + incl[it] - nn[it]);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t c = (cw[it] >> (8 * j)) & 0xffu;
+        if (c) {
+          const int32_t k = kk[j];
+          mysq += (unsigned long long)c * (unsigned long long)((int64_t)k * k);
+          er[pos++] = pack_entry((uint32_t)(row0 + j), k, c);
+        }
       }
     }
     itbase += (unsigned long long)total;
@@ -1045,8 +1071,13 @@ void launch_compact(hipStream_t st, const uint8_t* counts, int64_t N, int R, con
                     uint64_t* ent, int64_t cap, unsigned long long* d_cursor,
                     unsigned long long* d_wsum, unsigned int* d_cmax, unsigned long long* d_sqsum) {
   const int64_t chunks = (N + 8191) / 8192;
-  hipLaunchKernelGGL(k_compact, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, d_labk,
-                     ent, cap, d_cursor, d_wsum, d_cmax, d_sqsum, R);
+  static const bool stg = !getenv("SBAG_COMPACT_STG") || atoi(getenv("SBAG_COMPACT_STG")) != 0;  // (A/B)
+  if (stg)
+    hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, d_labk,
+                       ent, cap, d_cursor, d_wsum, d_cmax, d_sqsum, R);
+  else
+    hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, N, d_labk,
+                       ent, cap, d_cursor, d_wsum, d_cmax, d_sqsum, R);
 }
 
 // ======================================================================
