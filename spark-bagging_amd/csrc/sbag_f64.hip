@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "sbag_internal.h"
 
@@ -178,7 +179,10 @@ __global__ __launch_bounds__(256) void k_chunk_scan(const uint32_t* __restrict__
   if (threadIdx.x == 0) cursor[r] = carry;
 }
 
-// one entry per in-bag row, in row order
+// one entry per in-bag row, in row order.  STG: the block's entries of an iteration (and
+// their labels), contiguous in the output, are staged in LDS and stored by consecutive
+// threads, instead of each thread's up to 4 entries at its own scattered positions
+template <bool STG>
 __global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restrict__ counts,
                                                          const int32_t* __restrict__ labk, int64_t N,
                                                          int R, int64_t chunks,
@@ -193,24 +197,48 @@ __global__ __launch_bounds__(256) void k_compact_ordered(const uint8_t* __restri
   uint64_t* er = ent + (int64_t)r * cap;
   double* eyr = ey ? ey + (int64_t)r * cap : nullptr;  // (the carried fp64 labels, same positions)
   unsigned long long pos0 = base[(int64_t)r * chunks + chunk];
+  __shared__ uint64_t s_e[STG ? 1024 : 1];
+  __shared__ double s_y[STG ? 1024 : 1];
+  const bool vec = ((N | (int64_t)(uintptr_t)cr) & 3) == 0;
   for (int it = 0; it < kChunkRows / 1024; it++) {
     const int64_t row0 = chunk * kChunkRows + (int64_t)it * 1024 + (int64_t)threadIdx.x * 4;
     uint32_t c[4];
     int n = 0;
+    if (vec && row0 + 3 < N) {
+      const uint32_t w = *(const uint32_t*)(cr + row0);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      c[j] = row0 + j < N ? cr[row0 + j] : 0u;
-      n += c[j] ? 1 : 0;
+      for (int j = 0; j < 4; j++) c[j] = (w >> (8 * j)) & 0xffu;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) c[j] = row0 + j < N ? cr[row0 + j] : 0u;
     }
+#pragma unroll
+    for (int j = 0; j < 4; j++) n += c[j] ? 1 : 0;
     int tot;
     const int ex = block_excl_scan256(n, s_wave, &tot);
-    unsigned long long pos = pos0 + (unsigned long long)ex;
+    if (STG) {
+      int lp = ex;
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (c[j]) {
-        if (eyr) eyr[pos] = y[row0 + j];
-        er[pos++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
+      for (int j = 0; j < 4; j++)
+        if (c[j]) {
+          if (eyr) s_y[lp] = y[row0 + j];
+          s_e[lp++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
+        }
+      block_sync();
+      for (int q = threadIdx.x; q < tot; q += 256) {
+        er[pos0 + q] = s_e[q];
+        if (eyr) eyr[pos0 + q] = s_y[q];
       }
+      block_sync();  // (the staging is rewritten by the next iteration)
+    } else {
+      unsigned long long pos = pos0 + (unsigned long long)ex;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (c[j]) {
+          if (eyr) eyr[pos] = y[row0 + j];
+          er[pos++] = pack_entry((uint32_t)(row0 + j), labk[row0 + j], c[j]);
+        }
+    }
     pos0 += (unsigned long long)tot;
   }
 }
@@ -228,8 +256,13 @@ void launch_compact_ordered(hipStream_t st, const uint8_t* counts, const int32_t
                             double* ey) {
   const int64_t chunks = compact_ordered_chunks(N);
   hipLaunchKernelGGL(k_chunk_scan, dim3(R), dim3(256), 0, st, d_ncnt, chunks, d_base, d_cursor);
-  hipLaunchKernelGGL(k_compact_ordered, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, labk,
-                     N, R, chunks, d_base, ent, cap, y, ey);
+  static const bool stg = !getenv("SBAG_COMPACT_STG") || atoi(getenv("SBAG_COMPACT_STG")) != 0;  // (A/B)
+  if (stg)
+    hipLaunchKernelGGL(k_compact_ordered<true>, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, labk,
+                       N, R, chunks, d_base, ent, cap, y, ey);
+  else
+    hipLaunchKernelGGL(k_compact_ordered<false>, dim3((unsigned)(chunks * R)), dim3(256), 0, st, counts, labk,
+                       N, R, chunks, d_base, ent, cap, y, ey);
 }
 
 int64_t compact_ordered_chunks(int64_t N) { return (N + kChunkRows - 1) / kChunkRows; }
